@@ -1,0 +1,78 @@
+"""ctypes binding of libdmlp.so (the in-tree native core).
+
+The library is loaded from the package directory only; if it is missing we raise instead of
+silently falling back to a Python path (GPU code must be the native HIP code).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "libdmlp.so"
+
+_lib = None
+
+vp, i32, i64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_float
+i64p = C.POINTER(C.c_int64)
+i32p = C.POINTER(C.c_int)
+
+_SIGS = {
+    "dmlp_center": (i32, [vp, i64, i32, vp, vp]),
+    "dmlp_prep_data": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp]),
+    "dmlp_prep_queries": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp]),
+    "dmlp_screen_kmax": (i32, [i32]),
+    "dmlp_screen_lds_bytes": (i32, [i32, i32]),
+    "dmlp_screen_waves": (i32, [i32, i32]),
+    "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
+                          vp, vp]),
+    "dmlp_refine": (i32, [i32, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, i32, i32,
+                          vp, vp, vp, vp]),
+    "dmlp_exact_rows": (i32, [vp, i64, i32, vp, vp, i32, vp, i64, vp]),
+    "dmlp_merge": (i32, [vp, vp, i32, i64, i32, vp, i32, vp, vp, i32, vp]),
+    "dmlp_finalize": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp]),
+    "dmlp_format_bound": (i64, [i32]),
+    "dmlp_format_report": (i32, [vp, i32, i32, vp, vp, vp]),
+    "dmlp_cpu_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp, i32]),
+    "dmlp_cpu_finalize": (i32, [vp, vp, i32, vp, i64, vp, vp, vp]),
+    "dmlp_cpu_merge": (i32, [vp, vp, i32, i64, i32, vp, i64, vp, vp, i32]),
+    "dmlp_kdtree_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp]),
+    "dmlp_cpu_format_report": (i64, [vp, i64, i64, vp]),
+    "dmlp_cpu_format_debug": (i64, [vp, vp, i32, vp, vp, i64, vp, i64]),
+    "dmlp_parse_header": (i32, [vp, i64, i64p, i64p, i32p, i64p]),
+    "dmlp_parse_body": (i64, [vp, i64, i64, i64, i64, i32, vp, vp, vp, vp, i32]),
+    "dmlp_version": (C.c_char_p, []),
+    "dmlp_device_count": (i32, []),
+}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle of libdmlp.so."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        if os.environ.get("DMLP_AUTOBUILD", "1") == "1":
+            from . import build as _build
+            _build.build(engine=False)
+        if not LIB_PATH.exists():
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not built; run `python -m distributed_machine_learning_project_amd.build`")
+    h = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(h, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = h
+    return h
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+    return rc

@@ -1,0 +1,112 @@
+// dmlp.h — C ABI of libdmlp.so, the native core of the MI355X k-NN framework.
+//
+// Everything the reference computes in its hot loops is exposed
+// here as plain C entry points so that (a) Python binds them with ctypes (no torch headers,
+// no hipify, no JIT) and (b) the standalone MPI/RCCL `knn_engine` binary links the very same
+// code.  All GPU entry points are asynchronous on the given HIP stream and return 0 on a
+// successful launch, or a negative error code.  CPU entry points are synchronous.
+//
+// Numerical contract (reference common.cpp:57-79, engine.cpp:12-18):
+//   dist(q,x) = sum_{a=0}^{A-1} (q_a - x_a)^2, IEEE double, left to right, no FMA;
+//   order     = (dist ascending, id descending);
+//   vote      = max count, ties -> larger label; empty -> -1;
+//   checksum  = FNV-1a-64: h ^= (u64)label; h *= P; for id in order: h ^= (u64)(id+1); h *= P.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// ---------------------------------------------------------------- device: data preparation (K1)
+// mu[A] = mean of the first min(N, 4096) rows (centering offset for the screen; any value is
+// correct, a good one only tightens the screen).
+int dmlp_center(const double* X, int64_t N, int A, double* mu, void* stream);
+
+// X [N][A] fp64 -> fragment-native bf16 hi/lo tiles (64 points x 32*KT attrs per tile),
+// xinit[n_tiles*64] = -(|x-mu|^2)/2 (fp32; -inf for padding), xnmax_bits = max |x-mu|^2 (fp32
+// bits), bad |= 1 if any value is non-finite or too large for the bf16x3 screen.
+int dmlp_prep_data(const double* X, int64_t N, int A, const double* mu, int KT, void* xfrag,
+                   float* xinit, unsigned* xnmax_bits, unsigned* bad, void* stream);
+
+// Qx [Q][A] fp64 -> qhi/qlo [Q][32*KT] bf16, qn[Q] = |q-mu|^2 (fp32).
+int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT, void* qhi,
+                      void* qlo, float* qn, unsigned* bad, void* stream);
+
+// ---------------------------------------------------------------- device: screen (K2+K3, fused)
+// bf16x3 MFMA screen + per-query streaming threshold + candidate compaction.  Queries are the
+// class list qidx[0..nq); data is split into S slices.  Output: for class position p and slice s,
+// cand_cnt[p*S+s] candidates (or -1 on overflow) stored at cand_ids[(p*S+s)*cap ...].
+// cap in {128, 256}; the k of every query in the list must be <= dmlp_screen_kmax(cap).
+int dmlp_screen_kmax(int cap);
+// xnmax_bits / bad are the device words written by dmlp_prep_data (no host round trip).
+int dmlp_screen(int KT, int cap, const void* xfrag, const float* xinit, int64_t n_tiles,
+                const void* qhi, const void* qlo, const float* qn, const int* qidx, const int* qk,
+                int nq, const unsigned* xnmax_bits, const unsigned* bad, float eps_rel, int S,
+                int* cand_ids, int* cand_cnt, void* stream);
+int dmlp_screen_lds_bytes(int KT, int cap);
+int dmlp_screen_waves(int KT, int cap);
+
+// ---------------------------------------------------------------- device: exact refine (K2 exact + K3 + K6)
+// Exact fp64 distances of the candidates, exact top-k under (dist asc, id desc).
+// Writes out_d/out_i[q*kstride + i], i < k_q (rest untouched).  status[q] = 1 if the query
+// overflowed and must take the exact fallback path, else 0.  If labels != NULL the vote and
+// checksum are fused (out_label[q], out_cs[q]); label_lo/label_hi give the label range.
+int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const double* X,
+                int A, const double* Qx, const int* qidx, const int* qk, int nq, double* out_d,
+                int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
+                int* out_label, uint64_t* out_cs, int* status, void* stream);
+
+// ---------------------------------------------------------------- device: exact rows (K2, fallback)
+// D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).
+int dmlp_exact_rows(const double* X, int64_t N, int A, const double* Qx, const int* qidx, int nq,
+                    double* D, int64_t ldd, void* stream);
+
+// ---------------------------------------------------------------- device: top-k merge (K4)
+// L sorted lists per query (list l of query q at in_*[l*list_stride + q*kin + j]), padded with
+// (+inf, -1).  Writes the merged top-k_q of every query q < nq to out_*[q*kout + i].
+int dmlp_merge(const double* in_d, const int* in_i, int L, int64_t list_stride, int kin,
+               const int* qk, int nq, double* out_d, int* out_i, int kout, void* stream);
+
+// ---------------------------------------------------------------- device: vote + checksum (K5, K7)
+// Rows qidx[i] (or i if qidx == NULL), i < nq.
+int dmlp_finalize(const double* d, const int* ids, int kstride, const int* qk, const int* qidx,
+                  int nq, const int* labels, int label_lo, int label_hi, int* out_label,
+                  uint64_t* out_cs, void* stream);
+
+// ---------------------------------------------------------------- device: report formatting (K7)
+// "Query <qid> checksum: <cs>\n" for q < nq into out (needs dmlp_format_bound bytes).
+// line_off[nq+1] is scratch (int64) that receives the line offsets; *total_out (device) = bytes.
+int64_t dmlp_format_bound(int nq);
+int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off, char* out,
+                       void* stream);
+
+// ---------------------------------------------------------------- host (CPU) implementations
+int dmlp_cpu_knn(const double* X, int64_t N, int A, const double* Qx, int64_t Q, const int* qk,
+                 int kstride, double* out_d, int* out_i, int nthreads);
+int dmlp_cpu_finalize(const double* d, const int* ids, int kstride, const int* qk, int64_t Q,
+                      const int* labels, int* out_label, uint64_t* out_cs);
+int dmlp_cpu_merge(const double* in_d, const int* in_i, int L, int64_t list_stride, int kin,
+                   const int* qk, int64_t Q, double* out_d, int* out_i, int kout);
+int dmlp_kdtree_knn(const double* X, int64_t N, int A, const double* Qx, int64_t Q,
+                    const int* qk, int kstride, double* out_d, int* out_i);
+// Text report, host side.  Returns bytes written (buffer must hold 48*Q bytes).
+int64_t dmlp_cpu_format_report(const uint64_t* cs, int64_t Q, int64_t qid_base, char* out);
+int64_t dmlp_cpu_format_debug(const double* d, const int* ids, int kstride, const int* qk,
+                              const int* labels_pred, int64_t Q, char* out, int64_t cap);
+
+// ---------------------------------------------------------------- host: input parsing (common.cpp:12-44)
+// Parses the header.  Returns 0 on success.
+int dmlp_parse_header(const char* buf, int64_t len, int64_t* N, int64_t* Q, int* A,
+                      int64_t* body_off);
+// Parses N data lines and Q query lines starting at body_off (multi-threaded).
+// Returns 0, or -(line_no+1) of the first malformed line.
+int64_t dmlp_parse_body(const char* buf, int64_t len, int64_t body_off, int64_t N, int64_t Q,
+                        int A, int* labels, double* X, int* qk, double* Qx, int nthreads);
+
+const char* dmlp_version(void);
+int dmlp_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,178 @@
+// prep.hip — K1: layout transforms feeding the bf16x3 MFMA screen.
+//
+// The reference packs AoS vector<DataPoint> into flat arrays on rank 0 (engine.cpp:79-96,
+// bench_1 @0xe1b0).  Here the flat fp64 rows are already on the GPU; this pass converts them
+// ONCE per KNN call into the exact register image the MFMA A-operand wants, so the screen
+// kernel's staging is a straight lane-linear global_load_lds of 1 KiB fragments:
+//
+//   tile t (64 points) = [rt 0..3][kt 0..KT-1][hl 0..1][lane 0..63][8 x bf16]
+//   lane l of fragment (rt,kt,hl) holds point t*64 + rt*16 + (l&15),
+//   attributes kt*32 + (l>>4)*8 + j, j = 0..7  (mfma_f32_16x16x32_bf16 A map).
+//   hl = 0: hi = bf16(x - mu), hl = 1: lo = bf16((x - mu) - hi).
+//   xinit[t*64 + r] = -(|x-mu|^2)/2 in fp32 (the MFMA C-init; -inf for padding rows).
+#include "dmlp.h"
+#include "dmlp_device.h"
+#include <float.h>
+
+namespace {
+
+constexpr double kMaxAbs = 1.0e15;  // |x - mu| bound for the screen's fp32 range analysis
+
+__device__ __forceinline__ unsigned short bf16_rn_bits(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32, round-to-nearest-even
+  return __builtin_bit_cast(unsigned short, b);
+}
+
+// hi/lo split: hi = bf16(c), lo = bf16(c - hi) with c - hi exact in fp64.
+__device__ __forceinline__ void split_bf16(double c, unsigned short& hi, unsigned short& lo) {
+  const float cf = (float)c;
+  hi = bf16_rn_bits(cf);
+  const float hf = __uint_as_float(((unsigned)hi) << 16);
+  const double r = c - (double)hf;
+  lo = bf16_rn_bits((float)r);
+}
+
+__global__ void k_center(const double* __restrict__ X, int64_t N, int A, double* __restrict__ mu) {
+  const int64_t n = N < 4096 ? N : 4096;
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += X[i * A + a];
+    mu[a] = n > 0 ? s / (double)n : 0.0;
+  }
+}
+
+// One thread per (point, 8-attribute group).
+__global__ void k_prep_frag(const double* __restrict__ X, int64_t N, int A,
+                            const double* __restrict__ mu, int KT, int64_t n_tiles,
+                            uint4* __restrict__ frag, unsigned* __restrict__ bad) {
+  const int groups = KT * 4;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = n_tiles * 64 * groups;
+  if (gid >= total) return;
+  const int64_t p = gid / groups;
+  const int g = (int)(gid - p * groups);
+  const int kt = g >> 2, kg = g & 3;
+  const int64_t t = p >> 6;
+  const int pl = (int)(p & 63);
+  const int rt = pl >> 4, r = pl & 15;
+  const int lane = r + 16 * kg;
+  unsigned short hi[8], lo[8];
+  unsigned badv = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int a = kt * 32 + kg * 8 + j;
+    double c = 0.0;
+    if (p < N && a < A) {
+      const double x = X[p * A + a];
+      c = x - mu[a];
+      if (!(fabs(c) < kMaxAbs)) { badv = 1; c = 0.0; }
+    }
+    split_bf16(c, hi[j], lo[j]);
+  }
+  if (badv) atomicOr(bad, 1u);
+  const int64_t fbase = t * (int64_t)(4 * KT * 2) * 64;  // in uint4 (16 B) units
+  const int64_t f_hi = fbase + (int64_t)((rt * KT + kt) * 2 + 0) * 64 + lane;
+  const int64_t f_lo = fbase + (int64_t)((rt * KT + kt) * 2 + 1) * 64 + lane;
+  uint4 vh, vl;
+  vh.x = hi[0] | ((unsigned)hi[1] << 16); vh.y = hi[2] | ((unsigned)hi[3] << 16);
+  vh.z = hi[4] | ((unsigned)hi[5] << 16); vh.w = hi[6] | ((unsigned)hi[7] << 16);
+  vl.x = lo[0] | ((unsigned)lo[1] << 16); vl.y = lo[2] | ((unsigned)lo[3] << 16);
+  vl.z = lo[4] | ((unsigned)lo[5] << 16); vl.w = lo[6] | ((unsigned)lo[7] << 16);
+  frag[f_hi] = vh;
+  frag[f_lo] = vl;
+}
+
+// One thread per point: xinit and the running max norm.
+__global__ void k_prep_norm(const double* __restrict__ X, int64_t N, int A,
+                            const double* __restrict__ mu, int64_t n_pad,
+                            float* __restrict__ xinit, unsigned* __restrict__ xnmax_bits) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pad) return;
+  if (p >= N) { xinit[p] = -INFINITY; return; }
+  double s = 0.0;
+  for (int a = 0; a < A; ++a) {
+    double c = X[p * A + a] - mu[a];
+    if (!(fabs(c) < kMaxAbs)) c = 0.0;
+    s += c * c;
+  }
+  xinit[p] = (float)(-0.5 * s);
+  // round the max up so the bound stays conservative
+  const float sf = (float)s;
+  const float up = sf * (1.0f + 1.0e-6f) + 1.0e-30f;
+  atomicMax(xnmax_bits, __float_as_uint(up));
+}
+
+__global__ void k_prep_queries(const double* __restrict__ Qx, int64_t Q, int A,
+                               const double* __restrict__ mu, int KT,
+                               unsigned short* __restrict__ qhi, unsigned short* __restrict__ qlo,
+                               float* __restrict__ qn, unsigned* __restrict__ bad) {
+  const int64_t q = (int64_t)blockIdx.x;
+  if (q >= Q) return;
+  const int W = KT * 32;
+  __shared__ double red[256];
+  double s = 0.0;
+  unsigned badv = 0;
+  for (int a = threadIdx.x; a < W; a += blockDim.x) {
+    double c = 0.0;
+    if (a < A) {
+      c = Qx[q * A + a] - mu[a];
+      if (!(fabs(c) < kMaxAbs)) { badv = 1; c = 0.0; }
+    }
+    unsigned short h, l;
+    split_bf16(c, h, l);
+    qhi[q * W + a] = h;
+    qlo[q * W + a] = l;
+    s += c * c;
+  }
+  if (badv) atomicOr(bad, 1u);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) qn[q] = (float)red[0];
+}
+
+}  // namespace
+
+extern "C" int dmlp_center(const double* X, int64_t N, int A, double* mu, void* stream) {
+  hipLaunchKernelGGL(k_center, dim3(1), dim3(256), 0, (hipStream_t)stream, X, N, A, mu);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
+                              void* xfrag, float* xinit, unsigned* xnmax_bits, unsigned* bad,
+                              void* stream) {
+  if (KT < 1 || A > KT * 32) return -1;
+  const int64_t n_tiles = (N + 63) / 64;
+  const int64_t total = n_tiles * 64 * KT * 4;
+  if (total > 0) {
+    const int64_t blocks = (total + 255) / 256;
+    hipLaunchKernelGGL(k_prep_frag, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X,
+                       N, A, mu, KT, n_tiles, (uint4*)xfrag, bad);
+    DMLP_LAUNCH_CHECK();
+    const int64_t n_pad = n_tiles * 64;
+    hipLaunchKernelGGL(k_prep_norm, dim3((unsigned)((n_pad + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, X, N, A, mu, n_pad, xinit, xnmax_bits);
+    DMLP_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
+                                 void* qhi, void* qlo, float* qn, unsigned* bad, void* stream) {
+  if (KT < 1 || A > KT * 32) return -1;
+  if (Q <= 0) return 0;
+  hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)Q), dim3(64), 0, (hipStream_t)stream, Qx, Q,
+                     A, mu, KT, (unsigned short*)qhi, (unsigned short*)qlo, qn, bad);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}

@@ -1,0 +1,412 @@
+// refine.hip — exact re-ranking, top-k merge, vote/checksum and report formatting.
+//
+//  * k_refine   : exact fp64 distances (reference order, no FMA: engine.cpp:12-18) of the
+//                 screen's survivors and an exact top-k under (dist asc, id desc)
+//                 (SURVEY.md §2.5 K2/K3/K6).  One wave per query; a P-slot running top-k in
+//                 LDS absorbs 64 candidates per step and is re-sorted (register bitonic) only
+//                 when full.  Vote + FNV checksum are fused when labels are given (K5/K7).
+//  * k_merge    : K-way merge of sorted per-shard top-k lists — the device analog of bench_2's
+//                 user MPI_Op (@0xbc70) and bench_1's root sort (@0xdae6); RCCL has no user
+//                 reductions, so strategies call this between send/recv rounds (K4).
+//  * k_finalize : vote (max count, tie -> larger label; engine.cpp:319-332) + FNV-1a checksum
+//                 (common.cpp:59-70) of sorted lists.
+//  * k_exact_rows: full exact distance rows (fallback for k > screen kmax, overflowing queries,
+//                 or data outside the screen's range).
+//  * k_format_* : "Query <id> checksum: <u64>\n" rendered on the GPU (common.cpp:70).
+#include "dmlp.h"
+#include "dmlp_device.h"
+#include <float.h>
+
+namespace {
+
+constexpr int kHistCap = 1024;  // per-wave label histogram (labels in [lo, lo+1024))
+
+__device__ __forceinline__ double exact_dist_row(const double* __restrict__ q,
+                                                 const double* __restrict__ x, int A) {
+  double s = 0.0;
+  if ((A & 1) == 0) {
+    const double2* x2 = (const double2*)x;
+    for (int a = 0; a < (A >> 1); ++a) {
+      const double2 v = x2[a];
+      const double d0 = __dsub_rn(q[2 * a], v.x);
+      s = __dadd_rn(s, __dmul_rn(d0, d0));
+      const double d1 = __dsub_rn(q[2 * a + 1], v.y);
+      s = __dadd_rn(s, __dmul_rn(d1, d1));
+    }
+  } else {
+    for (int a = 0; a < A; ++a) {
+      const double d = __dsub_rn(q[a], x[a]);
+      s = __dadd_rn(s, __dmul_rn(d, d));
+    }
+  }
+  return s;
+}
+
+// Running top-k of one wave, P = E*64 slots in LDS: [0,k) current best (sorted), new
+// candidates appended at k+fill; re-sorted when fewer than 64 free slots remain.
+template <int E>
+struct RunTopK {
+  static constexpr int P = E * 64;
+  double* d;
+  int* id;
+  int k;
+  int fill;
+  __device__ void init(double* d_, int* id_, int k_) {
+    d = d_; id = id_; k = k_; fill = 0;
+    for (int i = dmlp::lane_id(); i < P; i += 64) { d[i] = INFINITY; id[i] = -1; }
+    dmlp::wave_sync();
+  }
+  __device__ void flush() {
+    if (fill == 0) return;
+    double rd[E]; int ri[E];
+    const int lane = dmlp::lane_id();
+    dmlp::wave_sync();
+#pragma unroll
+    for (int r = 0; r < E; ++r) { rd[r] = d[r * 64 + lane]; ri[r] = id[r * 64 + lane]; }
+    dmlp::wave_sort_keys<E>(rd, ri);
+    dmlp::wave_sync();
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int i = r * 64 + lane;
+      d[i] = i < k ? rd[r] : INFINITY;
+      id[i] = i < k ? ri[r] : -1;
+    }
+    dmlp::wave_sync();
+    fill = 0;
+  }
+  __device__ void push(bool valid, double dv, int iv) {
+    const unsigned long long m = __ballot(valid);
+    if (valid) {
+      const int pos = k + fill + __popcll(m & dmlp::lanemask_lt());
+      d[pos] = dv;
+      id[pos] = iv;
+    }
+    fill += __popcll(m);
+    if (k + fill + 64 > P) flush();
+  }
+};
+
+__device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* __restrict__ labels,
+                                              int label_lo, int label_hi, int* hist,
+                                              int* out_label, uint64_t* out_cs) {
+  const int lane = dmlp::lane_id();
+  // labels of ids < 0 (padding) are never read
+  const int label = k > 0 ? dmlp::wave_vote(ids, k, labels, label_lo, label_hi, hist, kHistCap) : -1;
+  if (lane == 0) {
+    *out_label = label;
+    *out_cs = dmlp::fnv_checksum(label, ids, k);
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void k_refine(
+    const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int S, int cap,
+    const double* __restrict__ X, int A, const double* __restrict__ Qx,
+    const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
+    int* __restrict__ out_i, int kstride, const int* __restrict__ labels, int label_lo,
+    int label_hi, int* __restrict__ out_label, uint64_t* __restrict__ out_cs,
+    int* __restrict__ status) {
+  constexpr int P = E * 64;
+  constexpr int SMAX = 256;
+  __shared__ double s_d[4][P];
+  __shared__ int s_i[4][P];
+  __shared__ int s_pre[4][SMAX + 1];
+  __shared__ int s_hist[4][kHistCap];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int p = blockIdx.x * 4 + wave;
+  if (p >= nq) return;
+  const int q = __builtin_amdgcn_readfirstlane(qidx[p]);
+  const int k = __builtin_amdgcn_readfirstlane(qk[q]);
+  const int* cnt = cand_cnt + (int64_t)p * S;
+  // prefix of candidate counts over slices (S <= SMAX)
+  int* pre = s_pre[wave];
+  bool ovf = false;
+  if (lane == 0) {
+    int acc = 0;
+    pre[0] = 0;
+    for (int s = 0; s < S; ++s) {
+      const int n = cnt[s];
+      if (n < 0) ovf = true;
+      acc += n < 0 ? 0 : n;
+      pre[s + 1] = acc;
+    }
+  }
+  ovf = __shfl(ovf ? 1 : 0, 0) != 0;
+  if (ovf) {
+    if (lane == 0) status[q] = 1;
+    return;
+  }
+  if (lane == 0) status[q] = 0;
+  dmlp::wave_sync();
+  const int M = pre[S];
+  RunTopK<E> tk;
+  tk.init(s_d[wave], s_i[wave], k);
+  const double* qv = Qx + (int64_t)q * A;
+  for (int j0 = 0; j0 < M; j0 += 64) {
+    const int j = j0 + lane;
+    const bool valid = j < M;
+    int id = 0;
+    double dv = INFINITY;
+    if (valid) {
+      // slice containing flat index j: largest s with pre[s] <= j
+      int lo = 0, hi = S;  // pre[lo] <= j < pre[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= j) lo = mid; else hi = mid;
+      }
+      id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
+      dv = exact_dist_row(qv, X + (int64_t)id * A, A);
+    }
+    tk.push(valid, dv, id);
+  }
+  tk.flush();
+  for (int i = lane; i < k; i += 64) {
+    out_d[(int64_t)q * kstride + i] = tk.d[i];
+    out_i[(int64_t)q * kstride + i] = tk.id[i];
+  }
+  if (labels) {
+    dmlp::wave_sync();
+    finalize_wave(tk.id, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q);
+  }
+}
+
+// Sequential k-way merge, one thread per query (lists are short and already sorted).
+__global__ void k_merge(const double* __restrict__ in_d, const int* __restrict__ in_i, int L,
+                        int64_t list_stride, int kin, const int* __restrict__ qk, int nq,
+                        double* __restrict__ out_d, int* __restrict__ out_i, int kout) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const int k = qk[q];
+  constexpr int LMAX = 64;
+  int head[LMAX];
+  for (int l = 0; l < L; ++l) head[l] = 0;
+  const int lim = k < kin ? k : kin;
+  for (int o = 0; o < k; ++o) {
+    int best = -1;
+    double bd = INFINITY;
+    int bi = -1;
+    for (int l = 0; l < L; ++l) {
+      if (head[l] >= lim) continue;
+      const int64_t off = l * list_stride + (int64_t)q * kin + head[l];
+      const int ii = in_i[off];
+      if (ii < 0) continue;  // padding
+      const double dd = in_d[off];
+      if (best < 0 || dmlp::key_less(dd, ii, bd, bi)) { best = l; bd = dd; bi = ii; }
+    }
+    if (best < 0) { bd = INFINITY; bi = -1; }
+    else head[best]++;
+    out_d[(int64_t)q * kout + o] = bd;
+    out_i[(int64_t)q * kout + o] = bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ d,
+                                                  const int* __restrict__ ids, int kstride,
+                                                  const int* __restrict__ qk,
+                                                  const int* __restrict__ qidx, int nq,
+                                                  const int* __restrict__ labels, int label_lo,
+                                                  int label_hi, int* __restrict__ out_label,
+                                                  uint64_t* __restrict__ out_cs) {
+  __shared__ int s_hist[4][kHistCap];
+  const int wave = threadIdx.x >> 6;
+  const int i = blockIdx.x * 4 + wave;
+  if (i >= nq) return;
+  const int q = qidx ? qidx[i] : i;
+  const int k = qk[q];
+  finalize_wave(ids + (int64_t)q * kstride, k, labels, label_lo, label_hi, s_hist[wave],
+                out_label + q, out_cs + q);
+}
+
+// 64 queries x 64 points per 256-thread block; each thread a 4x4 micro-tile; attributes staged
+// through LDS in chunks of 16 and accumulated strictly in attribute order.
+__global__ __launch_bounds__(256) void k_exact_rows(const double* __restrict__ X, int64_t N, int A,
+                                                    const double* __restrict__ Qx,
+                                                    const int* __restrict__ qidx, int nq,
+                                                    double* __restrict__ D, int64_t ldd) {
+  constexpr int AC = 16;
+  __shared__ double Qs[64][AC + 1];
+  __shared__ double Xs[64][AC + 1];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t pt0 = (int64_t)blockIdx.x * 64;
+  const int qt0 = blockIdx.y * 64;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  for (int a0 = 0; a0 < A; a0 += AC) {
+    const int ac = A - a0 < AC ? A - a0 : AC;
+    for (int e = tid; e < 64 * AC; e += 256) {
+      const int r = e / AC, a = e % AC;
+      const int qi = qt0 + r;
+      Qs[r][a] = (qi < nq && a < ac) ? Qx[(int64_t)qidx[qi] * A + a0 + a] : 0.0;
+      const int64_t pi = pt0 + r;
+      Xs[r][a] = (pi < N && a < ac) ? X[pi * A + a0 + a] : 0.0;
+    }
+    __syncthreads();
+    for (int a = 0; a < ac; ++a) {
+      double qv[4], xv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qv[i] = Qs[ty + 16 * i][a];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xv[j] = Xs[tx + 16 * j][a];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const double dd = __dsub_rn(qv[i], xv[j]);
+          acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(dd, dd));
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int qi = qt0 + ty + 16 * i;
+    if (qi >= nq) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t pi = pt0 + tx + 16 * j;
+      if (pi < N) D[(int64_t)qi * ldd + pi] = acc[i][j];
+    }
+  }
+}
+
+// ---- report formatting: "Query <qid> checksum: <cs>\n"
+__device__ __forceinline__ int ndig_u64(uint64_t v) {
+  int n = 1;
+  while (v >= 10) { v /= 10; ++n; }
+  return n;
+}
+__device__ __forceinline__ int line_len(int64_t qid, uint64_t cs) {
+  return 6 + ndig_u64((uint64_t)qid) + 11 + ndig_u64(cs) + 1;
+}
+
+__global__ void k_fmt_len(const uint64_t* __restrict__ cs, int nq, int qid_base,
+                          int64_t* __restrict__ off, int64_t* __restrict__ blocksum) {
+  __shared__ int64_t sh[1024];
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  const int64_t v = i < nq ? line_len((int64_t)qid_base + i, cs[i]) : 0;
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int64_t t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (i < nq) off[i + 1] = sh[threadIdx.x];  // block-local inclusive
+  if (threadIdx.x == 1023) blocksum[blockIdx.x] = sh[1023];
+}
+
+__global__ void k_fmt_scan_blocks(int64_t* __restrict__ blocksum, int nb) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int64_t acc = 0;
+    for (int b = 0; b < nb; ++b) { const int64_t v = blocksum[b]; blocksum[b] = acc; acc += v; }
+    blocksum[nb] = acc;
+  }
+}
+
+__global__ void k_fmt_write(const uint64_t* __restrict__ cs, int nq, int qid_base,
+                            int64_t* __restrict__ off, const int64_t* __restrict__ blocksum,
+                            char* __restrict__ out) {
+  const int i = blockIdx.x * 1024 + threadIdx.x;
+  if (i >= nq) return;
+  const int64_t qid = (int64_t)qid_base + i;
+  const uint64_t v = cs[i];
+  const int len = line_len(qid, v);
+  const int64_t end = blocksum[blockIdx.x] + off[i + 1];
+  int64_t pos = end - len;
+  const char* pre = "Query ";
+  for (int c = 0; c < 6; ++c) out[pos++] = pre[c];
+  char tmp[24];
+  int n = 0;
+  uint64_t t = (uint64_t)qid;
+  do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
+  while (n) out[pos++] = tmp[--n];
+  const char* mid = " checksum: ";
+  for (int c = 0; c < 11; ++c) out[pos++] = mid[c];
+  t = v;
+  do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
+  while (n) out[pos++] = tmp[--n];
+  out[pos++] = '\n';
+  off[i + 1] = end;
+  if (i == 0) off[0] = 0;
+}
+
+}  // namespace
+
+extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S,
+                           const double* X, int A, const double* Qx, const int* qidx,
+                           const int* qk, int nq, double* out_d, int* out_i, int kstride,
+                           const int* labels, int label_lo, int label_hi, int* out_label,
+                           uint64_t* out_cs, int* status, void* stream) {
+  if (nq <= 0) return 0;
+  if (S < 1 || S > 256) return -1;
+  const dim3 grid((nq + 3) / 4), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  // P must exceed k + 64; k <= dmlp_screen_kmax(cap)
+  if (cap == 128) {
+    hipLaunchKernelGGL(k_refine<4>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
+                       qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
+                       out_label, out_cs, status);
+  } else if (cap == 256) {
+    hipLaunchKernelGGL(k_refine<8>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
+                       qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
+                       out_label, out_cs, status);
+  } else {
+    return -2;
+  }
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_exact_rows(const double* X, int64_t N, int A, const double* Qx,
+                               const int* qidx, int nq, double* D, int64_t ldd, void* stream) {
+  if (nq <= 0 || N <= 0) return 0;
+  const dim3 grid((unsigned)((N + 63) / 64), (unsigned)((nq + 63) / 64));
+  hipLaunchKernelGGL(k_exact_rows, grid, dim3(256), 0, (hipStream_t)stream, X, N, A, Qx, qidx,
+                     nq, D, ldd);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_merge(const double* in_d, const int* in_i, int L, int64_t list_stride,
+                          int kin, const int* qk, int nq, double* out_d, int* out_i, int kout,
+                          void* stream) {
+  if (nq <= 0) return 0;
+  if (L < 1 || L > 64) return -1;
+  hipLaunchKernelGGL(k_merge, dim3((nq + 127) / 128), dim3(128), 0, (hipStream_t)stream, in_d,
+                     in_i, L, list_stride, kin, qk, nq, out_d, out_i, kout);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_finalize(const double* d, const int* ids, int kstride, const int* qk,
+                             const int* qidx, int nq, const int* labels, int label_lo, int label_hi, int* out_label,
+                             uint64_t* out_cs, void* stream) {
+  if (nq <= 0) return 0;
+  hipLaunchKernelGGL(k_finalize, dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, d, ids,
+                     kstride, qk, qidx, nq, labels, label_lo, label_hi, out_label, out_cs);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int64_t dmlp_format_bound(int nq) { return (int64_t)nq * 48 + 64; }
+
+// line_off needs nq + 1 + (nq/1024 + 2) int64 of scratch; on completion line_off[nq] = bytes.
+extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off,
+                                  char* out, void* stream) {
+  if (nq <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (nq + 1023) / 1024;
+  int64_t* blocksum = line_off + nq + 1;
+  hipLaunchKernelGGL(k_fmt_len, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off, blocksum);
+  DMLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fmt_scan_blocks, dim3(1), dim3(64), 0, st, blocksum, nb);
+  DMLP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_fmt_write, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off,
+                     blocksum, out);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,56 @@
+"""Single-GPU micro benchmark of the local KNN pipeline phases (no distribution).
+
+    python tools/quick_gpu_bench.py --n 100000 --q 100000 --a 32 --k 16
+"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import distributed_machine_learning_project_amd as dmlp  # noqa: E402
+from distributed_machine_learning_project_amd.ops import knn as K  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--q", type=int, default=100000)
+    ap.add_argument("--a", type=int, default=32)
+    ap.add_argument("--kmin", type=int, default=16)
+    ap.add_argument("--kmax", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--exact", action="store_true")
+    ap.add_argument("--check", type=int, default=200, help="queries to verify against CPU")
+    a = ap.parse_args()
+    inp = dmlp.generate(a.n, a.q, a.a, 0.0, 1000.0, a.kmin, a.kmax, 10, seed=42)
+    X = torch.from_numpy(inp.X).cuda()
+    lab = torch.from_numpy(inp.labels).cuda()
+    Qx = torch.from_numpy(inp.Qx).cuda()
+    times = []
+    for it in range(a.iters + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ds = K.prepare_dataset(X, lab, (0, 10))
+        r = K.knn_gpu(ds, Qx, inp.k, exact=a.exact)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if it:
+            times.append(t1 - t0)
+    ms = 1e3 * float(np.median(times))
+    print(f"N={a.n} Q={a.q} A={a.a} k=[{a.kmin},{a.kmax}] exact={a.exact}: {ms:.3f} ms "
+          f"-> {a.q / ms * 1e3:.0f} queries/s  fallback={r.n_fallback}")
+    if a.check:
+        nc = min(a.check, a.q)
+        d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx[:nc], inp.k[:nc], kstride=r.ids.shape[1])
+        ids = r.ids[:nc].cpu().numpy()
+        ok = all((ids[q, :inp.k[q]] == i_ref[q, :inp.k[q]]).all() for q in range(nc))
+        print("check vs CPU:", "OK" if ok else "MISMATCH")
+
+
+if __name__ == "__main__":
+    main()
