@@ -32,13 +32,20 @@ __device__ __forceinline__ void split_bf16(double c, unsigned short& hi, unsigne
   lo = bf16_rn_bits((float)r);
 }
 
+// One block per attribute; deterministic tree reduction over the first min(N, 4096) rows.
 __global__ void k_center(const double* __restrict__ X, int64_t N, int A, double* __restrict__ mu) {
+  __shared__ double red[256];
+  const int a = blockIdx.x;
   const int64_t n = N < 4096 ? N : 4096;
-  for (int a = threadIdx.x; a < A; a += blockDim.x) {
-    double s = 0.0;
-    for (int64_t i = 0; i < n; ++i) s += X[i * A + a];
-    mu[a] = n > 0 ? s / (double)n : 0.0;
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += X[i * A + a];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) mu[a] = n > 0 ? red[0] / (double)n : 0.0;
 }
 
 // One thread per (point, 8-attribute group).
@@ -137,7 +144,8 @@ __global__ void k_prep_queries(const double* __restrict__ Qx, int64_t Q, int A,
 }  // namespace
 
 extern "C" int dmlp_center(const double* X, int64_t N, int A, double* mu, void* stream) {
-  hipLaunchKernelGGL(k_center, dim3(1), dim3(256), 0, (hipStream_t)stream, X, N, A, mu);
+  if (A <= 0) return 0;
+  hipLaunchKernelGGL(k_center, dim3(A), dim3(256), 0, (hipStream_t)stream, X, N, A, mu);
   DMLP_LAUNCH_CHECK();
   return 0;
 }

@@ -19,7 +19,7 @@
 
 namespace {
 
-constexpr int kHistCap = 1024;  // per-wave label histogram (labels in [lo, lo+1024))
+constexpr int kHistCap = 512;  // per-wave label histogram (labels in [lo, lo+512))
 
 __device__ __forceinline__ double exact_dist_row(const double* __restrict__ q,
                                                  const double* __restrict__ x, int A) {
@@ -108,8 +108,11 @@ __global__ __launch_bounds__(256) void k_refine(
     int* __restrict__ status) {
   constexpr int P = E * 64;
   constexpr int SMAX = 256;
+  constexpr int KMAX = 128;
   __shared__ double s_d[4][P];
   __shared__ int s_i[4][P];
+  __shared__ double s_rd[4][KMAX];
+  __shared__ int s_ri[4][KMAX];
   __shared__ int s_pre[4][SMAX + 1];
   __shared__ int s_hist[4][kHistCap];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -139,34 +142,64 @@ __global__ __launch_bounds__(256) void k_refine(
   if (lane == 0) status[q] = 0;
   dmlp::wave_sync();
   const int M = pre[S];
-  RunTopK<E> tk;
-  tk.init(s_d[wave], s_i[wave], k);
   const double* qv = Qx + (int64_t)q * A;
-  for (int j0 = 0; j0 < M; j0 += 64) {
-    const int j = j0 + lane;
-    const bool valid = j < M;
-    int id = 0;
-    double dv = INFINITY;
-    if (valid) {
-      // slice containing flat index j: largest s with pre[s] <= j
-      int lo = 0, hi = S;  // pre[lo] <= j < pre[hi]
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pre[mid] <= j) lo = mid; else hi = mid;
-      }
-      id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
-      dv = exact_dist_row(qv, X + (int64_t)id * A, A);
+  auto cand = [&](int j, double& dv, int& id) {
+    // slice containing flat index j: largest s with pre[s] <= j
+    int lo = 0, hi = S;  // pre[lo] <= j < pre[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] <= j) lo = mid; else hi = mid;
     }
-    tk.push(valid, dv, id);
+    id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
+    dv = exact_dist_row(qv, X + (int64_t)id * A, A);
+  };
+  const double* res_d;
+  const int* res_i;
+  if (M <= P && k <= KMAX) {
+    // rank select: keys are unique (distinct ids), so rank(i) = #{j : key_j < key_i} places
+    // every member of the top-k directly at its sorted position.
+    double* cd = s_d[wave];
+    int* ci = s_i[wave];
+    for (int j = lane; j < M; j += 64) {
+      double dv; int id;
+      cand(j, dv, id);
+      cd[j] = dv;
+      ci[j] = id;
+    }
+    for (int i = lane; i < k; i += 64) { s_rd[wave][i] = INFINITY; s_ri[wave][i] = -1; }
+    dmlp::wave_sync();
+    for (int i = lane; i < M; i += 64) {
+      const double di = cd[i];
+      const int ii = ci[i];
+      int rank = 0;
+      for (int j = 0; j < M; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
+      if (rank < k) { s_rd[wave][rank] = di; s_ri[wave][rank] = ii; }
+    }
+    dmlp::wave_sync();
+    res_d = s_rd[wave];
+    res_i = s_ri[wave];
+  } else {
+    RunTopK<E> tk;
+    tk.init(s_d[wave], s_i[wave], k);
+    for (int j0 = 0; j0 < M; j0 += 64) {
+      const int j = j0 + lane;
+      const bool valid = j < M;
+      int id = 0;
+      double dv = INFINITY;
+      if (valid) cand(j, dv, id);
+      tk.push(valid, dv, id);
+    }
+    tk.flush();
+    res_d = tk.d;
+    res_i = tk.id;
   }
-  tk.flush();
   for (int i = lane; i < k; i += 64) {
-    out_d[(int64_t)q * kstride + i] = tk.d[i];
-    out_i[(int64_t)q * kstride + i] = tk.id[i];
+    out_d[(int64_t)q * kstride + i] = res_d[i];
+    out_i[(int64_t)q * kstride + i] = res_i[i];
   }
   if (labels) {
     dmlp::wave_sync();
-    finalize_wave(tk.id, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q);
+    finalize_wave(res_i, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q);
   }
 }
 

@@ -7,7 +7,7 @@
 //     a(q,x) = <q-mu, x-mu> - |x-mu|^2 / 2   ( = (|q-mu|^2 - d(q,x)) / 2 )
 // on the matrix cores with a 3-term bf16 split (hi*hi + hi*lo + lo*hi, fp32 accumulate;
 // mfma_f32_16x16x32_bf16), then keeps, per query, every point whose score could still belong
-// to the exact top-k.  With |a - a_exact| <= eps_q (rigorous bound, see knn.py) and a_k the
+// to the exact top-k.  With |a - a_exact| <= eps_q (rigorous bound, see ops/knn.py) and a_k the
 // k-th largest score buffered so far, every point with a < a_k - 2*eps_q is provably outside
 // the exact top-k (and not even tied), so the per-query threshold h = a_k - 2*eps_q only rises.
 // Survivors are re-ranked exactly (fp64, no FMA, reference order) by refine.hip, so the final
@@ -15,13 +15,14 @@
 //
 // Geometry (gfx950): one workgroup = WAVES waves, each wave owns 16 queries (one MFMA column
 // tile) for the whole stream; query bf16 fragments live in VGPRs.  The data slice streams
-// through an NBUF-deep LDS ring in 64-point tiles staged with global_load_lds (1 KiB
-// lane-linear fragments laid out by prep.hip), counted vmcnt + raw s_barrier so the DMA of
-// tile i+NBUF-1 overlaps the MFMAs of tile i.  The per-query candidate buffers (CAP entries of
-// {score, id}) sit in LDS; appends use LDS atomics and are rare after the first tiles.  When a
-// buffer passes CAP-64 the owning wave compacts it alone (bitonic sort of the scores across the
-// wave), so no workgroup-wide synchronisation is needed beyond the tile ring.
-// Block -> (query block, data slice) is XCD-aware: with S % 8 == 0 every XCD streams only its
+// through a 2-deep LDS ring of 64-point tiles (lane-linear 1 KiB fragments laid out by
+// prep.hip).  Staging goes through registers (global_load_dwordx4 issued one step ahead,
+// ds_write_b128 after the barrier): no LDS-DMA is ever in flight, so hipcc never has to drain
+// vmcnt in front of the candidate-buffer LDS traffic.  Candidate buffers ({score, id} x CAP per
+// query) live in LDS; append offsets come from in-register per-column counts and a 4-lane
+// prefix (no LDS atomics).  When a buffer passes CAP-64 entries the owning wave compacts it
+// alone (bitonic sort of the scores across the wave).
+// Block -> (query block, data slice) is XCD-aware when S % 8 == 0: every XCD streams only its
 // own S/8 slices, so each slice is fetched into exactly one XCD's L2.
 #include "dmlp.h"
 #include "dmlp_device.h"
@@ -29,43 +30,51 @@
 
 namespace {
 
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+// Ablation switch for profiling only (bit 0: no candidate path, bit 1: no MFMA, bit 2: no tile
+// streaming).  Results are wrong unless it is 0; set through dmlp_set_screen_mode.
+int g_screen_mode = 0;
+// mode & 8: event counters (steps, candidate-path entries, appended entries, compactions)
+__device__ unsigned long long g_screen_dbg[8];
+#define DMLP_DBG(I, V)                                      \
+  do {                                                      \
+    if (mode & 8) {                                         \
+      const unsigned long long v_ = (V);                    \
+      if (lane == 0) atomicAdd(&g_screen_dbg[(I)], v_);     \
+    }                                                       \
+  } while (0)
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-template <int KT, int WAVES, int CAP, int NBUF>
+template <int KT, int WAVES, int CAP>
 struct ScreenCfg {
-  static constexpr int FRAGS = 4 * KT * 2;          // 1 KiB fragments per tile
+  static constexpr int FRAGS = 4 * KT * 2;  // 1 KiB fragments per tile
   static constexpr int TILE_BYTES = FRAGS * 1024 + 256;
-  static constexpr int G = FRAGS / WAVES;           // glds per wave per tile (+1 for wave 0)
-  static constexpr int LDS = NBUF * TILE_BYTES + WAVES * 16 * CAP * 8 + WAVES * 16 * 4;
+  static constexpr int G = FRAGS / WAVES;   // staged 16-B vectors per lane per tile
+  static constexpr int D = G <= 2 ? 4 : (G <= 4 ? 3 : 2);  // register-ring depth (tiles)
+  static constexpr int SUB = CAP / 4;      // per-lane sub-buffer entries
+  static constexpr int LDS = 2 * TILE_BYTES + WAVES * 64 * (SUB + 1) * 8;
   static_assert(FRAGS % WAVES == 0, "fragments must split evenly over waves");
   static_assert(LDS <= 163840, "LDS budget");
   static_assert(CAP % 64 == 0, "CAP multiple of 64");
 };
 
-template <int KT, int WAVES, int CAP, int NBUF>
+template <int KT, int WAVES, int CAP>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
-    const uint4* __restrict__ xfrag, const float* __restrict__ xinit, int n_tiles,
+    const u32x4* __restrict__ xfrag, const float* __restrict__ xinit, int n_tiles,
     const bf16x8* __restrict__ qhi, const bf16x8* __restrict__ qlo, const float* __restrict__ qn,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq,
     const unsigned* __restrict__ xnmax_bits, const unsigned* __restrict__ bad, float eps_rel,
-    int S, int tiles_per_slice, int n_qblocks, int* __restrict__ cand_ids,
+    int S, int tiles_per_slice, int n_qblocks, int mode, int* __restrict__ cand_ids,
     int* __restrict__ cand_cnt) {
-  using C = ScreenCfg<KT, WAVES, CAP, NBUF>;
+  using C = ScreenCfg<KT, WAVES, CAP>;
   constexpr int E = CAP / 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* tiles = smem;
-  int2* bufs = (int2*)(smem + NBUF * C::TILE_BYTES);
-  int* cnts = (int*)(smem + NBUF * C::TILE_BYTES + WAVES * 16 * CAP * 8);
+  char* const tiles = smem;
+  i32x2* const bufs = (i32x2*)(smem + 2 * C::TILE_BYTES);
+  constexpr int SUB = C::SUB;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int c = lane & 15;       // MFMA column = query of this lane
-  const int kg = lane >> 4;      // k-group / row group
+  const int c = lane & 15;   // MFMA column = query of this lane
+  const int kg = lane >> 4;  // k-group / row group
 
   // ---- block -> (query block, slice), XCD-aware when S % 8 == 0
   const int b = blockIdx.x;
@@ -103,164 +112,233 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   const float eps = eps_rel * (qn[q] + xnmax);
   const int kq = valid ? qk[q] : 0;
   float h = valid ? -FLT_MAX : INFINITY;
+  int cnt = 0;  // entries in this lane's own sub-buffer (negative: column overflowed)
+  i32x2* const wbuf = bufs + wave * 64 * (SUB + 1);
 
-  int2* const wbuf = bufs + wave * 16 * CAP;
-  int* const wcnt = cnts + wave * 16;
-  if (lane < 16) wcnt[lane] = 0;
-  wait_vmcnt<0>();
+  // ---- D-deep register ring for the tile stream: tile j lives in register set j % D, so D-1
+  // tiles are in flight while one is consumed (the stream is latency-bound otherwise).
+  // Macros, not lambdas, and native vector types: HIP's uint4 (a union struct) and captured
+  // arrays both defeat SROA and end up in scratch.
+  constexpr int D = C::D;
+  u32x4 stg[D][C::G];
+  float stx[D];
+  // Loads are issued unconditionally (tile index clamped, every wave fetches the 256-B xinit
+  // row) so the vmcnt bookkeeping is path-independent and hipcc emits counted waits.
+#define DMLP_LOAD_TILE(I, R)                                                      \
+  do {                                                                            \
+    const int t_ = t0 + ((I) < nt ? (I) : nt - 1);                                \
+    const u32x4* src_ = xfrag + (int64_t)t_ * (C::FRAGS * 64);                    \
+    _Pragma("unroll") for (int g = 0; g < C::G; ++g) stg[R][g] =                  \
+        src_[(wave + g * WAVES) * 64 + lane];                                     \
+    stx[R] = xinit[(int64_t)t_ * 64 + lane];                                      \
+  } while (0)
+#define DMLP_STORE_TILE(I, R)                                                     \
+  do {                                                                            \
+    char* dst_ = tiles + ((I) & 1) * C::TILE_BYTES;                               \
+    _Pragma("unroll") for (int g = 0; g < C::G; ++g)                              \
+        *(u32x4*)(dst_ + (wave + g * WAVES) * 1024 + lane * 16) = stg[R][g];      \
+    if (wave == 0) ((float*)(dst_ + C::FRAGS * 1024))[lane] = stx[R];             \
+  } while (0)
 
-  // ---- tile staging (lane-linear 1 KiB fragments, global -> LDS DMA)
-  auto issue = [&](int i) {
-    int ti = i < nt ? i : (nt > 0 ? nt - 1 : 0);  // past the end: re-stage the last tile (keeps
-    const int t = t0 + ti;                          // vmcnt bookkeeping constant)
-    char* dst = tiles + (i % NBUF) * C::TILE_BYTES;
-    const uint4* src = xfrag + (int64_t)t * (C::FRAGS * 64);
-#pragma unroll
-    for (int g = 0; g < C::G; ++g) {
-      const int f = wave + g * WAVES;
-      __builtin_amdgcn_global_load_lds((const void*)(src + f * 64 + lane), (lds_ptr_t)(dst + f * 1024),
-                                       16, 0, 0);
-    }
-    if (wave == 0)
-      __builtin_amdgcn_global_load_lds((const void*)(xinit + (int64_t)t * 64 + lane),
-                                       (lds_ptr_t)(dst + C::FRAGS * 1024), 4, 0, 0);
-  };
+  // ---- candidate buffers: column c owns 4 sub-buffers of SUB entries, one per row-group lane
+  // (kg), so a lane appends to its own sub-buffer with no cross-lane coordination.  Each lane
+  // appends at most 16 entries per tile; a column is compacted once any of its lanes holds more
+  // than SUB-16 (its entries are then re-dealt round-robin over the 4 sub-buffers).
+  i32x2* const wsub = wbuf;
+  auto sub_ptr = [&](int cc, int m) { return wsub + (cc * 4 + m) * (SUB + 1); };
 
-  // ---- wave-local compaction of column cc's buffer
+  // gather column cc's entries (E per lane, element idx = r*64 + lane) into registers
+#define DMLP_GATHER(CC, EV, VALID, NTOT)                                                       \
+  const int c0_ = __shfl(cnt, (CC)), c1_ = __shfl(cnt, (CC) + 16), c2_ = __shfl(cnt, (CC) + 32), \
+            c3_ = __shfl(cnt, (CC) + 48);                                                      \
+  const int NTOT = c0_ + c1_ + c2_ + c3_;                                                      \
+  i32x2 EV[E];                                                                                 \
+  bool VALID[E];                                                                               \
+  _Pragma("unroll") for (int r = 0; r < E; ++r) {                                              \
+    const int idx_ = r * 64 + lane;                                                            \
+    const int m_ = idx_ / SUB, j_ = idx_ - m_ * SUB;                                           \
+    const int cm_ = m_ == 0 ? c0_ : (m_ == 1 ? c1_ : (m_ == 2 ? c2_ : c3_));                   \
+    VALID[r] = j_ < cm_;                                                                       \
+    EV[r] = VALID[r] ? sub_ptr((CC), m_)[j_] : (i32x2){__float_as_int(-INFINITY), -1};         \
+  }
+
   auto compact = [&](int cc) {
-    int2* qbuf = wbuf + cc * CAP;
-    const int n = wcnt[cc];
-    int2 e[E];
-    float v[E];
-#pragma unroll
-    for (int r = 0; r < E; ++r) {
-      const int idx = r * 64 + lane;
-      e[r] = idx < n ? qbuf[idx] : make_int2(__float_as_int(-INFINITY), -1);
-      v[r] = __int_as_float(e[r].x);
-    }
-    dmlp::wave_sort_desc<E>(v);
+    DMLP_GATHER(cc, e, ok, ntot)
     const int kc = __shfl(kq, cc);
-    const float ec = __shfl(eps, cc);
-    const float ak = dmlp::wave_pick<E, float>(v, kc - 1);
-    const float hn = ak - 2.0f * ec;
-    if (c == cc) h = fmaxf(h, hn);
+    DMLP_DBG(3, 1);
+    if (ntot >= kc) {
+      // k-th largest score by a 32-step radix descent over order-preserving keys (ballots only)
+      unsigned u[E];
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const unsigned bits = (unsigned)e[r].x;
+        u[r] = ok[r] ? (bits ^ ((bits >> 31) ? 0xffffffffu : 0x80000000u)) : 0u;
+      }
+      unsigned T = 0;
+      // stopping at bit 12 leaves T <= the exact k-th key (low bits zero), i.e. a valid but
+      // ~2^-11-relative-looser threshold; 20 ballot rounds instead of 32
+      for (int bit = 31; bit >= 12; --bit) {
+        const unsigned cand = T | (1u << bit);
+        int cntge = 0;
+#pragma unroll
+        for (int r = 0; r < E; ++r) cntge += __popcll(__ballot(u[r] >= cand));
+        if (cntge >= kc) T = cand;
+      }
+      const unsigned tb = (T >> 31) ? (T ^ 0x80000000u) : ~T;
+      const float ak = __uint_as_float(tb);
+      const float hn = ak - 2.0f * __shfl(eps, cc);
+      if (c == cc) h = fmaxf(h, hn);
+    }
     const float hc = __shfl(h, cc);
     int base = 0;
     dmlp::wave_sync();
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      const int idx = r * 64 + lane;
-      const bool keep = idx < n && __int_as_float(e[r].x) >= hc;
+      const bool keep = ok[r] && __int_as_float(e[r].x) >= hc;
       const unsigned long long m = __ballot(keep);
-      if (keep) qbuf[base + __popcll(m & dmlp::lanemask_lt())] = e[r];
+      if (keep) {
+        const int pos = base + __popcll(m & dmlp::lanemask_lt());
+        sub_ptr(cc, pos & 3)[pos >> 2] = e[r];
+      }
       base += __popcll(m);
     }
     dmlp::wave_sync();
+    if (c == cc) cnt = (base + 3 - kg) >> 2;
     if (base > CAP - 64) {  // pathological ties: give up on this query, exact fallback
-      if (c == cc) h = INFINITY;
-      base = -1;
+      if (c == cc) { h = INFINITY; cnt = -(1 << 28); }
     }
-    if (lane == 0) wcnt[cc] = base;
-    dmlp::wave_sync();
   };
 
   // ---- prologue
   if (nt > 0) {
+    DMLP_LOAD_TILE(0, 0);
+    DMLP_STORE_TILE(0, 0);
 #pragma unroll
-    for (int i = 0; i < NBUF - 1; ++i) issue(i);
+    for (int r = 1; r < D; ++r) DMLP_LOAD_TILE(r, r);
   }
 
-  for (int i = 0; i < nt; ++i) {
-    if (wave == 0) wait_vmcnt<(NBUF - 2) * (C::G + 1)>();
-    else wait_vmcnt<(NBUF - 2) * C::G>();
+  for (int i0 = 0; i0 < nt; i0 += D) {
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    const int i = i0 + r;
+    if (i >= nt) break;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue(i + NBUF - 1);
+    // set r held tile i (already in LDS): refill it with tile i+D.  Tile i+1 (set r+1) goes to
+    // the other LDS buffer after this step's MFMAs; everyone finished reading that buffer at
+    // step i-1, before the barrier above.
+    if (!(mode & 4)) DMLP_LOAD_TILE(i + D, r);
 
-    const char* tb = tiles + (i % NBUF) * C::TILE_BYTES;
+    const char* tb = tiles + (i & 1) * C::TILE_BYTES;
     f32x4 acc[4];
+    bf16x8 ah[4][KT], al[4][KT];
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt)
+    for (int rt = 0; rt < 4; ++rt) {
       acc[rt] = *(const f32x4*)(tb + C::FRAGS * 1024 + rt * 64 + kg * 16);
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-#pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        const bf16x8 ahi = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 0) * 1024 + lane * 16);
-        const bf16x8 alo = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 1) * 1024 + lane * 16);
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bh[kt], acc[rt], 0, 0, 0);
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bl[kt], acc[rt], 0, 0, 0);
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bh[kt], acc[rt], 0, 0, 0);
+      for (int kt = 0; kt < KT; ++kt) {
+        ah[rt][kt] = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 0) * 1024 + lane * 16);
+        al[rt][kt] = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 1) * 1024 + lane * 16);
       }
     }
-    float m = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
 #pragma unroll
-    for (int rt = 1; rt < 4; ++rt)
-      m = fmaxf(m, fmaxf(fmaxf(acc[rt][0], acc[rt][1]), fmaxf(acc[rt][2], acc[rt][3])));
-    if (__ballot(m >= h)) {
-      // rare path: append every passing (score, id) to its query's buffer
+    for (int kt = 0; kt < KT; ++kt) {
+      if (mode & 2) break;  // ablation: no matrix work
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], bh[kt], acc[rt], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], bl[kt], acc[rt], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt][kt], bh[kt], acc[rt], 0, 0, 0);
+    }
+    float mr[4];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+      mr[rt] = fmaxf(fmaxf(acc[rt][0], acc[rt][1]), fmaxf(acc[rt][2], acc[rt][3]));
+    const float mx = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3]));
+    DMLP_DBG(0, 1);
+    if ((mode & 1) == 0 && __ballot(mx >= h)) {
+      DMLP_DBG(1, 1);
+      if (mode & 8) {
+        int np = 0;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) np += acc[rt][j] >= h ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) np += __shfl_xor(np, off);
+        DMLP_DBG(2, np);
+      }
+      // candidate path: append this lane's passing (score, id) pairs to its own sub-buffer
+      i32x2* mys = sub_ptr(c, kg);
       const int idbase = (t0 + i) * 64 + kg * 4;
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt) {
+        if (__ballot(mr[rt] >= h)) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (acc[rt][j] >= h) {
-            const int pos = atomicAdd(&wcnt[c], 1);
-            wbuf[c * CAP + pos] = make_int2(__float_as_int(acc[rt][j]), idbase + rt * 16 + j);
+          for (int j = 0; j < 4; ++j) {
+            if (acc[rt][j] >= h) {
+              mys[cnt] = (i32x2){__float_as_int(acc[rt][j]), idbase + rt * 16 + j};
+              ++cnt;
+            }
           }
         }
       }
-      dmlp::wave_sync();
-      const bool need = lane < 16 && wcnt[lane] > CAP - 64;
-      unsigned long long nm = __ballot(need);
-      while (nm) {
-        const int cc = __ffsll((long long)nm) - 1;
-        nm &= nm - 1;
+      unsigned long long nm = __ballot(cnt > SUB - 16);
+      unsigned cols = (unsigned)((nm | (nm >> 16) | (nm >> 32) | (nm >> 48)) & 0xffffull);
+      while (cols) {
+        const int cc = __ffs(cols) - 1;
+        cols &= cols - 1;
         compact(cc);
       }
     }
+    if (!(mode & 4)) DMLP_STORE_TILE(i + 1, (r + 1) % D);  // past the end: idle buffer
+    if (mode & 1) asm volatile("" ::"v"(mx));  // keep the epilogue alive in ablations
   }
-  wait_vmcnt<0>();
+  }
+#undef DMLP_LOAD_TILE
+#undef DMLP_STORE_TILE
 
-  // ---- write this slice's candidates
+  // ---- write this slice's candidates (ids only; refine recomputes exact distances)
+  dmlp::wave_sync();
   for (int cc = 0; cc < 16; ++cc) {
     const int pp = pbase + cc;
     if (pp >= nq) break;
-    const int n = wcnt[cc];
     int* out = cand_ids + ((int64_t)pp * S + s) * CAP;
-    if (n < 0) {
+    if (__shfl(cnt, cc) < 0) {
       if (lane == 0) cand_cnt[(int64_t)pp * S + s] = -1;
       continue;
     }
+    DMLP_GATHER(cc, e, ok, ntot)
+    (void)ntot;
     const float hc = __shfl(h, cc);
-    const int2* qbuf = wbuf + cc * CAP;
     int base = 0;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      const int idx = r * 64 + lane;
-      int2 e = make_int2(0, -1);
-      if (idx < n) e = qbuf[idx];
-      const bool keep = idx < n && __int_as_float(e.x) >= hc;
+      const bool keep = ok[r] && __int_as_float(e[r].x) >= hc;
       const unsigned long long m = __ballot(keep);
-      if (keep) out[base + __popcll(m & dmlp::lanemask_lt())] = e.y;
+      if (keep) out[base + __popcll(m & dmlp::lanemask_lt())] = e[r].y;
       base += __popcll(m);
     }
     if (lane == 0) cand_cnt[(int64_t)pp * S + s] = base;
   }
+#undef DMLP_GATHER
 }
 
-template <int KT, int WAVES, int CAP, int NBUF>
+template <int KT, int WAVES, int CAP>
 int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const void* qhi,
                   const void* qlo, const float* qn, const int* qidx, const int* qk, int nq,
                   const unsigned* xnmax, const unsigned* bad, float eps_rel, int S,
                   int* cand_ids, int* cand_cnt, hipStream_t stream) {
-  using C = ScreenCfg<KT, WAVES, CAP, NBUF>;
-  auto kern = k_screen<KT, WAVES, CAP, NBUF>;
+  using C = ScreenCfg<KT, WAVES, CAP>;
+  auto kern = k_screen<KT, WAVES, CAP>;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       C::LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return -(int)e;
     attr_set = true;
   }
@@ -269,32 +347,32 @@ int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const 
   const int64_t grid = (int64_t)n_qblocks * S;
   if (grid <= 0) return 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WAVES * 64), C::LDS, stream,
-                     (const uint4*)xfrag, xinit, (int)n_tiles, (const bf16x8*)qhi,
+                     (const u32x4*)xfrag, xinit, (int)n_tiles, (const bf16x8*)qhi,
                      (const bf16x8*)qlo, qn, qidx, qk, nq, xnmax, bad, eps_rel, S, tps,
-                     n_qblocks, cand_ids, cand_cnt);
+                     n_qblocks, g_screen_mode, cand_ids, cand_cnt);
   DMLP_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace
 
-// (KT, CAP) -> (WAVES, NBUF): LDS = NBUF*(8 KiB*KT + 256) + WAVES*16*CAP*8 <= 160 KiB.
-#define DMLP_SCREEN_CONFIGS(X)                                                                  \
-  X(1, 128, 8, 3) X(2, 128, 4, 3) X(3, 128, 4, 3) X(4, 128, 4, 2) X(1, 256, 4, 3)             \
-  X(2, 256, 2, 3) X(3, 256, 2, 3) X(4, 256, 2, 2)
+// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*KT + 256) + WAVES*16*CAP*8 <= 160 KiB.
+#define DMLP_SCREEN_CONFIGS(X)                                                                \
+  X(1, 128, 8) X(2, 128, 4) X(3, 128, 4) X(4, 128, 4) X(1, 256, 4) X(2, 256, 2) X(3, 256, 2) \
+  X(4, 256, 2)
 
 extern "C" int dmlp_screen_kmax(int cap) { return cap == 128 ? 32 : (cap == 256 ? 128 : 0); }
 
 extern "C" int dmlp_screen_lds_bytes(int KT, int cap) {
-#define DMLP_LDS_CASE(kt, cp, w, nb) \
-  if (KT == kt && cap == cp) return ScreenCfg<kt, w, cp, nb>::LDS;
+#define DMLP_LDS_CASE(kt, cp, w) \
+  if (KT == kt && cap == cp) return ScreenCfg<kt, w, cp>::LDS;
   DMLP_SCREEN_CONFIGS(DMLP_LDS_CASE)
 #undef DMLP_LDS_CASE
   return -1;
 }
 
 extern "C" int dmlp_screen_waves(int KT, int cap) {
-#define DMLP_W_CASE(kt, cp, w, nb) \
+#define DMLP_W_CASE(kt, cp, w) \
   if (KT == kt && cap == cp) return w;
   DMLP_SCREEN_CONFIGS(DMLP_W_CASE)
 #undef DMLP_W_CASE
@@ -308,11 +386,24 @@ extern "C" int dmlp_screen(int KT, int cap, const void* xfrag, const float* xini
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
   hipStream_t st = (hipStream_t)stream;
-#define DMLP_SCREEN_CASE(kt, cp, w, nb)                                                        \
-  if (KT == kt && cap == cp)                                                                   \
-    return launch_screen<kt, w, cp, nb>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq,     \
-                                        xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st);
+#define DMLP_SCREEN_CASE(kt, cp, w)                                                         \
+  if (KT == kt && cap == cp)                                                                \
+    return launch_screen<kt, w, cp>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq,      \
+                                    xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st);
   DMLP_SCREEN_CONFIGS(DMLP_SCREEN_CASE)
 #undef DMLP_SCREEN_CASE
   return -2;
+}
+
+extern "C" void dmlp_set_screen_mode(int mode) { g_screen_mode = mode; }
+
+extern "C" int dmlp_screen_debug_counters(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_screen_dbg), sizeof(g_screen_dbg));
+  if (e != hipSuccess) return -(int)e;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_screen_dbg), z, sizeof(z));
+    if (e != hipSuccess) return -(int)e;
+  }
+  return 0;
 }

@@ -19,6 +19,7 @@ Screen error bound (per query q, fp32 score a = <q',x'> - |x'|^2/2 with q' = q -
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -222,7 +223,8 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
                                        _p(ds.bad), s), "prep_queries")
         kdev_eff = torch.from_numpy(kk.astype(np.int32)).to(dev, non_blocking=True)
         er = eps_rel(A)
-        for idx, cap in ((cls_a, 128), (cls_b, 256)):
+        cap_a = int(os.environ.get("DMLP_SCREEN_CAP_A", "128"))
+        for idx, cap in ((cls_a, cap_a), (cls_b, 256)):
             nq = len(idx)
             if nq == 0:
                 continue
