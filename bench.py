@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Headline benchmark: bench_4-style distributed exact k-NN classification on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strategy farm] ...
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric (BASELINE.json): "samples/sec (whole node) on bench_4" = classified queries per second
+over all GPUs.  One step = one full Engine::KNN call exactly as the reference times it
+(common.cpp:122-131): rank 0 holds the parsed input in host memory; the step moves it to the
+GPUs, broadcasts the dataset (bench_4 replicates it), distributes the queries, runs the exact
+k-NN (bf16x3 MFMA screen + exact fp64 re-rank), votes, checksums, gathers the results to rank 0
+and renders the "Query <id> checksum: <u64>" report bytes on rank 0.
+
+Config: the reference's inputs (inputs.zip) are not in the repository, so the workload is
+synthetic data with generate_input.py's distribution at the only shape BASELINE.md quotes a
+number for: N=100000 points, A=32 attributes in [0,1000] (6 decimals), k=16, 10 labels, seed 42;
+Q = --q-per-gpu queries per GPU (weak scaling: per-GPU work is fixed).
+vs_baseline divides by 443.5 queries/s: BASELINE.md's best number at that shape (student
+engine.cpp, np=4: 1000 queries in 2255 ms; the CPU reference's cost per query does not depend on
+Q at fixed N, A, k).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+BASELINE_QPS = 1000.0 / 2.255  # engine.cpp np=4, N=1e5 Q=1e3 A=32 k=16 -> 2255 ms
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--strategy", default="farm")
+    ap.add_argument("--schedule", default="static", choices=["static", "dynamic"])
+    ap.add_argument("--n-data", type=int, default=100_000)
+    ap.add_argument("--q-per-gpu", type=int, default=100_000)
+    ap.add_argument("--attrs", type=int, default=32)
+    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--labels", type=int, default=10)
+    ap.add_argument("--exact", action="store_true", help="fp64-only path (no MFMA screen)")
+    ap.add_argument("--verify", action="store_true", help="check rank-0 report against the CPU path")
+    ap.add_argument("--no-busbw", action="store_true")
+    a = ap.parse_args(argv)
+
+    import numpy as np
+    import torch
+
+    from distributed_machine_learning_project_amd.parallel.comm import Comm
+    from distributed_machine_learning_project_amd.parallel.engine import Engine
+    from distributed_machine_learning_project_amd.utils.io import generate
+
+    comm = Comm.init("gpu" if torch.cuda.is_available() else "cpu")
+    world = comm.world
+    if a.gpus != world and comm.is_root:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    Q = a.q_per_gpu * world
+
+    inp = None
+    if comm.is_root:
+        inp = generate(a.n_data, Q, a.attrs, 0.0, 1000.0, a.k, a.k, a.labels, seed=42)
+        if comm.on_gpu:  # the "parsed input" lives in page-locked host memory (untimed, like parsing)
+            for name in ("X", "labels", "Qx", "k"):
+                setattr(inp, name + "_t", torch.from_numpy(getattr(inp, name)).pin_memory())
+    eng = Engine(a.strategy, comm=comm, exact=a.exact, schedule=a.schedule)
+
+    def step():
+        out = eng.KNN(inp.params if inp else None, inp, None)
+        return eng.report(out) if out is not None else None
+
+    for _ in range(a.warmup):
+        rep = step()
+    comm.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        rep = step()
+    comm.sync()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    # max over ranks
+    el = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms = elapsed / max(1, a.steps) * 1e3
+
+    extra = {}
+    if world > 1 and comm.on_gpu and not a.no_busbw:
+        extra["allreduce_busbw_GBps"] = round(_allreduce_busbw(comm), 1)
+    if a.verify and comm.is_root:
+        from distributed_machine_learning_project_amd.ops import knn as K
+        from distributed_machine_learning_project_amd.utils.io import format_report
+        nv = min(Q, 2000)
+        d, i = K.knn_cpu(inp.X, inp.Qx[:nv], inp.k[:nv])
+        _, cs = K.finalize_cpu(i, inp.k[:nv], inp.labels)
+        ref = format_report(cs)
+        extra["verified_queries"] = nv
+        extra["verify_ok"] = bool(rep[: len(ref)] == ref)
+
+    if comm.is_root:
+        value = Q / (ms / 1e3)
+        line = {
+            "metric": "samples/sec (whole node) on bench_4",
+            "value": round(value, 1),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_QPS, 1),
+            "dtype": "fp64",
+            "screen": "none" if a.exact else "bf16x3 MFMA screen, exact fp64 re-rank "
+                                             "(results bit-identical to the fp64 reference)",
+            "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",
+            "config": {
+                "model": f"bench_4 exact k-NN classifier N={a.n_data} A={a.attrs} k={a.k} "
+                         f"labels={a.labels}",
+                "global_batch": Q,
+                "seq_len": a.attrs,
+                "parallelism": f"{a.strategy}{world}" + ("" if a.schedule == "static" else "-dynamic"),
+                "num_data": a.n_data,
+                "queries_per_gpu": a.q_per_gpu,
+                "k": a.k,
+            },
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    eng.close()
+
+
+def _allreduce_busbw(comm, nbytes=256 << 20, iters=10):
+    """RCCL all-reduce bus bandwidth over xGMI (the BASELINE metric's second half; the k-NN
+    itself needs no all-reduce).  busbw = bytes * 2(P-1)/P / time."""
+    import torch
+    import torch.distributed as dist
+    x = torch.ones(nbytes // 4, dtype=torch.float32, device=comm.device)
+    for _ in range(3):
+        dist.all_reduce(x)
+    comm.sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(x)
+    comm.sync()
+    dt = (time.perf_counter() - t0) / iters
+    P = comm.world
+    return nbytes * 2 * (P - 1) / P / dt / 1e9
+
+
+if __name__ == "__main__":
+    main()

@@ -98,7 +98,11 @@ def _stream():
 
 
 def _p(t):
-    return None if t is None else t.data_ptr()
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("native kernels need contiguous tensors")
+    return t.data_ptr()
 
 
 @dataclass
@@ -320,6 +324,7 @@ def format_report_gpu(cs, qid_base: int = 0) -> bytes:
     """Render "Query <id> checksum: <u64>\\n" lines on the GPU; returns the bytes on the host."""
     torch = _torch()
     L = _lib.lib()
+    cs = cs.contiguous()
     nq = cs.numel()
     if nq == 0:
         return b""

@@ -1,0 +1,244 @@
+"""Process/device runtime and collectives (SURVEY.md §2.6, §5 "Distributed communication backend").
+
+One process per GPU.  On MI355X the data plane is RCCL over xGMI (torch.distributed backend
+"nccl" == RCCL on ROCm); on CPU-only hosts the same code runs over gloo.  The reference's MPI
+call sites map as follows (bench_* addresses from SURVEY.md §2.6):
+
+  MPI_Bcast (params, dataset, k, queries)   -> Comm.bcast            (ncclBroadcast)
+  MPI_Scatterv (shards)                     -> Comm.scatter_rows     (scatter, one xGMI hop each)
+  MPI_Gather/Gatherv (per-query results)    -> Comm.gather_rows      (batched, once per call)
+  MPI_Reduce + user MPI_Op (bench_2/3)      -> strategies.tree_merge (send/recv + merge kernel)
+  MPI_Cart_create/Cart_sub (engine.cpp)     -> Comm.grid_groups      (dist.new_group row/col)
+  MPI_Send/Recv ANY_SOURCE farming (bench_4)-> Comm.claim            (TCPStore atomic counter)
+
+Uneven splits are padded to the largest part (RCCL collectives need equal counts); padding
+rows are never read back.
+"""
+from __future__ import annotations
+
+import contextlib
+import datetime
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@contextlib.contextmanager
+def quiet_stdout():
+    """gloo prints connection banners on fd 1; the harness's stdout must carry only the report."""
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        os.close(devnull)
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def dims_create(nprocs: int):
+    """MPI_Dims_create(n, 2) equivalent: the most balanced factorisation, dims[0] >= dims[1]."""
+    best = (nprocs, 1)
+    r = 1
+    while r * r <= nprocs:
+        if nprocs % r == 0:
+            best = (nprocs // r, r)
+        r += 1
+    return best
+
+
+def block_partition(n: int, parts: int):
+    """Balanced block partition (bench_1 @0xc5b2): counts[i] = n//p + (i < n%p), displs prefix."""
+    base, rem = divmod(n, parts)
+    counts = [base + (1 if i < rem else 0) for i in range(parts)]
+    displs = [0] * parts
+    for i in range(1, parts):
+        displs[i] = displs[i - 1] + counts[i - 1]
+    return counts, displs
+
+
+@dataclass
+class Comm:
+    rank: int
+    world: int
+    local_rank: int
+    device: "object"       # torch.device
+    backend: str           # "nccl" (RCCL) or "gloo"
+    initialized_here: bool = False
+    _store: "object" = None
+
+    # ------------------------------------------------------------------ setup
+    @staticmethod
+    def init(device: str = "auto", timeout_s: int = 600) -> "Comm":
+        """Initialise torch.distributed from the launcher environment (RANK/WORLD_SIZE/
+        LOCAL_RANK/MASTER_ADDR/MASTER_PORT); a single process without them is world_size 1."""
+        torch = _torch()
+        import torch.distributed as dist
+        use_gpu = device == "gpu" or (device == "auto" and torch.cuda.is_available())
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if use_gpu:
+            ndev = torch.cuda.device_count()
+            torch.cuda.set_device(local_rank % max(1, ndev))
+            dev = torch.device("cuda", torch.cuda.current_device())
+        else:
+            dev = torch.device("cpu")
+        backend = "nccl" if use_gpu else "gloo"
+        here = False
+        if world > 1 and not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            kw = {}
+            if use_gpu:
+                kw["device_id"] = dev
+            with quiet_stdout():
+                dist.init_process_group(backend, rank=rank, world_size=world,
+                                        timeout=datetime.timedelta(seconds=timeout_s), **kw)
+                if not use_gpu:
+                    dist.barrier()
+            here = True
+        elif dist.is_initialized():
+            rank, world = dist.get_rank(), dist.get_world_size()
+            backend = dist.get_backend()
+        return Comm(rank, world, local_rank, dev, backend, here)
+
+    def finalize(self):
+        import torch.distributed as dist
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+
+    @property
+    def is_root(self):
+        return self.rank == 0
+
+    @property
+    def on_gpu(self):
+        return self.device.type == "cuda"
+
+    # ------------------------------------------------------------------ primitives
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            if self.on_gpu:
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def sync(self):
+        if self.on_gpu:
+            _torch().cuda.synchronize(self.device)
+
+    def bcast_ints(self, vals=None, n: int = 0):
+        """Broadcast a small int64 vector from rank 0 (the 3 x MPI_Bcast of Params)."""
+        torch = _torch()
+        if self.world == 1:
+            return list(vals)
+        import torch.distributed as dist
+        n = len(vals) if vals is not None else n
+        t = torch.zeros(n, dtype=torch.int64, device=self.device)
+        if self.is_root:
+            t.copy_(torch.tensor(list(vals), dtype=torch.int64))
+        dist.broadcast(t, 0)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def bcast(self, t, shape, dtype):
+        """Broadcast a tensor from rank 0 (allocated on the other ranks)."""
+        torch = _torch()
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+        if not self.is_root:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+        if t.numel():
+            dist.broadcast(t, 0)
+        return t
+
+    def scatter_rows(self, t, counts, row_shape, dtype):
+        """Scatter row blocks [counts[i] rows -> rank i] from rank 0 (MPI_Scatterv)."""
+        torch = _torch()
+        if self.world == 1:
+            return t[: counts[0]]
+        import torch.distributed as dist
+        mx = max(counts)
+        out = torch.empty((mx, *row_shape), dtype=dtype, device=self.device)
+        if mx == 0:
+            return out[:0]
+        chunks = None
+        if self.is_root:
+            chunks = []
+            off = 0
+            for c in counts:
+                blk = t[off:off + c]
+                if c < mx:
+                    pad = torch.zeros((mx - c, *row_shape), dtype=dtype, device=self.device)
+                    blk = torch.cat([blk, pad])
+                chunks.append(blk.contiguous())
+                off += c
+        dist.scatter(out, chunks, src=0)
+        return out[: counts[self.rank]]
+
+    def gather_rows(self, t, counts, row_shape, dtype):
+        """Gather row blocks to rank 0 in rank order (MPI_Gatherv); returns the concatenation on
+        rank 0 and None elsewhere."""
+        torch = _torch()
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+        mx = max(counts)
+        src = torch.zeros((mx, *row_shape), dtype=dtype, device=self.device)
+        if t is not None and t.shape[0]:
+            src[: t.shape[0]] = t
+        bufs = [torch.empty_like(src) for _ in range(self.world)] if self.is_root else None
+        dist.gather(src, bufs, dst=0)
+        if not self.is_root:
+            return None
+        return torch.cat([b[:c] for b, c in zip(bufs, counts)])
+
+    def send(self, t, dst):
+        import torch.distributed as dist
+        dist.send(t.contiguous(), dst)
+
+    def recv(self, shape, dtype, src):
+        torch = _torch()
+        import torch.distributed as dist
+        t = torch.empty(shape, dtype=dtype, device=self.device)
+        dist.recv(t, src)
+        return t
+
+    def new_group(self, ranks):
+        import torch.distributed as dist
+        if self.world == 1:
+            return None
+        with quiet_stdout():
+            g = dist.new_group(ranks=ranks)
+            if not self.on_gpu and self.rank in ranks:
+                dist.barrier(group=g)  # gloo connects (and prints) eagerly; finish it here
+        return g
+
+    # ------------------------------------------------------------------ dynamic farming
+    def store(self):
+        if self._store is None and self.world > 1:
+            import torch.distributed as dist
+            from torch.distributed import distributed_c10d as c10d
+            self._store = c10d._get_default_store()
+        return self._store
+
+    def claim(self, key: str) -> int:
+        """Atomically claim the next work item (the bench_4 master's ANY_SOURCE hand-out,
+        without a master rank): returns 0, 1, 2, ... across all ranks."""
+        st = self.store()
+        if st is None:
+            v = getattr(self, "_local_ctr", {}).get(key, 0)
+            self.__dict__.setdefault("_local_ctr", {})[key] = v + 1
+            return v
+        return int(st.add(key, 1)) - 1

@@ -1,0 +1,106 @@
+"""Engine — the engine.h API (`Engine::KNN(Params&, vector<DataPoint>&, vector<Query>&)`,
+engine.h:6-12) for one process per GPU.
+
+    eng = Engine(strategy="farm")            # untimed: process group, device, kernel warm-up
+    out = eng.KNN(params, dataset, queries)  # called on EVERY rank; rank 0 holds the data
+    if out is not None: sys.stdout.buffer.write(eng.report(out))
+
+Like the reference, only rank 0 has the parsed input on entry (common.cpp:93-117) and every
+rank calls KNN (common.cpp:126); the sizes are broadcast first (engine.cpp:27-35).  Results
+come back on rank 0 only, in query-id order, each query reported once (defect D3 fixed).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..utils.io import KNNInput, Params, format_debug
+from ..utils.trace import Tracer
+from .backend import Backend
+from .comm import Comm
+from .strategies import FUNCS, STRATEGIES, GridGroups
+
+
+@dataclass
+class KNNOutput:
+    """Rank-0 result.  Tensors stay on the device until asked for."""
+    label: "object"      # torch int32 [Q]
+    checksum: "object"   # torch int64 [Q] (uint64 bits)
+    dist: "object"       # torch f64 [Q, kmax] or None (debug)
+    ids: "object"        # torch int32 [Q, kmax] or None (debug)
+    k: np.ndarray
+
+    def labels_np(self):
+        return self.label.cpu().numpy().astype(np.int32)
+
+    def checksums_np(self):
+        return self.checksum.cpu().numpy().view(np.uint64)
+
+
+class Engine:
+    def __init__(self, strategy: str | None = None, device: str | None = None,
+                 exact: bool | None = None, debug: bool = False, schedule: str | None = None,
+                 comm: Comm | None = None, warmup: bool = True):
+        self.strategy = strategy or os.environ.get("KNN_STRATEGY", "farm")
+        if self.strategy not in STRATEGIES:
+            raise ValueError(f"unknown strategy {self.strategy!r}; one of {STRATEGIES}")
+        device = device or os.environ.get("KNN_DEVICE", "auto")
+        self.exact = (os.environ.get("KNN_EXACT", "0") == "1") if exact is None else exact
+        self.schedule = schedule or os.environ.get("KNN_SCHEDULE", "static")
+        self.debug = debug
+        self.comm = comm or Comm.init(device)
+        self.be = Backend(self.comm.device, exact=self.exact)
+        self.tracer = Tracer(self.comm.rank, sync=self.comm.sync if self.comm.on_gpu else None)
+        self.groups = GridGroups(self.comm) if (self.strategy == "grid2d" and self.comm.world > 1) else None
+        self.calls = 0
+        if warmup:
+            self._warmup()
+
+    def _warmup(self):
+        """Load the native library and every kernel once (Engine ctor is outside the timed
+        region, common.cpp:121-124)."""
+        from .. import _lib
+        _lib.lib()
+        if self.comm.on_gpu:
+            import torch
+            from ..utils.io import generate
+            w = generate(256, 64, 8, 0.0, 1.0, 1, 40, 3, seed=1)
+            X = self.be.tensor(w.X)
+            lab = self.be.tensor(w.labels)
+            Qx = self.be.tensor(w.Qx)
+            self.be.knn(X, Qx, w.k, labels=lab, label_range=(0, 3))
+            self.be.report(torch.zeros(4, dtype=torch.int64, device=self.comm.device))
+            self.comm.sync()
+        self.comm.barrier()
+
+    # ------------------------------------------------------------------ API
+    def KNN(self, p: Params | None = None, dataset=None, queries=None) -> KNNOutput | None:
+        inp = None
+        if self.comm.is_root:
+            inp = dataset if isinstance(dataset, KNNInput) else KNNInput.from_aos(dataset, queries)
+        fn = FUNCS[self.strategy]
+        res = fn(self.comm, self.be, inp, self.tracer, schedule=self.schedule,
+                 call_id=self.calls, debug=self.debug, groups=self.groups)
+        self.calls += 1
+        if res is None:
+            return None
+        lb, cs, d, i = res
+        return KNNOutput(lb, cs, d, i, np.asarray(inp.k))
+
+    def report(self, out: KNNOutput) -> bytes:
+        """stdout bytes of the reference harness (reportResult, common.cpp:57-79)."""
+        if self.debug:
+            d = out.dist.cpu().numpy() if out.dist is not None else None
+            i = out.ids.cpu().numpy() if out.ids is not None else None
+            if d is None:
+                raise RuntimeError("debug report needs an Engine(debug=True)")
+            return format_debug(d, i, out.k, out.labels_np())
+        cs = out.checksum
+        if cs.device.type != self.comm.device.type:
+            cs = cs.to(self.comm.device)
+        return self.be.report(cs)
+
+    def close(self):
+        self.comm.finalize()

@@ -1,0 +1,359 @@
+"""Distributed k-NN strategies — every parallelism of the reference,
+re-designed for one process per MI355X with RCCL over xGMI.  All of them produce byte-identical
+results (exact fp64 distances, (dist asc, id desc) order, vote tie -> larger label).
+
+  farm          bench_4 (B4 @0xbe50): dataset replicated by broadcast, queries farmed out.
+                schedule="static": one scatter of balanced query blocks (identical MI355Xs make
+                static optimal); schedule="dynamic": ranks claim query chunks from a shared
+                atomic counter (the master's ANY_SOURCE hand-out without a dedicated master),
+                results combined by a sum-reduce of disjoint slots.
+  shard_gather  bench_1 (B1 @0xc410): dataset sharded (scatter), all queries broadcast once,
+                local top-k per shard, ONE batched gather of the [P, Q, k] lists (not 2 per
+                query), K-way merge kernel at the root.
+  shard_reduce  bench_2/bench_3 (B2 @0xbdc0 + MPI_Op @0xbc70): same sharding, lists combined
+                by a log2(P) send/recv tree with the pairwise merge kernel at every interior
+                node (RCCL has no user reductions), batched over all queries (B3 style).
+  grid2d        engine.cpp (E2-E9, with defects D1-D6 fixed): R x C process grid
+                (MPI_Dims_create), data sharded over grid rows, queries over grid columns,
+                row/column sub-communicators (MPI_Cart_sub -> dist.new_group), column merge to
+                row 0, results gathered to rank 0.
+  serial        bench.debug (B0): KD-tree on rank 0's CPU, other ranks idle.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .comm import block_partition, dims_create
+
+STRATEGIES = ("farm", "shard_gather", "shard_reduce", "grid2d", "serial")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _offset_ids(ids, off):
+    torch = _torch()
+    if off == 0:
+        return ids
+    return torch.where(ids >= 0, ids + off, ids)
+
+
+def _root_arrays(be, inp):
+    """H2D of the root's host arrays (pinned torch tensors when the caller provided them)."""
+    torch = _torch()
+    g = lambda name, dt: be.tensor(getattr(inp, name + "_t", None) if getattr(inp, name + "_t", None)
+                                   is not None else getattr(inp, name), dt)
+    return (g("X", torch.float64), g("labels", torch.int32), g("Qx", torch.float64),
+            g("k", torch.int32))
+
+
+def _meta(comm, inp):
+    if comm.is_root:
+        N, A = inp.X.shape
+        Q = inp.Qx.shape[0]
+        lo = int(inp.labels.min()) if N else 0
+        hi = int(inp.labels.max()) + 1 if N else 1
+        kmax = max(1, int(inp.k.max())) if Q else 1
+        vals = [N, Q, A, lo, hi, kmax]
+    else:
+        vals = None
+    return comm.bcast_ints(vals, 6)
+
+
+def _k_host(comm, k_dev_or_none, Q):
+    """Every rank needs the per-query k on the host (it drives kernel dispatch)."""
+    torch = _torch()
+    k = comm.bcast(k_dev_or_none, (Q,), torch.int32)
+    return k, k.cpu().numpy()
+
+
+# ============================================================================ farm (bench_4)
+def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, debug=False, **_):
+    torch = _torch()
+    N, Q, A, lo, hi, kmax = _meta(comm, inp)
+    with tr.phase("h2d"):
+        X = lab = Qx = kd = None
+        if comm.is_root:
+            X, lab, Qx, kd = _root_arrays(be, inp)
+    with tr.phase("bcast_data"):
+        X = comm.bcast(X, (N, A), torch.float64)
+        lab = comm.bcast(lab, (N,), torch.int32)
+    if schedule == "static":
+        counts, displs = block_partition(Q, comm.world)
+        with tr.phase("scatter_queries"):
+            Ql = comm.scatter_rows(Qx, counts, (A,), torch.float64)
+            kl = comm.scatter_rows(kd, counts, (), torch.int32)
+            kl_h = kl.cpu().numpy()
+        with tr.phase("compute"):
+            d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
+        with tr.phase("gather"):
+            packed = torch.stack([lb.to(torch.int64), cs], dim=1)
+            allp = comm.gather_rows(packed, counts, (2,), torch.int64)
+            dd = ii = None
+            if debug:
+                dd = comm.gather_rows(d, counts, (kmax,), torch.float64)
+                ii = comm.gather_rows(i, counts, (kmax,), torch.int32)
+        if not comm.is_root:
+            return None
+        return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
+    # dynamic: every rank holds all queries; chunks are claimed from an atomic counter
+    with tr.phase("bcast_queries"):
+        Qx = comm.bcast(Qx, (Q, A), torch.float64)
+        kd, k_h = _k_host(comm, kd, Q)
+    nchunks = max(1, min(Q, comm.world * chunks_per_rank))
+    csz = (Q + nchunks - 1) // nchunks
+    out = torch.zeros((Q, 2), dtype=torch.int64, device=be.device)
+    dbg_d = torch.zeros((Q, kmax), dtype=torch.float64, device=be.device) if debug else None
+    dbg_i = torch.zeros((Q, kmax), dtype=torch.int32, device=be.device) if debug else None
+    with tr.phase("compute"):
+        key = f"dmlp_farm_{call_id}"
+        while True:
+            c = comm.claim(key)
+            if c >= nchunks:
+                break
+            a, b = c * csz, min(Q, (c + 1) * csz)
+            if a >= b:
+                continue
+            d, i, lb, cs = be.knn(X, Qx[a:b], k_h[a:b], labels=lab, label_range=(lo, hi),
+                                  kstride=kmax)
+            out[a:b, 0] = lb.to(torch.int64)
+            out[a:b, 1] = cs
+            if debug:
+                dbg_d[a:b] = d
+                dbg_i[a:b] = i
+    with tr.phase("reduce"):
+        if comm.world > 1:
+            import torch.distributed as dist
+            dist.reduce(out, 0, op=dist.ReduceOp.SUM)
+            if debug:
+                dist.reduce(dbg_d, 0, op=dist.ReduceOp.SUM)
+                dist.reduce(dbg_i, 0, op=dist.ReduceOp.SUM)
+    if not comm.is_root:
+        return None
+    return out[:, 0].to(torch.int32), out[:, 1].contiguous(), dbg_d, dbg_i
+
+
+# ============================================================================ sharded data
+def _shard_local(comm, be, inp, tr):
+    """Scatter the dataset in balanced blocks, broadcast queries, local top-k lists with
+    global ids.  Returns (meta, root labels tensor, k_host, d, i)."""
+    torch = _torch()
+    N, Q, A, lo, hi, kmax = _meta(comm, inp)
+    counts, displs = block_partition(N, comm.world)
+    with tr.phase("h2d"):
+        X = lab = Qx = kd = None
+        if comm.is_root:
+            X, lab, Qx, kd = _root_arrays(be, inp)
+    with tr.phase("scatter_data"):
+        Xl = comm.scatter_rows(X, counts, (A,), torch.float64)
+    with tr.phase("bcast_queries"):
+        Qx = comm.bcast(Qx, (Q, A), torch.float64)
+        kd, k_h = _k_host(comm, kd, Q)
+    with tr.phase("compute"):
+        d, i, _, _ = be.knn(Xl, Qx, k_h, finalize=False, kstride=kmax)
+        i = _offset_ids(i, displs[comm.rank])
+    return (N, Q, A, lo, hi, kmax), lab, k_h, d, i
+
+
+def shard_gather(comm, be, inp, tr, debug=False, **_):
+    torch = _torch()
+    (N, Q, A, lo, hi, kmax), lab, k_h, d, i = _shard_local(comm, be, inp, tr)
+    with tr.phase("gather"):
+        P = comm.world
+        if P > 1:
+            import torch.distributed as dist
+            bd = [torch.empty_like(d) for _ in range(P)] if comm.is_root else None
+            bi = [torch.empty_like(i) for _ in range(P)] if comm.is_root else None
+            dist.gather(d.contiguous(), bd, dst=0)
+            dist.gather(i.contiguous(), bi, dst=0)
+    if not comm.is_root:
+        return None
+    with tr.phase("merge"):
+        if P > 1:
+            d, i = be.merge(torch.stack(bd), torch.stack(bi), k_h, kmax)
+        lb, cs = be.finalize(lab, (lo, hi), d, i, k_h)
+    return lb, cs, d, i
+
+
+def tree_merge(comm, be, d, i, k_h, kmax, group_ranks=None, tr=None):
+    """Binomial-tree reduction of sorted top-k lists toward group_ranks[0] (the MPI_Reduce with
+    bench_2's commutative merge op): log2(P) rounds of send/recv, pairwise merge kernel at each
+    receiving node.  Returns the merged lists on the tree root, None elsewhere."""
+    torch = _torch()
+    ranks = group_ranks or list(range(comm.world))
+    P = len(ranks)
+    me = ranks.index(comm.rank)
+    step = 1
+    while step < P:
+        if me % (2 * step) == step:
+            comm.send(d, ranks[me - step])
+            comm.send(i, ranks[me - step])
+            return None
+        if me % (2 * step) == 0 and me + step < P:
+            od = comm.recv(d.shape, d.dtype, ranks[me + step])
+            oi = comm.recv(i.shape, i.dtype, ranks[me + step])
+            d, i = be.merge(torch.stack([d, od]), torch.stack([i, oi]), k_h, kmax)
+        step *= 2
+    return d, i
+
+
+def shard_reduce(comm, be, inp, tr, debug=False, **_):
+    (N, Q, A, lo, hi, kmax), lab, k_h, d, i = _shard_local(comm, be, inp, tr)
+    with tr.phase("tree_reduce"):
+        res = tree_merge(comm, be, d, i, k_h, kmax)
+    if not comm.is_root:
+        return None
+    d, i = res
+    with tr.phase("finalize"):
+        lb, cs = be.finalize(lab, (lo, hi), d, i, k_h)
+    return lb, cs, d, i
+
+
+# ============================================================================ grid2d (engine.cpp)
+class GridGroups:
+    """Row/column sub-communicators of the R x C grid (MPI_Cart_create + MPI_Cart_sub).
+    dist.new_group is collective over the world, so all groups are created once, in order."""
+
+    def __init__(self, comm):
+        self.R, self.C = dims_create(comm.world)
+        self.row, self.col = divmod(comm.rank, self.C)
+        self.row_ranks = [[r * self.C + c for c in range(self.C)] for r in range(self.R)]
+        self.col_ranks = [[r * self.C + c for r in range(self.R)] for c in range(self.C)]
+        self.row_groups = [comm.new_group(rk) for rk in self.row_ranks]
+        self.col_groups = [comm.new_group(rk) for rk in self.col_ranks]
+
+
+def _grp_scatter(comm, t, counts, row_shape, dtype, group, ranks, src_idx=0):
+    """MPI_Scatterv inside a sub-communicator (equal-size padded chunks)."""
+    torch = _torch()
+    import torch.distributed as dist
+    me = ranks.index(comm.rank)
+    mx = max(counts)
+    out = torch.empty((mx, *row_shape), dtype=dtype, device=be_device(comm))
+    if len(ranks) == 1:
+        return t[: counts[0]]
+    chunks = None
+    if me == src_idx:
+        chunks, off = [], 0
+        for c in counts:
+            blk = t[off:off + c]
+            if c < mx:
+                blk = torch.cat([blk, torch.zeros((mx - c, *row_shape), dtype=dtype, device=t.device)])
+            chunks.append(blk.contiguous())
+            off += c
+    if mx:
+        dist.scatter(out, chunks, src=ranks[src_idx], group=group)
+    return out[: counts[me]]
+
+
+def _grp_bcast(comm, t, shape, dtype, group, ranks, src_idx=0):
+    torch = _torch()
+    import torch.distributed as dist
+    if len(ranks) == 1:
+        return t
+    if ranks.index(comm.rank) != src_idx:
+        t = torch.empty(shape, dtype=dtype, device=be_device(comm))
+    if t.numel():
+        dist.broadcast(t, ranks[src_idx], group=group)
+    return t
+
+
+def be_device(comm):
+    return comm.device
+
+
+def grid2d(comm, be, inp, tr, groups=None, debug=False, **_):
+    torch = _torch()
+    import torch.distributed as dist
+    g = groups or GridGroups(comm)
+    N, Q, A, lo, hi, kmax = _meta(comm, inp)
+    dcounts, ddispl = block_partition(N, g.R)   # data over grid rows (engine.cpp:62-63)
+    qcounts, qdispl = block_partition(Q, g.C)   # queries over grid columns (engine.cpp:136-137)
+    with tr.phase("h2d"):
+        X = lab = Qx = kd = None
+        if comm.is_root:
+            X, lab, Qx, kd = _root_arrays(be, inp)
+    with tr.phase("distribute"):
+        # data: scatter down column 0 to the row leaders, then broadcast along each row
+        Xs = None
+        if g.col == 0:
+            Xs = _grp_scatter(comm, X, dcounts, (A,), torch.float64, g.col_groups[0], g.col_ranks[0])
+        Xs = _grp_bcast(comm, Xs, (dcounts[g.row], A), torch.float64, g.row_groups[g.row],
+                        g.row_ranks[g.row])
+        # queries (+k): scatter along row 0 to the column leaders, broadcast down each column
+        Qs = ks = None
+        if g.row == 0:
+            Qs = _grp_scatter(comm, Qx, qcounts, (A,), torch.float64, g.row_groups[0], g.row_ranks[0])
+            ks = _grp_scatter(comm, kd, qcounts, (), torch.int32, g.row_groups[0], g.row_ranks[0])
+        Qs = _grp_bcast(comm, Qs, (qcounts[g.col], A), torch.float64, g.col_groups[g.col],
+                        g.col_ranks[g.col])
+        ks = _grp_bcast(comm, ks, (qcounts[g.col],), torch.int32, g.col_groups[g.col],
+                        g.col_ranks[g.col])
+        k_h = ks.cpu().numpy()
+        # labels: only the row-0 ranks (column mergers) vote
+        if g.row == 0:
+            lab = _grp_bcast(comm, lab, (N,), torch.int32, g.row_groups[0], g.row_ranks[0])
+    with tr.phase("compute"):
+        d, i, _, _ = be.knn(Xs, Qs, k_h, finalize=False, kstride=kmax)
+        i = _offset_ids(i, ddispl[g.row])
+    with tr.phase("column_merge"):
+        cr = g.col_ranks[g.col]
+        if g.R > 1:
+            me = cr.index(comm.rank)
+            bd = [torch.empty_like(d) for _ in cr] if me == 0 else None
+            bi = [torch.empty_like(i) for _ in cr] if me == 0 else None
+            dist.gather(d.contiguous(), bd, dst=cr[0], group=g.col_groups[g.col])
+            dist.gather(i.contiguous(), bi, dst=cr[0], group=g.col_groups[g.col])
+            if me == 0:
+                d, i = be.merge(torch.stack(bd), torch.stack(bi), k_h, kmax)
+    if g.row != 0:
+        return None
+    with tr.phase("finalize"):
+        lb, cs = be.finalize(lab, (lo, hi), d, i, k_h)
+    with tr.phase("gather"):
+        rr = g.row_ranks[0]
+        packed = torch.stack([lb.to(torch.int64), cs], dim=1)
+        if g.C > 1:
+            mx = max(qcounts)
+            src = torch.zeros((mx, 2), dtype=torch.int64, device=be.device)
+            src[: packed.shape[0]] = packed
+            bufs = [torch.empty_like(src) for _ in rr] if comm.is_root else None
+            dist.gather(src, bufs, dst=0, group=g.row_groups[0])
+            dd = ii = None
+            if debug:
+                sd = torch.full((mx, kmax), float("inf"), dtype=torch.float64, device=be.device)
+                si = torch.full((mx, kmax), -1, dtype=torch.int32, device=be.device)
+                sd[: d.shape[0]] = d
+                si[: i.shape[0]] = i
+                bd = [torch.empty_like(sd) for _ in rr] if comm.is_root else None
+                bi = [torch.empty_like(si) for _ in rr] if comm.is_root else None
+                dist.gather(sd, bd, dst=0, group=g.row_groups[0])
+                dist.gather(si, bi, dst=0, group=g.row_groups[0])
+            if not comm.is_root:
+                return None
+            allp = torch.cat([b[:c] for b, c in zip(bufs, qcounts)])
+            if debug:
+                dd = torch.cat([b[:c] for b, c in zip(bd, qcounts)])
+                ii = torch.cat([b[:c] for b, c in zip(bi, qcounts)])
+            return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
+    return lb, cs, d, i
+
+
+# ============================================================================ serial (bench.debug)
+def serial(comm, be, inp, tr, debug=False, **_):
+    """KD-tree on rank 0 (exact search, tie-inclusive pruning), no communication at all."""
+    torch = _torch()
+    from ..ops import knn as K
+    if not comm.is_root:
+        return None
+    with tr.phase("compute"):
+        d, i = K.knn_cpu(inp.X, inp.Qx, inp.k, method="kdtree")
+        lb, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    return (torch.from_numpy(lb), torch.from_numpy(cs.view(np.int64)), torch.from_numpy(d),
+            torch.from_numpy(i))
+
+
+FUNCS = {"farm": farm, "shard_gather": shard_gather, "shard_reduce": shard_reduce,
+         "grid2d": grid2d, "serial": serial}

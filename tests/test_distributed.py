@@ -1,0 +1,93 @@
+"""Multi-process strategy tests on CPU (gloo), SURVEY.md §4 levels 3-5: every strategy, several
+(non-square, non-power-of-two) world sizes, the §2.2 defect scenarios (varying k, duplicate
+points, N/P < k shards, Q < P, k = N), byte-identical stdout against the NumPy oracle, each
+query printed exactly once in id order."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import distributed_machine_learning_project_amd as dmlp
+from distributed_machine_learning_project_amd.ops import reference as ref
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_port = [29800 + (os.getpid() % 500)]
+
+
+def _oracle_report(inp):
+    _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    return ref.report_lines(cs).encode()
+
+
+def _run(path, np_, strategy, extra=(), env_extra=None):
+    _port[0] += 1
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    env.update(env_extra or {})
+    if np_ == 1:
+        cmd = [sys.executable, "-m", "distributed_machine_learning_project_amd.harness"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+               str(np_), "--master-addr", "127.0.0.1", "--master-port", str(_port[0]), "-m",
+               "distributed_machine_learning_project_amd.harness"]
+    cmd += ["--strategy", strategy, "--device", "cpu", "--input", path, *extra]
+    r = subprocess.run(cmd, capture_output=True, env=env, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"Time taken:" in r.stderr
+    return r.stdout
+
+
+@pytest.fixture(scope="module")
+def workload(tmp_path_factory):
+    d = tmp_path_factory.mktemp("knn")
+    txt = dmlp.generate_text(257, 23, 6, 0, 100, 1, 40, 5, seed=7)  # varying k (D2)
+    p = d / "gen.in"
+    p.write_text(txt)
+    inp = dmlp.parse_input(txt)
+    return str(p), _oracle_report(inp)
+
+
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "serial"])
+@pytest.mark.parametrize("np_", [1, 2, 3])
+def test_strategy_matches_oracle(workload, strategy, np_):
+    path, expect = workload
+    assert _run(path, np_, strategy) == expect
+
+
+@pytest.mark.parametrize("strategy", ["grid2d", "shard_gather", "shard_reduce"])
+def test_four_and_six_ranks(workload, strategy):
+    path, expect = workload
+    assert _run(path, 4, strategy) == expect
+    assert _run(path, 6, strategy) == expect  # non-square grid (D1: heap overflow in engine.cpp)
+
+
+def test_dynamic_farm(workload):
+    path, expect = workload
+    assert _run(path, 3, "farm", env_extra={"KNN_SCHEDULE": "dynamic"}) == expect
+
+
+def test_edge_cases(tmp_path):
+    """Duplicates (ties broken by larger id), shards smaller than k (D4), Q < P, k = N."""
+    rng = np.random.default_rng(3)
+    base = np.round(rng.uniform(0, 3, size=(6, 3)), 0)
+    X = np.ascontiguousarray(base[rng.integers(0, 6, size=20)])
+    labels = rng.integers(0, 3, size=20).astype(np.int32)
+    Qx = np.round(rng.uniform(0, 3, size=(2, 3)), 0)
+    k = np.array([20, 13], np.int32)  # k = N and k > N/P
+    inp = dmlp.KNNInput(labels, X, k, Qx)
+    p = tmp_path / "edge.in"
+    p.write_text(dmlp.to_text(inp))
+    expect = _oracle_report(dmlp.parse_input(p.read_text()))
+    for s in ["farm", "shard_gather", "shard_reduce", "grid2d"]:
+        assert _run(str(p), 4, s) == expect, s
+
+
+def test_debug_output(workload):
+    """DEBUG build listing (common.cpp:72-78) from every strategy is identical."""
+    path, _ = workload
+    outs = {s: _run(path, 2, s, extra=["--debug"]) for s in ["farm", "shard_reduce", "grid2d"]}
+    assert len(set(outs.values())) == 1
+    first = list(outs.values())[0].decode().splitlines()
+    assert first[0].startswith("Label for Query 0 : ")
+    assert first[1].startswith("Top-")
