@@ -379,7 +379,7 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   const dim3 grid((nq + 3) / 4), block(256);
   hipStream_t st = (hipStream_t)stream;
   // P must exceed k + 64; k <= dmlp_screen_kmax(cap)
-  if (cap == 128) {
+  if (cap == 64 || cap == 128) {
     hipLaunchKernelGGL(k_refine<4>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
                        qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
                        out_label, out_cs, status);

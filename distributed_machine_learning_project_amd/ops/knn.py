@@ -30,6 +30,7 @@ SCREEN_KMAX_A = 32      # cap 128 class
 SCREEN_KMAX_B = 128     # cap 256 class
 SCREEN_MAX_KT = 4       # A <= 128 on the screen path
 NUM_CUS = 256
+SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "stream")  # "stream" | "lds" (profiling/A-B)
 
 
 def eps_rel(A: int) -> float:
@@ -178,6 +179,24 @@ class DeviceResult:
     n_fallback: int = 0
 
 
+def _choose_slices_stream(nq: int, qw: int, n_tiles: int) -> int:
+    """Data slices for the streaming screen: one wave per (query block, slice), 4 per CU.
+    Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best."""
+    nqb = (nq + qw - 1) // qw
+    slots = 4 * NUM_CUS
+    best, best_eff = 1, 0.0
+    for S in range(1, 65):
+        if S > max(1, n_tiles // 4):
+            break
+        w = nqb * S
+        eff = w / (math.ceil(w / slots) * slots)
+        if eff >= 0.9:
+            return S
+        if eff > best_eff + 1e-9:
+            best, best_eff = S, eff
+    return best
+
+
 def _choose_slices(nq: int, waves: int, n_tiles: int) -> int:
     nqb = (nq + waves * 16 - 1) // (waves * 16)
     S = 1
@@ -227,19 +246,30 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
                                        _p(ds.bad), s), "prep_queries")
         kdev_eff = torch.from_numpy(kk.astype(np.int32)).to(dev, non_blocking=True)
         er = eps_rel(A)
-        cap_a = int(os.environ.get("DMLP_SCREEN_CAP_A", "128"))
-        for idx, cap in ((cls_a, cap_a), (cls_b, 256)):
+        # k <= 32 and A <= 64: barrier-free streaming kernel (cap 64); otherwise LDS-shared kernel
+        stream_qw = L.dmlp_screen_stream_qw(KT) if SCREEN_IMPL != "lds" else 0
+        for idx, cap in ((cls_a, 64 if stream_qw else 128), (cls_b, 256)):
             nq = len(idx)
             if nq == 0:
                 continue
             qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
-            waves = L.dmlp_screen_waves(KT, cap)
-            S = _choose_slices(nq, waves, ds.n_tiles)
+            streaming = cap == 64
+            if streaming:
+                S = _choose_slices_stream(nq, stream_qw, ds.n_tiles)
+            else:
+                S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
             cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
-            _lib.check(L.dmlp_screen(KT, cap, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, _p(qhi),
-                                     _p(qlo), _p(qn), _p(qidx), _p(kdev_eff), nq, _p(ds.xnmax_bits),
-                                     _p(ds.bad), er, S, _p(cand_ids), _p(cand_cnt), s), "screen")
+            if streaming:
+                _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
+                                                _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff),
+                                                nq, _p(ds.xnmax_bits), _p(ds.bad), er, S,
+                                                _p(cand_ids), _p(cand_cnt), s), "screen_stream")
+            else:
+                _lib.check(L.dmlp_screen(KT, cap, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
+                                         _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff), nq,
+                                         _p(ds.xnmax_bits), _p(ds.bad), er, S, _p(cand_ids),
+                                         _p(cand_cnt), s), "screen")
             _lib.check(L.dmlp_refine(cap, _p(cand_ids), _p(cand_cnt), S, _p(ds.X), A, _p(Qx),
                                      _p(qidx), _p(kdev_eff), nq, _p(out_d), _p(out_i), ks,
                                      _p(ds.labels) if want_fin else None, ds.label_lo,
