@@ -15,7 +15,8 @@ and renders the "Query <id> checksum: <u64>" report bytes on rank 0.
 Config: the reference's inputs (inputs.zip) are not in the repository, so the workload is
 synthetic data with generate_input.py's distribution at the only shape BASELINE.md quotes a
 number for: N=100000 points, A=32 attributes in [0,1000] (6 decimals), k=16, 10 labels, seed 42;
-Q = --q-per-gpu queries per GPU (weak scaling: per-GPU work is fixed).
+Q = --q-per-gpu queries per GPU (default 2^17: whole rounds of 64-query waves on the 1024 SIMDs;
+weak scaling: per-GPU work is fixed).
 vs_baseline divides by 443.5 queries/s: BASELINE.md's best number at that shape (student
 engine.cpp, np=4: 1000 queries in 2255 ms; the CPU reference's cost per query does not depend on
 Q at fixed N, A, k).
@@ -43,7 +44,7 @@ def main(argv=None):
     ap.add_argument("--strategy", default="farm")
     ap.add_argument("--schedule", default="static", choices=["static", "dynamic"])
     ap.add_argument("--n-data", type=int, default=100_000)
-    ap.add_argument("--q-per-gpu", type=int, default=100_000)
+    ap.add_argument("--q-per-gpu", type=int, default=131_072)
     ap.add_argument("--attrs", type=int, default=32)
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--labels", type=int, default=10)

@@ -59,7 +59,10 @@ def _compile(src: Path, force: bool) -> Path:
     if not force and not _stale(obj, [src] + _headers()):
         return obj
     if src.suffix == ".hip":
-        cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, "-c", str(src), "-o", str(obj)]
+        # MFMA results in VGPRs: the epilogue reads every accumulator with VALU, and AGPR
+        # results cost a v_accvgpr_read per value plus copies of the C-init operand
+        cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, "-mllvm", "-amdgpu-mfma-vgpr-form=true",
+               "-c", str(src), "-o", str(obj)]
     else:
         # host-only code: plain g++ without -march (no FMA contraction, SSE2 like the reference)
         cmd = ["g++", *COMMON, f"-I{CSRC}", "-pthread", "-c", str(src), "-o", str(obj)]

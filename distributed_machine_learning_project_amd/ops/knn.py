@@ -184,6 +184,10 @@ def _choose_slices_stream(nq: int, qw: int, n_tiles: int) -> int:
     Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best."""
     nqb = (nq + qw - 1) // qw
     slots = 4 * NUM_CUS
+    if nqb >= slots:
+        # every extra slice repeats each query's threshold warm-up (candidate work grows ~S):
+        # with a full round of waves already, a partial last round is cheaper than S > 1
+        return 1
     best, best_eff = 1, 0.0
     for S in range(1, 65):
         if S > max(1, n_tiles // 4):

@@ -37,6 +37,7 @@ def main():
         Qx = torch.from_numpy(inp.Qx).cuda()
         for m in [int(x) for x in a.modes.split(",")]:
             _lib.lib().dmlp_set_screen_mode(m)
+            _lib.lib().dmlp_set_stream_mode(m)
             ts = []
             for it in range(a.iters + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -52,6 +53,9 @@ def main():
             if m & 8:
                 cnt = np.zeros(8, np.uint64)
                 _lib.lib().dmlp_screen_debug_counters(cnt.ctypes.data, 1)
+                c2 = np.zeros(8, np.uint64)
+                _lib.lib().dmlp_stream_debug_counters(c2.ctypes.data, 1)
+                cnt += c2
                 calls = a.iters + 1
                 print("  per call: wave-steps %.4g  cand-path %.4g  appends %.4g  compactions %.4g"
                       % tuple(float(x) / calls for x in cnt[:4]))
