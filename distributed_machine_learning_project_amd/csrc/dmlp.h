@@ -62,6 +62,13 @@ int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const 
 int dmlp_exact_rows(const double* X, int64_t N, int A, const double* Qx, const int* qidx, int nq,
                     double* D, int64_t ldd, void* stream);
 
+// Exact top-k of the fallback queries qidx[0..nb): exact rows in descending-id order + stable
+// segmented radix sort; k from qk[qidx[i]] (clamped to N); nb*N < 2^31 (callers chunk).
+int64_t dmlp_fallback_bytes(int nb, int64_t N);
+int dmlp_fallback_topk(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
+                       const int* qk, int nb, void* ws, int64_t ws_bytes, double* out_d,
+                       int* out_i, int kstride, void* stream);
+
 // ---------------------------------------------------------------- device: top-k merge (K4)
 // L sorted lists per query (list l of query q at in_*[l*list_stride + q*kin + j]), padded with
 // (+inf, -1).  Writes the merged top-k_q of every query q < nq to out_*[q*kout + i].

@@ -302,32 +302,23 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
 
 
 def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d, out_i):
-    """Exact distance rows + stable sort (ties in descending id order via column reversal)."""
+    """Native exact path (fallback.hip): exact rows in descending-id order + stable segmented
+    radix sort, in chunks of rows that keep nb*N < 2^27 (and the workspace bounded)."""
     torch = _torch()
     L = _lib.lib()
     N, A = ds.N, ds.A
     dev = Qx.device
     s = _stream()
+    kdev = torch.from_numpy(np.ascontiguousarray(kk, np.int32)).to(dev, non_blocking=True)
     rows = max(1, min(len(fb), (1 << 27) // max(1, N)))
+    ws_bytes = L.dmlp_fallback_bytes(rows, N)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     for c0 in range(0, len(fb), rows):
         sub = fb[c0:c0 + rows]
-        nb = len(sub)
         qidx = torch.from_numpy(sub.astype(np.int32)).to(dev, non_blocking=True)
-        D = torch.empty((nb, N), dtype=torch.float64, device=dev)
-        _lib.check(L.dmlp_exact_rows(_p(ds.X), N, A, _p(Qx), _p(qidx), nb, _p(D), N, s),
-                   "exact_rows")
-        kmax = int(kk[sub].max())
-        Dr = D.flip(1)
-        vals, idx = torch.sort(Dr, dim=1, stable=True)
-        vals = vals[:, :kmax]
-        ids = (N - 1 - idx[:, :kmax]).to(torch.int32)
-        kk_sub = torch.from_numpy(kk[sub].astype(np.int64)).to(dev)
-        mask = torch.arange(kmax, device=dev)[None, :] < kk_sub[:, None]
-        qrows = qidx.long()
-        cur_d = out_d[qrows, :kmax]
-        cur_i = out_i[qrows, :kmax]
-        out_d[qrows, :kmax] = torch.where(mask, vals, cur_d)
-        out_i[qrows, :kmax] = torch.where(mask, ids, cur_i)
+        _lib.check(L.dmlp_fallback_topk(_p(ds.X), N, A, _p(Qx), _p(qidx), _p(kdev), len(sub),
+                                        _p(ws), ws_bytes, _p(out_d), _p(out_i), out_d.shape[1],
+                                        s), "fallback_topk")
 
 
 def merge_gpu(lists_d, lists_i, k_dev, kout: int):
