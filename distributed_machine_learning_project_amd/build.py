@@ -97,12 +97,27 @@ def build_engine(force: bool = False) -> Path | None:
     deps = srcs + _headers() + [LIB]
     if not force and not _stale(ENGINE, deps):
         return ENGINE
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
-           "-D__HIP_PLATFORM_AMD__", f"-I{CSRC}", f"-I{MPI_HOME}/include", f"-I{ROCM}/include",
-           *map(str, srcs), "-o", str(ENGINE), f"-L{PKG}", "-ldmlp", f"-Wl,-rpath,{PKG}",
-           "-Wl,-rpath,$ORIGIN", f"{MPI_HOME}/lib/libmpi.so", f"-Wl,-rpath,{MPI_HOME}/lib",
-           f"-L{ROCM}/lib", "-lrccl", "-pthread"]
-    _run(cmd)
+    BUILD.mkdir(exist_ok=True)
+    objs = []
+    for s in srcs:  # host-only C++ against the HIP runtime / RCCL / MPI headers
+        o = BUILD / (s.name + ".o")
+        _run(["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
+              f"-I{CSRC}", f"-I{MPI_HOME}/include", f"-I{ROCM}/include", "-c", str(s), "-o", str(o)])
+        objs.append(str(o))
+    # MPICH lives in the conda prefix next to an old libstdc++: never put that directory on the
+    # link/run path (ROCm needs the system libstdc++).  Link libmpi by its own path through a
+    # private symlink directory; libmpi finds its Fortran runtime through its own RUNPATH.
+    mpidir = PKG / "mpi_runtime"
+    mpidir.mkdir(exist_ok=True)
+    for name in ("libmpi.so.12", "libgfortran.so.4", "libquadmath.so.0"):
+        src = Path(MPI_HOME) / "lib" / name
+        dst = mpidir / name
+        if src.exists() and not dst.is_symlink():
+            dst.symlink_to(src)
+    link = mpidir / "libmpi.so.12"
+    _run(["g++", *objs, "-o", str(ENGINE), f"-L{PKG}", "-ldmlp", "-Wl,-rpath,$ORIGIN",
+          str(link), "-Wl,-rpath,$ORIGIN/mpi_runtime", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64",
+          f"-Wl,-rpath,{ROCM}/lib", "-pthread"])
     return ENGINE
 
 

@@ -81,6 +81,9 @@ int dmlp_finalize(const double* d, const int* ids, int kstride, const int* qk, c
                   int nq, const int* labels, int label_lo, int label_hi, int* out_label,
                   uint64_t* out_cs, void* stream);
 
+int dmlp_fill_f64(double* p, int64_t n, double v, void* stream);
+int dmlp_offset_ids(int* ids, int64_t n, int off, void* stream);
+
 // ---------------------------------------------------------------- device: report formatting (K7)
 // "Query <qid> checksum: <cs>\n" for q < nq into out (needs dmlp_format_bound bytes).
 // line_off[nq+1] is scratch (int64) that receives the line offsets; *total_out (device) = bytes.

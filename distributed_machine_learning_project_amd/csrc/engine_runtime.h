@@ -1,0 +1,266 @@
+// engine_runtime.h — native runtime of the standalone `knn_engine` binary: MPI for process
+// bootstrap and host-side control (like the reference's harness, common.cpp:82-133), RCCL over
+// xGMI for the data plane, HIP streams, RAII device buffers, and the single-GPU k-NN pipeline
+// that drives the libdmlp kernels (the C++ twin of ops/knn.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <mpi.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "dmlp.h"
+
+extern "C" {
+int dmlp_screen_waves(int KT, int cap);
+int dmlp_screen_stream_qw(int KT);
+int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_tiles,
+                       const void* qhi, const void* qlo, const float* qn, const int* qidx,
+                       const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
+                       float eps_rel, int S, int* cand_ids, int* cand_cnt, void* stream);
+}
+
+namespace dmlp_rt {
+
+#define HIPCHK(x)                                                                            \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) {                                                                  \
+      std::fprintf(stderr, "[knn_engine] HIP error %s at %s:%d\n", hipGetErrorString(e_),    \
+                   __FILE__, __LINE__);                                                      \
+      MPI_Abort(MPI_COMM_WORLD, 2);                                                          \
+    }                                                                                        \
+  } while (0)
+#define NCCLCHK(x)                                                                           \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess) {                                                                 \
+      std::fprintf(stderr, "[knn_engine] RCCL error %s at %s:%d\n", ncclGetErrorString(r_),  \
+                   __FILE__, __LINE__);                                                      \
+      MPI_Abort(MPI_COMM_WORLD, 3);                                                          \
+    }                                                                                        \
+  } while (0)
+#define DMLPCHK(x)                                                                           \
+  do {                                                                                       \
+    int r_ = (x);                                                                            \
+    if (r_ != 0) {                                                                           \
+      std::fprintf(stderr, "[knn_engine] libdmlp call failed (%d) at %s:%d\n", r_, __FILE__, \
+                   __LINE__);                                                                \
+      MPI_Abort(MPI_COMM_WORLD, 4);                                                          \
+    }                                                                                        \
+  } while (0)
+
+// Grow-only device buffer (reused across calls: no hipMalloc in steady state).
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  T* get(size_t n) {
+    if (n > cap) {
+      if (p) HIPCHK(hipFree(p));
+      cap = std::max<size_t>(n, 1);
+      HIPCHK(hipMalloc(&p, cap * sizeof(T)));
+    }
+    return p;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Runtime {
+  int rank = 0, world = 1, local = 0, device = 0;
+  ncclComm_t nccl = nullptr;
+  hipStream_t stream = nullptr;
+
+  bool gpu = false;
+
+  void init(bool need_gpu = true) {
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &world);
+    MPI_Comm shm;
+    MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &shm);
+    MPI_Comm_rank(shm, &local);
+    MPI_Comm_free(&shm);
+    if (!need_gpu) return;  // serial KD-tree strategy (bench.debug): host only
+    gpu = true;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (ndev == 0) throw std::runtime_error("no HIP device");
+    device = local % ndev;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    if (world > 1) {
+      ncclUniqueId id;
+      if (rank == 0) NCCLCHK(ncclGetUniqueId(&id));
+      MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, MPI_COMM_WORLD);
+      NCCLCHK(ncclCommInitRank(&nccl, world, id, rank));
+    }
+  }
+  void finalize() {
+    if (nccl) ncclCommDestroy(nccl);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  void sync() {
+    if (gpu) HIPCHK(hipStreamSynchronize(stream));
+  }
+};
+
+// Balanced block partition (bench_1 @0xc5b2).
+inline void block_partition(int64_t n, int parts, std::vector<int64_t>& cnt,
+                            std::vector<int64_t>& off) {
+  cnt.assign(parts, n / parts);
+  off.assign(parts, 0);
+  for (int i = 0; i < parts; ++i) cnt[i] += (i < n % parts) ? 1 : 0;
+  for (int i = 1; i < parts; ++i) off[i] = off[i - 1] + cnt[i - 1];
+}
+
+// ---------------------------------------------------------------- single-GPU k-NN pipeline
+struct LocalKnn {
+  hipStream_t st = nullptr;
+  DevBuf<double> mu;
+  DevBuf<char> xfrag;
+  DevBuf<float> xinit;
+  DevBuf<unsigned> words;  // [0] xnmax bits, [1] bad
+  DevBuf<short> qhi, qlo;
+  DevBuf<float> qn;
+  DevBuf<int> qidx_a, qidx_b, qidx_f, kdev, cand_ids, cand_cnt, status;
+  DevBuf<char> fb_ws;
+  int KT = 1;
+  int64_t N = 0;
+  int A = 0;
+  const double* X = nullptr;
+
+  static float eps_rel(int A) {
+    return 2.0f * (float)(3.0 * std::ldexp(1.0, -16) + (3 * A + 8) * std::ldexp(1.0, -24));
+  }
+
+  void prepare(const double* Xd, int64_t N_, int A_) {
+    X = Xd;
+    N = N_;
+    A = A_;
+    KT = std::max(1, (A + 31) / 32);
+    if (KT > 4 || N == 0) return;
+    const int64_t nt = (N + 63) / 64;
+    HIPCHK(hipMemsetAsync(words.get(2), 0, 2 * sizeof(unsigned), st));
+    DMLPCHK(dmlp_center(Xd, N, A, mu.get(A), st));
+    DMLPCHK(dmlp_prep_data(Xd, N, A, mu.p, KT, xfrag.get(nt * 64 * KT * 64), xinit.get(nt * 64),
+                           words.p, words.p + 1, st));
+  }
+
+  static int slices_stream(int nq, int qw, int64_t n_tiles) {
+    const int nqb = (nq + qw - 1) / qw;
+    const int slots = 1024;
+    if (nqb >= slots) return 1;
+    int best = 1;
+    double best_eff = 0;
+    for (int S = 1; S <= 64 && S <= std::max<int64_t>(1, n_tiles / 4); ++S) {
+      const double w = (double)nqb * S;
+      const double eff = w / (std::ceil(w / slots) * slots);
+      if (eff >= 0.9) return S;
+      if (eff > best_eff + 1e-9) { best = S; best_eff = eff; }
+    }
+    return best;
+  }
+  static int slices_lds(int nq, int waves, int64_t n_tiles) {
+    const int nqb = (nq + waves * 16 - 1) / (waves * 16);
+    int S = 1;
+    while ((int64_t)nqb * S < 512 && S * 2 <= std::max<int64_t>(1, n_tiles) && S < 256) S *= 2;
+    return S;
+  }
+
+  // Exact top-k (+ vote/checksum when labels != nullptr) of queries Qx [Q][A] (device).
+  // k_host drives dispatch; out_* are [Q][kstride]; lab/cs may be null.
+  void run(const double* Qx, int64_t Q, const int* k_host, int kstride, double* out_d,
+           int* out_i, const int* labels, int lab_lo, int lab_hi, int* lab, uint64_t* cs) {
+    if (Q == 0) return;
+    std::vector<int> kk(Q), a, b, f, rest;
+    for (int64_t q = 0; q < Q; ++q) kk[q] = (int)std::min<int64_t>(k_host[q], N);
+    const bool screen = KT <= 4 && N > 0;
+    for (int64_t q = 0; q < Q; ++q) {
+      if (kk[q] < 1) { rest.push_back((int)q); continue; }
+      if (screen && kk[q] <= 32) a.push_back((int)q);
+      else if (screen && kk[q] <= 128) b.push_back((int)q);
+      else f.push_back((int)q);
+      if (k_host[q] > N) rest.push_back((int)q);
+    }
+    int* kd = kdev.get(Q);
+    HIPCHK(hipMemcpyAsync(kd, kk.data(), Q * sizeof(int), hipMemcpyHostToDevice, st));
+    // padding (+inf, -1) for k > N, like bench_2's {1e18, -1} sentinel
+    HIPCHK(hipMemsetAsync(out_i, 0xff, (size_t)Q * kstride * sizeof(int), st));
+    DMLPCHK(dmlp_fill_f64(out_d, (int64_t)Q * kstride, INFINITY, st));
+    int* stat = status.get(Q);
+    HIPCHK(hipMemsetAsync(stat, 0, Q * sizeof(int), st));
+    const bool fin = labels != nullptr;
+    if (!a.empty() || !b.empty()) {
+      DMLPCHK(dmlp_prep_queries(Qx, Q, A, mu.p, KT, qhi.get(Q * KT * 32), qlo.get(Q * KT * 32),
+                                qn.get(Q), words.p + 1, st));
+      const float er = eps_rel(A);
+      const int64_t nt = (N + 63) / 64;
+      const int qw = dmlp_screen_stream_qw(KT);
+      for (int cls = 0; cls < 2; ++cls) {
+        std::vector<int>& idx = cls == 0 ? a : b;
+        if (idx.empty()) continue;
+        const int nq = (int)idx.size();
+        int* qi = (cls == 0 ? qidx_a : qidx_b).get(nq);
+        HIPCHK(hipMemcpyAsync(qi, idx.data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
+        const bool streaming = cls == 0 && qw > 0;
+        const int cap = streaming ? 64 : (cls == 0 ? 128 : 256);
+        const int S = streaming ? slices_stream(nq, qw, nt)
+                                : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
+        int* ci = cand_ids.get((size_t)nq * S * cap);
+        int* cc = cand_cnt.get((size_t)nq * S);
+        if (streaming)
+          DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,
+                                     words.p, words.p + 1, er, S, ci, cc, st));
+        else
+          DMLPCHK(dmlp_screen(KT, cap, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,
+                              words.p, words.p + 1, er, S, ci, cc, st));
+        DMLPCHK(dmlp_refine(cap, ci, cc, S, X, A, Qx, qi, kd, nq, out_d, out_i, kstride,
+                            fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, st));
+      }
+      // one host sync: which screened queries overflowed into the exact path
+      std::vector<int> sh(Q);
+      HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      for (int64_t q = 0; q < Q; ++q)
+        if (sh[q]) f.push_back((int)q);
+    }
+    if (!f.empty()) {
+      std::sort(f.begin(), f.end());
+      const int rows = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)f.size(),
+                                                                   (1ll << 27) / std::max<int64_t>(1, N)));
+      const int64_t wsb = dmlp_fallback_bytes(rows, N);
+      char* ws = fb_ws.get(wsb);
+      int* qi = qidx_f.get(f.size());
+      HIPCHK(hipMemcpyAsync(qi, f.data(), f.size() * sizeof(int), hipMemcpyHostToDevice, st));
+      for (size_t c0 = 0; c0 < f.size(); c0 += rows) {
+        const int nb = (int)std::min<size_t>(rows, f.size() - c0);
+        DMLPCHK(dmlp_fallback_topk(X, N, A, Qx, qi + c0, kd, nb, ws, wsb, out_d, out_i, kstride,
+                                   st));
+      }
+      rest.insert(rest.end(), f.begin(), f.end());
+    }
+    if (fin && !rest.empty()) {
+      std::sort(rest.begin(), rest.end());
+      rest.erase(std::unique(rest.begin(), rest.end()), rest.end());
+      // the vote/checksum of k > N queries covers the padding, so use the unclamped k
+      int* kfull = kdev.get(Q);  // safe: refine already consumed the clamped k on this stream
+      HIPCHK(hipMemcpyAsync(kfull, k_host, Q * sizeof(int), hipMemcpyHostToDevice, st));
+      int* qi = qidx_f.get(std::max<size_t>(rest.size(), f.size()));
+      HIPCHK(hipMemcpyAsync(qi, rest.data(), rest.size() * sizeof(int), hipMemcpyHostToDevice, st));
+      DMLPCHK(dmlp_finalize(out_d, out_i, kstride, kfull, qi, (int)rest.size(), labels, lab_lo,
+                            lab_hi, lab, cs, st));
+      HIPCHK(hipStreamSynchronize(st));  // host vectors above die at scope exit
+    }
+  }
+};
+
+}  // namespace dmlp_rt

@@ -17,6 +17,8 @@
 #include "dmlp_device.h"
 #include <float.h>
 
+#include <algorithm>
+
 namespace {
 
 constexpr int kHistCap = 512;  // per-wave label histogram (labels in [lo, lo+512))
@@ -421,6 +423,41 @@ extern "C" int dmlp_finalize(const double* d, const int* ids, int kstride, const
   if (nq <= 0) return 0;
   hipLaunchKernelGGL(k_finalize, dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, d, ids,
                      kstride, qk, qidx, nq, labels, label_lo, label_hi, out_label, out_cs);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+__global__ void k_fill_f64(double* __restrict__ p, int64_t n, double v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+}  // namespace
+
+namespace {
+__global__ void k_offset_ids(int* __restrict__ ids, int64_t n, int off) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (ids[i] >= 0) ids[i] += off;
+}
+}  // namespace
+
+// shard-local ids -> global ids (padding -1 kept)
+extern "C" int dmlp_offset_ids(int* ids, int64_t n, int off, void* stream) {
+  if (n <= 0 || off == 0) return 0;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_offset_ids, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ids,
+                     n, off);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_fill_f64(double* p, int64_t n, double v, void* stream) {
+  if (n <= 0) return 0;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, n,
+                     v);
   DMLP_LAUNCH_CHECK();
   return 0;
 }
