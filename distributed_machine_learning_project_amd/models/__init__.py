@@ -1,1 +1,2 @@
-"""Model front-ends (k-NN classifier, KD-tree)."""
+"""Model front-ends (exact k-NN classifier, serial KD-tree)."""
+from .knn_classifier import KDTree, KNNClassifier  # noqa: F401
