@@ -8,5 +8,5 @@ RCCL over xGMI (torch.distributed "nccl" backend) for the data plane, C++ for th
 """
 __version__ = "0.1.0"
 
-from .utils.io import (KNNInput, Params, DataPoint, Query, parse_input, read_input,  # noqa: F401
-                       generate, generate_text, format_report, format_debug, to_text)
+from .utils.io import (KNNInput, Params, DataPoint, Query, Update, parse_update,  # noqa: F401
+                       parse_input, read_input, generate, generate_text, format_report, format_debug, to_text)

@@ -42,6 +42,7 @@ _SIGS = {
     "dmlp_merge": (i32, [vp, vp, i32, i64, i32, vp, i32, vp, vp, i32, vp]),
     "dmlp_finalize": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp]),
     "dmlp_format_bound": (i64, [i32]),
+    "dmlp_format_scratch": (i64, [i32]),
     "dmlp_format_report": (i32, [vp, i32, i32, vp, vp, vp]),
     "dmlp_cpu_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp, i32]),
     "dmlp_cpu_finalize": (i32, [vp, vp, i32, vp, i64, vp, vp, vp]),

@@ -86,8 +86,10 @@ int dmlp_offset_ids(int* ids, int64_t n, int off, void* stream);
 
 // ---------------------------------------------------------------- device: report formatting (K7)
 // "Query <qid> checksum: <cs>\n" for q < nq into out (needs dmlp_format_bound bytes).
-// line_off[nq+1] is scratch (int64) that receives the line offsets; *total_out (device) = bytes.
+// line_off[dmlp_format_scratch(nq)] is int64 scratch: line_off[0..nq] receives the line offsets
+// (line_off[nq] = total bytes), the tail holds the per-block sums of the scan.
 int64_t dmlp_format_bound(int nq);
+int64_t dmlp_format_scratch(int nq);
 int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off, char* out,
                        void* stream);
 

@@ -1,7 +1,7 @@
 // engine_main.cpp — standalone MI355X `knn_engine`: the reference's harness contract
 // (common.cpp:81-135) and Engine::KNN (engine.h:10-11) in native C++.
 //
-//   mpirun -np P ./knn_engine [--strategy farm|shard_gather|shard_reduce|serial] [--debug]
+//   mpirun -np P ./knn_engine [--strategy farm|shard_gather|shard_reduce|grid2d|serial] [--debug]
 //          [--exact] [--input FILE] < input
 //
 // Process model: one MPI rank per GPU (MPI only bootstraps and carries tiny host-side control
@@ -71,8 +71,9 @@ class Engine {
   Engine(Runtime& rt, std::string strategy, bool debug, bool exact)
       : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact) {
     lk_.st = rt_.stream;
+    trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
-        strategy_ != "serial")
+        strategy_ != "serial" && strategy_ != "grid2d")
       throw std::runtime_error("unknown strategy " + strategy_);
     if (rt_.gpu) warmup();
   }
@@ -96,6 +97,7 @@ class Engine {
     lo_ = (int)meta[3]; hi_ = (int)meta[4]; kmax_ = (int)meta[5];
     if (strategy_ == "serial") return serial(in, out);
     if (strategy_ == "farm") return farm(in, out);
+    if (strategy_ == "grid2d") return grid2d(in, out);
     return sharded(in, out, strategy_ == "shard_reduce");
   }
 
@@ -111,6 +113,28 @@ class Engine {
   DevBuf<uint64_t> cs_;
   DevBuf<int64_t> off_;
   DevBuf<char> txt_;
+
+ public:
+  Trace trace;
+  int64_t sent_ = 0;  // bytes this rank put on the wire (RCCL sends + its share of broadcasts)
+
+ private:
+  template <typename T>
+  static ncclDataType_t nty();
+  template <typename T>
+  void snd(const T* p, int64_t n, int peer) {
+    NCCLCHK(ncclSend(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+    sent_ += n * (int64_t)sizeof(T);
+  }
+  template <typename T>
+  void rcv(T* p, int64_t n, int peer) {
+    NCCLCHK(ncclRecv(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+  }
+  template <typename T>
+  void bcast(T* p, int64_t n) {
+    NCCLCHK(ncclBroadcast(p, p, n, nty<T>(), 0, rt_.nccl, rt_.stream));
+    if (rt_.rank == 0) sent_ += n * (int64_t)sizeof(T) * (rt_.world - 1);
+  }
 
   void warmup() {
     // load every kernel once (module load + first-launch costs stay outside the timed region)
@@ -130,7 +154,7 @@ class Engine {
     lk_.prepare(xd, n, a);
     lk_.run(qd, q, k.data(), 64, d_.get(q * 64), ids_.get(q * 64), ld, 0, 3, labout_.get(q),
             cs_.get(q));
-    int64_t* off = off_.get(q + 4);
+    int64_t* off = off_.get(dmlp_format_scratch(q));
     DMLPCHK(dmlp_format_report(cs_.p, q, 0, off, txt_.get(dmlp_format_bound(q)), rt_.stream));
     rt_.sync();
     MPI_Barrier(MPI_COMM_WORLD);
@@ -143,11 +167,12 @@ class Engine {
     lk_.run(Qd, nq, kh, kmax_, od, oi, labels, lo_, hi_, lab, cs);
   }
 
+  // rank 0: the report (GPU formatter) or, with --debug, the host copies of the lists + labels
   void render(Output* out, const uint64_t* cs_dev, const int* lab_dev, const double* dd,
               const int* ii) {
     out->kstride = kmax_;
     if (!debug_) {
-      int64_t* off = off_.get(Q_ + Q_ / 1024 + 4);
+      int64_t* off = off_.get(dmlp_format_scratch((int)Q_));
       char* txt = txt_.get(dmlp_format_bound((int)Q_));
       DMLPCHK(dmlp_format_report(cs_dev, (int)Q_, 0, off, txt, rt_.stream));
       int64_t total = 0;
@@ -157,15 +182,13 @@ class Engine {
       HIPCHK(hipMemcpy(out->report.data(), txt, total, hipMemcpyDeviceToHost));
       return;
     }
+    rt_.sync();
     out->label.resize(Q_);
     out->dist.resize(Q_ * kmax_);
     out->ids.resize(Q_ * kmax_);
     HIPCHK(hipMemcpy(out->label.data(), lab_dev, Q_ * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(out->dist.data(), dd, Q_ * kmax_ * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(out->ids.data(), ii, Q_ * kmax_ * 4, hipMemcpyDeviceToHost));
-    std::vector<int> k(Q_);
-    std::vector<char> buf(64 * Q_ + 48 * Q_ * kmax_ + 64);
-    (void)k;
     out->report.clear();
   }
 
@@ -183,6 +206,7 @@ class Engine {
       HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(Qall, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
     }
+    trace.mark("h2d");
     // per-rank k on the host (tiny, MPI) — it drives kernel dispatch
     std::vector<int> kl(cnt[rt_.rank]);
     std::vector<int> sc(P), so(P);
@@ -191,47 +215,51 @@ class Engine {
                  kl.data(), sc[rt_.rank], MPI_INT, 0, MPI_COMM_WORLD);
     if (P > 1) {
       // replicate the dataset (MPI_Bcast of all rows in bench_4 -> ncclBroadcast over xGMI)
-      NCCLCHK(ncclBroadcast(Xd, Xd, N_ * A_, ncclFloat64, 0, rt_.nccl, st));
-      NCCLCHK(ncclBroadcast(Ld, Ld, N_, ncclInt32, 0, rt_.nccl, st));
+      bcast(Xd, N_ * A_);
+      bcast(Ld, N_);
       // static query blocks: one direct xGMI hop per rank
       NCCLCHK(ncclGroupStart());
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r)
-          if (cnt[r]) NCCLCHK(ncclSend(Qall + off[r] * A_, cnt[r] * A_, ncclFloat64, r, rt_.nccl, st));
+          if (cnt[r]) snd(Qall + off[r] * A_, cnt[r] * A_, r);
       } else if (cnt[rt_.rank]) {
-        NCCLCHK(ncclRecv(Qall, cnt[rt_.rank] * A_, ncclFloat64, 0, rt_.nccl, st));
+        rcv(Qall, cnt[rt_.rank] * A_, 0);
       }
       NCCLCHK(ncclGroupEnd());
     }
+    trace.mark("distribute");
     const int64_t nl = cnt[rt_.rank];
     double* dd = d_.get(std::max<int64_t>(1, (rt_.rank == 0 ? Q_ : nl)) * kmax_);
     int* ii = ids_.get(std::max<int64_t>(1, (rt_.rank == 0 ? Q_ : nl)) * kmax_);
     int* lb = labout_.get(rt_.rank == 0 ? Q_ : nl + 1);
     uint64_t* cs = cs_.get(rt_.rank == 0 ? Q_ : nl + 1);
     local_knn(Xd, N_, Qall, nl, kl.data(), dd, ii, Ld, lb, cs);
+    trace.mark("compute");
     if (P > 1) {  // gather (label, checksum [, lists]) to rank 0 in rank order
       NCCLCHK(ncclGroupStart());
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r) {
           if (!cnt[r]) continue;
-          NCCLCHK(ncclRecv(lb + off[r], cnt[r], ncclInt32, r, rt_.nccl, st));
-          NCCLCHK(ncclRecv(cs + off[r], cnt[r], ncclUint64, r, rt_.nccl, st));
+          rcv(lb + off[r], cnt[r], r);
+          rcv(cs + off[r], cnt[r], r);
           if (debug_) {
-            NCCLCHK(ncclRecv(dd + off[r] * kmax_, cnt[r] * kmax_, ncclFloat64, r, rt_.nccl, st));
-            NCCLCHK(ncclRecv(ii + off[r] * kmax_, cnt[r] * kmax_, ncclInt32, r, rt_.nccl, st));
+            rcv(dd + off[r] * kmax_, cnt[r] * kmax_, r);
+            rcv(ii + off[r] * kmax_, cnt[r] * kmax_, r);
           }
         }
       } else if (nl) {
-        NCCLCHK(ncclSend(lb, nl, ncclInt32, 0, rt_.nccl, st));
-        NCCLCHK(ncclSend(cs, nl, ncclUint64, 0, rt_.nccl, st));
+        snd(lb, nl, 0);
+        snd(cs, nl, 0);
         if (debug_) {
-          NCCLCHK(ncclSend(dd, nl * kmax_, ncclFloat64, 0, rt_.nccl, st));
-          NCCLCHK(ncclSend(ii, nl * kmax_, ncclInt32, 0, rt_.nccl, st));
+          snd(dd, nl * kmax_, 0);
+          snd(ii, nl * kmax_, 0);
         }
       }
       NCCLCHK(ncclGroupEnd());
     }
+    trace.mark("gather");
     if (rt_.rank == 0) render(out, cs, lb, dd, ii);
+    trace.mark("report");
     rt_.sync();
   }
 
@@ -250,6 +278,7 @@ class Engine {
       HIPCHK(hipMemcpyAsync(Qd, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
     }
+    trace.mark("h2d");
     std::vector<int> k(Q_);
     if (rt_.rank == 0) k = in->k;
     MPI_Bcast(k.data(), (int)Q_, MPI_INT, 0, MPI_COMM_WORLD);
@@ -257,21 +286,22 @@ class Engine {
       NCCLCHK(ncclGroupStart());  // MPI_Scatterv of the shards -> direct sends
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r)
-          if (cnt[r]) NCCLCHK(ncclSend(Xd + off[r] * A_, cnt[r] * A_, ncclFloat64, r, rt_.nccl, st));
+          if (cnt[r]) snd(Xd + off[r] * A_, cnt[r] * A_, r);
       } else if (nl) {
-        NCCLCHK(ncclRecv(Xd, nl * A_, ncclFloat64, 0, rt_.nccl, st));
+        rcv(Xd, nl * A_, 0);
       }
       NCCLCHK(ncclGroupEnd());
-      NCCLCHK(ncclBroadcast(Qd, Qd, Q_ * A_, ncclFloat64, 0, rt_.nccl, st));
+      bcast(Qd, Q_ * A_);
     }
+    trace.mark("distribute");
     const int64_t L = (int64_t)Q_ * kmax_;
     double* dd = d_.get(L);
     int* ii = ids_.get(L);
     local_knn(Xd, nl, Qd, Q_, k.data(), dd, ii, nullptr, nullptr, nullptr);
+    trace.mark("compute");
     DMLPCHK(dmlp_offset_ids(ii, L, (int)off[rt_.rank], st));
     int* kd = kd_.get(Q_);
     HIPCHK(hipMemcpyAsync(kd, k.data(), Q_ * 4, hipMemcpyHostToDevice, st));
-    bool root_has = true;
     if (P > 1 && !tree) {  // bench_1: ONE batched gather of all lists, K-way merge at the root
       double* all_d = dall_.get(rt_.rank == 0 ? L * P : 1);
       int* all_i = iall_.get(rt_.rank == 0 ? L * P : 1);
@@ -280,12 +310,12 @@ class Engine {
         HIPCHK(hipMemcpyAsync(all_d, dd, L * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(all_i, ii, L * 4, hipMemcpyDeviceToDevice, st));
         for (int r = 1; r < P; ++r) {
-          NCCLCHK(ncclRecv(all_d + r * L, L, ncclFloat64, r, rt_.nccl, st));
-          NCCLCHK(ncclRecv(all_i + r * L, L, ncclInt32, r, rt_.nccl, st));
+          rcv(all_d + r * L, L, r);
+          rcv(all_i + r * L, L, r);
         }
       } else {
-        NCCLCHK(ncclSend(dd, L, ncclFloat64, 0, rt_.nccl, st));
-        NCCLCHK(ncclSend(ii, L, ncclInt32, 0, rt_.nccl, st));
+        snd(dd, L, 0);
+        snd(ii, L, 0);
       }
       NCCLCHK(ncclGroupEnd());
       if (rt_.rank == 0) DMLPCHK(dmlp_merge(all_d, all_i, P, L, kmax_, kd, (int)Q_, dd, ii, kmax_, st));
@@ -295,29 +325,141 @@ class Engine {
       for (int step = 1; step < P; step *= 2) {
         if (rt_.rank % (2 * step) == step) {
           NCCLCHK(ncclGroupStart());
-          NCCLCHK(ncclSend(dd, L, ncclFloat64, rt_.rank - step, rt_.nccl, st));
-          NCCLCHK(ncclSend(ii, L, ncclInt32, rt_.rank - step, rt_.nccl, st));
+          snd(dd, L, rt_.rank - step);
+          snd(ii, L, rt_.rank - step);
           NCCLCHK(ncclGroupEnd());
-          root_has = false;
           break;
         }
         if (rt_.rank % (2 * step) == 0 && rt_.rank + step < P) {
           HIPCHK(hipMemcpyAsync(sd, dd, L * 8, hipMemcpyDeviceToDevice, st));
           HIPCHK(hipMemcpyAsync(si, ii, L * 4, hipMemcpyDeviceToDevice, st));
           NCCLCHK(ncclGroupStart());
-          NCCLCHK(ncclRecv(sd + L, L, ncclFloat64, rt_.rank + step, rt_.nccl, st));
-          NCCLCHK(ncclRecv(si + L, L, ncclInt32, rt_.rank + step, rt_.nccl, st));
+          rcv(sd + L, L, rt_.rank + step);
+          rcv(si + L, L, rt_.rank + step);
           NCCLCHK(ncclGroupEnd());
           DMLPCHK(dmlp_merge(sd, si, 2, L, kmax_, kd, (int)Q_, dd, ii, kmax_, st));
         }
       }
     }
-    (void)root_has;
+    trace.mark("merge");
     if (rt_.rank == 0) {
       int* lb = labout_.get(Q_ + 1);
       uint64_t* cs = cs_.get(Q_ + 1);
       DMLPCHK(dmlp_finalize(dd, ii, kmax_, kd, nullptr, (int)Q_, Ld, lo_, hi_, lb, cs, st));
       render(out, cs, lb, dd, ii);
+      trace.mark("report");
+    }
+    rt_.sync();
+  }
+
+  // ---------------------------------------------------------------- grid2d (student engine.cpp)
+  // R x C process grid (MPI_Dims_create): data split over grid rows, queries over grid columns,
+  // rank (r, c) = r*C + c computes query block c against data shard r.  The reference's
+  // two-hop scatter+row/column broadcasts become one direct xGMI send per rank from the root
+  // (xGMI is a full point-to-point mesh); the lists of column c are merged at (0, c), which
+  // votes and returns (label, checksum) to rank 0.  Fixes D1 (vote on the merged lists) and
+  // D3 (rank 0 prints everything, in query order).
+  void grid2d(Input* in, Output* out) {
+    const int P = rt_.world;
+    int dims[2] = {0, 0};
+    MPI_Dims_create(P, 2, dims);
+    const int R = dims[0], C = dims[1];
+    const int row = rt_.rank / C, col = rt_.rank % C;
+    std::vector<int64_t> dc, doff, qc, qoff;
+    block_partition(N_, R, dc, doff);
+    block_partition(Q_, C, qc, qoff);
+    hipStream_t st = rt_.stream;
+    const bool root = rt_.rank == 0;
+    double* Xd = X_.get((root ? N_ : dc[row]) * A_ + 1);
+    double* Qd = Qx_.get((root ? Q_ : qc[col]) * A_ + 1);
+    int* Ld = lab_.get(N_ + 1);
+    if (root) {
+      HIPCHK(hipMemcpyAsync(Xd, in->X.data(), N_ * A_ * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Qd, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
+    }
+    trace.mark("h2d");
+    std::vector<int> k(Q_);
+    if (root) k = in->k;
+    MPI_Bcast(k.data(), (int)Q_, MPI_INT, 0, MPI_COMM_WORLD);
+    if (P > 1) {
+      NCCLCHK(ncclGroupStart());
+      if (root) {
+        for (int r = 1; r < P; ++r) {
+          const int rr = r / C, cc = r % C;
+          if (dc[rr]) snd(Xd + doff[rr] * A_, dc[rr] * A_, r);
+          if (qc[cc]) snd(Qd + qoff[cc] * A_, qc[cc] * A_, r);
+          if (rr == 0 && N_) snd(Ld, N_, r);
+        }
+      } else {
+        if (dc[row]) rcv(Xd, dc[row] * A_, 0);
+        if (qc[col]) rcv(Qd, qc[col] * A_, 0);
+        if (row == 0 && N_) rcv(Ld, N_, 0);
+      }
+      NCCLCHK(ncclGroupEnd());
+    }
+    trace.mark("distribute");
+    const int64_t nq = qc[col];
+    const int64_t L = nq * kmax_;
+    const int64_t Lmax = (root ? Q_ : nq) * kmax_ + 1;
+    double* dd = d_.get(Lmax);
+    int* ii = ids_.get(Lmax);
+    const int* kh = k.data() + qoff[col];
+    local_knn(Xd, dc[row], Qd, nq, kh, dd, ii, nullptr, nullptr, nullptr);
+    trace.mark("compute");
+    DMLPCHK(dmlp_offset_ids(ii, L, (int)doff[row], st));
+    int* kd = kd_.get(nq + 1);
+    HIPCHK(hipMemcpyAsync(kd, kh, nq * 4, hipMemcpyHostToDevice, st));
+    if (R > 1 && L) {  // column merge at (0, col)
+      if (row == 0) {
+        double* all_d = dall_.get(L * R);
+        int* all_i = iall_.get(L * R);
+        HIPCHK(hipMemcpyAsync(all_d, dd, L * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(all_i, ii, L * 4, hipMemcpyDeviceToDevice, st));
+        NCCLCHK(ncclGroupStart());
+        for (int r = 1; r < R; ++r) {
+          rcv(all_d + r * L, L, r * C + col);
+          rcv(all_i + r * L, L, r * C + col);
+        }
+        NCCLCHK(ncclGroupEnd());
+        DMLPCHK(dmlp_merge(all_d, all_i, R, L, kmax_, kd, (int)nq, dd, ii, kmax_, st));
+      } else {
+        NCCLCHK(ncclGroupStart());
+        snd(dd, L, col);
+        snd(ii, L, col);
+        NCCLCHK(ncclGroupEnd());
+      }
+    }
+    trace.mark("merge");
+    if (row == 0) {
+      int* lb = labout_.get((root ? Q_ : nq) + 1);
+      uint64_t* cs = cs_.get((root ? Q_ : nq) + 1);
+      DMLPCHK(dmlp_finalize(dd, ii, kmax_, kd, nullptr, (int)nq, Ld, lo_, hi_, lb, cs, st));
+      if (C > 1) {  // row-0 gather of (label, checksum [, lists]) in query order
+        NCCLCHK(ncclGroupStart());
+        if (root) {
+          for (int c = 1; c < C; ++c) {
+            if (!qc[c]) continue;
+            rcv(lb + qoff[c], qc[c], c);
+            rcv(cs + qoff[c], qc[c], c);
+            if (debug_) {
+              rcv(dd + qoff[c] * kmax_, qc[c] * kmax_, c);
+              rcv(ii + qoff[c] * kmax_, qc[c] * kmax_, c);
+            }
+          }
+        } else if (nq) {
+          snd(lb, nq, 0);
+          snd(cs, nq, 0);
+          if (debug_) {
+            snd(dd, L, 0);
+            snd(ii, L, 0);
+          }
+        }
+        NCCLCHK(ncclGroupEnd());
+      }
+      trace.mark("gather");
+      if (root) render(out, cs, lb, dd, ii);
+      trace.mark("report");
     }
     rt_.sync();
   }
@@ -330,16 +472,42 @@ class Engine {
     out->ids.assign(Q_ * kmax_, -1);
     DMLPCHK(dmlp_kdtree_knn(in->X.data(), N_, A_, in->Qx.data(), Q_, in->k.data(), kmax_,
                             out->dist.data(), out->ids.data()));
+    trace.mark("kdtree");
     out->label.resize(Q_);
     out->cs.resize(Q_);
     DMLPCHK(dmlp_cpu_finalize(out->dist.data(), out->ids.data(), kmax_, in->k.data(), Q_,
                               in->labels.data(), out->label.data(), out->cs.data()));
+    trace.mark("vote");
     if (!debug_) {
       out->report.resize(48 * Q_ + 64);
       out->report.resize(dmlp_cpu_format_report(out->cs.data(), Q_, 0, out->report.data()));
     }
   }
 };
+
+template <> ncclDataType_t Engine::nty<double>() { return ncclFloat64; }
+template <> ncclDataType_t Engine::nty<int>() { return ncclInt32; }
+template <> ncclDataType_t Engine::nty<uint64_t>() { return ncclUint64; }
+
+// KNN_METRICS=<path>: JSON sidecar written by rank 0 after the run (SURVEY.md §5 metrics row).
+void write_metrics(const char* path, const std::string& strategy, const Runtime& rt, const Input& in,
+                   double ms, const std::vector<std::pair<std::string, double>>& phases,
+                   int64_t bytes_total) {
+  FILE* f = std::fopen(path, "w");
+  if (!f) return;
+  int kmax = 0;
+  for (int k : in.k) kmax = std::max(kmax, k);
+  std::fprintf(f, "{\"engine\": \"knn_engine\", \"strategy\": \"%s\", \"ranks\": %d, \"N\": %lld, "
+               "\"Q\": %lld, \"A\": %d, \"kmax\": %d, \"time_ms\": %.3f, \"queries_per_s\": %.1f, "
+               "\"bytes_on_wire\": %lld, \"effective_GBps\": %.3f, \"phases_ms_rank0\": {",
+               strategy.c_str(), rt.world, (long long)in.N, (long long)in.Q, in.A, kmax, ms,
+               ms > 0 ? in.Q / (ms * 1e-3) : 0.0, (long long)bytes_total,
+               ms > 0 ? bytes_total / (ms * 1e-3) / 1e9 : 0.0);
+  for (size_t i = 0; i < phases.size(); ++i)
+    std::fprintf(f, "%s\"%s\": %.3f", i ? ", " : "", phases[i].first.c_str(), phases[i].second);
+  std::fprintf(f, "}}\n");
+  std::fclose(f);
+}
 
 }  // namespace
 
@@ -357,6 +525,7 @@ int main(int argc, char** argv) {
   }
   Runtime rt;
   int rc = 0;
+  double total_ms = 0;
   try {
     rt.init(strategy != "serial");
     Input in;
@@ -372,6 +541,7 @@ int main(int argc, char** argv) {
     Engine eng(rt, strategy, debug, exact);
     Output out;
     auto t0 = std::chrono::steady_clock::now();
+    eng.trace.begin();
     eng.KNN(rt.rank == 0 ? &in : nullptr, rt.rank == 0 ? &out : nullptr);
     std::string text;
     if (rt.rank == 0) {
@@ -392,7 +562,14 @@ int main(int argc, char** argv) {
       std::fflush(stdout);
       std::fprintf(stderr, "Time taken: %lld ms\n",
                    (long long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count());
+      total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     }
+    // after the timed region: per-phase trace (KNN_TRACE=1) and the metrics sidecar
+    const auto phases = eng.trace.finish();
+    int64_t bytes = 0;
+    MPI_Reduce(&eng.sent_, &bytes, 1, MPI_INT64_T, MPI_SUM, 0, MPI_COMM_WORLD);
+    if (rt.rank == 0 && getenv("KNN_METRICS"))
+      write_metrics(getenv("KNN_METRICS"), strategy, rt, in, total_ms, phases, bytes);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "[knn_engine] rank %d: %s\n", rt.rank, e.what());
     rc = 1;

@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -113,6 +114,62 @@ struct Runtime {
   }
 };
 
+// Opt-in per-phase tracer (KNN_TRACE=1): phase boundaries are hipEvents recorded
+// on the engine stream (no host syncs inside the timed region), host clocks for CPU-only runs.
+// Lines go to stderr as "[dmlp-trace] rank r <phase> <ms> ms" — never starting with "Time taken"
+// (run_bench.sh:40 greps the first such line).
+struct Trace {
+  bool on = false;
+  int rank = 0;
+  hipStream_t st = nullptr;
+  std::vector<std::string> names;
+  std::vector<hipEvent_t> ev;
+  std::vector<double> host_ms;
+  std::chrono::steady_clock::time_point t0;
+
+  void init(int r, hipStream_t s) {
+    const char* e = getenv("KNN_TRACE");
+    on = e && *e && std::string(e) != "0";
+    rank = r;
+    st = s;
+  }
+  void begin() {
+    names.clear(); ev.clear(); host_ms.clear();
+    t0 = std::chrono::steady_clock::now();
+    if (on) mark("begin");
+  }
+  void mark(const char* name) {
+    if (!on) return;
+    names.emplace_back(name);
+    host_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    if (st) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      HIPCHK(hipEventRecord(e, st));
+      ev.push_back(e);
+    }
+  }
+  // Durations of the phases ending at each mark (after the run; synchronizes the stream).
+  std::vector<std::pair<std::string, double>> finish() {
+    std::vector<std::pair<std::string, double>> out;
+    if (!on) return out;
+    if (st) HIPCHK(hipStreamSynchronize(st));
+    for (size_t i = 1; i < names.size(); ++i) {
+      double ms = host_ms[i] - host_ms[i - 1];
+      if (st) {
+        float f = 0;
+        HIPCHK(hipEventElapsedTime(&f, ev[i - 1], ev[i]));
+        ms = f;
+      }
+      out.emplace_back(names[i], ms);
+      std::fprintf(stderr, "[dmlp-trace] rank %d %s %.3f ms\n", rank, names[i].c_str(), ms);
+    }
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    return out;
+  }
+};
+
 // Balanced block partition (bench_1 @0xc5b2).
 inline void block_partition(int64_t n, int parts, std::vector<int64_t>& cnt,
                             std::vector<int64_t>& off) {
@@ -151,7 +208,7 @@ struct LocalKnn {
     const int64_t nt = (N + 63) / 64;
     HIPCHK(hipMemsetAsync(words.get(2), 0, 2 * sizeof(unsigned), st));
     DMLPCHK(dmlp_center(Xd, N, A, mu.get(A), st));
-    DMLPCHK(dmlp_prep_data(Xd, N, A, mu.p, KT, xfrag.get(nt * 64 * KT * 64), xinit.get(nt * 64),
+    DMLPCHK(dmlp_prep_data(Xd, N, A, mu.p, KT, xfrag.get(nt * 64 * KT * 32 * 2 * sizeof(short)), xinit.get(nt * 64),
                            words.p, words.p + 1, st));
   }
 

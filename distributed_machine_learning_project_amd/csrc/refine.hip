@@ -465,6 +465,8 @@ extern "C" int dmlp_fill_f64(double* p, int64_t n, double v, void* stream) {
 extern "C" int64_t dmlp_format_bound(int nq) { return (int64_t)nq * 48 + 64; }
 
 // line_off needs nq + 1 + (nq/1024 + 2) int64 of scratch; on completion line_off[nq] = bytes.
+extern "C" int64_t dmlp_format_scratch(int nq) { return (int64_t)nq + 1 + (nq + 1023) / 1024 + 1; }
+
 extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off,
                                   char* out, void* stream) {
   if (nq <= 0) return 0;

@@ -43,6 +43,25 @@ class KNNClassifier:
                                          torch.from_numpy(self.y).cuda(), (lo, hi))
         return self
 
+    def update(self, updates):
+        """Apply Update records (common.h:22-25) to the fitted dataset: rows are replaced in the
+        host copy and, on a GPU, scattered into the device copy, after which the screen layout
+        (centering, bf16 fragments, norms) is rebuilt so later queries stay exact."""
+        updates = list(updates)
+        if not updates:
+            return self
+        for u in updates:
+            if not 0 <= u.id < self.X.shape[0] or len(u.new_attrs) != self.X.shape[1]:
+                raise ValueError(f"update {u.id}: id out of range or wrong attribute count")
+            self.X[u.id] = np.asarray(u.new_attrs, np.float64)
+        if self.on_gpu:
+            torch = _torch()
+            ids = np.array(sorted({u.id for u in updates}), np.int64)
+            Xd = self._ds.X
+            Xd[torch.from_numpy(ids).to(Xd.device)] = torch.from_numpy(self.X[ids]).to(Xd.device)
+            self._ds = K.prepare_dataset(Xd, self._ds.labels, (self._ds.label_lo, self._ds.label_hi))
+        return self
+
     def _k(self, Q, k):
         if np.isscalar(k):
             return np.full(Q.shape[0], int(k), np.int32)

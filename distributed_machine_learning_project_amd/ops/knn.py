@@ -353,7 +353,7 @@ def format_report_gpu(cs, qid_base: int = 0) -> bytes:
     nq = cs.numel()
     if nq == 0:
         return b""
-    off = torch.empty(nq + 1 + nq // 1024 + 2, dtype=torch.int64, device=cs.device)
+    off = torch.empty(L.dmlp_format_scratch(nq), dtype=torch.int64, device=cs.device)
     out = torch.empty(L.dmlp_format_bound(nq), dtype=torch.uint8, device=cs.device)
     _lib.check(L.dmlp_format_report(_p(cs), nq, qid_base, _p(off), _p(out), _stream()), "format")
     n = int(off[nq].item())

@@ -44,6 +44,25 @@ class Query:
 
 
 @dataclass
+class Update:
+    """common.h:22-25: replace the attributes of data point `id` (dead code in the reference's
+    harness; here it drives KNNInput.apply_updates / KNNClassifier.update)."""
+    id: int
+    new_attrs: list = field(default_factory=list)
+
+
+def parse_update(line: str) -> Update:
+    """common.cpp:46-55: "<id> <a_0> <a_1> ..." (every remaining token is an attribute)."""
+    tok = line.split()
+    if not tok:
+        raise InputFormatError("empty update line")
+    try:
+        return Update(int(tok[0]), [float(t) for t in tok[1:]])
+    except ValueError as e:
+        raise InputFormatError(f"malformed update line: {line!r}") from e
+
+
+@dataclass
 class KNNInput:
     """Parsed workload in flat, device-friendly form (ids are the row indices)."""
     labels: np.ndarray  # int32 [N]
@@ -72,6 +91,13 @@ class KNNInput:
 
     def queries(self):
         return [Query(i, int(self.k[i]), list(self.Qx[i])) for i in range(self.Q)]
+
+    def apply_updates(self, updates) -> None:
+        """Apply Update records in order (later updates of the same id win)."""
+        for u in updates:
+            if not 0 <= u.id < self.N or len(u.new_attrs) != self.A:
+                raise ValueError(f"update {u.id}: id out of range or wrong attribute count")
+            self.X[u.id] = np.asarray(u.new_attrs, np.float64)
 
     @staticmethod
     def from_aos(dataset, queries) -> "KNNInput":

@@ -1,0 +1,95 @@
+"""Standalone native `knn_engine` binary (csrc/engine_main.cpp) — host-only paths on the CPU
+(serial KD-tree strategy = bench.debug, under 1 and 2 MPI ranks), every GPU strategy on a GPU.
+Output is compared byte-for-byte with the float64 oracle's report (SURVEY.md §4 level 3/5)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import distributed_machine_learning_project_amd as dmlp
+from distributed_machine_learning_project_amd import build
+from distributed_machine_learning_project_amd.ops import reference as ref
+
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+def _engine():
+    e = build.build_engine()
+    if e is None or not os.path.exists(e):
+        pytest.skip("knn_engine not built (no MPI headers)")
+    return str(e)
+
+
+def _case(tmp_path, N=1500, Q=120, A=6, kmin=1, kmax=60, seed=9):
+    txt = dmlp.generate_text(N, Q, A, -20, 20, kmin, kmax, 5, seed=seed)
+    path = tmp_path / "in.txt"
+    path.write_text(txt)
+    inp = dmlp.parse_input(txt)
+    res, lab, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    return path, inp, res, lab, cs
+
+
+def _run(args, path, env=None, np_=1, timeout=120):
+    cmd = ([MPIEXEC, "-n", str(np_)] if np_ > 1 else []) + [_engine(), *args, "--input", str(path)]
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, timeout=timeout, env=e)
+    assert r.returncode == 0, r.stderr.decode()
+    return r.stdout, r.stderr.decode()
+
+
+def test_serial_matches_oracle(tmp_path):
+    path, inp, res, lab, cs = _case(tmp_path)
+    out, err = _run(["--strategy", "serial"], path)
+    assert out == dmlp.format_report(cs)
+    assert err.startswith("Time taken: ") and err.rstrip().endswith(" ms")
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+def test_serial_two_ranks_prints_once(tmp_path):
+    path, inp, res, lab, cs = _case(tmp_path, N=800, Q=50)
+    out, _ = _run(["--strategy", "serial"], path, np_=2)
+    assert out == dmlp.format_report(cs)
+
+
+def test_serial_debug_listing(tmp_path):
+    path, inp, res, lab, cs = _case(tmp_path, N=300, Q=12, kmax=9)
+    out, _ = _run(["--strategy", "serial", "--debug"], path)
+    K = max(int(k) for k in inp.k)
+    d = np.full((inp.Q, K), np.inf)
+    i = np.full((inp.Q, K), -1, np.int32)
+    for q, (dq, iq) in enumerate(res):
+        d[q, :len(dq)] = dq
+        i[q, :len(iq)] = iq
+    assert out == dmlp.format_debug(d, i, inp.k, lab)
+
+
+def test_trace_and_metrics_sidecar(tmp_path):
+    path, *_ = _case(tmp_path, N=500, Q=40)
+    mpath = tmp_path / "m.json"
+    out, err = _run(["--strategy", "serial"], path, env={"KNN_TRACE": "1", "KNN_METRICS": str(mpath)})
+    lines = err.splitlines()
+    assert lines[0].startswith("Time taken: ")           # run_bench.sh greps the first match
+    assert any(l.startswith("[dmlp-trace] rank 0 kdtree") for l in lines)
+    m = json.loads(mpath.read_text())
+    assert m["strategy"] == "serial" and m["N"] == 500 and m["Q"] == 40 and m["queries_per_s"] > 0
+
+
+def test_malformed_input_fails_loudly(tmp_path):
+    p = tmp_path / "bad.txt"
+    p.write_text("3 1 2\n0 1.0 2.0\n1 oops 2.0\n0 1 1\nQ 1 0 0\n")
+    r = subprocess.run([_engine(), "--strategy", "serial", "--input", str(p)], capture_output=True,
+                       timeout=60)
+    assert r.returncode != 0 and b"wrongly formatted" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d"])
+def test_gpu_strategies_match_oracle(tmp_path, strategy):
+    path, inp, res, lab, cs = _case(tmp_path, N=6000, Q=700, A=20, kmax=150)
+    out, _ = _run(["--strategy", strategy], path)
+    assert out == dmlp.format_report(cs)
+    out, _ = _run(["--strategy", strategy, "--exact"], path)
+    assert out == dmlp.format_report(cs)

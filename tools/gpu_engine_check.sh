@@ -17,7 +17,7 @@ for name, args in [("a", (20000, 3000, 32, 0, 1000, 1, 200, 10)), ("b", (5000, 7
 PY
 rc=0
 for f in a b; do
-  for s in farm shard_gather shard_reduce serial; do
+  for s in farm shard_gather shard_reduce grid2d serial; do
     timeout -k 10 120 $E --strategy $s --input gpurun_out/engine/$f.in > gpurun_out/engine/$f.$s.out 2> gpurun_out/engine/$f.$s.err; r=$?
     if [ $r -ne 0 ]; then echo "FAIL rc=$r $f $s"; cat gpurun_out/engine/$f.$s.err; exit $r; fi
     if cmp -s gpurun_out/engine/$f.$s.out gpurun_out/engine/$f.expect; then echo "OK $f $s $(cat gpurun_out/engine/$f.$s.err)"; else echo "MISMATCH $f $s"; rc=1; fi
