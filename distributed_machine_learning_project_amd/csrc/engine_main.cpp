@@ -71,6 +71,7 @@ class Engine {
   Engine(Runtime& rt, std::string strategy, bool debug, bool exact)
       : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact) {
     lk_.st = rt_.stream;
+    lk_.rt = &rt_;
     trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
         strategy_ != "serial" && strategy_ != "grid2d")

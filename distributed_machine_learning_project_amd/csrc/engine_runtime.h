@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -109,9 +110,39 @@ struct Runtime {
     if (nccl) ncclCommDestroy(nccl);
     if (stream) (void)hipStreamDestroy(stream);
   }
+  // Failure detection: with a communicator, wait for the stream by polling so a
+  // dead or faulted peer surfaces as an RCCL async error (or a KNN_TIMEOUT_S watchdog expiry,
+  // default 600 s) and the job aborts with a rank-tagged message instead of hanging in a
+  // collective.  Without one, a plain stream synchronize.
   void sync() {
-    if (gpu) HIPCHK(hipStreamSynchronize(stream));
+    if (!gpu) return;
+    if (!nccl) {
+      HIPCHK(hipStreamSynchronize(stream));
+      return;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+      const hipError_t e = hipStreamQuery(stream);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIPCHK(e);
+      ncclResult_t ae = ncclSuccess;
+      NCCLCHK(ncclCommGetAsyncError(nccl, &ae));
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (ae != ncclSuccess || s > timeout_s) {
+        if (ae != ncclSuccess)
+          std::fprintf(stderr, "[knn_engine] rank %d: RCCL async error: %s\n", rank,
+                       ncclGetErrorString(ae));
+        else
+          std::fprintf(stderr, "[knn_engine] rank %d: watchdog: stream not drained after %.0f s "
+                       "(peer failure?)\n", rank, s);
+        ncclCommAbort(nccl);
+        nccl = nullptr;
+        MPI_Abort(MPI_COMM_WORLD, 5);
+      }
+      if (spin > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
   }
+  double timeout_s = getenv("KNN_TIMEOUT_S") ? std::atof(getenv("KNN_TIMEOUT_S")) : 600.0;
 };
 
 // Opt-in per-phase tracer (KNN_TRACE=1): phase boundaries are hipEvents recorded
@@ -182,6 +213,11 @@ inline void block_partition(int64_t n, int parts, std::vector<int64_t>& cnt,
 // ---------------------------------------------------------------- single-GPU k-NN pipeline
 struct LocalKnn {
   hipStream_t st = nullptr;
+  Runtime* rt = nullptr;  // its sync() (watchdog) when set
+  void wait() {
+    if (rt) rt->sync();
+    else HIPCHK(hipStreamSynchronize(st));
+  }
   DevBuf<double> mu;
   DevBuf<char> xfrag;
   DevBuf<float> xinit;
@@ -286,7 +322,7 @@ struct LocalKnn {
       // one host sync: which screened queries overflowed into the exact path
       std::vector<int> sh(Q);
       HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      wait();
       for (int64_t q = 0; q < Q; ++q)
         if (sh[q]) f.push_back((int)q);
     }
@@ -315,7 +351,7 @@ struct LocalKnn {
       HIPCHK(hipMemcpyAsync(qi, rest.data(), rest.size() * sizeof(int), hipMemcpyHostToDevice, st));
       DMLPCHK(dmlp_finalize(out_d, out_i, kstride, kfull, qi, (int)rest.size(), labels, lab_lo,
                             lab_hi, lab, cs, st));
-      HIPCHK(hipStreamSynchronize(st));  // host vectors above die at scope exit
+      wait();  // host vectors above die at scope exit
     }
   }
 };

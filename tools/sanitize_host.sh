@@ -1,0 +1,17 @@
+#!/bin/bash
+# ASan + UBSan build of the host (CPU) half of libdmlp plus a driver that exercises it.
+# GPU sanitizers / xnack are unavailable on the MI355X pool, so device code is covered by the
+# numerics tests instead.  A second build runs the same driver under ThreadSanitizer (the parser
+# and the brute force are multi-threaded).   usage: tools/sanitize_host.sh [outdir]
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+OUT="${1:-/tmp/dmlp_asan}"
+mkdir -p "$OUT"
+SRC="$ROOT/distributed_machine_learning_project_amd/csrc"
+g++ -O1 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -fsanitize=address,undefined \
+    -fno-sanitize-recover=undefined -I"$SRC" "$SRC/cpu.cpp" "$ROOT/tests/native/host_driver.cpp" \
+    -pthread -o "$OUT/host_driver"
+ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_driver"
+g++ -O1 -g -std=c++17 -ffp-contract=off -fsanitize=thread -I"$SRC" "$SRC/cpu.cpp" \
+    "$ROOT/tests/native/host_driver.cpp" -pthread -o "$OUT/host_driver_tsan"
+TSAN_OPTIONS=halt_on_error=1 "$OUT/host_driver_tsan"
