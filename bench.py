@@ -49,6 +49,10 @@ def main(argv=None):
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--labels", type=int, default=10)
     ap.add_argument("--exact", action="store_true", help="fp64-only path (no MFMA screen)")
+    ap.add_argument("--ingress", default="shm", choices=["shm", "root"],
+                    help="shm: parsed input in a node-shared page-locked segment, every GPU "
+                         "copies its own part inside the timed step; root: rank 0 holds it and "
+                         "funnels it through GPU 0 (reference layout)")
     ap.add_argument("--verify", action="store_true", help="check rank-0 report against the CPU path")
     ap.add_argument("--no-busbw", action="store_true")
     a = ap.parse_args(argv)
@@ -69,13 +73,17 @@ def main(argv=None):
     inp = None
     if comm.is_root:
         inp = generate(a.n_data, Q, a.attrs, 0.0, 1000.0, a.k, a.k, a.labels, seed=42)
-        if comm.on_gpu:  # the "parsed input" lives in page-locked host memory (untimed, like parsing)
-            for name in ("X", "labels", "Qx", "k"):
-                setattr(inp, name + "_t", torch.from_numpy(getattr(inp, name)).pin_memory())
+    # the "parsed input" lives in page-locked host memory (untimed, like parsing)
+    if a.ingress == "shm":
+        from distributed_machine_learning_project_amd.utils.shm import share_input
+        inp = share_input(comm, inp)
+    elif comm.is_root and comm.on_gpu:
+        for name in ("X", "labels", "Qx", "k"):
+            setattr(inp, name + "_t", torch.from_numpy(getattr(inp, name)).pin_memory())
     eng = Engine(a.strategy, comm=comm, exact=a.exact, schedule=a.schedule)
 
     def step():
-        out = eng.KNN(inp.params if inp else None, inp, None)
+        out = eng.KNN(inp.params if comm.is_root else None, inp, None)
         return eng.report(out) if out is not None else None
 
     for _ in range(a.warmup):
@@ -134,11 +142,14 @@ def main(argv=None):
                 "parallelism": f"{a.strategy}{world}" + ("" if a.schedule == "static" else "-dynamic"),
                 "num_data": a.n_data,
                 "queries_per_gpu": a.q_per_gpu,
+                "ingress": a.ingress,
                 "k": a.k,
             },
         }
         line.update(extra)
         print(json.dumps(line), flush=True)
+    if a.ingress == "shm":
+        inp.close()
     eng.close()
 
 

@@ -54,6 +54,8 @@ _SIGS = {
     "dmlp_parse_body": (i64, [vp, i64, i64, i64, i64, i32, vp, vp, vp, vp, i32]),
     "dmlp_version": (C.c_char_p, []),
     "dmlp_device_count": (i32, []),
+    "dmlp_host_register": (i32, [vp, i64]),
+    "dmlp_host_unregister": (i32, [vp]),
 }
 
 

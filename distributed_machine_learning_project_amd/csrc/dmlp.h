@@ -116,6 +116,10 @@ int dmlp_parse_header(const char* buf, int64_t len, int64_t* N, int64_t* Q, int*
 int64_t dmlp_parse_body(const char* buf, int64_t len, int64_t body_off, int64_t N, int64_t Q,
                         int A, int* labels, double* X, int* qk, double* Qx, int nthreads);
 
+// Page-lock / unlock an existing host range (node-shared input segments).  0 or a hipError_t.
+int dmlp_host_register(void* p, int64_t bytes);
+int dmlp_host_unregister(void* p);
+
 const char* dmlp_version(void);
 int dmlp_device_count(void);
 

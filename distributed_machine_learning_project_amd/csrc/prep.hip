@@ -184,3 +184,15 @@ extern "C" int dmlp_device_count(void) {
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
 }
+
+// Page-lock an existing host range (e.g. a node-shared /dev/shm mapping) so H2D copies from it
+// run as DMA at full PCIe rate.  Returns 0 or the hipError_t code.
+extern "C" int dmlp_host_register(void* p, int64_t bytes) {
+  if (!p || bytes <= 0) return 0;
+  return (int)hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault);
+}
+
+extern "C" int dmlp_host_unregister(void* p) {
+  if (!p) return 0;
+  return (int)hipHostUnregister(p);
+}

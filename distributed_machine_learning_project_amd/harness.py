@@ -26,6 +26,9 @@ def main(argv=None):
     ap.add_argument("--schedule", default=os.environ.get("KNN_SCHEDULE", "static"),
                     choices=["static", "dynamic"])
     ap.add_argument("--input", default="-", help="input file (default: stdin)")
+    ap.add_argument("--ingress", default=os.environ.get("KNN_INGRESS", "root"), choices=["root", "shm"],
+                    help="root: rank 0 holds the parsed input (reference); shm: node-shared "
+                         "segment, every GPU copies its own part (utils/shm.py)")
     a = ap.parse_args(argv)
 
     from .parallel.comm import Comm
@@ -36,17 +39,17 @@ def main(argv=None):
     inp = None
     if comm.is_root:
         inp = read_input(a.input)
-        try:  # page-locked copies so the timed H2D runs at full PCIe speed
-            import torch
-            if comm.on_gpu:
-                for name in ("X", "labels", "Qx", "k"):
-                    setattr(inp, name + "_t", torch.from_numpy(getattr(inp, name)).pin_memory())
-        except Exception:
-            pass
+    if a.ingress == "shm":  # part of ingest (untimed): the parsed arrays go to a shared segment
+        from .utils.shm import share_input
+        inp = share_input(comm, inp)
+    elif comm.is_root and comm.on_gpu:
+        import torch  # page-locked copies so the timed H2D runs at full PCIe speed
+        for name in ("X", "labels", "Qx", "k"):
+            setattr(inp, name + "_t", torch.from_numpy(getattr(inp, name)).pin_memory())
     comm.barrier()
     eng = Engine(a.strategy, comm=comm, exact=a.exact or None, debug=a.debug, schedule=a.schedule)
     t0 = time.perf_counter() if comm.is_root else 0.0
-    out = eng.KNN(inp.params if inp else None, inp, None)
+    out = eng.KNN(inp.params if inp is not None and comm.is_root else None, inp, None)
     rep = eng.report(out) if out is not None else b""
     comm.sync()
     comm.barrier()
@@ -55,6 +58,8 @@ def main(argv=None):
         sys.stdout.buffer.write(rep)
         sys.stdout.flush()
         print(f"Time taken: {ms} ms", file=sys.stderr, flush=True)
+    if a.ingress == "shm":
+        inp.close()
     eng.close()
     return 0
 

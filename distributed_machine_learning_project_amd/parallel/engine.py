@@ -80,6 +80,8 @@ class Engine:
         inp = None
         if self.comm.is_root:
             inp = dataset if isinstance(dataset, KNNInput) else KNNInput.from_aos(dataset, queries)
+        elif getattr(dataset, "shared", False):
+            inp = dataset  # node-shared segment (utils/shm.py): mapped on every rank
         fn = FUNCS[self.strategy]
         res = fn(self.comm, self.be, inp, self.tracer, schedule=self.schedule,
                  call_id=self.calls, debug=self.debug, groups=self.groups)

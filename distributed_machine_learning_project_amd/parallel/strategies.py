@@ -49,17 +49,22 @@ def _root_arrays(be, inp):
             g("k", torch.int32))
 
 
-def _meta(comm, inp):
+def _meta(comm, inp, with_shared=False):
+    """Sizes, label range, kmax (engine.cpp:27-35) [+ whether the input is a node-shared
+    segment that every rank has mapped]."""
     if comm.is_root:
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
         lo = int(inp.labels.min()) if N else 0
         hi = int(inp.labels.max()) + 1 if N else 1
         kmax = max(1, int(inp.k.max())) if Q else 1
-        vals = [N, Q, A, lo, hi, kmax]
+        vals = [N, Q, A, lo, hi, kmax, int(bool(getattr(inp, "shared", False)))]
     else:
         vals = None
-    return comm.bcast_ints(vals, 6)
+    out = comm.bcast_ints(vals, 7)
+    if out[6] and not getattr(inp, "shared", False):
+        raise RuntimeError("rank 0 passed a node-shared input but this rank has none mapped")
+    return out if with_shared else out[:6]
 
 
 def _k_host(comm, k_dev_or_none, Q):
@@ -72,14 +77,19 @@ def _k_host(comm, k_dev_or_none, Q):
 # ============================================================================ farm (bench_4)
 def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, debug=False, **_):
     torch = _torch()
-    N, Q, A, lo, hi, kmax = _meta(comm, inp)
+    N, Q, A, lo, hi, kmax, shared = _meta(comm, inp, with_shared=True)
+    if shared and schedule == "static":
+        return _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug)
     with tr.phase("h2d"):
         X = lab = Qx = kd = None
-        if comm.is_root:
+        if shared:  # dynamic schedule over a node-shared segment: per-rank dataset H2D
+            X, lab = be.tensor(inp.X), be.tensor(inp.labels)
+        elif comm.is_root:
             X, lab, Qx, kd = _root_arrays(be, inp)
-    with tr.phase("bcast_data"):
-        X = comm.bcast(X, (N, A), torch.float64)
-        lab = comm.bcast(lab, (N,), torch.int32)
+    if not shared:
+        with tr.phase("bcast_data"):
+            X = comm.bcast(X, (N, A), torch.float64)
+            lab = comm.bcast(lab, (N,), torch.int32)
     if schedule == "static":
         counts, displs = block_partition(Q, comm.world)
         with tr.phase("scatter_queries"):
@@ -100,8 +110,11 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
         return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
     # dynamic: every rank holds all queries; chunks are claimed from an atomic counter
     with tr.phase("bcast_queries"):
-        Qx = comm.bcast(Qx, (Q, A), torch.float64)
-        kd, k_h = _k_host(comm, kd, Q)
+        if shared:  # claimed chunks are copied straight from the segment
+            k_h = np.array(inp.k)
+        else:
+            Qx = comm.bcast(Qx, (Q, A), torch.float64)
+            kd, k_h = _k_host(comm, kd, Q)
     nchunks = max(1, min(Q, comm.world * chunks_per_rank))
     csz = (Q + nchunks - 1) // nchunks
     out = torch.zeros((Q, 2), dtype=torch.int64, device=be.device)
@@ -116,7 +129,8 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
             a, b = c * csz, min(Q, (c + 1) * csz)
             if a >= b:
                 continue
-            d, i, lb, cs = be.knn(X, Qx[a:b], k_h[a:b], labels=lab, label_range=(lo, hi),
+            Qc = be.tensor(inp.Qx[a:b]) if shared else Qx[a:b]
+            d, i, lb, cs = be.knn(X, Qc, k_h[a:b], labels=lab, label_range=(lo, hi),
                                   kstride=kmax)
             out[a:b, 0] = lb.to(torch.int64)
             out[a:b, 1] = cs
@@ -135,22 +149,64 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
     return out[:, 0].to(torch.int32), out[:, 1].contiguous(), dbg_d, dbg_i
 
 
+def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
+    """Static farm over a node-shared input segment (utils/shm.py): every rank copies its own
+    query block (and the dataset) host->GPU over its own PCIe link — no funnel through GPU 0.
+    KNN_DATA_INGRESS=bcast instead H2Ds the dataset on rank 0 and broadcasts it over xGMI."""
+    import os
+    torch = _torch()
+    counts, displs = block_partition(Q, comm.world)
+    a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
+    bcast_data = os.environ.get("KNN_DATA_INGRESS", "h2d") == "bcast" and comm.world > 1
+    with tr.phase("h2d"):
+        X = lab = None
+        if not bcast_data or comm.is_root:
+            X = be.tensor(inp.X)
+            lab = be.tensor(inp.labels)
+        Ql = be.tensor(inp.Qx[a:b])
+        kl_h = np.array(inp.k[a:b])
+    if bcast_data:
+        with tr.phase("bcast_data"):
+            X = comm.bcast(X, (N, A), torch.float64)
+            lab = comm.bcast(lab, (N,), torch.int32)
+    with tr.phase("compute"):
+        d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
+    with tr.phase("gather"):
+        packed = torch.stack([lb.to(torch.int64), cs], dim=1)
+        allp = comm.gather_rows(packed, counts, (2,), torch.int64)
+        dd = ii = None
+        if debug:
+            dd = comm.gather_rows(d, counts, (kmax,), torch.float64)
+            ii = comm.gather_rows(i, counts, (kmax,), torch.int32)
+    if not comm.is_root:
+        return None
+    return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
+
+
 # ============================================================================ sharded data
 def _shard_local(comm, be, inp, tr):
     """Scatter the dataset in balanced blocks, broadcast queries, local top-k lists with
     global ids.  Returns (meta, root labels tensor, k_host, d, i)."""
     torch = _torch()
-    N, Q, A, lo, hi, kmax = _meta(comm, inp)
+    N, Q, A, lo, hi, kmax, shared = _meta(comm, inp, with_shared=True)
     counts, displs = block_partition(N, comm.world)
-    with tr.phase("h2d"):
-        X = lab = Qx = kd = None
-        if comm.is_root:
-            X, lab, Qx, kd = _root_arrays(be, inp)
-    with tr.phase("scatter_data"):
-        Xl = comm.scatter_rows(X, counts, (A,), torch.float64)
-    with tr.phase("bcast_queries"):
-        Qx = comm.bcast(Qx, (Q, A), torch.float64)
-        kd, k_h = _k_host(comm, kd, Q)
+    if shared:  # node-shared segment: each rank copies its own shard and the queries
+        with tr.phase("h2d"):
+            a = displs[comm.rank]
+            Xl = be.tensor(inp.X[a:a + counts[comm.rank]])
+            Qx = be.tensor(inp.Qx)
+            k_h = np.array(inp.k)
+            lab = be.tensor(inp.labels) if comm.is_root else None
+    else:
+        with tr.phase("h2d"):
+            X = lab = Qx = kd = None
+            if comm.is_root:
+                X, lab, Qx, kd = _root_arrays(be, inp)
+        with tr.phase("scatter_data"):
+            Xl = comm.scatter_rows(X, counts, (A,), torch.float64)
+        with tr.phase("bcast_queries"):
+            Qx = comm.bcast(Qx, (Q, A), torch.float64)
+            kd, k_h = _k_host(comm, kd, Q)
     with tr.phase("compute"):
         d, i, _, _ = be.knn(Xl, Qx, k_h, finalize=False, kstride=kmax)
         i = _offset_ids(i, displs[comm.rank])

@@ -1,0 +1,122 @@
+"""Node-shared input segment: the parsed workload placed in one /dev/shm mapping that every
+rank of the node maps, so each GPU pulls ITS part of the input over its own PCIe link.
+
+The reference harness parses stdin on rank 0 only (common.cpp:93-117) and every engine then
+pushes all data out of rank 0 (bench_4 @0xc199 broadcasts the dataset, @0xd64c hands out
+queries).  On one MI355X node the 8 GPUs hang off separate PCIe x16 links: funnelling every
+byte through GPU 0's link serialises 8x the H2D volume (≈300 MB at 8 GPUs for the bench),
+while per-rank copies from a node-shared page-locked segment run all 8 links concurrently
+("per-GPU H2D from shared pinned host memory").  Placing the parsed arrays
+in the segment is part of ingest (untimed, like parsing); every byte that moves host->GPU is
+still moved inside the timed KNN call.
+
+Layout: 64-byte header (magic, N, Q, A), then labels i32[N], k i32[Q], X f64[N*A],
+Qx f64[Q*A], each section 4096-byte aligned.
+"""
+from __future__ import annotations
+
+import os
+import uuid
+
+import numpy as np
+
+from .io import KNNInput
+
+_MAGIC = 0x444D4C50534D4831  # "DMLPSMH1"
+_ALIGN = 4096
+
+
+def _up(x):
+    return (x + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def _layout(N, Q, A):
+    off = {}
+    o = _ALIGN
+    for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A)):
+        off[name] = o
+        o += _up(max(nbytes, 1))
+    return off, o
+
+
+class SharedInput(KNNInput):
+    """KNNInput whose arrays are views of a node-shared mapping (same on every rank)."""
+    shared = True
+
+    def __init__(self, mm, path, N, Q, A, owner):
+        off, total = _layout(N, Q, A)
+        labels = np.frombuffer(mm, np.int32, N, off["labels"])
+        k = np.frombuffer(mm, np.int32, Q, off["k"])
+        X = np.frombuffer(mm, np.float64, N * A, off["X"]).reshape(N, A)
+        Qx = np.frombuffer(mm, np.float64, Q * A, off["Qx"]).reshape(Q, A)
+        super().__init__(labels, X, k, Qx)
+        self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
+        self._pinned = False
+
+    @staticmethod
+    def create(inp: KNNInput, directory: str = "/dev/shm") -> "SharedInput":
+        N, A = inp.X.shape
+        Q = inp.Qx.shape[0]
+        _, total = _layout(N, Q, A)
+        path = os.path.join(directory, f"dmlp_input_{os.getpid()}_{uuid.uuid4().hex[:8]}")
+        mm = np.memmap(path, np.uint8, "w+", shape=(total,))
+        np.frombuffer(mm, np.int64, 4, 0)[:] = [_MAGIC, N, Q, A]
+        s = SharedInput(mm, path, N, Q, A, owner=True)
+        s.labels[:] = inp.labels
+        s.k[:] = inp.k
+        s.X[:] = inp.X
+        s.Qx[:] = inp.Qx
+        mm.flush()
+        return s
+
+    @staticmethod
+    def attach(path: str) -> "SharedInput":
+        mm = np.memmap(path, np.uint8, "r+")
+        magic, N, Q, A = (int(v) for v in np.frombuffer(mm, np.int64, 4, 0))
+        if magic != _MAGIC:
+            raise ValueError(f"{path}: not a dmlp input segment")
+        return SharedInput(mm, path, N, Q, A, owner=False)
+
+    def pin(self) -> bool:
+        """Page-lock the mapping for DMA (GPU ranks).  Returns False if HIP refused it (copies
+        then fall back to staged pageable transfers; still correct)."""
+        if self._pinned:
+            return True
+        from .. import _lib
+        rc = _lib.lib().dmlp_host_register(self._mm.ctypes.data, self.nbytes)
+        self._pinned = rc == 0
+        return self._pinned
+
+    def unlink(self):
+        """Remove the name (mappings stay valid until closed): called once all ranks attached."""
+        if self.owner and os.path.exists(self.path):
+            os.unlink(self.path)
+
+    def close(self):
+        if self._pinned:
+            from .. import _lib
+            _lib.lib().dmlp_host_unregister(self._mm.ctypes.data)
+            self._pinned = False
+        self.unlink()
+
+
+def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedInput:
+    """Collective: rank 0 places `inp` in a node-shared segment, every rank maps it.  Single
+    node only (all ranks must see the same /dev/shm)."""
+    import torch.distributed as dist
+    path = None
+    s = None
+    if comm.is_root:
+        s = SharedInput.create(inp)
+        path = s.path
+    if comm.world > 1:
+        obj = [path]
+        dist.broadcast_object_list(obj, 0, device=comm.device if comm.on_gpu else None)
+        path = obj[0]
+        if not comm.is_root:
+            s = SharedInput.attach(path)
+        comm.barrier()
+    s.unlink()  # every rank holds a mapping: drop the name so nothing leaks in /dev/shm
+    if pin if pin is not None else comm.on_gpu:
+        s.pin()
+    return s

@@ -67,6 +67,21 @@ def test_dynamic_farm(workload):
     assert _run(path, 3, "farm", env_extra={"KNN_SCHEDULE": "dynamic"}) == expect
 
 
+@pytest.mark.parametrize("schedule", ["static", "dynamic"])
+def test_shared_ingress_farm(workload, schedule):
+    """Node-shared input segment (utils/shm.py): every rank copies its own query block."""
+    path, expect = workload
+    env = {"KNN_INGRESS": "shm", "KNN_SCHEDULE": schedule}
+    assert _run(path, 3, "farm", env_extra=env) == expect
+    assert _run(path, 1, "farm", env_extra=env) == expect
+
+
+def test_shared_ingress_other_strategies(workload):
+    path, expect = workload
+    for strategy in ("shard_reduce", "grid2d"):
+        assert _run(path, 2, strategy, env_extra={"KNN_INGRESS": "shm"}) == expect
+
+
 def test_edge_cases(tmp_path):
     """Duplicates (ties broken by larger id), shards smaller than k (D4), Q < P, k = N."""
     rng = np.random.default_rng(3)
