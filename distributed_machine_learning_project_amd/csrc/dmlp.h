@@ -69,6 +69,15 @@ int dmlp_fallback_topk(const double* X, int64_t N, int A, const double* Qx, cons
                        const int* qk, int nb, void* ws, int64_t ws_bytes, double* out_d,
                        int* out_i, int kstride, void* stream);
 
+// Same contract for k <= dmlp_fallback_select_kmax() (2048) by a per-row radix select over the
+// exact distance bits + an LDS bitonic sort of the survivors (rows with larger k are skipped;
+// callers send those to dmlp_fallback_topk).  Workspace: dmlp_fallback_select_bytes(nb, N).
+int dmlp_fallback_select_kmax(void);
+int64_t dmlp_fallback_select_bytes(int nb, int64_t N);
+int dmlp_fallback_select(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
+                         const int* qk, int nb, void* ws, int64_t ws_bytes, double* out_d,
+                         int* out_i, int kstride, void* stream);
+
 // ---------------------------------------------------------------- device: top-k merge (K4)
 // L sorted lists per query (list l of query q at in_*[l*list_stride + q*kin + j]), padded with
 // (+inf, -1).  Writes the merged top-k_q of every query q < nq to out_*[q*kout + i].

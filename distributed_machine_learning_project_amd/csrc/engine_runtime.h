@@ -328,16 +328,30 @@ struct LocalKnn {
     }
     if (!f.empty()) {
       std::sort(f.begin(), f.end());
-      const int rows = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)f.size(),
-                                                                   (1ll << 27) / std::max<int64_t>(1, N)));
-      const int64_t wsb = dmlp_fallback_bytes(rows, N);
-      char* ws = fb_ws.get(wsb);
+      // k <= 2048: radix select over exact rows; larger k: rows + segmented sort
+      std::vector<int> small, big;
+      const int ksel = dmlp_fallback_select_kmax();
+      for (int q : f) (kk[q] <= ksel ? small : big).push_back(q);
       int* qi = qidx_f.get(f.size());
-      HIPCHK(hipMemcpyAsync(qi, f.data(), f.size() * sizeof(int), hipMemcpyHostToDevice, st));
-      for (size_t c0 = 0; c0 < f.size(); c0 += rows) {
-        const int nb = (int)std::min<size_t>(rows, f.size() - c0);
-        DMLPCHK(dmlp_fallback_topk(X, N, A, Qx, qi + c0, kd, nb, ws, wsb, out_d, out_i, kstride,
-                                   st));
+      size_t base = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<int>& v = pass == 0 ? small : big;
+        if (v.empty()) continue;
+        HIPCHK(hipMemcpyAsync(qi + base, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        const int rows = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)v.size(),
+                                                                     (1ll << 27) / std::max<int64_t>(1, N)));
+        const int64_t wsb = pass == 0 ? dmlp_fallback_select_bytes(rows, N) : dmlp_fallback_bytes(rows, N);
+        char* ws = fb_ws.get(wsb);
+        for (size_t c0 = 0; c0 < v.size(); c0 += rows) {
+          const int nb = (int)std::min<size_t>(rows, v.size() - c0);
+          if (pass == 0)
+            DMLPCHK(dmlp_fallback_select(X, N, A, Qx, qi + base + c0, kd, nb, ws, wsb, out_d, out_i,
+                                         kstride, st));
+          else
+            DMLPCHK(dmlp_fallback_topk(X, N, A, Qx, qi + base + c0, kd, nb, ws, wsb, out_d, out_i,
+                                       kstride, st));
+        }
+        base += v.size();
       }
       rest.insert(rest.end(), f.begin(), f.end());
     }

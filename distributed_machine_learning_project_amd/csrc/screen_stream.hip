@@ -226,18 +226,19 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
         if (lane == 0) { atomicAdd(&g_stream_dbg[1], 1ull);                                     \
                          atomicAdd(&g_stream_dbg[2], (unsigned long long)np_); }                \
       }                                                                                         \
+      /* branch-free appends: every lane writes each value to its next free slot and only  \
+         advances the slot on a hit (slots cnt..cnt+3 <= SUB-1 exist; a miss is overwritten  \
+         later and never read).  Per-lane branches here cost a taken s_cbranch each. */      \
       bool trig_ = false;                                                                       \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
-        if (m_[ct] >= h[ct]) {                                                                  \
-          i32x2* mys_ = sub_ptr(ct * 16 + c, kg);                                               \
-          _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                       \
-            if (acc[AB][ct][j] >= h[ct]) {                                                      \
-              mys_[cnt[ct]] = (i32x2){__float_as_int(acc[AB][ct][j]), idbase_ + j};             \
-              ++cnt[ct];                                                                        \
-            }                                                                                   \
-          }                                                                                     \
-          trig_ |= cnt[ct] > SUB - 4;                                                           \
+        i32x2* mys_ = sub_ptr(ct * 16 + c, kg);                                                 \
+        int cn_ = cnt[ct];                                                                      \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                         \
+          mys_[cn_] = (i32x2){__float_as_int(acc[AB][ct][j]), idbase_ + j};                     \
+          cn_ += acc[AB][ct][j] >= h[ct] ? 1 : 0;                                               \
         }                                                                                       \
+        cnt[ct] = cn_;                                                                          \
+        trig_ |= cn_ > SUB - 4;                                                                 \
       }                                                                                         \
       if (__ballot(trig_)) compact_pending();                                                   \
     }                                                                                           \

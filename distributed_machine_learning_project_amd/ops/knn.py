@@ -302,23 +302,31 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
 
 
 def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d, out_i):
-    """Native exact path (fallback.hip): exact rows in descending-id order + stable segmented
-    radix sort, in chunks of rows that keep nb*N < 2^27 (and the workspace bounded)."""
+    """Native exact path (fallback.hip) in row chunks that keep nb*N < 2^27: k <= 2048 by a
+    per-row radix select over the exact distance bits (+ LDS bitonic sort of the survivors);
+    larger k by exact rows in descending-id order + a stable segmented radix sort."""
     torch = _torch()
     L = _lib.lib()
     N, A = ds.N, ds.A
     dev = Qx.device
     s = _stream()
     kdev = torch.from_numpy(np.ascontiguousarray(kk, np.int32)).to(dev, non_blocking=True)
-    rows = max(1, min(len(fb), (1 << 27) // max(1, N)))
-    ws_bytes = L.dmlp_fallback_bytes(rows, N)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    for c0 in range(0, len(fb), rows):
-        sub = fb[c0:c0 + rows]
-        qidx = torch.from_numpy(sub.astype(np.int32)).to(dev, non_blocking=True)
-        _lib.check(L.dmlp_fallback_topk(_p(ds.X), N, A, _p(Qx), _p(qidx), _p(kdev), len(sub),
-                                        _p(ws), ws_bytes, _p(out_d), _p(out_i), out_d.shape[1],
-                                        s), "fallback_topk")
+    ksel = L.dmlp_fallback_select_kmax()
+    small = fb[kk[fb] <= ksel]
+    big = fb[kk[fb] > ksel]
+    for rows_idx, sel in ((small, True), (big, False)):
+        if len(rows_idx) == 0:
+            continue
+        rows = max(1, min(len(rows_idx), (1 << 27) // max(1, N)))
+        ws_bytes = L.dmlp_fallback_select_bytes(rows, N) if sel else L.dmlp_fallback_bytes(rows, N)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        fn = L.dmlp_fallback_select if sel else L.dmlp_fallback_topk
+        for c0 in range(0, len(rows_idx), rows):
+            sub = rows_idx[c0:c0 + rows]
+            qidx = torch.from_numpy(sub.astype(np.int32)).to(dev, non_blocking=True)
+            _lib.check(fn(_p(ds.X), N, A, _p(Qx), _p(qidx), _p(kdev), len(sub), _p(ws), ws_bytes,
+                          _p(out_d), _p(out_i), out_d.shape[1], s),
+                       "fallback_select" if sel else "fallback_topk")
 
 
 def merge_gpu(lists_d, lists_i, k_dev, kout: int):

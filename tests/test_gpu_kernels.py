@@ -66,6 +66,33 @@ def test_large_k_fallback(torch_cuda):
     assert_same(r, refs)
 
 
+def test_select_and_sort_fallback_paths(torch_cuda):
+    """k <= 2048 -> radix-select path, k > 2048 -> segmented-sort path; duplicate-heavy data so
+    the k-th distance is tied across the selection boundary."""
+    rng = np.random.default_rng(11)
+    base = np.round(rng.uniform(0, 3, size=(300, 5)), 1)
+    X = base[rng.integers(0, 300, size=6000)]
+    labels = rng.integers(0, 6, size=6000).astype(np.int32)
+    Qx = np.round(rng.uniform(0, 3, size=(60, 5)), 1)
+    k = np.concatenate([rng.integers(129, 2049, 40), rng.integers(2049, 6001, 20)]).astype(np.int32)
+    inp = dmlp.KNNInput(labels, np.ascontiguousarray(X), k, Qx)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 60
+    assert_same(r, refs)
+
+
+def test_select_tie_overflow(torch_cuda):
+    """Every distance equal: the select keeps the LARGEST ids among the ties (id desc order)."""
+    X = np.full((7000, 3), 2.0)
+    X[::97] = 5.0  # a few farther points
+    labels = (np.arange(7000) % 4).astype(np.int32)
+    Qx = np.zeros((9, 3))
+    k = np.array([129, 500, 1000, 2048, 2047, 3000, 6900, 7000, 1500], np.int32)
+    inp = dmlp.KNNInput(labels, X, k, Qx)
+    r, refs = run_both(torch_cuda, inp)
+    assert_same(r, refs)
+
+
 def test_k_zero_and_k_gt_n(torch_cuda):
     inp = dmlp.generate(50, 20, 8, 0.0, 10.0, 1, 10, 3, seed=5)
     inp.k[:5] = 0
