@@ -32,7 +32,8 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unus
 
 def _sources():
     hip = sorted(CSRC.glob("*.hip"))
-    cpp = sorted(p for p in CSRC.glob("*.cpp") if not p.name.startswith("engine_"))
+    cpp = sorted(p for p in CSRC.glob("*.cpp")
+                 if not p.name.startswith(("engine_", "dropin_")))
     return hip, cpp
 
 
@@ -121,6 +122,31 @@ def build_engine(force: bool = False) -> Path | None:
     return ENGINE
 
 
+def _engine_link_flags():
+    mpidir = PKG / "mpi_runtime"
+    return [f"-L{PKG}", "-ldmlp", f"-Wl,-rpath,{PKG}", str(mpidir / "libmpi.so.12"),
+            f"-Wl,-rpath,{mpidir}", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib",
+            "-pthread"]
+
+
+def build_dropin(common_cpp: str, out: str | None = None, debug: bool = False,
+                 extra_flags=()) -> Path:
+    """Link the reference's own harness (its unmodified common.cpp, next to its common.h)
+    with include/engine.h + dropin_engine.cpp into a reference-compatible `engine` binary
+    (Makefile:10-15 equivalent; debug=True is the engine.debug target)."""
+    build(engine=True)  # libdmlp + the MPI runtime links
+    common_cpp = Path(common_cpp).resolve()
+    out = Path(out or (common_cpp.parent / ("engine.debug" if debug else "engine"))).resolve()
+    flags = ["-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
+             f"-I{PKG / 'include'}", f"-I{common_cpp.parent}", f"-I{CSRC}", f"-I{MPI_HOME}/include",
+             f"-I{ROCM}/include", *extra_flags]
+    if debug:
+        flags += ["-g", "-DDEBUG"]
+    _run(["g++", *flags, str(common_cpp), str(CSRC / "dropin_engine.cpp"), "-o", str(out),
+          *_engine_link_flags()])
+    return out
+
+
 def build(force: bool = False, engine: bool = True) -> Path:
     if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
@@ -134,9 +160,15 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-engine", action="store_true")
+    ap.add_argument("--dropin", metavar="COMMON_CPP",
+                    help="build a reference-compatible engine from the reference's common.cpp")
+    ap.add_argument("--dropin-out", default=None)
+    ap.add_argument("--dropin-debug", action="store_true", help="engine.debug (-DDEBUG)")
     a = ap.parse_args(argv)
     p = build(force=a.force, engine=not a.no_engine)
     print(f"built {p}")
+    if a.dropin:
+        print(f"built {build_dropin(a.dropin, a.dropin_out, a.dropin_debug)}")
 
 
 if __name__ == "__main__":

@@ -20,15 +20,6 @@
 
 #include "dmlp.h"
 
-extern "C" {
-int dmlp_screen_waves(int KT, int cap);
-int dmlp_screen_stream_qw(int KT);
-int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_tiles,
-                       const void* qhi, const void* qlo, const float* qn, const int* qidx,
-                       const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
-                       float eps_rel, int S, int* cand_ids, int* cand_cnt, void* stream);
-}
-
 namespace dmlp_rt {
 
 #define HIPCHK(x)                                                                            \
@@ -305,7 +296,7 @@ struct LocalKnn {
         int* qi = (cls == 0 ? qidx_a : qidx_b).get(nq);
         HIPCHK(hipMemcpyAsync(qi, idx.data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
         const bool streaming = cls == 0 && qw > 0;
-        const int cap = streaming ? 64 : (cls == 0 ? 128 : 256);
+        const int cap = streaming ? dmlp_screen_stream_cap() : (cls == 0 ? 128 : 256);
         const int S = streaming ? slices_stream(nq, qw, nt)
                                 : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);

@@ -27,11 +27,14 @@ namespace {
 
 int g_stream_mode = 0;  // profiling ablations (bit 0 no candidates, 1 no MFMA, 2 no streaming,
                         // 3 event counters into g_stream_dbg)
+int g_stream_groups = 1;  // 1: append 4-row groups (one entry per column tile and step)
 __device__ unsigned long long g_stream_dbg[8];
 
-template <int KT, int CT, int SUB>
+template <int KT, int CT, int SUB, bool G>
 struct StreamCfg {
-  static constexpr int CAP = 4 * SUB;             // candidates per (query, slice)
+  static constexpr int CAP = 4 * SUB;             // buffered entries per (query, slice)
+  static constexpr int APPEND = G ? 1 : 4;        // entries a lane appends per column and step
+  static constexpr int IDCAP = G ? 4 * CAP : CAP; // candidate ids written per (query, slice)
   static constexpr int QW = 16 * CT;              // queries per wave / workgroup
   static constexpr int NCOL = QW;
   static constexpr int FRAGS = 4 * KT * 2;        // 1 KiB fragments per 64-point tile
@@ -41,7 +44,7 @@ struct StreamCfg {
   static_assert(CAP <= 64, "one buffered entry per lane in compaction");
 };
 
-template <int KT, int CT, int SUB, int mode>
+template <int KT, int CT, int SUB, int mode, bool G>
 __global__ __launch_bounds__(64, 1) void k_screen_stream(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles,
     const bf16x8* __restrict__ qhi, const bf16x8* __restrict__ qlo, const float* __restrict__ qn,
@@ -49,8 +52,9 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     const unsigned* __restrict__ xnmax_bits, const unsigned* __restrict__ bad, float eps_rel,
     int S, int tiles_per_slice, int n_qblocks, int* __restrict__ cand_ids,
     int* __restrict__ cand_cnt) {
-  using C = StreamCfg<KT, CT, SUB>;
+  using C = StreamCfg<KT, CT, SUB, G>;
   constexpr int CAP = C::CAP;
+  constexpr int APPEND = C::APPEND;
   constexpr int D = C::D;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   i32x2* const sbuf = (i32x2*)smem;                               // sub-buffers
@@ -128,7 +132,7 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     unsigned long long pend = 0;  // bit col
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const unsigned long long bm = __ballot(cnt[ct] > SUB - 4);
+      const unsigned long long bm = __ballot(cnt[ct] > SUB - APPEND);
       pend |= ((bm | (bm >> 16) | (bm >> 32) | (bm >> 48)) & 0xffffull) << (16 * ct);
     }
     if ((mode & 8) && lane == 0) atomicAdd(&g_stream_dbg[3], (unsigned long long)__popcll(pend));
@@ -144,9 +148,22 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
       if (ntot >= kc) {
         const unsigned bits = (unsigned)e.x;
         const unsigned u = ok ? (bits ^ ((bits >> 31) ? 0xffffffffu : 0x80000000u)) : 0u;
-        unsigned T = 0;
+        // the k-th largest key lies in [min, max] of the buffered keys: start below their
+        // common prefix (scores of one column share their leading bits, so this skips most
+        // of the 20 ballot rounds)
+        unsigned umx = u, umn = ok ? u : 0xffffffffu;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          umx = max(umx, (unsigned)__shfl_xor((int)umx, o));
+          umn = min(umn, (unsigned)__shfl_xor((int)umn, o));
+        }
+        const unsigned dif = umx ^ umn;
+        const int top = dif ? 31 - __clz((int)dif) : -1;
+        unsigned T = umx;  // top < 0: every buffered key is equal
+        if (top >= 31) T = 0u;
+        else if (top >= 0) T = umx & ~((2u << top) - 1u);
 #pragma unroll 1
-        for (int bit = 31; bit >= 12; --bit) {  // low bits left 0: T <= exact k-th key
+        for (int bit = top; bit >= 12; --bit) {  // low bits left 0: T <= exact k-th key
           const unsigned cand = T | (1u << bit);
           if (__popcll(__ballot(u >= cand)) >= kc) T = cand;
         }
@@ -161,8 +178,9 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
         const int pos = __popcll(km & dmlp::lanemask_lt());
         sub_ptr(col, pos & 3)[pos >> 2] = e;
       }
-      if (lane < 4) lcnt[col * 4 + lane] = kept > 4 * (SUB - 4) ? -(1 << 28) : (kept + 3 - lane) >> 2;
-      if (lane == 0) lh[col] = kept > 4 * (SUB - 4) ? INFINITY : hc;  // overflow: exact path
+      if (lane < 4)
+        lcnt[col * 4 + lane] = kept > 4 * (SUB - APPEND) ? -(1 << 28) : (kept + 3 - lane) >> 2;
+      if (lane == 0) lh[col] = kept > 4 * (SUB - APPEND) ? INFINITY : hc;  // overflow: exact path
       dmlp::wave_sync();
     }
 #pragma unroll
@@ -233,12 +251,19 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
         i32x2* mys_ = sub_ptr(ct * 16 + c, kg);                                                 \
         int cn_ = cnt[ct];                                                                      \
-        _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                         \
-          mys_[cn_] = (i32x2){__float_as_int(acc[AB][ct][j]), idbase_ + j};                     \
-          cn_ += acc[AB][ct][j] >= h[ct] ? 1 : 0;                                               \
+        if (G) {                                                                                \
+          /* one entry per lane, column and step: the 4-row group (ids idbase..idbase+3)     \
+             scored by its max; the k-th largest group max is still a lower bound on a_k */   \
+          mys_[cn_] = (i32x2){__float_as_int(m_[ct]), idbase_};                                 \
+          cn_ += m_[ct] >= h[ct] ? 1 : 0;                                                       \
+        } else {                                                                                \
+          _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                       \
+            mys_[cn_] = (i32x2){__float_as_int(acc[AB][ct][j]), idbase_ + j};                   \
+            cn_ += acc[AB][ct][j] >= h[ct] ? 1 : 0;                                             \
+          }                                                                                     \
         }                                                                                       \
         cnt[ct] = cn_;                                                                          \
-        trig_ |= cn_ > SUB - 4;                                                                 \
+        trig_ |= cn_ > SUB - APPEND;                                                            \
       }                                                                                         \
       if (__ballot(trig_)) compact_pending();                                                   \
     }                                                                                           \
@@ -273,7 +298,7 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
   for (int col = 0; col < C::NCOL; ++col) {
     const int pp = pbase + col;
     if (pp >= nq) break;
-    int* out = cand_ids + ((int64_t)pp * S + s) * CAP;
+    int* out = cand_ids + ((int64_t)pp * S + s) * C::IDCAP;
     if (lcnt[col * 4] < 0) {
       if (lane == 0) cand_cnt[(int64_t)pp * S + s] = -1;
       continue;
@@ -283,18 +308,32 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     const i32x2 e = ok ? sub_ptr(col, kg)[c] : (i32x2){0, -1};
     const float hc = lh[col];
     const bool keep = ok && __int_as_float(e.x) >= hc;
-    const unsigned long long m = __ballot(keep);
-    if (keep) out[__popcll(m & dmlp::lanemask_lt())] = e.y;
-    if (lane == 0) cand_cnt[(int64_t)pp * S + s] = __popcll(m);
+    if (G) {
+      // expand kept groups to their member ids; padding members (xinit = -inf) are dropped
+      const float* xinit = (const float*)xinit4;
+      int nout = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool v = keep && xinit[e.y + j] != -INFINITY;
+        const unsigned long long mj = __ballot(v);
+        if (v) out[nout + __popcll(mj & dmlp::lanemask_lt())] = e.y + j;
+        nout += __popcll(mj);
+      }
+      if (lane == 0) cand_cnt[(int64_t)pp * S + s] = nout;
+    } else {
+      const unsigned long long m = __ballot(keep);
+      if (keep) out[__popcll(m & dmlp::lanemask_lt())] = e.y;
+      if (lane == 0) cand_cnt[(int64_t)pp * S + s] = __popcll(m);
+    }
   }
 }
 
-template <int KT, int CT, int SUB>
+template <int KT, int CT, int SUB, bool G>
 int launch_stream(const void* xfrag, const float* xinit, int64_t n_tiles, const void* qhi,
                   const void* qlo, const float* qn, const int* qidx, const int* qk, int nq,
                   const unsigned* xnmax, const unsigned* bad, float eps_rel, int S,
                   int* cand_ids, int* cand_cnt, hipStream_t stream) {
-  using C = StreamCfg<KT, CT, SUB>;
+  using C = StreamCfg<KT, CT, SUB, G>;
   const int n_qblocks = (nq + C::QW - 1) / C::QW;
   const int tps = (int)((n_tiles + S - 1) / S);
   const int64_t grid = (int64_t)n_qblocks * S;
@@ -302,7 +341,7 @@ int launch_stream(const void* xfrag, const float* xinit, int64_t n_tiles, const 
   // the ablation mode is a template parameter: a runtime branch in the hot loop made hipcc
   // hoist the ablation's register copies and drain vmcnt every iteration
 #define DMLP_STREAM_LAUNCH(M)                                                                  \
-  hipLaunchKernelGGL((k_screen_stream<KT, CT, SUB, M>), dim3((unsigned)grid), dim3(64), C::LDS, \
+  hipLaunchKernelGGL((k_screen_stream<KT, CT, SUB, M, G>), dim3((unsigned)grid), dim3(64), C::LDS, \
                      stream, (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles,           \
                      (const bf16x8*)qhi, (const bf16x8*)qlo, qn, qidx, qk, nq, xnmax, bad,     \
                      eps_rel, S, tps, n_qblocks, cand_ids, cand_cnt)
@@ -321,12 +360,14 @@ int launch_stream(const void* xfrag, const float* xinit, int64_t n_tiles, const 
 
 }  // namespace
 
-// Streaming screen for k <= 32 (cap 64) and A <= 64 (KT <= 2); 64 queries per workgroup.
+// Streaming screen for k <= 32 and A <= 64 (KT <= 2); 64 queries per workgroup.  Candidate
+// ids per (query, slice): dmlp_screen_stream_cap() (256 in group mode, 64 per-point).
 extern "C" int dmlp_screen_stream_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
-extern "C" int dmlp_screen_stream_cap(void) { return 64; }
+extern "C" int dmlp_screen_stream_cap(void) { return g_stream_groups ? 256 : 64; }
 extern "C" int dmlp_screen_stream_kmax(void) { return 32; }
 
 extern "C" void dmlp_set_stream_mode(int mode) { g_stream_mode = mode; }
+extern "C" void dmlp_set_stream_groups(int on) { g_stream_groups = on ? 1 : 0; }
 
 extern "C" int dmlp_stream_debug_counters(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stream_dbg), sizeof(g_stream_dbg));
@@ -347,11 +388,14 @@ extern "C" int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit,
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
   hipStream_t st = (hipStream_t)stream;
-  if (KT == 1)
-    return launch_stream<1, 4, 16>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, xnmax_bits,
-                                   bad, eps_rel, S, cand_ids, cand_cnt, st);
-  if (KT == 2)
-    return launch_stream<2, 4, 16>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, xnmax_bits,
-                                   bad, eps_rel, S, cand_ids, cand_cnt, st);
+#define DMLP_STREAM_KT(KTV)                                                                    \
+  return g_stream_groups                                                                       \
+             ? launch_stream<KTV, 4, 16, true>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, \
+                                               xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st) \
+             : launch_stream<KTV, 4, 16, false>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, \
+                                                xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st)
+  if (KT == 1) { DMLP_STREAM_KT(1); }
+  if (KT == 2) { DMLP_STREAM_KT(2); }
+#undef DMLP_STREAM_KT
   return -2;
 }

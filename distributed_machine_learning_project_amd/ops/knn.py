@@ -232,6 +232,7 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
     N = ds.N
     kk = np.minimum(k_host, N)  # k > N: pad with (+inf,-1) like bench_2's sentinel
 
+    _apply_env_switches(L)
     use_screen = ds.screen_ok and not exact and Q > 0
     cls_a = np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if use_screen else np.empty(0, np.int64)
     cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
@@ -252,12 +253,12 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
         er = eps_rel(A)
         # k <= 32 and A <= 64: barrier-free streaming kernel (cap 64); otherwise LDS-shared kernel
         stream_qw = L.dmlp_screen_stream_qw(KT) if SCREEN_IMPL != "lds" else 0
-        for idx, cap in ((cls_a, 64 if stream_qw else 128), (cls_b, 256)):
+        for idx, streaming in ((cls_a, bool(stream_qw)), (cls_b, False)):
             nq = len(idx)
             if nq == 0:
                 continue
+            cap = L.dmlp_screen_stream_cap() if streaming else (128 if idx is cls_a else 256)
             qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
-            streaming = cap == 64
             if streaming:
                 S = _choose_slices_stream(nq, stream_qw, ds.n_tiles)
             else:
@@ -299,6 +300,17 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
                                        _p(ds.labels), ds.label_lo, ds.label_hi, _p(lab), _p(cs),
                                        s), "finalize")
     return DeviceResult(out_d, out_i, lab, cs, k_host, int(len(fb)))
+
+
+_ENV_APPLIED = [False]
+
+
+def _apply_env_switches(L):
+    """DMLP_STREAM_GROUPS=0 switches the streaming screen to per-point appends (A/B only)."""
+    if not _ENV_APPLIED[0]:
+        if os.environ.get("DMLP_STREAM_GROUPS", "1") == "0":
+            L.dmlp_set_stream_groups(0)
+        _ENV_APPLIED[0] = True
 
 
 def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d, out_i):

@@ -93,3 +93,54 @@ def test_gpu_strategies_match_oracle(tmp_path, strategy):
     assert out == dmlp.format_report(cs)
     out, _ = _run(["--strategy", strategy, "--exact"], path)
     assert out == dmlp.format_report(cs)
+
+
+# ---------------------------------------------------------------- include/engine.h drop-in
+NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+
+
+def _dropin(tmp_path, debug=False):
+    try:
+        return str(build.build_dropin(os.path.join(NATIVE, "mini_harness.cpp"),
+                                      str(tmp_path / ("engine.debug" if debug else "engine")),
+                                      debug=debug,
+                                      extra_flags=['-DDMLP_COMMON_HEADER="contract_types.h"']))
+    except RuntimeError as e:
+        pytest.skip(f"drop-in build unavailable: {e}")
+
+
+def _run_dropin(exe, path, env, np_=1):
+    cmd = ([MPIEXEC, "-n", str(np_)] if np_ > 1 else []) + [exe]
+    e = dict(os.environ)
+    e.update(env)
+    with open(path, "rb") as f:
+        r = subprocess.run(cmd, stdin=f, capture_output=True, timeout=180, env=e)
+    assert r.returncode == 0, r.stderr.decode()
+    assert b"Time taken: " in r.stderr
+    return r.stdout
+
+
+def test_dropin_engine_h_cpu(tmp_path):
+    """engine.h + dropin_engine.cpp driven by a harness with the reference's contract."""
+    path, inp, res, lab, cs = _case(tmp_path, N=900, Q=70)
+    exe = _dropin(tmp_path)
+    assert _run_dropin(exe, path, {"KNN_DEVICE": "cpu"}) == dmlp.format_report(cs)
+    if os.path.exists(MPIEXEC):
+        assert _run_dropin(exe, path, {"KNN_DEVICE": "cpu"}, np_=2) == dmlp.format_report(cs)
+
+
+def test_dropin_engine_h_debug_cpu(tmp_path):
+    path, inp, res, lab, cs = _case(tmp_path, N=200, Q=9, kmax=7)
+    out = _run_dropin(_dropin(tmp_path, debug=True), path, {"KNN_DEVICE": "cpu"})
+    lines = out.decode().splitlines()
+    assert lines[0] == f"Label for Query 0 : {lab[0]}"
+    assert lines[1] == f"Top-{inp.k[0]} neighbors:"
+    assert lines[2].split(" : ")[0] == str(res[0][1][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["farm", "shard_reduce"])
+def test_dropin_engine_h_gpu(tmp_path, strategy):
+    path, inp, res, lab, cs = _case(tmp_path, N=5000, Q=400, A=12, kmax=150)
+    out = _run_dropin(_dropin(tmp_path), path, {"KNN_STRATEGY": strategy})
+    assert out == dmlp.format_report(cs)
