@@ -188,6 +188,10 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
       cnt[ct] = lcnt[(ct * 16 + c) * 4 + kg];
       h[ct] = lh[ct * 16 + c];
     }
+    // resolve these LDS loads here: otherwise the waitcnt pass sees h / cnt possibly pending
+    // at the merge after `if (trig) compact_pending()` and makes EVERY following step wait
+    // for all outstanding LDS traffic (i.e. the previous step's appends)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
   };
 
   // ---- D-deep register ring of step fragments + double-buffered accumulators

@@ -365,16 +365,40 @@ def finalize_gpu(ds_labels, label_range, dist, ids, k_dev):
     return lab, cs
 
 
-def format_report_gpu(cs, qid_base: int = 0) -> bytes:
-    """Render "Query <id> checksum: <u64>\\n" lines on the GPU; returns the bytes on the host."""
+def format_report_dev(cs, qid_base: int = 0):
+    """Render "Query <id> checksum: <u64>\\n" lines on the GPU.  Returns (device uint8 tensor,
+    byte count); one host sync for the count."""
     torch = _torch()
     L = _lib.lib()
     cs = cs.contiguous()
     nq = cs.numel()
     if nq == 0:
-        return b""
+        return torch.empty(0, dtype=torch.uint8, device=cs.device), 0
     off = torch.empty(L.dmlp_format_scratch(nq), dtype=torch.int64, device=cs.device)
     out = torch.empty(L.dmlp_format_bound(nq), dtype=torch.uint8, device=cs.device)
     _lib.check(L.dmlp_format_report(_p(cs), nq, qid_base, _p(off), _p(out), _stream()), "format")
-    n = int(off[nq].item())
-    return out[:n].cpu().numpy().tobytes()
+    return out, int(off[nq].item())
+
+
+_PINNED = {}
+
+
+def _pinned_bytes(n: int):
+    """Grow-only page-locked host staging buffer (D2H at DMA rate, no per-call pinning)."""
+    torch = _torch()
+    buf = _PINNED.get("report")
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8).pin_memory()
+        _PINNED["report"] = buf
+    return buf
+
+
+def format_report_gpu(cs, qid_base: int = 0):
+    """Report bytes on the host: GPU formatter + one D2H into a pinned staging buffer.
+    Returns a read-only memoryview valid until the next call (write it out or copy it)."""
+    dev_text, n = format_report_dev(cs, qid_base)
+    if n == 0:
+        return memoryview(b"")
+    host = _pinned_bytes(n)
+    host[:n].copy_(dev_text[:n])
+    return memoryview(host.numpy())[:n].toreadonly()

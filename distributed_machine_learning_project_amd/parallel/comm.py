@@ -151,6 +151,19 @@ class Comm:
         dist.broadcast(t, 0)
         return [int(x) for x in t.cpu().tolist()]
 
+    def allgather_ints(self, vals):
+        """Every rank's small int vector, concatenated in rank order (host list)."""
+        torch = _torch()
+        if self.world == 1:
+            return [list(vals)]
+        import torch.distributed as dist
+        t = torch.tensor(list(vals), dtype=torch.int64, device=self.device)
+        out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.device)
+        dist.all_gather_into_tensor(out, t)
+        flat = [int(x) for x in out.cpu().tolist()]
+        n = t.numel()
+        return [flat[r * n:(r + 1) * n] for r in range(self.world)]
+
     def bcast(self, t, shape, dtype):
         """Broadcast a tensor from rank 0 (allocated on the other ranks)."""
         torch = _torch()

@@ -31,6 +31,7 @@ class KNNOutput:
     dist: "object"       # torch f64 [Q, kmax] or None (debug)
     ids: "object"        # torch int32 [Q, kmax] or None (debug)
     k: np.ndarray
+    text: "object" = None  # report bytes already rendered on the host (node-shared egress)
 
     def labels_np(self):
         return self.label.cpu().numpy().astype(np.int32)
@@ -88,17 +89,21 @@ class Engine:
         self.calls += 1
         if res is None:
             return None
-        lb, cs, d, i = res
-        return KNNOutput(lb, cs, d, i, np.asarray(inp.k))
+        lb, cs, d, i = res[:4]
+        return KNNOutput(lb, cs, d, i, np.asarray(inp.k), res[4] if len(res) > 4 else None)
 
-    def report(self, out: KNNOutput) -> bytes:
-        """stdout bytes of the reference harness (reportResult, common.cpp:57-79)."""
+    def report(self, out: KNNOutput):
+        """stdout bytes of the reference harness (reportResult, common.cpp:57-79), as a
+        bytes-like object (a view into a reused host buffer: write it out before the next
+        KNN/report call, or copy it with bytes())."""
         if self.debug:
             d = out.dist.cpu().numpy() if out.dist is not None else None
             i = out.ids.cpu().numpy() if out.ids is not None else None
             if d is None:
                 raise RuntimeError("debug report needs an Engine(debug=True)")
             return format_debug(d, i, out.k, out.labels_np())
+        if out.text is not None:
+            return out.text
         cs = out.checksum
         if cs.device.type != self.comm.device.type:
             cs = cs.to(self.comm.device)

@@ -171,6 +171,10 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             lab = comm.bcast(lab, (N,), torch.int32)
     with tr.phase("compute"):
         d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
+    text = None
+    if not debug:
+        with tr.phase("report"):
+            text = _shared_egress(comm, be, inp, cs, a)
     with tr.phase("gather"):
         packed = torch.stack([lb.to(torch.int64), cs], dim=1)
         allp = comm.gather_rows(packed, counts, (2,), torch.int64)
@@ -180,7 +184,31 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             ii = comm.gather_rows(i, counts, (kmax,), torch.int32)
     if not comm.is_root:
         return None
-    return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
+    return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii, text
+
+
+def _shared_egress(comm, be, inp, cs, qid_base):
+    """Every rank renders its block's report lines and copies them straight into the shared
+    segment's output region at its byte offset; rank 0 gets a view of the whole report."""
+    torch = _torch()
+    if be.on_gpu:
+        from ..ops import knn as K
+        dev_text, n = K.format_report_dev(cs, qid_base)
+    else:
+        from ..utils.io import format_report
+        host = format_report(cs.numpy().view(np.uint64), qid_base)
+        n = len(host)
+    lens = [v[0] for v in comm.allgather_ints([n])]
+    off = sum(lens[:comm.rank])
+    if n:
+        dst = torch.from_numpy(inp.out[off:off + n])
+        if be.on_gpu:
+            dst.copy_(dev_text[:n])  # D2H into the page-locked segment
+            torch.cuda.current_stream().synchronize()
+        else:
+            dst.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
+    comm.barrier()
+    return memoryview(inp.out)[:sum(lens)].toreadonly() if comm.is_root else None
 
 
 # ============================================================================ sharded data

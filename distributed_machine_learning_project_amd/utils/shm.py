@@ -10,8 +10,12 @@ while per-rank copies from a node-shared page-locked segment run all 8 links con
 in the segment is part of ingest (untimed, like parsing); every byte that moves host->GPU is
 still moved inside the timed KNN call.
 
+Egress is symmetric: with the static farm each rank renders the report lines of its own query
+block on its GPU and copies them over its own PCIe link into the segment's output region at its
+byte offset, so rank 0 ends up holding the whole report in host memory without a funnel.
+
 Layout: 64-byte header (magic, N, Q, A), then labels i32[N], k i32[Q], X f64[N*A],
-Qx f64[Q*A], each section 4096-byte aligned.
+Qx f64[Q*A], out u8[48*Q + 64] (report text), each section 4096-byte aligned.
 """
 from __future__ import annotations
 
@@ -33,7 +37,8 @@ def _up(x):
 def _layout(N, Q, A):
     off = {}
     o = _ALIGN
-    for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A)):
+    for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A),
+                         ("out", 48 * Q + 64)):
         off[name] = o
         o += _up(max(nbytes, 1))
     return off, o
@@ -50,6 +55,7 @@ class SharedInput(KNNInput):
         X = np.frombuffer(mm, np.float64, N * A, off["X"]).reshape(N, A)
         Qx = np.frombuffer(mm, np.float64, Q * A, off["Qx"]).reshape(Q, A)
         super().__init__(labels, X, k, Qx)
+        self.out = np.frombuffer(mm, np.uint8, 48 * Q + 64, off["out"])
         self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
         self._pinned = False
 

@@ -27,7 +27,7 @@ def main():
     Qx = torch.from_numpy(inp.Qx).cuda()
     ds = K.prepare_dataset(X, lab, (0, 10))
     r = K.knn_gpu(ds, Qx, inp.k)
-    rep = K.format_report_gpu(r.checksum)
+    rep = bytes(K.format_report_gpu(r.checksum))
     torch.cuda.synchronize()
     nc = min(a.check, a.q)
     d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx[:nc], inp.k[:nc], kstride=r.ids.shape[1])
