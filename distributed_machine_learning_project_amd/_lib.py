@@ -28,11 +28,12 @@ _SIGS = {
     "dmlp_set_screen_mode": (None, [i32]),
     "dmlp_set_stream_mode": (None, [i32]),
     "dmlp_set_stream_groups": (None, [i32]),
-    "dmlp_screen_stream_cap": (i32, []),
+    "dmlp_screen_stream_cap": (i32, [i32]),
+    "dmlp_set_stream_sub": (None, [i32]),
     "dmlp_screen_stream_kmax": (i32, []),
     "dmlp_stream_debug_counters": (i32, [vp, i32]),
     "dmlp_screen_stream_qw": (i32, [i32]),
-    "dmlp_screen_stream": (i32, [i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
+    "dmlp_screen_stream": (i32, [i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp, vp, f32, i32, vp,
                                  vp, vp]),
     "dmlp_screen_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,

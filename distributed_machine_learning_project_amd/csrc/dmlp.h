@@ -48,18 +48,22 @@ int dmlp_screen_lds_bytes(int KT, int cap);
 int dmlp_screen_waves(int KT, int cap);
 
 // Barrier-free streaming screen (screen_stream.hip) for k <= dmlp_screen_stream_kmax() and
-// KT <= 2: dmlp_screen_stream_qw(KT) queries per workgroup (0 = unsupported KT); candidate ids
-// per (query, slice) = dmlp_screen_stream_cap(); same output contract as dmlp_screen.
+// KT <= 2: dmlp_screen_stream_qw(KT) queries per workgroup (0 = unsupported KT); kmax = the
+// largest k in the query list; candidate ids per (query, slice) = dmlp_screen_stream_cap(kmax);
+// same output contract as dmlp_screen.
 int dmlp_screen_stream_qw(int KT);
-int dmlp_screen_stream_cap(void);
+int dmlp_screen_stream_cap(int kmax);
 int dmlp_screen_stream_kmax(void);
 int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_tiles,
                        const void* qhi, const void* qlo, const float* qn, const int* qidx,
-                       const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
-                       float eps_rel, int S, int* cand_ids, int* cand_cnt, void* stream);
-// Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off.
+                       const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
+                       const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
+                       void* stream);
+// Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off,
+// sub-buffer depth (8 / 16, 0 = automatic).
 void dmlp_set_stream_mode(int mode);
 void dmlp_set_stream_groups(int on);
+void dmlp_set_stream_sub(int sub);
 
 // ---------------------------------------------------------------- device: exact refine (K2 exact + K3 + K6)
 // Exact fp64 distances of the candidates, exact top-k under (dist asc, id desc).

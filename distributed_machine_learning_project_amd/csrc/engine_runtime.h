@@ -296,13 +296,15 @@ struct LocalKnn {
         int* qi = (cls == 0 ? qidx_a : qidx_b).get(nq);
         HIPCHK(hipMemcpyAsync(qi, idx.data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
         const bool streaming = cls == 0 && qw > 0;
-        const int cap = streaming ? dmlp_screen_stream_cap() : (cls == 0 ? 128 : 256);
+        int kcls = 1;
+        for (int q : idx) kcls = std::max(kcls, kk[q]);
+        const int cap = streaming ? dmlp_screen_stream_cap(kcls) : (cls == 0 ? 128 : 256);
         const int S = streaming ? slices_stream(nq, qw, nt)
                                 : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);
         if (streaming)
-          DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,
+          DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq, kcls,
                                      words.p, words.p + 1, er, S, ci, cc, st));
         else
           DMLPCHK(dmlp_screen(KT, cap, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,

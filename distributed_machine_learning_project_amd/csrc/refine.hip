@@ -170,11 +170,49 @@ __global__ __launch_bounds__(256) void k_refine(
     }
     for (int i = lane; i < k; i += 64) { s_rd[wave][i] = INFINITY; s_ri[wave][i] = -1; }
     dmlp::wave_sync();
-    for (int i = lane; i < M; i += 64) {
+    int Ms = M;
+    if (M > 64 && k <= 64) {
+      // O(M^2) ranking is the cost when the screen hands over a few hundred ids (4-row group
+      // mode): the k-th smallest key of ANY subset bounds the k-th smallest of all from above,
+      // so rank the first 64 candidates, keep only keys <= that bound (always >= k of them,
+      // every true top-k member among them), and rank the survivors.
+      const double di = cd[lane];
+      const int ii = ci[lane];
+      int rank = 0;
+      for (int j = 0; j < 64; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
+      const unsigned long long hit = __ballot(rank == k - 1);
+      const int src = __ffsll((long long)hit) - 1;
+      const double td = __shfl(di, src);
+      const int ti = __shfl(ii, src);
+      dmlp::wave_sync();
+      int kept = 0;
+      for (int j0 = 0; j0 < M; j0 += 64) {
+        const int j = j0 + lane;
+        double dj = INFINITY;
+        int ij = -1;
+        bool keep = false;
+        if (j < M) {
+          dj = cd[j];
+          ij = ci[j];
+          keep = !dmlp::key_less(td, ti, dj, ij);  // key_j <= bound
+        }
+        const unsigned long long km = __ballot(keep);
+        dmlp::wave_sync();  // slots < j0 + 64 already read by every lane
+        if (keep) {
+          const int pos = kept + __popcll(km & dmlp::lanemask_lt());
+          cd[pos] = dj;
+          ci[pos] = ij;
+        }
+        kept += __popcll(km);
+      }
+      dmlp::wave_sync();
+      Ms = kept;
+    }
+    for (int i = lane; i < Ms; i += 64) {
       const double di = cd[i];
       const int ii = ci[i];
       int rank = 0;
-      for (int j = 0; j < M; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
+      for (int j = 0; j < Ms; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
       if (rank < k) { s_rd[wave][rank] = di; s_ri[wave][rank] = ii; }
     }
     dmlp::wave_sync();

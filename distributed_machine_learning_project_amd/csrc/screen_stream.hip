@@ -26,9 +26,29 @@
 namespace {
 
 int g_stream_mode = 0;  // profiling ablations (bit 0 no candidates, 1 no MFMA, 2 no streaming,
-                        // 3 event counters into g_stream_dbg)
+                        // 3 event counters into g_stream_dbg, 4 s_memtime cycle accounting)
 int g_stream_groups = 1;  // 1: append 4-row groups (one entry per column tile and step)
 __device__ unsigned long long g_stream_dbg[8];
+
+// Wave-wide max / min of a u32 through DPP row shifts + row broadcasts (no LDS traffic; the
+// __shfl_xor form lowers to six dependent ds_bpermute round trips).  Result is wave-uniform.
+template <bool MAX>
+__device__ __forceinline__ unsigned wave_reduce_u32(unsigned v) {
+  const int idn = MAX ? 0 : -1;
+#define DMLP_DPP_STEP(CTRL, ROWMASK)                                                          \
+  {                                                                                           \
+    const unsigned o_ = (unsigned)__builtin_amdgcn_update_dpp(idn, (int)v, CTRL, ROWMASK, 0xf, false); \
+    v = MAX ? (v > o_ ? v : o_) : (v < o_ ? v : o_);                                          \
+  }
+  DMLP_DPP_STEP(0x111, 0xf)  // row_shr:1
+  DMLP_DPP_STEP(0x112, 0xf)  // row_shr:2
+  DMLP_DPP_STEP(0x114, 0xf)  // row_shr:4
+  DMLP_DPP_STEP(0x118, 0xf)  // row_shr:8  -> lane 15 of each row holds the row's result
+  DMLP_DPP_STEP(0x142, 0xa)  // row_bcast:15 into rows 1, 3
+  DMLP_DPP_STEP(0x143, 0xc)  // row_bcast:31 into rows 2, 3 -> lane 63 holds the wave's
+#undef DMLP_DPP_STEP
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
 
 template <int KT, int CT, int SUB, bool G>
 struct StreamCfg {
@@ -45,7 +65,7 @@ struct StreamCfg {
 };
 
 template <int KT, int CT, int SUB, int mode, bool G>
-__global__ __launch_bounds__(64, 1) void k_screen_stream(
+__global__ __launch_bounds__(64) void k_screen_stream(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles,
     const bf16x8* __restrict__ qhi, const bf16x8* __restrict__ qlo, const float* __restrict__ qn,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq,
@@ -124,8 +144,12 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     return sbuf + (((col >> 4) * 4 + m) * 16 + (col & 15)) * (SUB + 1);
   };
 
+  // (mode & 16) cycle accounting: loop, compaction, append path (s_memtime, core clock)
+  unsigned long long t_comp = 0, t_app = 0;
+
   // ---- compaction of every column whose sub-buffer passed SUB-4 (state in LDS, runtime loop)
   auto compact_pending = [&]() {
+    const unsigned long long tc0_ = (mode & 16) ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = cnt[ct];
     dmlp::wave_sync();
@@ -139,24 +163,23 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     while (pend) {
       const int col = __ffsll((long long)pend) - 1;
       pend &= pend - 1;
+      // all of the column's state in one batch of LDS reads (one latency, not five)
       const int nmine = lcnt[col * 4 + kg];
-      const bool ok = c < nmine;
-      const i32x2 e = ok ? sub_ptr(col, kg)[c] : (i32x2){__float_as_int(-INFINITY), -1};
-      const int ntot = __popcll(__ballot(ok));
-      const int kc = lk[col];
+      const i32x2 eraw = sub_ptr(col, kg)[c];  // slot c < SUB+1 always exists
+      const int kc = __builtin_amdgcn_readfirstlane(lk[col]);
       float hc = lh[col];
+      const float epc = leps[col];
+      const bool ok = c < nmine;
+      const i32x2 e = ok ? eraw : (i32x2){__float_as_int(-INFINITY), -1};
+      const int ntot = __popcll(__ballot(ok));
       if (ntot >= kc) {
         const unsigned bits = (unsigned)e.x;
         const unsigned u = ok ? (bits ^ ((bits >> 31) ? 0xffffffffu : 0x80000000u)) : 0u;
-        // the k-th largest key lies in [min, max] of the buffered keys: start below their
-        // common prefix (scores of one column share their leading bits, so this skips most
-        // of the 20 ballot rounds)
-        unsigned umx = u, umn = ok ? u : 0xffffffffu;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          umx = max(umx, (unsigned)__shfl_xor((int)umx, o));
-          umn = min(umn, (unsigned)__shfl_xor((int)umn, o));
-        }
+        // the k-th largest key lies in [min, max] of the buffered keys: the radix search
+        // starts below their common prefix (DPP reductions, no LDS round trips), and runs as
+        // a scalar loop (T, bit uniform in SGPRs)
+        const unsigned umx = wave_reduce_u32<true>(u);
+        const unsigned umn = wave_reduce_u32<false>(ok ? u : 0xffffffffu);
         const unsigned dif = umx ^ umn;
         const int top = dif ? 31 - __clz((int)dif) : -1;
         unsigned T = umx;  // top < 0: every buffered key is equal
@@ -168,7 +191,7 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
           if (__popcll(__ballot(u >= cand)) >= kc) T = cand;
         }
         const float ak = __uint_as_float((T >> 31) ? (T ^ 0x80000000u) : ~T);
-        hc = fmaxf(hc, ak - 2.0f * leps[col]);
+        hc = fmaxf(hc, ak - 2.0f * epc);
       }
       const bool keep = ok && __int_as_float(e.x) >= hc;
       const unsigned long long km = __ballot(keep);
@@ -192,6 +215,7 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
     // at the merge after `if (trig) compact_pending()` and makes EVERY following step wait
     // for all outstanding LDS traffic (i.e. the previous step's appends)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    if (mode & 16) t_comp += __builtin_amdgcn_s_memtime() - tc0_;
   };
 
   // ---- D-deep register ring of step fragments + double-buffered accumulators
@@ -251,6 +275,7 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
       /* branch-free appends: every lane writes each value to its next free slot and only  \
          advances the slot on a hit (slots cnt..cnt+3 <= SUB-1 exist; a miss is overwritten  \
          later and never read).  Per-lane branches here cost a taken s_cbranch each. */      \
+      const unsigned long long ta0_ = (mode & 16) ? __builtin_amdgcn_s_memtime() : 0;         \
       bool trig_ = false;                                                                       \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
         i32x2* mys_ = sub_ptr(ct * 16 + c, kg);                                                 \
@@ -269,10 +294,15 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
         cnt[ct] = cn_;                                                                          \
         trig_ |= cn_ > SUB - APPEND;                                                            \
       }                                                                                         \
+      if (mode & 16) {                                                                          \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                                                     \
+        t_app += __builtin_amdgcn_s_memtime() - ta0_;                                           \
+      }                                                                                         \
       if (__ballot(trig_)) compact_pending();                                                   \
     }                                                                                           \
   } while (0)
 
+  const unsigned long long tl0_ = (mode & 16) ? __builtin_amdgcn_s_memtime() : 0;
   if (nsteps > 0) {
 #pragma unroll
     for (int r = 0; r < D; ++r) DMLP_LOAD(r, r);
@@ -286,6 +316,11 @@ __global__ __launch_bounds__(64, 1) void k_screen_stream(
       }
     }
     DMLP_EPILOGUE((nsteps - 1) & 1, nsteps - 1);
+  }
+  if ((mode & 16) && lane == 0) {
+    atomicAdd(&g_stream_dbg[4], __builtin_amdgcn_s_memtime() - tl0_);
+    atomicAdd(&g_stream_dbg[5], t_comp);
+    atomicAdd(&g_stream_dbg[6], t_app);
   }
   if (mode & 1) {
 #pragma unroll
@@ -355,6 +390,7 @@ int launch_stream(const void* xfrag, const float* xinit, int64_t n_tiles, const 
     case 5: DMLP_STREAM_LAUNCH(5); break;
     case 7: DMLP_STREAM_LAUNCH(7); break;
     case 8: DMLP_STREAM_LAUNCH(8); break;
+    case 16: DMLP_STREAM_LAUNCH(16); break;
     default: DMLP_STREAM_LAUNCH(0); break;
   }
 #undef DMLP_STREAM_LAUNCH
@@ -365,10 +401,20 @@ int launch_stream(const void* xfrag, const float* xinit, int64_t n_tiles, const 
 }  // namespace
 
 // Streaming screen for k <= 32 and A <= 64 (KT <= 2); 64 queries per workgroup.  Candidate
-// ids per (query, slice): dmlp_screen_stream_cap() (256 in group mode, 64 per-point).
+// ids per (query, slice): dmlp_screen_stream_cap(kmax) for the class's largest k.  Group mode
+// with kmax <= 16 uses 8-entry sub-buffers (19.8 KiB LDS: two waves per SIMD, so one wave's
+// candidate work overlaps the other's MFMAs); otherwise 16 (36.6 KiB, one wave per SIMD).
+int g_stream_sub = 0;  // 0 auto, 8 / 16 forced (A/B)
+static int stream_sub(int kmax) {
+  if (g_stream_sub) return g_stream_sub;
+  return (g_stream_groups && kmax <= 16) ? 8 : 16;
+}
 extern "C" int dmlp_screen_stream_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
-extern "C" int dmlp_screen_stream_cap(void) { return g_stream_groups ? 256 : 64; }
+extern "C" int dmlp_screen_stream_cap(int kmax) {
+  return 4 * stream_sub(kmax) * (g_stream_groups ? 4 : 1);
+}
 extern "C" int dmlp_screen_stream_kmax(void) { return 32; }
+extern "C" void dmlp_set_stream_sub(int sub) { g_stream_sub = (sub == 8 || sub == 16) ? sub : 0; }
 
 extern "C" void dmlp_set_stream_mode(int mode) { g_stream_mode = mode; }
 extern "C" void dmlp_set_stream_groups(int on) { g_stream_groups = on ? 1 : 0; }
@@ -386,20 +432,25 @@ extern "C" int dmlp_stream_debug_counters(unsigned long long* out, int reset) {
 
 extern "C" int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_tiles,
                                   const void* qhi, const void* qlo, const float* qn,
-                                  const int* qidx, const int* qk, int nq,
+                                  const int* qidx, const int* qk, int nq, int kmax,
                                   const unsigned* xnmax_bits, const unsigned* bad, float eps_rel,
                                   int S, int* cand_ids, int* cand_cnt, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
+  if (kmax > 32) return -3;
   hipStream_t st = (hipStream_t)stream;
+  const int sub = stream_sub(kmax);
+  if (sub == 8 && kmax > 16) return -3;
+#define DMLP_STREAM_ARGS xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, xnmax_bits, bad, \
+                         eps_rel, S, cand_ids, cand_cnt, st
 #define DMLP_STREAM_KT(KTV)                                                                    \
-  return g_stream_groups                                                                       \
-             ? launch_stream<KTV, 4, 16, true>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, \
-                                               xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st) \
-             : launch_stream<KTV, 4, 16, false>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq, \
-                                                xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st)
-  if (KT == 1) { DMLP_STREAM_KT(1); }
-  if (KT == 2) { DMLP_STREAM_KT(2); }
+  if (g_stream_groups)                                                                         \
+    return sub == 8 ? launch_stream<KTV, 4, 8, true>(DMLP_STREAM_ARGS)                         \
+                    : launch_stream<KTV, 4, 16, true>(DMLP_STREAM_ARGS);                       \
+  return launch_stream<KTV, 4, 16, false>(DMLP_STREAM_ARGS);
+  if (KT == 1) { DMLP_STREAM_KT(1) }
+  if (KT == 2) { DMLP_STREAM_KT(2) }
 #undef DMLP_STREAM_KT
+#undef DMLP_STREAM_ARGS
   return -2;
 }

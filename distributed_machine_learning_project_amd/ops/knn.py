@@ -257,7 +257,8 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
             nq = len(idx)
             if nq == 0:
                 continue
-            cap = L.dmlp_screen_stream_cap() if streaming else (128 if idx is cls_a else 256)
+            kcls = int(kk[idx].max())
+            cap = L.dmlp_screen_stream_cap(kcls) if streaming else (128 if idx is cls_a else 256)
             qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
             if streaming:
                 S = _choose_slices_stream(nq, stream_qw, ds.n_tiles)
@@ -268,7 +269,7 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
             if streaming:
                 _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
                                                 _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff),
-                                                nq, _p(ds.xnmax_bits), _p(ds.bad), er, S,
+                                                nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), er, S,
                                                 _p(cand_ids), _p(cand_cnt), s), "screen_stream")
             else:
                 _lib.check(L.dmlp_screen(KT, cap, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
@@ -310,6 +311,8 @@ def _apply_env_switches(L):
     if not _ENV_APPLIED[0]:
         if os.environ.get("DMLP_STREAM_GROUPS", "1") == "0":
             L.dmlp_set_stream_groups(0)
+        if os.environ.get("DMLP_STREAM_SUB"):
+            L.dmlp_set_stream_sub(int(os.environ["DMLP_STREAM_SUB"]))
         _ENV_APPLIED[0] = True
 
 

@@ -50,6 +50,14 @@ def main():
                 if it:
                     ts.append(e0.elapsed_time(e1))
             print(f"mode {m}: {np.median(ts):.3f} ms")
+            if m & 16:
+                c2 = np.zeros(8, np.uint64)
+                _lib.lib().dmlp_stream_debug_counters(c2.ctypes.data, 1)
+                calls = a.iters + 1
+                tl, tcp, tap = (float(x) / calls for x in c2[4:7])
+                print("  cycles/call (summed over waves): loop %.4g  compaction %.4g (%.1f%%)  "
+                      "appends %.4g (%.1f%%)" % (tl, tcp, 100 * tcp / max(tl, 1), tap,
+                                                 100 * tap / max(tl, 1)))
             if m & 8:
                 cnt = np.zeros(8, np.uint64)
                 _lib.lib().dmlp_screen_debug_counters(cnt.ctypes.data, 1)
