@@ -31,6 +31,7 @@ _SIGS = {
     "dmlp_screen_stream_cap": (i32, [i32]),
     "dmlp_set_stream_sub": (None, [i32]),
     "dmlp_screen_stream_kmax": (i32, []),
+    "dmlp_screen_stream_waves_per_cu": (i32, [i32]),
     "dmlp_stream_debug_counters": (i32, [vp, i32]),
     "dmlp_screen_stream_qw": (i32, [i32]),
     "dmlp_screen_stream": (i32, [i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, vp, vp, f32, i32, vp,

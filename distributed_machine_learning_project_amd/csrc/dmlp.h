@@ -54,6 +54,7 @@ int dmlp_screen_waves(int KT, int cap);
 int dmlp_screen_stream_qw(int KT);
 int dmlp_screen_stream_cap(int kmax);
 int dmlp_screen_stream_kmax(void);
+int dmlp_screen_stream_waves_per_cu(int kmax);
 int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_tiles,
                        const void* qhi, const void* qlo, const float* qn, const int* qidx,
                        const int* qk, int nq, int kmax, const unsigned* xnmax_bits,

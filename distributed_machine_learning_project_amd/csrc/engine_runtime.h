@@ -239,13 +239,14 @@ struct LocalKnn {
                            words.p, words.p + 1, st));
   }
 
-  static int slices_stream(int nq, int qw, int64_t n_tiles) {
+  static int slices_stream(int nq, int qw, int64_t n_tiles, int waves_per_cu) {
     const int nqb = (nq + qw - 1) / qw;
-    const int slots = 1024;
-    if (nqb >= slots) return 1;
-    int best = 1;
+    const int slots = waves_per_cu * 256;
+    const int s_min = (int)std::max<int64_t>(1, (n_tiles * 64 + (1ll << 29) - 1) >> 29);
+    if (nqb >= slots) return s_min;
+    int best = s_min;
     double best_eff = 0;
-    for (int S = 1; S <= 64 && S <= std::max<int64_t>(1, n_tiles / 4); ++S) {
+    for (int S = s_min; S < s_min + 64 && S <= std::max<int64_t>(s_min, n_tiles / 4); ++S) {
       const double w = (double)nqb * S;
       const double eff = w / (std::ceil(w / slots) * slots);
       if (eff >= 0.9) return S;
@@ -299,7 +300,7 @@ struct LocalKnn {
         int kcls = 1;
         for (int q : idx) kcls = std::max(kcls, kk[q]);
         const int cap = streaming ? dmlp_screen_stream_cap(kcls) : (cls == 0 ? 128 : 256);
-        const int S = streaming ? slices_stream(nq, qw, nt)
+        const int S = streaming ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))
                                 : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);

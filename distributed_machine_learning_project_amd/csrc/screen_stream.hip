@@ -283,7 +283,11 @@ __global__ __launch_bounds__(64) void k_screen_stream(
         if (G) {                                                                                \
           /* one entry per lane, column and step: the 4-row group (ids idbase..idbase+3)     \
              scored by its max; the k-th largest group max is still a lower bound on a_k */   \
-          mys_[cn_] = (i32x2){__float_as_int(m_[ct]), idbase_};                                 \
+          const int mk_ = (acc[AB][ct][0] >= h[ct] ? 1 : 0) | (acc[AB][ct][1] >= h[ct] ? 2 : 0) | \
+                          (acc[AB][ct][2] >= h[ct] ? 4 : 0) | (acc[AB][ct][3] >= h[ct] ? 8 : 0);  \
+          /* (group base << 2) | member hit mask: members below the threshold at append time  \
+             can never re-enter (h only rises), so the final write emits only masked ids */   \
+          mys_[cn_] = (i32x2){__float_as_int(m_[ct]), ((idbase_ - t0 * 64) << 2) | mk_};        \
           cn_ += m_[ct] >= h[ct] ? 1 : 0;                                                       \
         } else {                                                                                \
           _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                       \
@@ -348,14 +352,15 @@ __global__ __launch_bounds__(64) void k_screen_stream(
     const float hc = lh[col];
     const bool keep = ok && __int_as_float(e.x) >= hc;
     if (G) {
-      // expand kept groups to their member ids; padding members (xinit = -inf) are dropped
-      const float* xinit = (const float*)xinit4;
+      // expand kept groups to the members that were above the threshold when appended
+      // (padding members score -inf and are never in the mask)
+      const int gbase = ((e.y >> 2) & ~3) + t0 * 64;  // slice-relative group base
       int nout = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bool v = keep && xinit[e.y + j] != -INFINITY;
+        const bool v = keep && ((e.y >> j) & 1);
         const unsigned long long mj = __ballot(v);
-        if (v) out[nout + __popcll(mj & dmlp::lanemask_lt())] = e.y + j;
+        if (v) out[nout + __popcll(mj & dmlp::lanemask_lt())] = gbase + j;
         nout += __popcll(mj);
       }
       if (lane == 0) cand_cnt[(int64_t)pp * S + s] = nout;
@@ -414,6 +419,8 @@ extern "C" int dmlp_screen_stream_cap(int kmax) {
   return 4 * stream_sub(kmax) * (g_stream_groups ? 4 : 1);
 }
 extern "C" int dmlp_screen_stream_kmax(void) { return 32; }
+// resident workgroups (= waves) per CU of the variant chosen for kmax (LDS-bound)
+extern "C" int dmlp_screen_stream_waves_per_cu(int kmax) { return stream_sub(kmax) == 8 ? 8 : 4; }
 extern "C" void dmlp_set_stream_sub(int sub) { g_stream_sub = (sub == 8 || sub == 16) ? sub : 0; }
 
 extern "C" void dmlp_set_stream_mode(int mode) { g_stream_mode = mode; }
@@ -437,6 +444,8 @@ extern "C" int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit,
                                   int S, int* cand_ids, int* cand_cnt, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
+  // group entries carry slice-relative ids << 2: a slice must stay below 2^29 points
+  if ((n_tiles + S - 1) / S > (1 << 29) / 64) return -4;
   if (kmax > 32) return -3;
   hipStream_t st = (hipStream_t)stream;
   const int sub = stream_sub(kmax);

@@ -179,18 +179,20 @@ class DeviceResult:
     n_fallback: int = 0
 
 
-def _choose_slices_stream(nq: int, qw: int, n_tiles: int) -> int:
-    """Data slices for the streaming screen: one wave per (query block, slice), 4 per CU.
-    Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best."""
+def _choose_slices_stream(nq: int, qw: int, n_tiles: int, waves_per_cu: int = 4) -> int:
+    """Data slices for the streaming screen: one wave per (query block, slice).
+    Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best;
+    never fewer than needed to keep a slice below 2^29 points (group-entry id range)."""
     nqb = (nq + qw - 1) // qw
-    slots = 4 * NUM_CUS
+    slots = waves_per_cu * NUM_CUS
+    s_min = max(1, -(-n_tiles * 64 // (1 << 29)))
     if nqb >= slots:
         # every extra slice repeats each query's threshold warm-up (candidate work grows ~S):
         # with a full round of waves already, a partial last round is cheaper than S > 1
-        return 1
-    best, best_eff = 1, 0.0
-    for S in range(1, 65):
-        if S > max(1, n_tiles // 4):
+        return s_min
+    best, best_eff = s_min, 0.0
+    for S in range(s_min, s_min + 64):
+        if S > max(s_min, n_tiles // 4):
             break
         w = nqb * S
         eff = w / (math.ceil(w / slots) * slots)
@@ -199,7 +201,6 @@ def _choose_slices_stream(nq: int, qw: int, n_tiles: int) -> int:
         if eff > best_eff + 1e-9:
             best, best_eff = S, eff
     return best
-
 
 def _choose_slices(nq: int, waves: int, n_tiles: int) -> int:
     nqb = (nq + waves * 16 - 1) // (waves * 16)
@@ -261,7 +262,8 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
             cap = L.dmlp_screen_stream_cap(kcls) if streaming else (128 if idx is cls_a else 256)
             qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
             if streaming:
-                S = _choose_slices_stream(nq, stream_qw, ds.n_tiles)
+                S = _choose_slices_stream(nq, stream_qw, ds.n_tiles,
+                                          L.dmlp_screen_stream_waves_per_cu(kcls))
             else:
                 S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
