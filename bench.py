@@ -9,7 +9,7 @@ Metric (BASELINE.json): "samples/sec (whole node) on bench_4" = classified queri
 over all GPUs.  One step = one full Engine::KNN call exactly as the reference times it
 (common.cpp:122-131): rank 0 holds the parsed input in host memory; the step moves it to the
 GPUs, broadcasts the dataset (bench_4 replicates it), distributes the queries, runs the exact
-k-NN (bf16x3 MFMA screen + exact fp64 re-rank), votes, checksums, gathers the results to rank 0
+k-NN (bf16 MFMA screen + exact fp64 re-rank), votes, checksums, gathers the results to rank 0
 and renders the "Query <id> checksum: <u64>" report bytes on rank 0.
 
 Config: the reference's inputs (inputs.zip) are not in the repository, so the workload is
@@ -131,8 +131,9 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_QPS, 1),
             "dtype": "fp64",
-            "screen": "none" if a.exact else "bf16x3 MFMA screen, exact fp64 re-rank "
-                                             "(results bit-identical to the fp64 reference)",
+            "screen": "none" if a.exact else "single-term bf16 MFMA screen (3-term escalation), "
+                                             "exact fp64 re-rank (results bit-identical to the "
+                                             "fp64 reference)",
             "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",
             "config": {
                 "model": f"bench_4 exact k-NN classifier N={a.n_data} A={a.attrs} k={a.k} "

@@ -29,6 +29,10 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
+# screen_x1: fmaxf over MFMA results without the IEEE-mode NaN quieting (v_max_f32 x, x, x per
+# operand); the kernel never produces or compares NaN
+PER_FILE = {"screen_x1.hip": ["-fno-honor-nans"]}
+
 
 def _sources():
     hip = sorted(CSRC.glob("*.hip"))
@@ -63,7 +67,7 @@ def _compile(src: Path, force: bool) -> Path:
         # MFMA results in VGPRs: the epilogue reads every accumulator with VALU, and AGPR
         # results cost a v_accvgpr_read per value plus copies of the C-init operand
         cmd = [HIPCC, f"--offload-arch={ARCH}", *COMMON, "-mllvm", "-amdgpu-mfma-vgpr-form=true",
-               "-c", str(src), "-o", str(obj)]
+               *PER_FILE.get(src.name, []), "-c", str(src), "-o", str(obj)]
     else:
         # host-only code: plain g++ without -march (no FMA contraction, SSE2 like the reference)
         cmd = ["g++", *COMMON, f"-I{CSRC}", "-pthread", "-c", str(src), "-o", str(obj)]

@@ -60,6 +60,22 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
                        const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
                        const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
                        void* stream);
+// Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT <= 2: 64 queries
+// per workgroup, candidate ids per (query, slice) = dmlp_screen_x1_cap(kmax); A and the real point
+// count are needed for the error bound and to drop padding rows.  S >= dmlp_screen_x1_min_slices.
+// Same output contract as dmlp_screen.
+int dmlp_screen_x1_kmax(void);
+int dmlp_screen_x1_qw(int KT);
+int dmlp_screen_x1_cap(int kmax);
+int dmlp_screen_x1_waves_per_cu(int kmax);
+int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
+void dmlp_screen_x1_bound(int A, float* r1, float* r2);
+int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
+                   int64_t n_points, const void* qhi, const float* qn, const int* qidx,
+                   const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
+                   const unsigned* bad, int S, int* cand_ids, int* cand_cnt, void* stream);
+void dmlp_set_x1_mode(int mode);
+int dmlp_x1_debug_counters(unsigned long long* out, int reset);
 // Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off,
 // sub-buffer depth (8 / 16, 0 = automatic).
 void dmlp_set_stream_mode(int mode);

@@ -215,7 +215,7 @@ struct LocalKnn {
   DevBuf<unsigned> words;  // [0] xnmax bits, [1] bad
   DevBuf<short> qhi, qlo;
   DevBuf<float> qn;
-  DevBuf<int> qidx_a, qidx_b, qidx_f, kdev, cand_ids, cand_cnt, status;
+  DevBuf<int> qidx_a, qidx_b, qidx_e, qidx_f, kdev, cand_ids, cand_cnt, status;
   DevBuf<char> fb_ws;
   int KT = 1;
   int64_t N = 0;
@@ -239,10 +239,11 @@ struct LocalKnn {
                            words.p, words.p + 1, st));
   }
 
-  static int slices_stream(int nq, int qw, int64_t n_tiles, int waves_per_cu) {
+  static int slices_stream(int nq, int qw, int64_t n_tiles, int waves_per_cu, int64_t s_lo = 1) {
     const int nqb = (nq + qw - 1) / qw;
     const int slots = waves_per_cu * 256;
-    const int s_min = (int)std::max<int64_t>(1, (n_tiles * 64 + (1ll << 29) - 1) >> 29);
+    const int s_min = (int)std::max<int64_t>(std::max<int64_t>(1, s_lo),
+                                             (n_tiles * 64 + (1ll << 29) - 1) >> 29);
     if (nqb >= slots) return s_min;
     int best = s_min;
     double best_eff = 0;
@@ -290,21 +291,29 @@ struct LocalKnn {
       const float er = eps_rel(A);
       const int64_t nt = (N + 63) / 64;
       const int qw = dmlp_screen_stream_qw(KT);
-      for (int cls = 0; cls < 2; ++cls) {
-        std::vector<int>& idx = cls == 0 ? a : b;
-        if (idx.empty()) continue;
+      // default: single-term bf16 screen (screen_x1.hip); KNN_SCREEN=stream: 3-term streaming
+      const char* impl = std::getenv("KNN_SCREEN");
+      const bool x1 = dmlp_screen_x1_qw(KT) > 0 && !(impl && std::string(impl) == "stream");
+      // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 128)
+      auto pass = [&](const std::vector<int>& idx, int impl, DevBuf<int>& qbuf) {
         const int nq = (int)idx.size();
-        int* qi = (cls == 0 ? qidx_a : qidx_b).get(nq);
+        int* qi = qbuf.get(nq);
         HIPCHK(hipMemcpyAsync(qi, idx.data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
-        const bool streaming = cls == 0 && qw > 0;
         int kcls = 1;
         for (int q : idx) kcls = std::max(kcls, kk[q]);
-        const int cap = streaming ? dmlp_screen_stream_cap(kcls) : (cls == 0 ? 128 : 256);
-        const int S = streaming ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))
-                                : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
+        const int cap = impl == 0 ? dmlp_screen_x1_cap(kcls)
+                        : impl == 1 ? dmlp_screen_stream_cap(kcls) : (kcls <= 32 ? 128 : 256);
+        const int S = impl == 0 ? slices_stream(nq, dmlp_screen_x1_qw(KT), nt,
+                                                dmlp_screen_x1_waves_per_cu(kcls),
+                                                dmlp_screen_x1_min_slices(nt))
+                      : impl == 1 ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))
+                                  : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);
-        if (streaming)
+        if (impl == 0)
+          DMLPCHK(dmlp_screen_x1(KT, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
+                                 words.p, words.p + 1, S, ci, cc, st));
+        else if (impl == 1)
           DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq, kcls,
                                      words.p, words.p + 1, er, S, ci, cc, st));
         else
@@ -312,11 +321,25 @@ struct LocalKnn {
                               words.p, words.p + 1, er, S, ci, cc, st));
         DMLPCHK(dmlp_refine(cap, ci, cc, S, X, A, Qx, qi, kd, nq, out_d, out_i, kstride,
                             fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, st));
-      }
-      // one host sync: which screened queries overflowed into the exact path
+      };
+      const int first_a = x1 ? 0 : (qw > 0 ? 1 : 2);
+      if (!a.empty()) pass(a, first_a, qidx_a);
+      if (!b.empty()) pass(b, 2, qidx_b);
+      // one host sync: which screened queries overflowed
       std::vector<int> sh(Q);
       HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
       wait();
+      if (first_a == 0) {
+        // single-term overflow (data too tight for its bound): escalate to the 3-term screen
+        std::vector<int> esc;
+        for (int q : a)
+          if (sh[q]) esc.push_back(q);
+        if (!esc.empty()) {
+          pass(esc, qw > 0 ? 1 : 2, qidx_e);
+          HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+          wait();
+        }
+      }
       for (int64_t q = 0; q < Q; ++q)
         if (sh[q]) f.push_back((int)q);
     }

@@ -418,17 +418,16 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   if (S < 1 || S > 256) return -1;
   const dim3 grid((nq + 3) / 4), block(256);
   hipStream_t st = (hipStream_t)stream;
-  // P must exceed k + 64; k <= dmlp_screen_kmax(cap)
-  if (cap == 64 || cap == 128) {
+  // cap is the id stride per (query, slice); P = E*64 must exceed k + 64 (k <= 128)
+  if (cap < 1) return -2;
+  if (cap <= 128) {
     hipLaunchKernelGGL(k_refine<4>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
                        qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
                        out_label, out_cs, status);
-  } else if (cap == 256) {
+  } else {
     hipLaunchKernelGGL(k_refine<8>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
                        qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
                        out_label, out_cs, status);
-  } else {
-    return -2;
   }
   DMLP_LAUNCH_CHECK();
   return 0;

@@ -1,0 +1,412 @@
+// screen_x1.hip — single-term bf16 MFMA screen with lane-parallel batched threshold compaction.
+//
+// Same contract as screen_stream.hip (candidate ids per (query, slice), exact fp64 re-rank in
+// refine.hip), different balance:
+//
+//  * ONE bf16 product per attribute (hi(q') * hi(x')), not the 3-term split: a third of the MFMA
+//    work and half the fragment bytes.  The price is a wider error bound,
+//        |a - a_exact| <= r1 * |q'| * max|x'| + r2 * max|x'|^2,
+//    r1 ~ 2^-8 (bf16 rounding of both operands) — on the generate_input.py distribution that
+//    lets ~2x k candidates through instead of ~k, which the exact re-rank absorbs easily.
+//  * Candidate buffers hold 4-byte entries (top 16 bits of the fp32 4-row group max | 16-bit
+//    slice-relative group index), so a wave's 64 columns x 64 entries fit in 17 KiB of LDS and
+//    two waves share every SIMD (one wave's VALU epilogue overlaps the other's MFMAs).
+//  * Threshold maintenance is batched and lane-parallel: when any lane's sub-buffer fills, the
+//    whole wave compacts ALL 64 columns at once, lane j owning column j (per-lane radix select of
+//    the k-th largest key over <= 64 register-resident entries).  The streaming kernel's
+//    one-column-at-a-time ballot radix cost ~2.5k cycles per column; here a batch costs about as
+//    much for all 64 columns, and every column's threshold rises at each batch.
+//
+// Layout (mfma_f32_16x16x32_bf16): lane (c = lane & 15, kg = lane >> 4) of column tile ct holds
+// query column ct*16 + c and rows kg*4 .. kg*4+3 of the 16-point step.  The A operand (data
+// fragments, hi half of prep.hip's hi/lo image) streams from L2 into a D-deep register ring; the
+// C operand is the row's -|x'|^2/2, so acc = a directly.
+#include "dmlp.h"
+#include "dmlp_device.h"
+#include <float.h>
+
+#include <cmath>
+
+namespace {
+
+int g_x1_mode = 0;  // profiling: 1 no candidate path, 8 event counters (g_x1_dbg)
+__device__ unsigned long long g_x1_dbg[8];
+
+template <int KT, int SUB>
+struct X1Cfg {
+  static constexpr int CT = 4;                  // MFMA column tiles per wave
+  static constexpr int NCOL = 16 * CT;          // queries per wave (= workgroup)
+  static constexpr int SUBP = SUB + 1;          // pitch: the 64 lanes of an append hit 64 banks
+  static constexpr int CAPE = 4 * (SUB - 1);    // group entries a column may keep
+  static constexpr int IDCAP = 4 * CAPE;        // candidate ids per (query, slice)
+  static constexpr int FRAGS = 4 * KT * 2;      // 1 KiB fragments per 64-point tile (hi, lo)
+  static constexpr int SBUF = NCOL * 4 * SUBP * 4;
+  static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4;
+  static constexpr int D = 4;                   // register-ring depth (steps in flight)
+};
+
+// fp32 bits -> order-preserving u32 (only the top 16 bits are meaningful for a truncated key)
+__device__ __forceinline__ unsigned ord32(unsigned b) {
+  return b ^ ((unsigned)((int)b >> 31) | 0x80000000u);
+}
+__device__ __forceinline__ unsigned unord32(unsigned o) {
+  return o ^ ((o >> 31) ? 0x80000000u : 0xffffffffu);
+}
+
+template <int KT, int SUB, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_screen_x1(
+    const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
+    const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
+    const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
+    const unsigned* __restrict__ bad, float r1, float r2, int S, int tiles_per_slice,
+    int n_qblocks, int* __restrict__ cand_ids, int* __restrict__ cand_cnt) {
+  using C = X1Cfg<KT, SUB>;
+  constexpr int CT = C::CT;
+  constexpr int SUBP = C::SUBP;
+  constexpr int D = C::D;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned* const sbuf = (unsigned*)smem;                    // [col][m][SUBP] entries
+  int* const lcnt = (int*)(smem + C::SBUF);                  // [col][m] counts
+  float* const lh = (float*)(lcnt + C::NCOL * 4);            // [col] threshold
+  int* const lk = (int*)(lh + C::NCOL);                      // [col] k
+  float* const leps = (float*)(lk + C::NCOL);                // [col] eps
+  int* const lflag = (int*)(leps + C::NCOL);                 // [col] 1 = overflowed
+
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 15;
+  const int kg = lane >> 4;
+
+  // ---- block -> (query block, slice); XCD-aware when S % 8 == 0 (slice s stays on one XCD's L2)
+  const int b = blockIdx.x;
+  int qb, s;
+  if ((S & 7) == 0) {
+    const int xcd = b & 7, local = b >> 3, m = S >> 3;
+    const int sl = local / n_qblocks;
+    qb = local - sl * n_qblocks;
+    s = xcd * m + sl;
+  } else {
+    s = b % S;
+    qb = b / S;
+  }
+  const int t0 = s * tiles_per_slice;
+  int t1 = t0 + tiles_per_slice;
+  if (t1 > n_tiles) t1 = n_tiles;
+  const int nt = t1 > t0 ? t1 - t0 : 0;
+  const int nsteps = nt * 4;
+  const int pbase = qb * C::NCOL;
+
+  if (*bad) {
+    if (lane < C::NCOL && pbase + lane < nq) cand_cnt[(int64_t)(pbase + lane) * S + s] = -1;
+    return;
+  }
+  const float xnmax = __uint_as_float(*xnmax_bits);
+
+  bf16x8 bh[CT][KT];
+  float h[CT];
+  int cnt[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int p = pbase + ct * 16 + c;
+    const bool valid = p < nq;
+    const int q = valid ? qidx[p] : 0;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) bh[ct][kt] = qhi[(q * KT + kt) * 4 + kg];
+    h[ct] = valid ? -FLT_MAX : INFINITY;
+    cnt[ct] = 0;
+    if (lane < 16) {
+      const int col = ct * 16 + c;
+      lh[col] = h[ct];
+      lk[col] = valid ? qk[q] : 0;
+      leps[col] = valid ? r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax : 0.0f;
+      lflag[col] = 0;
+    }
+  }
+  // slice-local buffer resources: step j's fragments sit at j * KT * 2 KiB (hi at +0, lo at
+  // +1 KiB per kt) and its -|x|^2/2 at j * 64 B, so the ring loads need no address arithmetic
+  // beyond one scalar offset; prefetches past the slice read zeros instead of faulting
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(xfrag + (int64_t)t0 * (C::FRAGS * 64)), (short)0, nt * C::FRAGS * 64 * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
+  // this lane's sub-buffer of column tile 0; tile ct adds ct * 64 * SUBP entries
+  unsigned* const mysub = sbuf + ((c * 4) + kg) * SUBP;
+
+  // ---- batched compaction: lane j owns column j.  FINAL: write the column's candidate ids.
+  auto compact = [&](const bool final_pass) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = cnt[ct];
+    dmlp::wave_sync();
+    const int j = lane;
+    unsigned* const colbuf = sbuf + j * 4 * SUBP;
+    const int4 n4 = *(const int4*)(lcnt + j * 4);
+    const int nm[4] = {n4.x, n4.y, n4.z, n4.w};
+    const int kc = lk[j];
+    const float epc = leps[j];
+    const int flag = lflag[j];
+    float hc = lh[j];
+    // entries -> ordered keys in place (0 = empty slot)
+    unsigned e[4][SUB];
+    unsigned mx = 0u, mn = 0xffffffffu;
+    int ntot = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int i = 0; i < SUB; ++i) {
+        // validity as arithmetic (all-ones iff i < count), not a predicate: 64 live lane masks
+        // would spill SGPRs into the hot loop
+        const unsigned vm = (unsigned)((i - nm[m]) >> 31);
+        const unsigned raw = colbuf[m * SUBP + i];
+        e[m][i] = ord32(raw) & vm;
+        mx = max(mx, e[m][i]);
+        mn = min(mn, e[m][i] | ~vm);
+      }
+      ntot += nm[m];
+    }
+    const bool sel = !flag && kc >= 1 && ntot >= kc;
+    // k-th largest 16-bit key: radix search below the common prefix of [min, max]
+    const unsigned dif = (mx ^ mn) >> 16;
+    const int top = (sel && dif) ? 31 - __clz((int)dif) : -1;
+    unsigned T = mx >> 16;
+    if (top >= 0) T &= ~((2u << top) - 1u);
+    int topw = top;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int t = __shfl_xor(topw, o);
+      topw = t > topw ? t : topw;
+    }
+    for (int bit = topw; bit >= 0; --bit) {
+      const unsigned cand = (T | (1u << bit)) << 16;
+      int ge = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < SUB; ++i) ge += e[m][i] >= cand ? 1 : 0;
+      if (ge >= kc) T |= 1u << bit;
+    }
+    if (sel) {
+      // decode(T << 16) <= the k-th largest group max: a lower bound on the k-th best score
+      const float ak = __uint_as_float(unord32(T << 16));
+      hc = fmaxf(hc, ak - 2.0f * epc);
+    }
+    // keep every entry whose truncated key can be >= hc (floor(key) >= floor(key(hc)))
+    const unsigned kh = ord32(__float_as_uint(hc)) & 0xffff0000u;
+    if (MODE & 8) {
+      if (lane == 0) atomicAdd(&g_x1_dbg[3], 1ull);
+    }
+    if (!final_pass) {
+      int pos = 0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < SUB; ++i) {
+          const bool keep = !flag && e[m][i] >= kh && e[m][i] != 0u;
+          // every lane stores; a dropped entry lands in sub-buffer 3's pad slot (never read)
+          colbuf[keep ? (pos & 3) * SUBP + (pos >> 2) : 3 * SUBP + SUB] = unord32(e[m][i]);
+          pos += keep ? 1 : 0;
+        }
+      const bool ovf = flag || pos > C::CAPE;
+      int4 nn;
+      nn.x = ovf ? 0 : (pos + 3) >> 2;
+      nn.y = ovf ? 0 : (pos + 2) >> 2;
+      nn.z = ovf ? 0 : (pos + 1) >> 2;
+      nn.w = ovf ? 0 : pos >> 2;
+      *(int4*)(lcnt + j * 4) = nn;
+      lh[j] = ovf ? INFINITY : hc;
+      lflag[j] = ovf ? 1 : 0;
+      dmlp::wave_sync();
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        cnt[ct] = lcnt[(ct * 16 + c) * 4 + kg];
+        h[ct] = lh[ct * 16 + c];
+      }
+      // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
+      // pending after the conditional call and drains lgkmcnt at every following step
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    } else {
+      const int p = pbase + j;
+      if (p < nq) {
+        int* const out = cand_ids + ((int64_t)p * S + s) * C::IDCAP;
+        int nout = 0;
+        int kept = 0;
+        const int gbase = t0 * 64;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int i = 0; i < SUB; ++i) {
+            const bool keep = !flag && e[m][i] >= kh && e[m][i] != 0u;
+            if (keep && kept < C::CAPE) {
+              const int base = gbase + (int)(unord32(e[m][i]) & 0xffffu) * 4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (base + r < n_points) out[nout++] = base + r;
+            }
+            kept += keep ? 1 : 0;
+          }
+        cand_cnt[(int64_t)p * S + s] = (flag || kept > C::CAPE) ? -1 : nout;
+      }
+    }
+  };
+
+  // ---- D-deep register ring of step fragments + double-buffered accumulators
+  bf16x8 A[D][KT];
+  f32x4 Xi[D];
+  f32x4 acc[2][CT];
+#define DMLP_LOAD(J, R)                                                                         \
+  do {                                                                                          \
+    _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
+      A[R][kt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(              \
+          xr, lane * 16 + kt * 2048, (J) * (KT * 2048), 0));                                    \
+    Xi[R] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ir, kg * 16, (J) * 64, 0)); \
+  } while (0)
+#define DMLP_MFMA(R, AB)                                                                        \
+  do {                                                                                          \
+    _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
+      acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][0], bh[ct][0], Xi[R], 0, 0, 0); \
+      _Pragma("unroll") for (int kt = 1; kt < KT; ++kt)                                         \
+        acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][kt], bh[ct][kt], acc[AB][ct], 0, 0, 0); \
+    }                                                                                           \
+  } while (0)
+#define DMLP_EPILOGUE(AB, J)                                                                    \
+  do {                                                                                          \
+    float m_[CT];                                                                               \
+    bool hit_[CT];                                                                              \
+    bool any_ = false;                                                                          \
+    _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
+      m_[ct] = fmaxf(fmaxf(acc[AB][ct][0], acc[AB][ct][1]), fmaxf(acc[AB][ct][2], acc[AB][ct][3])); \
+      hit_[ct] = m_[ct] >= h[ct];                                                               \
+      any_ |= hit_[ct];                                                                         \
+    }                                                                                           \
+    if (MODE & 8) {                                                                             \
+      if (lane == 0) atomicAdd(&g_x1_dbg[0], 1ull);                                             \
+    }                                                                                           \
+    if (!(MODE & 1) && __ballot(any_)) {                                                        \
+      if (MODE & 8) {                                                                           \
+        int np_ = 0;                                                                            \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += hit_[ct] ? 1 : 0;              \
+        for (int o_ = 32; o_ > 0; o_ >>= 1) np_ += __shfl_xor(np_, o_);                         \
+        if (lane == 0) { atomicAdd(&g_x1_dbg[1], 1ull);                                         \
+                         atomicAdd(&g_x1_dbg[2], (unsigned long long)np_); }                    \
+      }                                                                                         \
+      /* branch-free: every lane writes its entry to the next free slot and advances only on  \
+         a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
+      const unsigned gl_ = (unsigned)((J) * 4 + kg);                                            \
+      bool trig_ = false;                                                                       \
+      _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
+        mysub[ct * 64 * SUBP + cnt[ct]] = (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;        \
+        cnt[ct] += hit_[ct] ? 1 : 0;                                                            \
+        trig_ |= cnt[ct] >= SUB;                                                                \
+      }                                                                                         \
+      if (__ballot(trig_)) compact(false);                                                      \
+    }                                                                                           \
+  } while (0)
+
+  if (nsteps > 0) {
+    // prologue in the loop's issue order (A, Xi per step), so the waitcnt at the loop head is
+    // the steady-state vmcnt(2 * (D - 1)), not a merge with a reordered prologue
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+      DMLP_LOAD(r, r);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int j0 = 0; j0 < nsteps; j0 += D) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
+        const int j = j0 + r;  // nsteps % 4 == 0 and D == 4: j < nsteps inside the body
+        DMLP_MFMA(r, r & 1);
+        DMLP_LOAD(j + D, r);
+        if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
+      }
+    }
+    DMLP_EPILOGUE((nsteps - 1) & 1, nsteps - 1);
+  }
+#undef DMLP_LOAD
+#undef DMLP_MFMA
+#undef DMLP_EPILOGUE
+  if (MODE & 1) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[0][ct]), "v"(acc[1][ct]));
+  }
+  // final threshold over everything buffered, then the candidate ids
+  compact(true);
+}
+
+int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
+
+template <int KT, int SUB>
+int launch_x1(const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
+              const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
+              const unsigned* xnmax, const unsigned* bad, float r1, float r2, int S,
+              int* cand_ids, int* cand_cnt, hipStream_t stream) {
+  using C = X1Cfg<KT, SUB>;
+  const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
+  const int tps = (int)((n_tiles + S - 1) / S);
+  const int64_t grid = (int64_t)n_qblocks * S;
+  if (grid <= 0) return 0;
+#define DMLP_X1_LAUNCH(M)                                                                      \
+  hipLaunchKernelGGL((k_screen_x1<KT, SUB, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
+                     (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
+                     (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, S, tps,          \
+                     n_qblocks, cand_ids, cand_cnt)
+  switch (g_x1_mode) {
+    case 1: DMLP_X1_LAUNCH(1); break;
+    case 8: DMLP_X1_LAUNCH(8); break;
+    default: DMLP_X1_LAUNCH(0); break;
+  }
+#undef DMLP_X1_LAUNCH
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+// Screen error bound of the single-term form, per query q (fp32 score a = <q',x'> - |x'|^2/2):
+//   hi() = bf16(fp32(c)): |c - hi(c)| <= u|c|, u = 2^-9 (1 + 2^-15);  bf16 x bf16 products are
+//   exact in fp32; the MFMA chain rounds at most A + 1 partial sums, each bounded by
+//   sum|hi(q)hi(x)| + |x'|^2/2; xinit carries one fp32 rounding of |x'|^2/2.  With |x'| <= max:
+//     |a - a_exact| <= r1 |q'| max|x'| + r2 max|x'|^2,
+//     r1 = 2u + u^2 + (A+2) 2^-24 (1+u)^2,   r2 = (A+2) 2^-24 / 2 + 2^-24,
+//   both taken x1.25 for the fp32 evaluation of the bound itself.
+extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
+  const double u = std::ldexp(1.0, -9) * (1.0 + std::ldexp(1.0, -15));
+  const double e24 = std::ldexp(1.0, -24);
+  *r1 = (float)(1.25 * (2.0 * u + u * u + (A + 2) * e24 * (1.0 + u) * (1.0 + u)));
+  *r2 = (float)(1.25 * ((A + 2) * e24 * 0.5 + e24));
+}
+extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
+extern "C" int dmlp_screen_x1_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
+extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * 4 * (x1_sub(kmax) - 1); }
+// resident workgroups (= waves) per CU, LDS-bound: 19.5 KiB (SUB 16) / 36.3 KiB (SUB 32)
+extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }
+// a slice must stay below 2^16 4-row groups (16-bit group index in an entry)
+extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles + 4095) / 4096; }
+extern "C" void dmlp_set_x1_mode(int mode) { g_x1_mode = mode; }
+extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_dbg), sizeof(g_x1_dbg));
+  if (e != hipSuccess) return -(int)e;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_x1_dbg), z, sizeof(z));
+    if (e != hipSuccess) return -(int)e;
+  }
+  return 0;
+}
+
+extern "C" int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xinit,
+                              int64_t n_tiles, int64_t n_points, const void* qhi, const float* qn,
+                              const int* qidx, const int* qk, int nq, int kmax,
+                              const unsigned* xnmax_bits, const unsigned* bad, int S,
+                              int* cand_ids, int* cand_cnt, void* stream) {
+  if (nq <= 0) return 0;
+  if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 || n_points > n_tiles * 64) return -1;
+  if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
+  if (kmax > 32 || KT < 1 || KT > 2 || A > KT * 32) return -3;
+  float r1, r2;
+  dmlp_screen_x1_bound(A, &r1, &r2);
+  hipStream_t st = (hipStream_t)stream;
+#define DMLP_X1_ARGS xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
+                     r2, S, cand_ids, cand_cnt, st
+  const int sub = x1_sub(kmax);
+  if (KT == 1) return sub == 16 ? launch_x1<1, 16>(DMLP_X1_ARGS) : launch_x1<1, 32>(DMLP_X1_ARGS);
+  return sub == 16 ? launch_x1<2, 16>(DMLP_X1_ARGS) : launch_x1<2, 32>(DMLP_X1_ARGS);
+#undef DMLP_X1_ARGS
+}

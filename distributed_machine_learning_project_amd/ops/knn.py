@@ -30,7 +30,8 @@ SCREEN_KMAX_A = 32      # cap 128 class
 SCREEN_KMAX_B = 128     # cap 256 class
 SCREEN_MAX_KT = 4       # A <= 128 on the screen path
 NUM_CUS = 256
-SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "stream")  # "stream" | "lds" (profiling/A-B)
+# "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
+SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
 
 
 def eps_rel(A: int) -> float:
@@ -177,15 +178,17 @@ class DeviceResult:
     checksum: "object"  # torch i64 [Q] (uint64 bits) or None
     k: np.ndarray
     n_fallback: int = 0
+    n_escalated: int = 0   # single-term screen overflows re-screened with the 3-term kernel
 
 
-def _choose_slices_stream(nq: int, qw: int, n_tiles: int, waves_per_cu: int = 4) -> int:
-    """Data slices for the streaming screen: one wave per (query block, slice).
+def _choose_slices_stream(nq: int, qw: int, n_tiles: int, waves_per_cu: int = 4,
+                          s_min: int = 1) -> int:
+    """Data slices for the streaming screens: one wave per (query block, slice).
     Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best;
-    never fewer than needed to keep a slice below 2^29 points (group-entry id range)."""
+    never fewer than needed to keep a slice inside the kernel's group-index range (s_min)."""
     nqb = (nq + qw - 1) // qw
     slots = waves_per_cu * NUM_CUS
-    s_min = max(1, -(-n_tiles * 64 // (1 << 29)))
+    s_min = max(1, s_min, -(-n_tiles * 64 // (1 << 29)))
     if nqb >= slots:
         # every extra slice repeats each query's threshold warm-up (candidate work grows ~S):
         # with a full round of waves already, a partial last round is cheaper than S > 1
@@ -252,23 +255,37 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
                                        _p(ds.bad), s), "prep_queries")
         kdev_eff = torch.from_numpy(kk.astype(np.int32)).to(dev, non_blocking=True)
         er = eps_rel(A)
-        # k <= 32 and A <= 64: barrier-free streaming kernel (cap 64); otherwise LDS-shared kernel
-        stream_qw = L.dmlp_screen_stream_qw(KT) if SCREEN_IMPL != "lds" else 0
-        for idx, streaming in ((cls_a, bool(stream_qw)), (cls_b, False)):
+        # k <= 32 and A <= 64: single-term (x1) or 3-term barrier-free streaming kernel;
+        # otherwise the LDS-shared 3-term kernel.  x1 queries whose candidates overflow (data
+        # too tight for the single-term bound) escalate to the 3-term screen, and only what
+        # overflows there takes the exact fallback.
+        x1_ok = SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(KT) > 0
+        stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
+
+        def screen_pass(idx, impl):
             nq = len(idx)
-            if nq == 0:
-                continue
             kcls = int(kk[idx].max())
-            cap = L.dmlp_screen_stream_cap(kcls) if streaming else (128 if idx is cls_a else 256)
-            qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
-            if streaming:
-                S = _choose_slices_stream(nq, stream_qw, ds.n_tiles,
+            if impl == "x1":
+                cap = L.dmlp_screen_x1_cap(kcls)
+                S = _choose_slices_stream(nq, L.dmlp_screen_x1_qw(KT), ds.n_tiles,
+                                          L.dmlp_screen_x1_waves_per_cu(kcls),
+                                          int(L.dmlp_screen_x1_min_slices(ds.n_tiles)))
+            elif impl == "stream":
+                cap = L.dmlp_screen_stream_cap(kcls)
+                S = _choose_slices_stream(nq, L.dmlp_screen_stream_qw(KT), ds.n_tiles,
                                           L.dmlp_screen_stream_waves_per_cu(kcls))
             else:
+                cap = 128 if kcls <= SCREEN_KMAX_A else 256
                 S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
+            qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
             cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
-            if streaming:
+            if impl == "x1":
+                _lib.check(L.dmlp_screen_x1(KT, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
+                                            _p(qhi), _p(qn), _p(qidx), _p(kdev_eff), nq, kcls,
+                                            _p(ds.xnmax_bits), _p(ds.bad), S, _p(cand_ids),
+                                            _p(cand_cnt), s), "screen_x1")
+            elif impl == "stream":
                 _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
                                                 _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff),
                                                 nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), er, S,
@@ -282,10 +299,24 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
                                      _p(qidx), _p(kdev_eff), nq, _p(out_d), _p(out_i), ks,
                                      _p(ds.labels) if want_fin else None, ds.label_lo,
                                      ds.label_hi, _p(lab), _p(cs), _p(status), s), "refine")
+
+        n_esc = 0
+        first_a = "x1" if x1_ok else ("stream" if stream_ok else "lds")
+        if len(cls_a):
+            screen_pass(cls_a, first_a)
+        if len(cls_b):
+            screen_pass(cls_b, "lds")
         # one host sync: which screened queries overflowed?
         n_ovf = int(status.sum().item())
+        if n_ovf and first_a == "x1":
+            st = status.cpu().numpy()
+            esc = cls_a[st[cls_a] != 0]
+            n_esc = len(esc)
+            if n_esc:
+                screen_pass(esc, "stream" if stream_ok else "lds")
+                n_ovf = int(status.sum().item())
     else:
-        n_ovf = 0
+        n_ovf = n_esc = 0
 
     fb = np.nonzero(~on_screen & (kk >= 1))[0]
     if n_ovf:
@@ -302,7 +333,7 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
             _lib.check(L.dmlp_finalize(_p(out_d), _p(out_i), ks, _p(k_dev), _p(ridx), len(rest),
                                        _p(ds.labels), ds.label_lo, ds.label_hi, _p(lab), _p(cs),
                                        s), "finalize")
-    return DeviceResult(out_d, out_i, lab, cs, k_host, int(len(fb)))
+    return DeviceResult(out_d, out_i, lab, cs, k_host, int(len(fb)), int(n_esc))
 
 
 _ENV_APPLIED = [False]

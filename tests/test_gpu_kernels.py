@@ -145,6 +145,40 @@ def test_many_slices_small_q(torch_cuda):
     assert_same(r, refs)
 
 
+@pytest.mark.parametrize("impl", ["x1", "stream", "lds"])
+def test_screen_impls_bench_distribution(torch_cuda, impl, monkeypatch):
+    """Every screen implementation is exact on the bench distribution (generate_input.py,
+    A=32, k=16); the single-term screen needs no 3-term escalation there."""
+    monkeypatch.setattr(K, "SCREEN_IMPL", impl)
+    inp = dmlp.generate(20000, 700, 32, 0.0, 1000.0, 16, 16, 10, seed=12)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 0
+    if impl == "x1":
+        assert r.n_escalated == 0
+    assert_same(r, refs)
+
+
+@pytest.mark.parametrize("A,kmax", [(8, 16), (32, 32), (64, 16), (40, 30)])
+def test_x1_screen_shapes(torch_cuda, A, kmax, monkeypatch):
+    """Single-term screen: KT 1/2, both sub-buffer depths (k <= 16 / <= 32), ragged tails."""
+    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    inp = dmlp.generate(7777, 333, A, -100.0, 100.0, 1, kmax, 6, seed=A + kmax)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 0
+    assert_same(r, refs)
+
+
+def test_x1_escalates_tight_data(torch_cuda, monkeypatch):
+    """Dense 1-D data: the single-term bound admits ~900 points per query (> its 60-group
+    buffer), so queries escalate to the 3-term screen (or on to the exact path) and stay exact."""
+    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    monkeypatch.setattr(K, "NUM_CUS", 1)  # few slices: ~5000 points per query block and slice
+    inp = dmlp.generate(20000, 100, 1, 0.0, 1000.0, 8, 16, 4, seed=2)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_escalated > 0
+    assert_same(r, refs)
+
+
 def test_merge_and_finalize(torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(1)
