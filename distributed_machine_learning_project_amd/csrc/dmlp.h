@@ -61,9 +61,10 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
                        const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
                        void* stream);
 // Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT <= 2: 64 queries
-// per workgroup, candidate ids per (query, slice) = dmlp_screen_x1_cap(kmax); A and the real point
-// count are needed for the error bound and to drop padding rows.  S >= dmlp_screen_x1_min_slices.
-// Same output contract as dmlp_screen.
+// per workgroup; A and the real point count are needed for the error bound and to drop padding
+// rows; S >= dmlp_screen_x1_min_slices.  Output per (query, slice): up to dmlp_screen_x1_cap(kmax)
+// 4-row GROUPS (first member id; count -1 = overflow) and the final threshold cand_h — consumed
+// by dmlp_refine_groups.
 int dmlp_screen_x1_kmax(void);
 int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cap(int kmax);
@@ -73,8 +74,11 @@ void dmlp_screen_x1_bound(int A, float* r1, float* r2);
 int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
                    int64_t n_points, const void* qhi, const float* qn, const int* qidx,
                    const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
-                   const unsigned* bad, int S, int* cand_ids, int* cand_cnt, void* stream);
+                   const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
+                   void* stream);
 void dmlp_set_x1_mode(int mode);
+
+void dmlp_set_x1_check(int steps);
 int dmlp_x1_debug_counters(unsigned long long* out, int reset);
 // Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off,
 // sub-buffer depth (8 / 16, 0 = automatic).
@@ -91,6 +95,15 @@ int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const 
                 int A, const double* Qx, const int* qidx, const int* qk, int nq, double* out_d,
                 int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
                 int* out_label, uint64_t* out_cs, int* status, void* stream);
+// Same for the single-term screen's group output: members of each group whose single-term score
+// (recomputed from xfrag / xinit / qhi, KT <= 2) reaches the (query, slice) threshold cand_h get
+// exact distances.  status = 1 also when the survivors exceed 256 (pathological ties).
+int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
+                       int S, const double* X, int A, const double* Qx, const void* xfrag,
+                       const float* xinit, const void* qhi, int KT, int64_t n_points,
+                       const int* qidx, const int* qk, int nq, double* out_d, int* out_i,
+                       int kstride, const int* labels, int label_lo, int label_hi,
+                       int* out_label, uint64_t* out_cs, int* status, void* stream);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

@@ -124,6 +124,36 @@ __device__ __forceinline__ T wave_pick(const T (&v)[E], int idx) {
   return __shfl(x, idx & 63);
 }
 
+// Histogram h[256] (LDS) of keys: the bin b holding the kk-th largest key, i.e.
+// sum(h[b+1..255]) < kk <= sum(h[b..255]); `above` += sum(h[b+1..255]).  -1 if sum(h) < kk.
+// One wave; lane L owns bins 255-4L .. 252-4L (top first).
+__device__ __forceinline__ int wave_kth_bin(const int* h, int kk, int& above) {
+  const int lane = threadIdx.x & 63;
+  int c[4], s = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { c[i] = h[255 - (4 * lane + i)]; s += c[i]; }
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  const unsigned long long hit = __ballot(incl >= kk);
+  if (!hit) return -1;
+  const int F = __ffsll((long long)hit) - 1;
+  int b = -1, acc = incl - s, ab = 0;
+  if (lane == F) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (b < 0 && acc + c[i] >= kk) { b = 255 - (4 * lane + i); ab = acc; }
+      acc += c[i];
+    }
+  }
+  b = __shfl(b, F);
+  above += __shfl(ab, F);
+  return b;
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   const int lane = lane_id();
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));

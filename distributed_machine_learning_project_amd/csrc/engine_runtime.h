@@ -214,7 +214,7 @@ struct LocalKnn {
   DevBuf<float> xinit;
   DevBuf<unsigned> words;  // [0] xnmax bits, [1] bad
   DevBuf<short> qhi, qlo;
-  DevBuf<float> qn;
+  DevBuf<float> qn, cand_h;
   DevBuf<int> qidx_a, qidx_b, qidx_e, qidx_f, kdev, cand_ids, cand_cnt, status;
   DevBuf<char> fb_ws;
   int KT = 1;
@@ -310,10 +310,16 @@ struct LocalKnn {
                                   : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);
-        if (impl == 0)
+        if (impl == 0) {
+          float* ch = cand_h.get((size_t)nq * S);
           DMLPCHK(dmlp_screen_x1(KT, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
-                                 words.p, words.p + 1, S, ci, cc, st));
-        else if (impl == 1)
+                                 words.p, words.p + 1, S, ci, cc, ch, st));
+          DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, N,
+                                     qi, kd, nq, out_d, out_i, kstride, fin ? labels : nullptr,
+                                     lab_lo, lab_hi, lab, cs, stat, st));
+          return;
+        }
+        if (impl == 1)
           DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq, kcls,
                                      words.p, words.p + 1, er, S, ci, cc, st));
         else

@@ -100,14 +100,30 @@ __device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* 
   }
 }
 
-template <int E>
+// Group-mode inputs (single-term screen, screen_x1.hip): candidates are 4-row group entries
+// (ordered 16-bit group-max key << 16 | slice-relative group index) and cand_h holds the query's
+// screen error bound eps.  The k-th largest key over all slices gives h = a_k' - 2 eps (a lower
+// bound on a_k - eps, exactly the screen's own rule, but global); a member survives iff its
+// single-term score  s = -|x'|^2/2 + <hi(q'), hi(x')>  (recomputed from the screen's bf16 image;
+// any summation order obeys the same error bound) is >= h.  Only survivors get exact distances.
+struct GroupIn {
+  const float* cand_h;    // [nq * S]
+  const u32x4* xfrag;     // prep.hip tile image (hi at hl = 0)
+  const float* xinit;     // -|x'|^2/2 per point
+  const bf16x8* qhi;      // [Q][KT*4] query hi fragments
+  int KT;
+  int n_points;
+  int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
+};
+
+template <int E, bool GROUPS>
 __global__ __launch_bounds__(256) void k_refine(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int S, int cap,
     const double* __restrict__ X, int A, const double* __restrict__ Qx,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
     int* __restrict__ out_i, int kstride, const int* __restrict__ labels, int label_lo,
     int label_hi, int* __restrict__ out_label, uint64_t* __restrict__ out_cs,
-    int* __restrict__ status) {
+    int* __restrict__ status, const GroupIn gin) {
   constexpr int P = E * 64;
   constexpr int SMAX = 256;
   constexpr int KMAX = 128;
@@ -143,18 +159,122 @@ __global__ __launch_bounds__(256) void k_refine(
   }
   if (lane == 0) status[q] = 0;
   dmlp::wave_sync();
-  const int M = pre[S];
+  int M = pre[S];
   const double* qv = Qx + (int64_t)q * A;
-  auto cand = [&](int j, double& dv, int& id) {
+  auto slice_of = [&](int j) {
     // slice containing flat index j: largest s with pre[s] <= j
     int lo = 0, hi = S;  // pre[lo] <= j < pre[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
       if (pre[mid] <= j) lo = mid; else hi = mid;
     }
-    id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
+    return lo;
+  };
+  auto cand = [&](int j, double& dv, int& id) {
+    if (GROUPS) {
+      id = s_i[wave][j];  // filtered members, staged below
+    } else {
+      const int lo = slice_of(j);
+      id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
+    }
     dv = exact_dist_row(qv, X + (int64_t)id * A, A);
   };
+  if (GROUPS) {
+    // ---- global threshold: k-th largest group key over all slices (two 8-bit histogram passes)
+    auto entry = [&](int j) {
+      const int lo = slice_of(j);
+      return (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
+    };
+    int* hist = s_hist[wave];
+    const float eps = gin.cand_h[(int64_t)p * S];
+    float hq = -INFINITY;
+    if (M >= k && k >= 1) {
+      int above = 0;
+      int b1 = -1, b2 = -1;
+#pragma unroll 1
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int i = lane; i < 256; i += 64) hist[i] = 0;
+        dmlp::wave_sync();
+        for (int j = lane; j < M; j += 64) {
+          const unsigned e = entry(j);
+          if (pass == 0) atomicAdd(&hist[e >> 24], 1);
+          else if ((int)(e >> 24) == b1) atomicAdd(&hist[(e >> 16) & 255], 1);
+        }
+        dmlp::wave_sync();
+        const int b = dmlp::wave_kth_bin(hist, k - above, above);
+        dmlp::wave_sync();
+        if (pass == 0) b1 = b; else b2 = b;
+      }
+      const unsigned T = ((unsigned)b1 << 24) | ((unsigned)b2 << 16);
+      const unsigned tb = T ^ ((T >> 31) ? 0x80000000u : 0xffffffffu);  // ordered -> fp32 bits
+      hq = __uint_as_float(tb) - 2.0f * eps;
+    }
+    const unsigned tq = __float_as_uint(hq);
+    const unsigned kh = (tq ^ ((unsigned)((int)tq >> 31) | 0x80000000u)) & 0xffff0000u;
+    // ---- expand surviving groups; keep members whose single-term score reaches hq
+    const int KT = gin.KT;
+    float qf[2 * 32];  // KT <= 2: hi(q') as fp32, k-fragment order
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      if (f < KT * 4) {
+        const u32x4 w = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qf[f * 8 + 2 * e] = __uint_as_float(w[e] << 16);
+          qf[f * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+        }
+      }
+    }
+    int nm = 0;
+    for (int g0 = 0; g0 < M; g0 += 64) {
+      const int g = g0 + lane;
+      bool gv = g < M;
+      int base = 0;
+      if (gv) {
+        const int lo = slice_of(g);
+        const unsigned e = (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (g - pre[lo])];
+        gv = e >= kh;
+        base = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int id = base + r;
+        bool keep = false;
+        if (gv && id < gin.n_points) {
+          const int64_t t = id >> 6;
+          const int pl = id & 63;
+          const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * 2 * 64) + (pl & 15);
+          float sc = gin.xinit[id];
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) {
+            if (kt >= KT) break;
+            const u32x4* fk = fr + (int64_t)(((pl >> 4) * KT + kt) * 2) * 64;
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {
+              const u32x4 w = fk[16 * kq];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                sc += qf[(kt * 4 + kq) * 8 + 2 * e] * __uint_as_float(w[e] << 16);
+                sc += qf[(kt * 4 + kq) * 8 + 2 * e + 1] * __uint_as_float(w[e] & 0xffff0000u);
+              }
+            }
+          }
+          keep = sc >= hq;
+        }
+        const unsigned long long km = __ballot(keep);
+        const int pos = nm + __popcll(km & dmlp::lanemask_lt());
+        if (keep && pos < P) s_i[wave][pos] = id;
+        nm += __popcll(km);
+      }
+    }
+    if (nm > P) {
+      // pathological ties: hand the query back (x1 overflow -> 3-term screen escalation)
+      if (lane == 0) status[q] = 1;
+      return;
+    }
+    M = nm;
+    dmlp::wave_sync();
+  }
   const double* res_d;
   const int* res_i;
   if (M <= P && k <= KMAX) {
@@ -166,7 +286,7 @@ __global__ __launch_bounds__(256) void k_refine(
       double dv; int id;
       cand(j, dv, id);
       cd[j] = dv;
-      ci[j] = id;
+      if (!GROUPS) ci[j] = id;
     }
     for (int i = lane; i < k; i += 64) { s_rd[wave][i] = INFINITY; s_ri[wave][i] = -1; }
     dmlp::wave_sync();
@@ -418,17 +538,31 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   if (S < 1 || S > 256) return -1;
   const dim3 grid((nq + 3) / 4), block(256);
   hipStream_t st = (hipStream_t)stream;
-  // cap is the id stride per (query, slice); P = E*64 must exceed k + 64 (k <= 128)
+  // cap is only the id stride per (query, slice).  P = 256 slots cover k + 64 for every screened
+  // k (<= 128); a larger P would cut the resident waves that hide the row-gather latency
   if (cap < 1) return -2;
-  if (cap <= 128) {
-    hipLaunchKernelGGL(k_refine<4>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
-                       qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
-                       out_label, out_cs, status);
-  } else {
-    hipLaunchKernelGGL(k_refine<8>, grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A, Qx,
-                       qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
-                       out_label, out_cs, status);
-  }
+  hipLaunchKernelGGL((k_refine<4, false>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
+                     Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
+                     out_label, out_cs, status, GroupIn{});
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt,
+                                  const float* cand_h, int S, const double* X, int A,
+                                  const double* Qx, const void* xfrag, const float* xinit,
+                                  const void* qhi, int KT, int64_t n_points, const int* qidx,
+                                  const int* qk, int nq, double* out_d, int* out_i, int kstride,
+                                  const int* labels, int label_lo, int label_hi, int* out_label,
+                                  uint64_t* out_cs, int* status, void* stream) {
+  if (nq <= 0) return 0;
+  if (S < 1 || S > 256 || cap < 1 || KT < 1 || KT > 2 || n_points > 0x7fffffff) return -1;
+  const int64_t n_tiles = (n_points + 63) / 64;
+  const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, (int)n_points,
+                    (int)((n_tiles + S - 1) / S)};
+  hipLaunchKernelGGL((k_refine<4, true>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride,
+                     labels, label_lo, label_hi, out_label, out_cs, status, gin);
   DMLP_LAUNCH_CHECK();
   return 0;
 }

@@ -32,17 +32,19 @@ namespace {
 int g_x1_mode = 0;  // profiling: 1 no candidate path, 8 event counters (g_x1_dbg)
 __device__ unsigned long long g_x1_dbg[8];
 
-template <int KT, int SUB>
+template <int KT, int SUB, int DEPTH, int CHECK>
 struct X1Cfg {
   static constexpr int CT = 4;                  // MFMA column tiles per wave
   static constexpr int NCOL = 16 * CT;          // queries per wave (= workgroup)
   static constexpr int SUBP = SUB + 1;          // pitch: the 64 lanes of an append hit 64 banks
-  static constexpr int CAPE = 4 * (SUB - 1);    // group entries a column may keep
-  static constexpr int IDCAP = 4 * CAPE;        // candidate ids per (query, slice)
+  // the fill check runs every CHECK steps, so a sub-buffer is compacted once it holds more than
+  // SUB - CHECK entries (CHECK more appends always fit) and keeps at most SUB - CHECK of them
+  static constexpr int CAPE = 4 * (SUB - CHECK);  // group entries a column may keep
+  static constexpr int IDCAP = 4 * (SUB - 1);  // group-id stride per (query, slice), any CHECK
   static constexpr int FRAGS = 4 * KT * 2;      // 1 KiB fragments per 64-point tile (hi, lo)
   static constexpr int SBUF = NCOL * 4 * SUBP * 4;
   static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4;
-  static constexpr int D = 4;                   // register-ring depth (steps in flight)
+  static constexpr int D = DEPTH;               // register-ring depth (steps in flight)
 };
 
 // fp32 bits -> order-preserving u32 (only the top 16 bits are meaningful for a truncated key)
@@ -53,14 +55,15 @@ __device__ __forceinline__ unsigned unord32(unsigned o) {
   return o ^ ((o >> 31) ? 0x80000000u : 0xffffffffu);
 }
 
-template <int KT, int SUB, int MODE>
+template <int KT, int SUB, int DEPTH, int CHECK, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_screen_x1(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
     const unsigned* __restrict__ bad, float r1, float r2, int S, int tiles_per_slice,
-    int n_qblocks, int* __restrict__ cand_ids, int* __restrict__ cand_cnt) {
-  using C = X1Cfg<KT, SUB>;
+    int n_qblocks, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
+    float* __restrict__ cand_h) {
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
   constexpr int CT = C::CT;
   constexpr int SUBP = C::SUBP;
   constexpr int D = C::D;
@@ -223,26 +226,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       // pending after the conditional call and drains lgkmcnt at every following step
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     } else {
+      // kept entries out as (ordered 16-bit key << 16 | slice-relative group index): the refine
+      // takes the k-th largest key over ALL slices of the query (a global threshold, as tight as
+      // one slice), then keeps the members whose recomputed single-term score reaches it
       const int p = pbase + j;
       if (p < nq) {
         int* const out = cand_ids + ((int64_t)p * S + s) * C::IDCAP;
-        int nout = 0;
         int kept = 0;
-        const int gbase = t0 * 64;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
           for (int i = 0; i < SUB; ++i) {
             const bool keep = !flag && e[m][i] >= kh && e[m][i] != 0u;
-            if (keep && kept < C::CAPE) {
-              const int base = gbase + (int)(unord32(e[m][i]) & 0xffffu) * 4;
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (base + r < n_points) out[nout++] = base + r;
-            }
+            if (keep && kept < C::CAPE)
+              out[kept] = (int)((e[m][i] & 0xffff0000u) | (unord32(e[m][i]) & 0xffffu));
             kept += keep ? 1 : 0;
           }
-        cand_cnt[(int64_t)p * S + s] = (flag || kept > C::CAPE) ? -1 : nout;
+        cand_cnt[(int64_t)p * S + s] = (flag || kept > C::CAPE) ? -1 : kept;
+        cand_h[(int64_t)p * S + s] = epc;
       }
     }
   };
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     if (MODE & 8) {                                                                             \
       if (lane == 0) atomicAdd(&g_x1_dbg[0], 1ull);                                             \
     }                                                                                           \
-    if (!(MODE & 1) && __ballot(any_)) {                                                        \
+    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && __ballot(any_)) {                        \
       if (MODE & 8) {                                                                           \
         int np_ = 0;                                                                            \
         _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += hit_[ct] ? 1 : 0;              \
@@ -290,16 +291,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       /* branch-free: every lane writes its entry to the next free slot and advances only on  \
          a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
       const unsigned gl_ = (unsigned)((J) * 4 + kg);                                            \
-      bool trig_ = false;                                                                       \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
         mysub[ct * 64 * SUBP + cnt[ct]] = (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;        \
         cnt[ct] += hit_[ct] ? 1 : 0;                                                            \
-        trig_ |= cnt[ct] >= SUB;                                                                \
+        trig |= cnt[ct] > SUB - CHECK;                                                          \
       }                                                                                         \
-      if (__ballot(trig_)) compact(false);                                                      \
     }                                                                                           \
   } while (0)
+  // one compaction call site per CHECK steps (each inlined copy is ~8 KiB of code: one per
+  // step of the unrolled ring would not stay in the instruction cache)
+#define DMLP_CHECK()                                                                            \
+  do {                                                                                          \
+    if (__ballot(trig)) compact(false);                                                         \
+    trig = false;                                                                               \
+  } while (0)
 
+  bool trig = false;
   if (nsteps > 0) {
     // prologue in the loop's issue order (A, Xi per step), so the waitcnt at the loop head is
     // the steady-state vmcnt(2 * (D - 1)), not a merge with a reordered prologue
@@ -311,17 +318,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     for (int j0 = 0; j0 < nsteps; j0 += D) {
 #pragma unroll
       for (int r = 0; r < D; ++r) {
-        const int j = j0 + r;  // nsteps % 4 == 0 and D == 4: j < nsteps inside the body
+        const int j = j0 + r;  // D = 4: j < nsteps (nsteps % 4 == 0); D = 8: guarded epilogue
         DMLP_MFMA(r, r & 1);
         DMLP_LOAD(j + D, r);
         if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
+        if (r % CHECK == CHECK - 1) DMLP_CHECK();
       }
     }
-    DMLP_EPILOGUE((nsteps - 1) & 1, nsteps - 1);
+    // the last issued step (padded up to a multiple of D; the guard skips padding for D = 8)
+    const int jl = ((nsteps + D - 1) / D) * D - 1;
+    DMLP_EPILOGUE(jl & 1, jl);
   }
 #undef DMLP_LOAD
 #undef DMLP_MFMA
 #undef DMLP_EPILOGUE
+#undef DMLP_CHECK
   if (MODE & 1) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[0][ct]), "v"(acc[1][ct]));
@@ -332,21 +343,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
 int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
 
-template <int KT, int SUB>
+int g_x1_check = 2;
+
+template <int KT, int SUB, int DEPTH, int CHECK>
 int launch_x1(const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, int S,
-              int* cand_ids, int* cand_cnt, hipStream_t stream) {
-  using C = X1Cfg<KT, SUB>;
+              int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream) {
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
   const int64_t grid = (int64_t)n_qblocks * S;
   if (grid <= 0) return 0;
 #define DMLP_X1_LAUNCH(M)                                                                      \
-  hipLaunchKernelGGL((k_screen_x1<KT, SUB, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
+  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, S, tps,          \
-                     n_qblocks, cand_ids, cand_cnt)
+                     n_qblocks, cand_ids, cand_cnt, cand_h)
   switch (g_x1_mode) {
     case 1: DMLP_X1_LAUNCH(1); break;
     case 8: DMLP_X1_LAUNCH(8); break;
@@ -374,12 +387,15 @@ extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
 }
 extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
 extern "C" int dmlp_screen_x1_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
-extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * 4 * (x1_sub(kmax) - 1); }
+// group ids per (query, slice) (refine expands each to its 4 members)
+extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
 // resident workgroups (= waves) per CU, LDS-bound: 19.5 KiB (SUB 16) / 36.3 KiB (SUB 32)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }
 // a slice must stay below 2^16 4-row groups (16-bit group index in an entry)
 extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles + 4095) / 4096; }
 extern "C" void dmlp_set_x1_mode(int mode) { g_x1_mode = mode; }
+// steps between fill checks (1, 2, 4) of the KT = 1, k <= 16 variant (A/B)
+extern "C" void dmlp_set_x1_check(int c) { g_x1_check = (c == 1 || c == 4) ? c : 2; }
 extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_dbg), sizeof(g_x1_dbg));
   if (e != hipSuccess) return -(int)e;
@@ -395,7 +411,7 @@ extern "C" int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xin
                               int64_t n_tiles, int64_t n_points, const void* qhi, const float* qn,
                               const int* qidx, const int* qk, int nq, int kmax,
                               const unsigned* xnmax_bits, const unsigned* bad, int S,
-                              int* cand_ids, int* cand_cnt, void* stream) {
+                              int* cand_ids, int* cand_cnt, float* cand_h, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 || n_points > n_tiles * 64) return -1;
   if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
@@ -404,9 +420,14 @@ extern "C" int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xin
   dmlp_screen_x1_bound(A, &r1, &r2);
   hipStream_t st = (hipStream_t)stream;
 #define DMLP_X1_ARGS xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
-                     r2, S, cand_ids, cand_cnt, st
+                     r2, S, cand_ids, cand_cnt, cand_h, st
   const int sub = x1_sub(kmax);
-  if (KT == 1) return sub == 16 ? launch_x1<1, 16>(DMLP_X1_ARGS) : launch_x1<1, 32>(DMLP_X1_ARGS);
-  return sub == 16 ? launch_x1<2, 16>(DMLP_X1_ARGS) : launch_x1<2, 32>(DMLP_X1_ARGS);
+  if (KT == 1 && sub == 16) {  // A/B variants of the bench shape: fill-check period
+    if (g_x1_check == 1) return launch_x1<1, 16, 4, 1>(DMLP_X1_ARGS);
+    if (g_x1_check == 4) return launch_x1<1, 16, 4, 4>(DMLP_X1_ARGS);
+    return launch_x1<1, 16, 4, 2>(DMLP_X1_ARGS);
+  }
+  if (KT == 1) return launch_x1<1, 32, 4, 2>(DMLP_X1_ARGS);
+  return sub == 16 ? launch_x1<2, 16, 4, 2>(DMLP_X1_ARGS) : launch_x1<2, 32, 4, 2>(DMLP_X1_ARGS);
 #undef DMLP_X1_ARGS
 }

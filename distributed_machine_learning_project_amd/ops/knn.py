@@ -281,10 +281,17 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
             cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
             if impl == "x1":
+                cand_h = torch.empty(nq * S, dtype=torch.float32, device=dev)
                 _lib.check(L.dmlp_screen_x1(KT, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
                                             _p(qhi), _p(qn), _p(qidx), _p(kdev_eff), nq, kcls,
                                             _p(ds.xnmax_bits), _p(ds.bad), S, _p(cand_ids),
-                                            _p(cand_cnt), s), "screen_x1")
+                                            _p(cand_cnt), _p(cand_h), s), "screen_x1")
+                _lib.check(L.dmlp_refine_groups(
+                    cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(Qx),
+                    _p(ds.xfrag), _p(ds.xinit), _p(qhi), KT, N, _p(qidx), _p(kdev_eff), nq,
+                    _p(out_d), _p(out_i), ks, _p(ds.labels) if want_fin else None, ds.label_lo,
+                    ds.label_hi, _p(lab), _p(cs), _p(status), s), "refine_groups")
+                return
             elif impl == "stream":
                 _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
                                                 _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff),
@@ -344,6 +351,8 @@ def _apply_env_switches(L):
     if not _ENV_APPLIED[0]:
         if os.environ.get("DMLP_STREAM_GROUPS", "1") == "0":
             L.dmlp_set_stream_groups(0)
+        if os.environ.get("DMLP_X1_CHECK"):
+            L.dmlp_set_x1_check(int(os.environ["DMLP_X1_CHECK"]))
         if os.environ.get("DMLP_STREAM_SUB"):
             L.dmlp_set_stream_sub(int(os.environ["DMLP_STREAM_SUB"]))
         _ENV_APPLIED[0] = True

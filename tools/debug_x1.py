@@ -37,10 +37,11 @@ def run(name, inp):
     kd = torch.from_numpy(kk).cuda()
     ci = torch.empty(Q * S * cap, dtype=torch.int32, device="cuda")
     cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
+    ch = torch.empty(Q * S, dtype=torch.float32, device="cuda")
     _lib.check(L.dmlp_screen_x1(KT, A, ds.xfrag.data_ptr(), ds.xinit.data_ptr(), ds.n_tiles, ds.N,
                                 qhi.data_ptr(), qn.data_ptr(), qidx.data_ptr(), kd.data_ptr(), Q,
                                 kmax, ds.xnmax_bits.data_ptr(), ds.bad.data_ptr(), S,
-                                ci.data_ptr(), cc.data_ptr(), s), "x1")
+                                ci.data_ptr(), cc.data_ptr(), ch.data_ptr(), s), "x1")
     torch.cuda.synchronize()
     import ctypes
     r1, r2 = ctypes.c_float(), ctypes.c_float()
@@ -49,7 +50,7 @@ def run(name, inp):
     c = cc.cpu().numpy()
     print(f"{name}: N={ds.N} A={A} Q={Q} cap={cap} r1={r1.value:.3g} r2={r2.value:.3g} "
           f"xnmax={xn:.4g} qn[0]={qn[0].item():.4g}")
-    print(f"   cand_cnt: min {c.min()} mean {c[c >= 0].mean() if (c >= 0).any() else -1:.1f} "
+    print(f"   groups: min {c.min()} mean {c[c >= 0].mean() if (c >= 0).any() else -1:.1f} "
           f"max {c.max()} overflow {(c < 0).sum()}")
     # true candidates within the bound for query 0
     Xc = inp.X - ds.mu.cpu().numpy()
@@ -64,7 +65,64 @@ def run(name, inp):
 def main():
     run("bench", dmlp.generate(20000, 512, 32, 0.0, 1000.0, 16, 16, 10, seed=12))
     run("dense1d", dmlp.generate(20000, 128, 1, 0.0, 1000.0, 8, 16, 4, seed=2))
+    run("bench100k", dmlp.generate(100000, 4096, 32, 0.0, 1000.0, 16, 16, 10, seed=42))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("REFINE_CHECK"):
     main()
+
+
+def refine_check():
+    """Run screen_x1 + refine_groups on a small bench-shaped input and print statuses."""
+    L = _lib.lib()
+    inp = dmlp.generate(20000, 700, 32, 0.0, 1000.0, 16, 16, 10, seed=12)
+    X = torch.from_numpy(inp.X).cuda()
+    Qx = torch.from_numpy(inp.Qx).cuda()
+    lab = torch.from_numpy(inp.labels).cuda()
+    ds = K.prepare_dataset(X, lab, (0, 10))
+    r = K.knn_gpu(ds, Qx, inp.k)
+    print("knn_gpu: escalated", r.n_escalated, "fallback", r.n_fallback)
+    Q, A = inp.Qx.shape
+    KT = ds.KT
+    kk = np.minimum(inp.k, ds.N).astype(np.int32)
+    qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device="cuda")
+    qlo = torch.empty_like(qhi)
+    qn = torch.empty(Q, dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    P = lambda t: t.data_ptr()
+    _lib.check(L.dmlp_prep_queries(P(Qx), Q, A, P(ds.mu), KT, P(qhi), P(qlo), P(qn), P(ds.bad), s), "prep")
+    for S in (1, 8):
+        cap = L.dmlp_screen_x1_cap(16)
+        qidx = torch.arange(Q, dtype=torch.int32, device="cuda")
+        kd = torch.from_numpy(kk).cuda()
+        ci = torch.zeros(Q * S * cap, dtype=torch.int32, device="cuda")
+        cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
+        ch = torch.empty(Q * S, dtype=torch.float32, device="cuda")
+        _lib.check(L.dmlp_screen_x1(KT, A, P(ds.xfrag), P(ds.xinit), ds.n_tiles, ds.N, P(qhi), P(qn),
+                                    P(qidx), P(kd), Q, 16, P(ds.xnmax_bits), P(ds.bad), S, P(ci),
+                                    P(cc), P(ch), s), "x1")
+        od = torch.full((Q, 16), float("inf"), dtype=torch.float64, device="cuda")
+        oi = torch.full((Q, 16), -1, dtype=torch.int32, device="cuda")
+        lb = torch.empty(Q, dtype=torch.int32, device="cuda")
+        cs = torch.empty(Q, dtype=torch.int64, device="cuda")
+        st = torch.zeros(Q, dtype=torch.int32, device="cuda")
+        _lib.check(L.dmlp_refine_groups(cap, P(ci), P(cc), P(ch), S, P(ds.X), A, P(Qx), P(ds.xfrag),
+                                        P(ds.xinit), P(qhi), KT, ds.N, P(qidx), P(kd), Q, P(od),
+                                        P(oi), 16, P(lab), 0, 10, P(lb), P(cs), P(st), s), "rg")
+        torch.cuda.synchronize()
+        c = cc.cpu().numpy().reshape(Q, S)
+        h = ch.cpu().numpy().reshape(Q, S)
+        print(f"S={S}: groups/slice min {c.min()} max {c.max()} mean {c.mean():.1f}; h[0]={h[0]}; "
+              f"status sum {int(st.sum())}")
+        g0 = ci.cpu().numpy()[:c[0, 0]]
+        print("   q0 groups:", g0[:12])
+        Xc = inp.X - ds.mu.cpu().numpy()
+        q0 = inp.Qx[0] - ds.mu.cpu().numpy()
+        a = Xc @ q0 - (Xc ** 2).sum(1) / 2
+        mem = np.concatenate([np.arange(g, g + 4) for g in g0])
+        print("   q0 members with exact a >= h:", int((a[mem] >= h[0].max()).sum()), "of", len(mem),
+              " exact a_k", np.sort(a)[-16])
+
+
+if __name__ == "__main__" and os.environ.get("REFINE_CHECK"):
+    refine_check()

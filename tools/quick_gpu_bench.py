@@ -93,7 +93,8 @@ def main():
             times.append(t1 - t0)
     ms = 1e3 * float(np.median(times))
     print(f"N={a.n} Q={a.q} A={a.a} k=[{a.kmin},{a.kmax}] exact={a.exact}: {ms:.3f} ms "
-          f"-> {a.q / ms * 1e3:.0f} queries/s  fallback={r.n_fallback}")
+          f"-> {a.q / ms * 1e3:.0f} queries/s  fallback={r.n_fallback} "
+          f"escalated={r.n_escalated}")
     if a.check:
         nc = min(a.check, a.q)
         d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx[:nc], inp.k[:nc], kstride=r.ids.shape[1])
