@@ -63,8 +63,8 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
 // Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT <= 2: 64 queries
 // per workgroup; A and the real point count are needed for the error bound and to drop padding
 // rows; S >= dmlp_screen_x1_min_slices.  Output per (query, slice): up to dmlp_screen_x1_cap(kmax)
-// 4-row GROUPS (first member id; count -1 = overflow) and the final threshold cand_h — consumed
-// by dmlp_refine_groups.
+// 4-row group entries (ordered 16-bit key << 16 | slice-relative group index; count -1 =
+// overflow) and cand_h[2] = {slice threshold, query eps} — consumed by dmlp_refine_groups.
 int dmlp_screen_x1_kmax(void);
 int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cap(int kmax);

@@ -311,7 +311,7 @@ struct LocalKnn {
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);
         if (impl == 0) {
-          float* ch = cand_h.get((size_t)nq * S);
+          float* ch = cand_h.get((size_t)nq * S * 2);
           DMLPCHK(dmlp_screen_x1(KT, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
                                  words.p, words.p + 1, S, ci, cc, ch, st));
           DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, N,

@@ -101,13 +101,13 @@ __device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* 
 }
 
 // Group-mode inputs (single-term screen, screen_x1.hip): candidates are 4-row group entries
-// (ordered 16-bit group-max key << 16 | slice-relative group index) and cand_h holds the query's
-// screen error bound eps.  The k-th largest key over all slices gives h = a_k' - 2 eps (a lower
+// (ordered 16-bit group-max key << 16 | slice-relative group index) and cand_h holds each
+// slice's final threshold and the query's screen error bound eps.  The k-th largest key over all slices gives h = a_k' - 2 eps (a lower
 // bound on a_k - eps, exactly the screen's own rule, but global); a member survives iff its
 // single-term score  s = -|x'|^2/2 + <hi(q'), hi(x')>  (recomputed from the screen's bf16 image;
 // any summation order obeys the same error bound) is >= h.  Only survivors get exact distances.
 struct GroupIn {
-  const float* cand_h;    // [nq * S]
+  const float* cand_h;    // [nq * S][2]: slice threshold, query eps
   const u32x4* xfrag;     // prep.hip tile image (hi at hl = 0)
   const float* xinit;     // -|x'|^2/2 per point
   const bf16x8* qhi;      // [Q][KT*4] query hi fragments
@@ -186,9 +186,9 @@ __global__ __launch_bounds__(256) void k_refine(
       return (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
     };
     int* hist = s_hist[wave];
-    const float eps = gin.cand_h[(int64_t)p * S];
-    float hq = -INFINITY;
-    if (M >= k && k >= 1) {
+    const float eps = gin.cand_h[2 * (int64_t)p * S + 1];
+    float hq = S == 1 ? gin.cand_h[2 * (int64_t)p] : -INFINITY;  // one slice: already global
+    if (S > 1 && M >= k && k >= 1) {
       int above = 0;
       int b1 = -1, b2 = -1;
 #pragma unroll 1

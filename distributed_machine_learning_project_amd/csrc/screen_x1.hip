@@ -243,7 +243,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             kept += keep ? 1 : 0;
           }
         cand_cnt[(int64_t)p * S + s] = (flag || kept > C::CAPE) ? -1 : kept;
-        cand_h[(int64_t)p * S + s] = epc;
+        cand_h[2 * ((int64_t)p * S + s)] = hc;       // this slice's final threshold
+        cand_h[2 * ((int64_t)p * S + s) + 1] = epc;  // the query's error bound
       }
     }
   };

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -182,12 +183,12 @@ class DeviceResult:
 
 
 def _choose_slices_stream(nq: int, qw: int, n_tiles: int, waves_per_cu: int = 4,
-                          s_min: int = 1) -> int:
+                          s_min: int = 1, cus: int = NUM_CUS) -> int:
     """Data slices for the streaming screens: one wave per (query block, slice).
     Pick the smallest S whose last round of waves is >= 90 % full (the tail), else the best;
     never fewer than needed to keep a slice inside the kernel's group-index range (s_min)."""
     nqb = (nq + qw - 1) // qw
-    slots = waves_per_cu * NUM_CUS
+    slots = waves_per_cu * cus
     s_min = max(1, s_min, -(-n_tiles * 64 // (1 << 29)))
     if nqb >= slots:
         # every extra slice repeats each query's threshold warm-up (candidate work grows ~S):
@@ -218,129 +219,298 @@ def knn_gpu(ds: DeviceDataset, Qx, k_host: np.ndarray, finalize: bool = True,
     """Exact top-k of every query row of Qx (torch f64 cuda [Q, A]) against ds.
 
     k_host: numpy int32 [Q] (host copy of the per-query k; drives the dispatch)."""
-    torch = _torch()
-    L = _lib.lib()
-    Qx = Qx.contiguous()
-    Q, A = Qx.shape
-    assert A == ds.A
-    dev = Qx.device
-    k_host = np.ascontiguousarray(k_host, np.int32)
-    ks = max(1, int(k_host.max()) if Q else 1) if kstride is None else kstride
-    k_dev = torch.from_numpy(k_host).to(dev, non_blocking=True)
-    out_d = torch.full((Q, ks), float("inf"), dtype=torch.float64, device=dev)
-    out_i = torch.full((Q, ks), -1, dtype=torch.int32, device=dev)
-    want_fin = finalize and ds.labels is not None
-    lab = torch.empty(Q, dtype=torch.int32, device=dev) if want_fin else None
-    cs = torch.empty(Q, dtype=torch.int64, device=dev) if want_fin else None
-    s = _stream()
-    N = ds.N
-    kk = np.minimum(k_host, N)  # k > N: pad with (+inf,-1) like bench_2's sentinel
+    _ARENA.reset()
+    r = _KnnCall(ds, Qx, k_host, finalize, exact, kstride).launch().finish()
+    _ARENA.mark()
+    return r
 
-    _apply_env_switches(L)
-    use_screen = ds.screen_ok and not exact and Q > 0
-    cls_a = np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if use_screen else np.empty(0, np.int64)
-    cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
-             if use_screen else np.empty(0, np.int64))
-    on_screen = np.zeros(Q, bool)
-    on_screen[cls_a] = True
-    on_screen[cls_b] = True
-    status = torch.zeros(Q, dtype=torch.int32, device=dev)
 
-    if use_screen and (len(cls_a) or len(cls_b)):
+class _KnnCall:
+    """One local k-NN call split into an asynchronous launch (prep + screen + refine on the
+    current stream, no host sync) and a finish (one sync for the overflow status, then the
+    3-term escalation / exact fallback / finalize of the few queries that need it).  The split
+    lets knn_gpu_pipelined keep several query chunks in flight on their own streams."""
+
+    def __init__(self, ds, Qx, k_host, finalize=True, exact=False, kstride=None, gpu_share=1.0):
+        torch = _torch()
+        self.ds = ds
+        self.Qx = Qx.contiguous()
+        self.Q, self.A = self.Qx.shape
+        assert self.A == ds.A
+        self.dev = self.Qx.device
+        self.k_host = np.ascontiguousarray(k_host, np.int32)
+        Q = self.Q
+        self.ks = max(1, int(self.k_host.max()) if Q else 1) if kstride is None else kstride
+        self.exact = exact
+        self.gpu_share = gpu_share
+        self.want_fin = finalize and ds.labels is not None
+        self.kk = np.minimum(self.k_host, ds.N)  # k > N: pad with (+inf,-1) like bench_2
+        dev = self.dev
+        self.k_dev = _h2d(self.k_host, dev)
+        self.out_d = torch.full((Q, self.ks), float("inf"), dtype=torch.float64, device=dev)
+        self.out_i = torch.full((Q, self.ks), -1, dtype=torch.int32, device=dev)
+        self.lab = torch.empty(Q, dtype=torch.int32, device=dev) if self.want_fin else None
+        self.cs = torch.empty(Q, dtype=torch.int64, device=dev) if self.want_fin else None
+        self.status = torch.zeros(Q, dtype=torch.int32, device=dev)
+
+    # ------------------------------------------------------------------ launch (async)
+    def launch(self):
+        torch = _torch()
+        L = _lib.lib()
+        _apply_env_switches(L)
+        ds, kk, Q, A = self.ds, self.kk, self.Q, self.A
+        self.use_screen = ds.screen_ok and not self.exact and Q > 0
+        empty = np.empty(0, np.int64)
+        self.cls_a = np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if self.use_screen else empty
+        self.cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
+                      if self.use_screen else empty)
+        self.on_screen = np.zeros(Q, bool)
+        self.on_screen[self.cls_a] = True
+        self.on_screen[self.cls_b] = True
+        self.screened = self.use_screen and (len(self.cls_a) or len(self.cls_b))
+        self.stream = _torch().cuda.current_stream()
+        if not self.screened:
+            return self
         KT = ds.KT
-        qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
-        qlo = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
-        qn = torch.empty(Q, dtype=torch.float32, device=dev)
-        _lib.check(L.dmlp_prep_queries(_p(Qx), Q, A, _p(ds.mu), KT, _p(qhi), _p(qlo), _p(qn),
-                                       _p(ds.bad), s), "prep_queries")
-        kdev_eff = torch.from_numpy(kk.astype(np.int32)).to(dev, non_blocking=True)
-        er = eps_rel(A)
+        dev = self.dev
+        self.qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
+        self.qlo = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
+        self.qn = torch.empty(Q, dtype=torch.float32, device=dev)
+        _lib.check(L.dmlp_prep_queries(_p(self.Qx), Q, A, _p(ds.mu), KT, _p(self.qhi),
+                                       _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
+                   "prep_queries")
+        self.kdev_eff = _h2d(kk.astype(np.int32), dev)
         # k <= 32 and A <= 64: single-term (x1) or 3-term barrier-free streaming kernel;
         # otherwise the LDS-shared 3-term kernel.  x1 queries whose candidates overflow (data
         # too tight for the single-term bound) escalate to the 3-term screen, and only what
         # overflows there takes the exact fallback.
         x1_ok = SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(KT) > 0
-        stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
+        self.stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
+        self.first_a = "x1" if x1_ok else ("stream" if self.stream_ok else "lds")
+        if len(self.cls_a):
+            self._screen_pass(self.cls_a, self.first_a)
+        if len(self.cls_b):
+            self._screen_pass(self.cls_b, "lds")
+        return self
 
-        def screen_pass(idx, impl):
-            nq = len(idx)
-            kcls = int(kk[idx].max())
-            if impl == "x1":
-                cap = L.dmlp_screen_x1_cap(kcls)
-                S = _choose_slices_stream(nq, L.dmlp_screen_x1_qw(KT), ds.n_tiles,
-                                          L.dmlp_screen_x1_waves_per_cu(kcls),
-                                          int(L.dmlp_screen_x1_min_slices(ds.n_tiles)))
-            elif impl == "stream":
-                cap = L.dmlp_screen_stream_cap(kcls)
-                S = _choose_slices_stream(nq, L.dmlp_screen_stream_qw(KT), ds.n_tiles,
-                                          L.dmlp_screen_stream_waves_per_cu(kcls))
-            else:
-                cap = 128 if kcls <= SCREEN_KMAX_A else 256
-                S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
-            qidx = torch.from_numpy(idx.astype(np.int32)).to(dev, non_blocking=True)
-            cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
-            cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
-            if impl == "x1":
-                cand_h = torch.empty(nq * S, dtype=torch.float32, device=dev)
-                _lib.check(L.dmlp_screen_x1(KT, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
-                                            _p(qhi), _p(qn), _p(qidx), _p(kdev_eff), nq, kcls,
-                                            _p(ds.xnmax_bits), _p(ds.bad), S, _p(cand_ids),
-                                            _p(cand_cnt), _p(cand_h), s), "screen_x1")
-                _lib.check(L.dmlp_refine_groups(
-                    cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(Qx),
-                    _p(ds.xfrag), _p(ds.xinit), _p(qhi), KT, N, _p(qidx), _p(kdev_eff), nq,
-                    _p(out_d), _p(out_i), ks, _p(ds.labels) if want_fin else None, ds.label_lo,
-                    ds.label_hi, _p(lab), _p(cs), _p(status), s), "refine_groups")
-                return
-            elif impl == "stream":
-                _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
-                                                _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff),
-                                                nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), er, S,
-                                                _p(cand_ids), _p(cand_cnt), s), "screen_stream")
-            else:
-                _lib.check(L.dmlp_screen(KT, cap, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
-                                         _p(qhi), _p(qlo), _p(qn), _p(qidx), _p(kdev_eff), nq,
-                                         _p(ds.xnmax_bits), _p(ds.bad), er, S, _p(cand_ids),
-                                         _p(cand_cnt), s), "screen")
-            _lib.check(L.dmlp_refine(cap, _p(cand_ids), _p(cand_cnt), S, _p(ds.X), A, _p(Qx),
-                                     _p(qidx), _p(kdev_eff), nq, _p(out_d), _p(out_i), ks,
-                                     _p(ds.labels) if want_fin else None, ds.label_lo,
-                                     ds.label_hi, _p(lab), _p(cs), _p(status), s), "refine")
+    def _screen_pass(self, idx, impl):
+        torch = _torch()
+        L = _lib.lib()
+        ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
+        N = ds.N
+        s = _stream()
+        nq = len(idx)
+        kcls = int(kk[idx].max())
+        cus = max(1, int(round(NUM_CUS * self.gpu_share)))
+        if impl == "x1":
+            cap = L.dmlp_screen_x1_cap(kcls)
+            S = _choose_slices_stream(nq, L.dmlp_screen_x1_qw(KT), ds.n_tiles,
+                                      L.dmlp_screen_x1_waves_per_cu(kcls),
+                                      int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
+        elif impl == "stream":
+            cap = L.dmlp_screen_stream_cap(kcls)
+            S = _choose_slices_stream(nq, L.dmlp_screen_stream_qw(KT), ds.n_tiles,
+                                      L.dmlp_screen_stream_waves_per_cu(kcls), 1, cus)
+        else:
+            cap = 128 if kcls <= SCREEN_KMAX_A else 256
+            S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
+        qidx = _h2d(idx.astype(np.int32), dev)
+        cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
+        cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
+        fin = (_p(ds.labels) if self.want_fin else None, ds.label_lo, ds.label_hi, _p(self.lab),
+               _p(self.cs), _p(self.status), s)
+        if impl == "x1":
+            cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
+            _lib.check(L.dmlp_screen_x1(KT, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
+                                        _p(self.qhi), _p(self.qn), _p(qidx), _p(self.kdev_eff),
+                                        nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
+                                        _p(cand_ids), _p(cand_cnt), _p(cand_h), s), "screen_x1")
+            _lib.check(L.dmlp_refine_groups(
+                cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
+                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, N, _p(qidx), _p(self.kdev_eff), nq,
+                _p(self.out_d), _p(self.out_i), self.ks, *fin), "refine_groups")
+            self._keep = (qidx, cand_ids, cand_cnt, cand_h)
+            return
+        er = eps_rel(A)
+        if impl == "stream":
+            _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
+                                            _p(self.qhi), _p(self.qlo), _p(self.qn), _p(qidx),
+                                            _p(self.kdev_eff), nq, kcls, _p(ds.xnmax_bits),
+                                            _p(ds.bad), er, S, _p(cand_ids), _p(cand_cnt), s),
+                       "screen_stream")
+        else:
+            _lib.check(L.dmlp_screen(KT, cap, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
+                                     _p(self.qhi), _p(self.qlo), _p(self.qn), _p(qidx),
+                                     _p(self.kdev_eff), nq, _p(ds.xnmax_bits), _p(ds.bad), er, S,
+                                     _p(cand_ids), _p(cand_cnt), s), "screen")
+        _lib.check(L.dmlp_refine(cap, _p(cand_ids), _p(cand_cnt), S, _p(ds.X), A, _p(self.Qx),
+                                 _p(qidx), _p(self.kdev_eff), nq, _p(self.out_d), _p(self.out_i),
+                                 self.ks, *fin), "refine")
+        self._keep = (qidx, cand_ids, cand_cnt)
 
-        n_esc = 0
-        first_a = "x1" if x1_ok else ("stream" if stream_ok else "lds")
-        if len(cls_a):
-            screen_pass(cls_a, first_a)
-        if len(cls_b):
-            screen_pass(cls_b, "lds")
-        # one host sync: which screened queries overflowed?
-        n_ovf = int(status.sum().item())
-        if n_ovf and first_a == "x1":
-            st = status.cpu().numpy()
-            esc = cls_a[st[cls_a] != 0]
-            n_esc = len(esc)
-            if n_esc:
-                screen_pass(esc, "stream" if stream_ok else "lds")
-                n_ovf = int(status.sum().item())
-    else:
+    # ------------------------------------------------------------------ finish (one sync)
+    def finish(self) -> DeviceResult:
+        torch = _torch()
+        L = _lib.lib()
+        ds, kk, dev = self.ds, self.kk, self.dev
+        N = ds.N
+        if torch.cuda.current_stream() != self.stream:
+            # finishing on another stream (pipelined chunks): keep the allocator from recycling
+            # this call's buffers before that stream's escalation / finalize work has run
+            cur = torch.cuda.current_stream()
+            for t in (self.Qx, self.k_dev, self.out_d, self.out_i, self.lab, self.cs, self.status,
+                      getattr(self, "qhi", None), getattr(self, "qlo", None),
+                      getattr(self, "qn", None), getattr(self, "kdev_eff", None)):
+                if t is not None:
+                    t.record_stream(cur)
         n_ovf = n_esc = 0
+        if self.screened:
+            n_ovf = int(self.status.sum().item())
+            if n_ovf and self.first_a == "x1":
+                st = self.status.cpu().numpy()
+                esc = self.cls_a[st[self.cls_a] != 0]
+                n_esc = len(esc)
+                if n_esc:
+                    self._screen_pass(esc, "stream" if self.stream_ok else "lds")
+                    n_ovf = int(self.status.sum().item())
+        fb = np.nonzero(~self.on_screen & (kk >= 1))[0]
+        if n_ovf:
+            fb = np.union1d(fb, np.nonzero(self.status.cpu().numpy())[0])
+        if len(fb):
+            _fallback_exact(ds, self.Qx, fb, kk, self.out_d, self.out_i)
+        if self.want_fin:
+            # queries not (correctly) finalized by refine: fallback ones, k == 0, and k > N
+            # (the checksum then also covers the (+inf, -1) padding, as the CPU path does)
+            rest = np.union1d(fb, np.nonzero((kk < 1) | (self.k_host > N))[0]).astype(np.int32)
+            if len(rest):
+                ridx = _h2d(rest, dev)
+                _lib.check(L.dmlp_finalize(_p(self.out_d), _p(self.out_i), self.ks,
+                                           _p(self.k_dev), _p(ridx), len(rest), _p(ds.labels),
+                                           ds.label_lo, ds.label_hi, _p(self.lab), _p(self.cs),
+                                           _stream()), "finalize")
+        return DeviceResult(self.out_d, self.out_i, self.lab, self.cs, self.k_host,
+                            int(len(fb)), int(n_esc))
 
-    fb = np.nonzero(~on_screen & (kk >= 1))[0]
-    if n_ovf:
-        ovf = np.nonzero(status.cpu().numpy())[0]
-        fb = np.union1d(fb, ovf)
-    if len(fb):
-        _fallback_exact(ds, Qx, fb, kk, out_d, out_i)
-    if want_fin:
-        # queries not (correctly) finalized by refine: fallback ones, k == 0, and k > N (the
-        # checksum then also covers the (+inf, -1) padding, as the CPU path does)
-        rest = np.union1d(fb, np.nonzero((kk < 1) | (k_host > N))[0]).astype(np.int32)
-        if len(rest):
-            ridx = torch.from_numpy(rest).to(dev, non_blocking=True)
-            _lib.check(L.dmlp_finalize(_p(out_d), _p(out_i), ks, _p(k_dev), _p(ridx), len(rest),
-                                       _p(ds.labels), ds.label_lo, ds.label_hi, _p(lab), _p(cs),
-                                       s), "finalize")
-    return DeviceResult(out_d, out_i, lab, cs, k_host, int(len(fb)), int(n_esc))
+
+class _PinnedArena:
+    """Grow-only page-locked staging for the small per-call host arrays (k, query index lists):
+    a pageable source would make the runtime wait for the stream (i.e. for every kernel queued
+    before the copy), and a fresh pinned allocation per copy can synchronize the device.
+    Reset at the start of each top-level call, after the previous call's copies completed."""
+
+    def __init__(self):
+        self.buf = None
+        self.off = 0
+        self.events = []
+        self.old = []
+
+    def reset(self):
+        for e in self.events:
+            e.synchronize()
+        self.events = []
+        self.old = []
+        self.off = 0
+
+    def put(self, a: np.ndarray):
+        torch = _torch()
+        a = np.ascontiguousarray(a)
+        n = a.nbytes
+        if self.buf is None or self.off + n > self.buf.numel():
+            if self.buf is not None:
+                self.old.append(self.buf)  # in-flight copies may still read it
+            self.buf = torch.empty(max(4 << 20, 2 * (self.off + n)), dtype=torch.uint8).pin_memory()
+            self.off = 0
+        view = self.buf[self.off:self.off + n]
+        view.numpy()[:] = a.view(np.uint8).reshape(-1)
+        self.off = (self.off + n + 255) & ~255
+        return view.view(torch.from_numpy(a[:0]).dtype)
+
+    def mark(self):
+        torch = _torch()
+        e = torch.cuda.Event()
+        e.record()
+        self.events.append(e)
+
+
+_ARENA = _PinnedArena()
+
+
+def _h2d(a: np.ndarray, dev):
+    """Small host array -> device as a real async DMA from the pinned arena."""
+    return _ARENA.put(a).to(dev, non_blocking=True)
+
+
+_SIDE_STREAMS = {}
+_PIPE_DEBUG = os.environ.get("DMLP_PIPE_DEBUG") == "1"
+
+
+def _side_stream(name):
+    torch = _torch()
+    key = (name, torch.cuda.current_device())
+    st = _SIDE_STREAMS.get(key)
+    if st is None:
+        st = _SIDE_STREAMS[key] = torch.cuda.Stream()
+    return st
+
+
+def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
+                      chunks: int = 2, finalize: bool = True, exact: bool = False):
+    """Host arrays in (page-locked for real overlap), device results out: the dataset and the
+    query chunks are copied on a copy stream while earlier chunks already screen on their own
+    compute streams, so the H2D of the queries hides behind the MFMA screen (SURVEY.md §7.2
+    step 6, "chunked H2D overlapped with compute").  Same results as prepare_dataset + knn_gpu.
+    Two chunks by default: a process gets 4 hardware queues (main, copy, 2 compute), and more
+    streams than queues share one in order, which serializes their kernels.
+    Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
+    torch = _torch()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    main = torch.cuda.current_stream()
+    copy = _side_stream("h2d")
+    t_enter = time.perf_counter()
+    _ARENA.reset()
+    copy.wait_stream(main)
+    Q = len(Q_host)
+    A = X_host.shape[1]
+    with torch.cuda.stream(copy):
+        X = torch.from_numpy(np.ascontiguousarray(X_host)).to(dev, non_blocking=True)
+        lab = (torch.from_numpy(np.ascontiguousarray(labels_host)).to(dev, non_blocking=True)
+               if labels_host is not None else None)
+        Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
+    main.wait_stream(copy)
+    ds = prepare_dataset(X, lab if finalize else None, label_range)
+    for t in (X, Qd) + ((lab,) if lab is not None else ()):
+        t.record_stream(main)
+    chunks = max(1, min(chunks, Q // 2048 if Q >= 4096 else 1))
+    bounds = [Q * c // chunks for c in range(chunks + 1)]
+    calls = []
+    for c in range(chunks):
+        a, b = bounds[c], bounds[c + 1]
+        with torch.cuda.stream(copy):
+            Qd[a:b].copy_(torch.from_numpy(np.ascontiguousarray(Q_host[a:b])), non_blocking=True)
+        sc = _side_stream(f"chunk{c}")
+        sc.wait_stream(main)   # dataset prep
+        sc.wait_stream(copy)   # this chunk's queries
+        with torch.cuda.stream(sc):
+            Qd.record_stream(sc)
+            calls.append(_KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, kstride,
+                                  gpu_share=1.0 / chunks).launch())
+    t_launched = time.perf_counter()
+    results = []
+    for c, call in enumerate(calls):
+        main.wait_stream(_side_stream(f"chunk{c}"))
+        results.append(call.finish())
+    _ARENA.mark()
+    if _PIPE_DEBUG:
+        import sys
+        print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms, finish "
+              f"{1e3 * (time.perf_counter() - t_launched):.3f} ms", file=sys.stderr)
+    if chunks == 1:
+        r = results[0]
+        return ds, r.dist, r.ids, r.label, r.checksum, r.n_fallback
+    cat = lambda xs: torch.cat(xs) if xs[0] is not None else None
+    return (ds, cat([r.dist for r in results]), cat([r.ids for r in results]),
+            cat([r.label for r in results]), cat([r.checksum for r in results]),
+            sum(r.n_fallback for r in results))
 
 
 _ENV_APPLIED = [False]
@@ -367,7 +537,7 @@ def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d
     N, A = ds.N, ds.A
     dev = Qx.device
     s = _stream()
-    kdev = torch.from_numpy(np.ascontiguousarray(kk, np.int32)).to(dev, non_blocking=True)
+    kdev = _h2d(np.ascontiguousarray(kk, np.int32), dev)
     ksel = L.dmlp_fallback_select_kmax()
     small = fb[kk[fb] <= ksel]
     big = fb[kk[fb] > ksel]
@@ -380,7 +550,7 @@ def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d
         fn = L.dmlp_fallback_select if sel else L.dmlp_fallback_topk
         for c0 in range(0, len(rows_idx), rows):
             sub = rows_idx[c0:c0 + rows]
-            qidx = torch.from_numpy(sub.astype(np.int32)).to(dev, non_blocking=True)
+            qidx = _h2d(sub.astype(np.int32), dev)
             _lib.check(fn(_p(ds.X), N, A, _p(Qx), _p(qidx), _p(kdev), len(sub), _p(ws), ws_bytes,
                           _p(out_d), _p(out_i), out_d.shape[1], s),
                        "fallback_select" if sel else "fallback_topk")

@@ -51,6 +51,21 @@ class Backend:
             lab, cs = torch.from_numpy(l), torch.from_numpy(c.view(np.int64))
         return torch.from_numpy(d), torch.from_numpy(i), lab, cs
 
+    def knn_host(self, X_host, labels_host, label_range, Q_host, k_host: np.ndarray,
+                 kstride=None):
+        """knn() from host arrays: on the GPU the dataset / query H2D is chunked and overlapped
+        with the screen of earlier chunks (ops.knn.knn_gpu_pipelined).  Returns (dist, ids,
+        label, checksum) like knn()."""
+        torch = _torch()
+        if self.on_gpu:
+            _, d, i, lab, cs, _ = K.knn_gpu_pipelined(X_host, labels_host, label_range, Q_host,
+                                                      k_host, kstride=kstride, exact=self.exact)
+            return d, i, lab, cs
+        return self.knn(torch.from_numpy(np.ascontiguousarray(X_host)),
+                        torch.from_numpy(np.ascontiguousarray(Q_host)), k_host,
+                        labels=torch.from_numpy(np.ascontiguousarray(labels_host)),
+                        label_range=label_range, kstride=kstride)
+
     def merge(self, lists_d, lists_i, k_host: np.ndarray, kout: int):
         torch = _torch()
         if self.on_gpu:

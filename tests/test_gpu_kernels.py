@@ -179,6 +179,22 @@ def test_x1_escalates_tight_data(torch_cuda, monkeypatch):
     assert_same(r, refs)
 
 
+def test_pipelined_chunks_match(torch_cuda):
+    """Host-array entry with the query H2D chunked over 4 streams == the exact CPU path."""
+    torch = torch_cuda
+    inp = dmlp.generate(30000, 9000, 32, 0.0, 1000.0, 1, 24, 10, seed=21)
+    Xp = torch.from_numpy(inp.X).pin_memory().numpy()
+    Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k, chunks=4)
+    torch.cuda.synchronize()
+    d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
 def test_merge_and_finalize(torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(1)

@@ -37,7 +37,7 @@ def run(name, inp):
     kd = torch.from_numpy(kk).cuda()
     ci = torch.empty(Q * S * cap, dtype=torch.int32, device="cuda")
     cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
-    ch = torch.empty(Q * S, dtype=torch.float32, device="cuda")
+    ch = torch.empty(Q * S * 2, dtype=torch.float32, device="cuda")
     _lib.check(L.dmlp_screen_x1(KT, A, ds.xfrag.data_ptr(), ds.xinit.data_ptr(), ds.n_tiles, ds.N,
                                 qhi.data_ptr(), qn.data_ptr(), qidx.data_ptr(), kd.data_ptr(), Q,
                                 kmax, ds.xnmax_bits.data_ptr(), ds.bad.data_ptr(), S,
@@ -97,7 +97,7 @@ def refine_check():
         kd = torch.from_numpy(kk).cuda()
         ci = torch.zeros(Q * S * cap, dtype=torch.int32, device="cuda")
         cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
-        ch = torch.empty(Q * S, dtype=torch.float32, device="cuda")
+        ch = torch.empty(Q * S * 2, dtype=torch.float32, device="cuda")
         _lib.check(L.dmlp_screen_x1(KT, A, P(ds.xfrag), P(ds.xinit), ds.n_tiles, ds.N, P(qhi), P(qn),
                                     P(qidx), P(kd), Q, 16, P(ds.xnmax_bits), P(ds.bad), S, P(ci),
                                     P(cc), P(ch), s), "x1")
@@ -111,7 +111,7 @@ def refine_check():
                                         P(oi), 16, P(lab), 0, 10, P(lb), P(cs), P(st), s), "rg")
         torch.cuda.synchronize()
         c = cc.cpu().numpy().reshape(Q, S)
-        h = ch.cpu().numpy().reshape(Q, S)
+        h = ch.cpu().numpy().reshape(Q, S, 2)[:, :, 0]
         print(f"S={S}: groups/slice min {c.min()} max {c.max()} mean {c.mean():.1f}; h[0]={h[0]}; "
               f"status sum {int(st.sum())}")
         g0 = ci.cpu().numpy()[:c[0, 0]]
