@@ -36,16 +36,21 @@ template <int KT, int SUB, int DEPTH, int CHECK>
 struct X1Cfg {
   static constexpr int CT = 4;                  // MFMA column tiles per wave
   static constexpr int NCOL = 16 * CT;          // queries per wave (= workgroup)
-  static constexpr int SUBP = SUB + 1;          // pitch: the 64 lanes of an append hit 64 banks
+  // column pitch in entries: 4 interleaved sub-buffers + 4 pad slots; 68 = 4 (mod 64) puts the
+  // 64 lanes of an append (16 columns x 4 sub-buffers, same fill) on 64 distinct banks
+  static constexpr int CP = 4 * SUB + 4;
   // the fill check runs every CHECK steps, so a sub-buffer is compacted once it holds more than
   // SUB - CHECK entries (CHECK more appends always fit) and keeps at most SUB - CHECK of them
   static constexpr int CAPE = 4 * (SUB - CHECK);  // group entries a column may keep
   static constexpr int IDCAP = 4 * (SUB - 1);  // group-id stride per (query, slice), any CHECK
   static constexpr int FRAGS = 4 * KT * 2;      // 1 KiB fragments per 64-point tile (hi, lo)
-  static constexpr int SBUF = NCOL * 4 * SUBP * 4;
+  static constexpr int SBUF = NCOL * CP * 4;
   static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4;
   static constexpr int D = DEPTH;               // register-ring depth (steps in flight)
 };
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // fp32 bits -> order-preserving u32 (only the top 16 bits are meaningful for a truncated key)
 __device__ __forceinline__ unsigned ord32(unsigned b) {
@@ -65,10 +70,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     float* __restrict__ cand_h) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
   constexpr int CT = C::CT;
-  constexpr int SUBP = C::SUBP;
   constexpr int D = C::D;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned* const sbuf = (unsigned*)smem;                    // [col][m][SUBP] entries
+  unsigned* const sbuf = (unsigned*)smem;                    // [col][CP] interleaved entries
   int* const lcnt = (int*)(smem + C::SBUF);                  // [col][m] counts
   float* const lh = (float*)(lcnt + C::NCOL * 4);            // [col] threshold
   int* const lk = (int*)(lh + C::NCOL);                      // [col] k
@@ -131,16 +135,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       (void*)(xfrag + (int64_t)t0 * (C::FRAGS * 64)), (short)0, nt * C::FRAGS * 64 * 16, 0x00020000);
   const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
-  // this lane's sub-buffer of column tile 0; tile ct adds ct * 64 * SUBP entries
-  unsigned* const mysub = sbuf + ((c * 4) + kg) * SUBP;
+  // this lane's sub-buffer of column tile 0 (slot i at i * 4); tile ct adds ct * 16 * CP entries
+  unsigned* const mysub = sbuf + c * C::CP + kg;
 
   // ---- batched compaction: lane j owns column j.  FINAL: write the column's candidate ids.
+  // A column's entries are interleaved: slot s holds entry s >> 2 of sub-buffer s & 3, so the
+  // lane reads its column as 16-byte vectors and re-deals the survivors by writing them back at
+  // consecutive slots (slot s -> sub-buffer s & 3 again, i.e. round-robin).
   auto compact = [&](const bool final_pass) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = cnt[ct];
     dmlp::wave_sync();
     const int j = lane;
-    unsigned* const colbuf = sbuf + j * 4 * SUBP;
+    unsigned* const colbuf = sbuf + j * C::CP;
     const int4 n4 = *(const int4*)(lcnt + j * 4);
     const int nm[4] = {n4.x, n4.y, n4.z, n4.w};
     const int kc = lk[j];
@@ -148,28 +155,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int flag = lflag[j];
     float hc = lh[j];
     // entries -> ordered keys in place (0 = empty slot)
-    unsigned e[4][SUB];
+    unsigned e[4 * SUB];
     unsigned mx = 0u, mn = 0xffffffffu;
-    int ntot = 0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int v = 0; v < SUB; ++v) {
+      const u32x4 raw = *(const u32x4*)(colbuf + 4 * v);
 #pragma unroll
-      for (int i = 0; i < SUB; ++i) {
-        // validity as arithmetic (all-ones iff i < count), not a predicate: 64 live lane masks
+      for (int m = 0; m < 4; ++m) {
+        // validity as arithmetic (all-ones iff v < count), not a predicate: 64 live lane masks
         // would spill SGPRs into the hot loop
-        const unsigned vm = (unsigned)((i - nm[m]) >> 31);
-        const unsigned raw = colbuf[m * SUBP + i];
-        e[m][i] = ord32(raw) & vm;
-        mx = max(mx, e[m][i]);
-        mn = min(mn, e[m][i] | ~vm);
+        const unsigned vm = (unsigned)((v - nm[m]) >> 31);
+        const unsigned o = ord32(raw[m]) & vm;
+        e[4 * v + m] = o;
+        mx = max(mx, o);
+        mn = min(mn, o | ~vm);
       }
-      ntot += nm[m];
     }
+    const int ntot = nm[0] + nm[1] + nm[2] + nm[3];
     const bool sel = !flag && kc >= 1 && ntot >= kc;
-    // k-th largest 16-bit key: radix search below the common prefix of [min, max]
-    const unsigned dif = (mx ^ mn) >> 16;
+    // k-th largest key, radix search below the common prefix of [min, max] on 15-bit keys
+    // (key16 >> 1) packed two per register: one v_pk_sub_i16 / v_pk_lshrrev_b16 / v_pk_add_u16
+    // triple counts two entries, with no VALU->SGPR->VALU carry chains.  Empty slots are 0 and
+    // always count as "below".  2*T15 is then a (one-LSB) lower bound on the 16-bit k-th key.
+    s16x2 pk[2 * SUB];
+#pragma unroll
+    for (int i = 0; i < 2 * SUB; ++i)
+      pk[i] = __builtin_bit_cast(s16x2, (e[2 * i] >> 17) | ((e[2 * i + 1] >> 17) << 16));
+    const unsigned dif = (mx ^ mn) >> 17;
     const int top = (sel && dif) ? 31 - __clz((int)dif) : -1;
-    unsigned T = mx >> 16;
+    unsigned T = mx >> 17;
     if (top >= 0) T &= ~((2u << top) - 1u);
     int topw = top;
 #pragma unroll
@@ -178,35 +192,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       topw = t > topw ? t : topw;
     }
     for (int bit = topw; bit >= 0; --bit) {
-      const unsigned cand = (T | (1u << bit)) << 16;
-      int ge = 0;
+      const short cand = (short)(T | (1u << bit));
+      const s16x2 cc = {cand, cand};
+      u16x2 lt = {0, 0};
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int i = 0; i < SUB; ++i) ge += e[m][i] >= cand ? 1 : 0;
+      for (int i = 0; i < 2 * SUB; ++i) lt += __builtin_bit_cast(u16x2, pk[i] - cc) >> (unsigned short)15;
+      const int ge = 4 * SUB - (int)lt.x - (int)lt.y;
       if (ge >= kc) T |= 1u << bit;
     }
+    T <<= 1;  // back to the 16-bit key space (floor)
     if (sel) {
       // decode(T << 16) <= the k-th largest group max: a lower bound on the k-th best score
       const float ak = __uint_as_float(unord32(T << 16));
       hc = fmaxf(hc, ak - 2.0f * epc);
     }
-    // keep every entry whose truncated key can be >= hc (floor(key) >= floor(key(hc)))
-    const unsigned kh = ord32(__float_as_uint(hc)) & 0xffff0000u;
+    // keep every entry whose truncated key can be >= hc (floor(key) >= floor(key(hc))); hc >=
+    // -FLT_MAX, so kh > 0 and empty slots (0) never pass; an overflowed column keeps nothing
+    const unsigned kh = flag ? 0xffffffffu : ord32(__float_as_uint(hc)) & 0xffff0000u;
     if (MODE & 8) {
       if (lane == 0) atomicAdd(&g_x1_dbg[3], 1ull);
     }
     if (!final_pass) {
       int pos = 0;
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int i = 0; i < SUB; ++i) {
-          const bool keep = !flag && e[m][i] >= kh && e[m][i] != 0u;
-          // every lane stores; a dropped entry lands in sub-buffer 3's pad slot (never read)
-          colbuf[keep ? (pos & 3) * SUBP + (pos >> 2) : 3 * SUBP + SUB] = unord32(e[m][i]);
-          pos += keep ? 1 : 0;
-        }
+      for (int i = 0; i < 4 * SUB; ++i) {
+        const bool keep = e[i] >= kh;
+        // every lane stores; a dropped entry lands in the column's pad slot (never read)
+        colbuf[keep ? pos : 4 * SUB] = unord32(e[i]);
+        pos += keep ? 1 : 0;
+      }
       const bool ovf = flag || pos > C::CAPE;
       int4 nn;
       nn.x = ovf ? 0 : (pos + 3) >> 2;
@@ -234,14 +248,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         int* const out = cand_ids + ((int64_t)p * S + s) * C::IDCAP;
         int kept = 0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
-#pragma unroll
-          for (int i = 0; i < SUB; ++i) {
-            const bool keep = !flag && e[m][i] >= kh && e[m][i] != 0u;
-            if (keep && kept < C::CAPE)
-              out[kept] = (int)((e[m][i] & 0xffff0000u) | (unord32(e[m][i]) & 0xffffu));
-            kept += keep ? 1 : 0;
-          }
+        for (int i = 0; i < 4 * SUB; ++i) {
+          const bool keep = e[i] >= kh;
+          if (keep && kept < C::CAPE)
+            out[kept] = (int)((e[i] & 0xffff0000u) | (unord32(e[i]) & 0xffffu));
+          kept += keep ? 1 : 0;
+        }
         cand_cnt[(int64_t)p * S + s] = (flag || kept > C::CAPE) ? -1 : kept;
         cand_h[2 * ((int64_t)p * S + s)] = hc;       // this slice's final threshold
         cand_h[2 * ((int64_t)p * S + s) + 1] = epc;  // the query's error bound
@@ -293,7 +305,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
          a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
       const unsigned gl_ = (unsigned)((J) * 4 + kg);                                            \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
-        mysub[ct * 64 * SUBP + cnt[ct]] = (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;        \
+        mysub[ct * 16 * C::CP + 4 * cnt[ct]] = (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;   \
         cnt[ct] += hit_[ct] ? 1 : 0;                                                            \
         trig |= cnt[ct] > SUB - CHECK;                                                          \
       }                                                                                         \
