@@ -225,22 +225,18 @@ __global__ __launch_bounds__(256) void k_refine(
         }
       }
     }
+    // one member per lane (4 lanes per group: their fragments are adjacent 16-byte chunks)
     int nm = 0;
-    for (int g0 = 0; g0 < M; g0 += 64) {
-      const int g = g0 + lane;
-      bool gv = g < M;
-      int base = 0;
-      if (gv) {
+    for (int j0 = 0; j0 < 4 * M; j0 += 64) {
+      const int jm = j0 + lane;
+      const int g = jm >> 2;
+      int id = 0;
+      bool keep = false;
+      if (g < M) {
         const int lo = slice_of(g);
         const unsigned e = (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (g - pre[lo])];
-        gv = e >= kh;
-        base = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int id = base + r;
-        bool keep = false;
-        if (gv && id < gin.n_points) {
+        id = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4 + (jm & 3);
+        if (e >= kh && id < gin.n_points) {
           const int64_t t = id >> 6;
           const int pl = id & 63;
           const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * 2 * 64) + (pl & 15);
@@ -253,19 +249,19 @@ __global__ __launch_bounds__(256) void k_refine(
             for (int kq = 0; kq < 4; ++kq) {
               const u32x4 w = fk[16 * kq];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                sc += qf[(kt * 4 + kq) * 8 + 2 * e] * __uint_as_float(w[e] << 16);
-                sc += qf[(kt * 4 + kq) * 8 + 2 * e + 1] * __uint_as_float(w[e] & 0xffff0000u);
+              for (int q2 = 0; q2 < 4; ++q2) {
+                sc += qf[(kt * 4 + kq) * 8 + 2 * q2] * __uint_as_float(w[q2] << 16);
+                sc += qf[(kt * 4 + kq) * 8 + 2 * q2 + 1] * __uint_as_float(w[q2] & 0xffff0000u);
               }
             }
           }
           keep = sc >= hq;
         }
-        const unsigned long long km = __ballot(keep);
-        const int pos = nm + __popcll(km & dmlp::lanemask_lt());
-        if (keep && pos < P) s_i[wave][pos] = id;
-        nm += __popcll(km);
       }
+      const unsigned long long km = __ballot(keep);
+      const int pos = nm + __popcll(km & dmlp::lanemask_lt());
+      if (keep && pos < P) s_i[wave][pos] = id;
+      nm += __popcll(km);
     }
     if (nm > P) {
       // pathological ties: hand the query back (x1 overflow -> 3-term screen escalation)
