@@ -110,7 +110,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
   bf16x8 bh[CT][KT];
   float h[CT];
-  int cnt[CT];
+  // per column tile: LDS byte address of this lane's next free slot (advances 16 B per append:
+  // slots of one sub-buffer are 4 entries apart), and the address past which it must compact
+  unsigned addr[CT], lim[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int p = pbase + ct * 16 + c;
@@ -119,7 +121,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) bh[ct][kt] = qhi[(q * KT + kt) * 4 + kg];
     h[ct] = valid ? -FLT_MAX : INFINITY;
-    cnt[ct] = 0;
+    addr[ct] = (unsigned)(((ct * 16 + c) * C::CP + kg) * 4);
+    lim[ct] = addr[ct] + (SUB - CHECK) * 16;
     if (lane < 16) {
       const int col = ct * 16 + c;
       lh[col] = h[ct];
@@ -135,8 +138,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       (void*)(xfrag + (int64_t)t0 * (C::FRAGS * 64)), (short)0, nt * C::FRAGS * 64 * 16, 0x00020000);
   const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
-  // this lane's sub-buffer of column tile 0 (slot i at i * 4); tile ct adds ct * 16 * CP entries
-  unsigned* const mysub = sbuf + c * C::CP + kg;
 
   // ---- batched compaction: lane j owns column j.  FINAL: write the column's candidate ids.
   // A column's entries are interleaved: slot s holds entry s >> 2 of sub-buffer s & 3, so the
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // consecutive slots (slot s -> sub-buffer s & 3 again, i.e. round-robin).
   auto compact = [&](const bool final_pass) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = cnt[ct];
+    for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = (int)(addr[ct] - (lim[ct] - (SUB - CHECK) * 16)) >> 4;
     dmlp::wave_sync();
     const int j = lane;
     unsigned* const colbuf = sbuf + j * C::CP;
@@ -156,7 +157,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     float hc = lh[j];
     // entries -> ordered keys in place (0 = empty slot)
     unsigned e[4 * SUB];
-    unsigned mx = 0u, mn = 0xffffffffu;
+    // every buffered key is >= key(hc): appended at h = hc or kept at the last compaction
+    unsigned mx = 0u;
+    const unsigned mn = ord32(__float_as_uint(hc)) & 0xffff0000u;
 #pragma unroll
     for (int v = 0; v < SUB; ++v) {
       const u32x4 raw = *(const u32x4*)(colbuf + 4 * v);
@@ -168,7 +171,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const unsigned o = ord32(raw[m]) & vm;
         e[4 * v + m] = o;
         mx = max(mx, o);
-        mn = min(mn, o | ~vm);
       }
     }
     const int ntot = nm[0] + nm[1] + nm[2] + nm[3];
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       dmlp::wave_sync();
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        cnt[ct] = lcnt[(ct * 16 + c) * 4 + kg];
+        addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * lcnt[(ct * 16 + c) * 4 + kg];
         h[ct] = lh[ct * 16 + c];
       }
       // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
@@ -303,11 +305,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       }                                                                                         \
       /* branch-free: every lane writes its entry to the next free slot and advances only on  \
          a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
-      const unsigned gl_ = (unsigned)((J) * 4 + kg);                                            \
+      unsigned gl_ = (unsigned)((J) * 4 + kg);                                                  \
+      asm volatile("" : "+v"(gl_)); /* one VGPR: each key is a single v_and_or / v_bfi */       \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
-        mysub[ct * 16 * C::CP + 4 * cnt[ct]] = (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;   \
-        cnt[ct] += hit_[ct] ? 1 : 0;                                                            \
-        trig |= cnt[ct] > SUB - CHECK;                                                          \
+        *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                       \
+            (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                      \
+        addr[ct] += hit_[ct] ? 16u : 0u;                                                        \
+        trig |= __ballot(addr[ct] > lim[ct]);                                                   \
       }                                                                                         \
     }                                                                                           \
   } while (0)
@@ -315,11 +319,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   // step of the unrolled ring would not stay in the instruction cache)
 #define DMLP_CHECK()                                                                            \
   do {                                                                                          \
-    if (__ballot(trig)) compact(false);                                                         \
-    trig = false;                                                                               \
+    if (trig) compact(false);                                                                   \
+    trig = 0;                                                                                   \
   } while (0)
 
-  bool trig = false;
+  unsigned long long trig = 0;  // wave-uniform: some lane's sub-buffer passed its limit
   if (nsteps > 0) {
     // prologue in the loop's issue order (A, Xi per step), so the waitcnt at the loop head is
     // the steady-state vmcnt(2 * (D - 1)), not a merge with a reordered prologue
