@@ -7,6 +7,7 @@ call sites map as follows (bench_* addresses from SURVEY.md §2.6):
   MPI_Bcast (params, dataset, k, queries)   -> Comm.bcast            (ncclBroadcast)
   MPI_Scatterv (shards)                     -> Comm.scatter_rows     (scatter, one xGMI hop each)
   MPI_Gather/Gatherv (per-query results)    -> Comm.gather_rows      (batched, once per call)
+  (dataset replication, node-shared input)  -> Comm.allgather_rows   (all-gather of H2D shards)
   MPI_Reduce + user MPI_Op (bench_2/3)      -> strategies.tree_merge (send/recv + merge kernel)
   MPI_Cart_create/Cart_sub (engine.cpp)     -> Comm.grid_groups      (dist.new_group row/col)
   MPI_Send/Recv ANY_SOURCE farming (bench_4)-> Comm.claim            (TCPStore atomic counter)
@@ -199,6 +200,26 @@ class Comm:
                 off += c
         dist.scatter(out, chunks, src=0)
         return out[: counts[self.rank]]
+
+    def allgather_rows(self, t, counts, row_shape, dtype):
+        """Every rank contributes counts[rank] rows; every rank gets the concatenation in rank
+        order (MPI_Allgatherv; one RCCL all-gather over xGMI, padded to the largest part)."""
+        torch = _torch()
+        if self.world == 1:
+            return t
+        import torch.distributed as dist
+        mx = max(counts)
+        if mx == 0:
+            return torch.empty((0, *row_shape), dtype=dtype, device=self.device)
+        src = t
+        if t.shape[0] != mx:
+            src = torch.zeros((mx, *row_shape), dtype=dtype, device=self.device)
+            src[: t.shape[0]] = t
+        out = torch.empty((self.world * mx, *row_shape), dtype=dtype, device=self.device)
+        dist.all_gather_into_tensor(out, src.contiguous())
+        if all(c == mx for c in counts):
+            return out
+        return torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
 
     def gather_rows(self, t, counts, row_shape, dtype):
         """Gather row blocks to rank 0 in rank order (MPI_Gatherv); returns the concatenation on

@@ -151,13 +151,33 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
 
 def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     """Static farm over a node-shared input segment (utils/shm.py): every rank copies its own
-    query block (and the dataset) host->GPU over its own PCIe link — no funnel through GPU 0.
-    KNN_DATA_INGRESS=bcast instead H2Ds the dataset on rank 0 and broadcasts it over xGMI."""
+    query block host->GPU over its own PCIe link — no funnel through GPU 0.  The replicated
+    dataset (bench_4 @0xc199 broadcasts it) arrives by KNN_DATA_INGRESS:
+      allgather (default, P > 1): each rank H2Ds 1/P of the rows, one RCCL all-gather over xGMI
+                 completes the replica — PCIe bytes per GPU drop from N*A*8 to N*A*8/P and the
+                 host memory reads from P*N*A*8 to N*A*8;
+      h2d:       every rank copies the whole dataset from the segment;
+      bcast:     rank 0 copies it, one RCCL broadcast."""
     import os
     torch = _torch()
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
-    bcast_data = os.environ.get("KNN_DATA_INGRESS", "h2d") == "bcast" and comm.world > 1
+    mode = os.environ.get("KNN_DATA_INGRESS", "allgather") if comm.world > 1 else "h2d"
+    if mode == "allgather":
+        with tr.phase("h2d"):
+            nc, nd = block_partition(N, comm.world)
+            r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
+            Xs = be.tensor(inp.X[r0:r1])
+            ls = be.tensor(inp.labels[r0:r1])
+            Ql = be.tensor(inp.Qx[a:b])
+            kl_h = np.array(inp.k[a:b])
+        with tr.phase("allgather_data"):
+            X = comm.allgather_rows(Xs, nc, (A,), torch.float64)
+            lab = comm.allgather_rows(ls, nc, (), torch.int32)
+        with tr.phase("compute"):
+            d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
+        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
+    bcast_data = mode == "bcast"
     if not bcast_data and os.environ.get("KNN_PIPELINE", "0") == "1":
         # per-GPU H2D chunked and overlapped with the screen of the chunks already resident
         # (opt-in: measured 4.59 vs 4.22 ms/step on the bench shape — two half-size screens

@@ -76,6 +76,15 @@ def test_shared_ingress_farm(workload, schedule):
     assert _run(path, 1, "farm", env_extra=env) == expect
 
 
+@pytest.mark.parametrize("data_ingress", ["allgather", "h2d", "bcast"])
+def test_shared_ingress_dataset_modes(workload, data_ingress):
+    """Replicated dataset over the node-shared segment: sharded H2D + all-gather (uneven
+    row blocks at P = 3), full per-rank H2D, or root H2D + broadcast."""
+    path, expect = workload
+    env = {"KNN_INGRESS": "shm", "KNN_DATA_INGRESS": data_ingress}
+    assert _run(path, 3, "farm", env_extra=env) == expect
+
+
 def test_shared_ingress_other_strategies(workload):
     path, expect = workload
     for strategy in ("shard_reduce", "grid2d"):
