@@ -240,11 +240,14 @@ class _KnnCall:
         self.dev = self.Qx.device
         self.k_host = np.ascontiguousarray(k_host, np.int32)
         Q = self.Q
-        self.ks = max(1, int(self.k_host.max()) if Q else 1) if kstride is None else kstride
+        self.kmin = int(self.k_host.min()) if Q else 0
+        self.kmax = int(self.k_host.max()) if Q else 0
+        self.ks = max(1, self.kmax) if kstride is None else kstride
         self.exact = exact
         self.gpu_share = gpu_share
         self.want_fin = finalize and ds.labels is not None
-        self.kk = np.minimum(self.k_host, ds.N)  # k > N: pad with (+inf,-1) like bench_2
+        # k > N: pad with (+inf,-1) like bench_2
+        self.kk = self.k_host if self.kmax <= ds.N else np.minimum(self.k_host, ds.N)
         dev = self.dev
         self.k_dev = _h2d(self.k_host, dev)
         self.out_d = torch.full((Q, self.ks), float("inf"), dtype=torch.float64, device=dev)
@@ -261,13 +264,20 @@ class _KnnCall:
         ds, kk, Q, A = self.ds, self.kk, self.Q, self.A
         self.use_screen = ds.screen_ok and not self.exact and Q > 0
         empty = np.empty(0, np.int64)
-        self.cls_a = np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if self.use_screen else empty
-        self.cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
-                      if self.use_screen else empty)
-        self.on_screen = np.zeros(Q, bool)
-        self.on_screen[self.cls_a] = True
-        self.on_screen[self.cls_b] = True
-        self.screened = self.use_screen and (len(self.cls_a) or len(self.cls_b))
+        # common case (every k in [1, 32], k <= N): one class, identity query index, no per-query
+        # host scans — this host path runs while the GPU waits for its first kernel
+        self.all_a = self.use_screen and self.kmin >= 1 and self.kmax <= min(SCREEN_KMAX_A, ds.N)
+        if self.all_a:
+            self.cls_a, self.cls_b = None, empty
+        else:
+            self.cls_a = (np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if self.use_screen
+                          else empty)
+            self.cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
+                          if self.use_screen else empty)
+            self.on_screen = np.zeros(Q, bool)
+            self.on_screen[self.cls_a] = True
+            self.on_screen[self.cls_b] = True
+        self.screened = self.use_screen and (self.all_a or len(self.cls_a) or len(self.cls_b))
         self.stream = _torch().cuda.current_stream()
         if not self.screened:
             return self
@@ -279,7 +289,7 @@ class _KnnCall:
         _lib.check(L.dmlp_prep_queries(_p(self.Qx), Q, A, _p(ds.mu), KT, _p(self.qhi),
                                        _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
                    "prep_queries")
-        self.kdev_eff = _h2d(kk.astype(np.int32), dev)
+        self.kdev_eff = self.k_dev if kk is self.k_host else _h2d(kk.astype(np.int32), dev)
         # k <= 32 and A <= 64: single-term (x1) or 3-term barrier-free streaming kernel;
         # otherwise the LDS-shared 3-term kernel.  x1 queries whose candidates overflow (data
         # too tight for the single-term bound) escalate to the 3-term screen, and only what
@@ -287,7 +297,7 @@ class _KnnCall:
         x1_ok = SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(KT) > 0
         self.stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
         self.first_a = "x1" if x1_ok else ("stream" if self.stream_ok else "lds")
-        if len(self.cls_a):
+        if self.all_a or len(self.cls_a):
             self._screen_pass(self.cls_a, self.first_a)
         if len(self.cls_b):
             self._screen_pass(self.cls_b, "lds")
@@ -299,8 +309,13 @@ class _KnnCall:
         ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
         N = ds.N
         s = _stream()
-        nq = len(idx)
-        kcls = int(kk[idx].max())
+        if idx is None:  # every query
+            nq, kcls = self.Q, self.kmax
+            qidx = _identity(nq, dev)
+        else:
+            nq = len(idx)
+            kcls = int(kk[idx].max())
+            qidx = _h2d(idx.astype(np.int32), dev)
         cus = max(1, int(round(NUM_CUS * self.gpu_share)))
         if impl == "x1":
             cap = L.dmlp_screen_x1_cap(kcls)
@@ -314,7 +329,6 @@ class _KnnCall:
         else:
             cap = 128 if kcls <= SCREEN_KMAX_A else 256
             S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
-        qidx = _h2d(idx.astype(np.int32), dev)
         cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
         cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
         fin = (_p(ds.labels) if self.want_fin else None, ds.label_lo, ds.label_hi, _p(self.lab),
@@ -368,17 +382,18 @@ class _KnnCall:
             n_ovf = int(self.status.sum().item())
             if n_ovf and self.first_a == "x1":
                 st = self.status.cpu().numpy()
-                esc = self.cls_a[st[self.cls_a] != 0]
+                esc = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
                 n_esc = len(esc)
                 if n_esc:
                     self._screen_pass(esc, "stream" if self.stream_ok else "lds")
                     n_ovf = int(self.status.sum().item())
-        fb = np.nonzero(~self.on_screen & (kk >= 1))[0]
+        fb = (np.empty(0, np.int64) if self.all_a
+              else np.nonzero(~self.on_screen & (kk >= 1))[0])
         if n_ovf:
             fb = np.union1d(fb, np.nonzero(self.status.cpu().numpy())[0])
         if len(fb):
             _fallback_exact(ds, self.Qx, fb, kk, self.out_d, self.out_i)
-        if self.want_fin:
+        if self.want_fin and (len(fb) or self.kmin < 1 or self.kmax > N):
             # queries not (correctly) finalized by refine: fallback ones, k == 0, and k > N
             # (the checksum then also covers the (+inf, -1) padding, as the CPU path does)
             rest = np.union1d(fb, np.nonzero((kk < 1) | (self.k_host > N))[0]).astype(np.int32)
@@ -438,6 +453,19 @@ _ARENA = _PinnedArena()
 def _h2d(a: np.ndarray, dev):
     """Small host array -> device as a real async DMA from the pinned arena."""
     return _ARENA.put(a).to(dev, non_blocking=True)
+
+
+_IDENTITY = {}
+
+
+def _identity(n: int, dev):
+    """Device arange(n) int32 (grow-only cache): the query index list of an all-queries pass."""
+    torch = _torch()
+    key = str(dev)
+    t = _IDENTITY.get(key)
+    if t is None or t.numel() < n:
+        t = _IDENTITY[key] = torch.arange(max(n, 1 << 16), dtype=torch.int32, device=dev)
+    return t[:n]
 
 
 _SIDE_STREAMS = {}
