@@ -584,6 +584,65 @@ def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d
                        "fallback_select" if sel else "fallback_topk")
 
 
+def knn_gpu_streamed(X_host, labels_host, label_range, Qx, k_host, chunk_rows: int,
+                     kstride=None, exact: bool = False):
+    """Out-of-core exact k-NN ("stream from host memory beyond HBM"): the dataset
+    stays in (page-locked) host memory and crosses PCIe in chunks of chunk_rows rows, double
+    buffered on a copy stream so chunk c+1 is in flight while chunk c is screened; each chunk's
+    top-k lists (global ids) are merged into the running lists by the K-way merge kernel, and
+    the vote / checksum run once at the end.  Device memory: 2 chunks + queries + labels.
+    Returns (dist, ids, label, checksum) on the current device."""
+    torch = _torch()
+    dev = Qx.device
+    main = torch.cuda.current_stream()
+    copy = _side_stream("h2d")
+    N, A = X_host.shape
+    Q = Qx.shape[0]
+    k_host = np.ascontiguousarray(k_host, np.int32)
+    ks = max(1, int(k_host.max()) if Q else 1) if kstride is None else kstride
+    chunk_rows = max(1, min(int(chunk_rows), N))
+    nchunks = (N + chunk_rows - 1) // chunk_rows
+    bufs = [torch.empty((chunk_rows, A), dtype=torch.float64, device=dev) for _ in range(2)]
+    ready = [torch.cuda.Event() for _ in range(2)]
+    freed = [None, None]
+    labels = None
+    copy.wait_stream(main)
+    with torch.cuda.stream(copy):
+        if labels_host is not None:
+            labels = torch.from_numpy(np.ascontiguousarray(labels_host)).to(dev, non_blocking=True)
+    def issue(c):
+        b = c % 2
+        a0, a1 = c * chunk_rows, min(N, (c + 1) * chunk_rows)
+        if freed[b] is not None:
+            copy.wait_event(freed[b])  # chunk c-2's screen is done with this buffer
+        with torch.cuda.stream(copy):
+            bufs[b][: a1 - a0].copy_(torch.from_numpy(np.ascontiguousarray(X_host[a0:a1])),
+                                     non_blocking=True)
+            ready[b].record(copy)
+    issue(0)
+    dr = ir = None
+    kd = torch.from_numpy(k_host).to(dev)
+    for c in range(nchunks):
+        b = c % 2
+        a0, a1 = c * chunk_rows, min(N, (c + 1) * chunk_rows)
+        if c + 1 < nchunks:
+            issue(c + 1)
+        main.wait_event(ready[b])
+        ds = prepare_dataset(bufs[b][: a1 - a0])
+        r = knn_gpu(ds, Qx, k_host, finalize=False, exact=exact, kstride=ks)
+        d, i = r.dist, torch.where(r.ids >= 0, r.ids + a0, r.ids)
+        if dr is None:
+            dr, ir = d, i
+        else:
+            dr, ir = merge_gpu(torch.stack([dr, d]), torch.stack([ir, i]), kd, ks)
+        freed[b] = main.record_event()
+    main.wait_stream(copy)
+    lab = cs = None
+    if labels is not None:
+        lab, cs = finalize_gpu(labels, label_range, dr, ir, kd)
+    return dr, ir, lab, cs
+
+
 def merge_gpu(lists_d, lists_i, k_dev, kout: int):
     """lists_*: torch [L, Q, kin] sorted lists on one GPU -> merged [Q, kout] (K4)."""
     torch = _torch()

@@ -66,6 +66,31 @@ class Backend:
                         labels=torch.from_numpy(np.ascontiguousarray(labels_host)),
                         label_range=label_range, kstride=kstride)
 
+    def knn_streamed(self, X_host, labels_host, label_range, Qx, k_host: np.ndarray,
+                     chunk_rows: int, kstride=None):
+        """Exact k-NN with the dataset left in host memory and processed chunk_rows rows at a
+        time (out-of-core: datasets beyond one device's memory), running top-k lists merged
+        after every chunk.  Returns (dist, ids, label, checksum) like knn()."""
+        torch = _torch()
+        if self.on_gpu:
+            return K.knn_gpu_streamed(X_host, labels_host, label_range, Qx, k_host, chunk_rows,
+                                      kstride=kstride, exact=self.exact)
+        N = X_host.shape[0]
+        dr = ir = None
+        ks = kstride or max(1, int(np.max(k_host)) if len(k_host) else 1)
+        for a0 in range(0, max(N, 1), max(1, chunk_rows)):
+            a1 = min(N, a0 + chunk_rows)
+            d, i, _, _ = self.knn(torch.from_numpy(np.ascontiguousarray(X_host[a0:a1])), Qx,
+                                  k_host, finalize=False, kstride=ks)
+            i = torch.where(i >= 0, i + a0, i)
+            if dr is None:
+                dr, ir = d, i
+            else:
+                dr, ir = self.merge(torch.stack([dr, d]), torch.stack([ir, i]), k_host, ks)
+        lab, cs = self.finalize(torch.from_numpy(np.ascontiguousarray(labels_host)), label_range,
+                                dr, ir, k_host)
+        return dr, ir, lab, cs
+
     def merge(self, lists_d, lists_i, k_host: np.ndarray, kout: int):
         torch = _torch()
         if self.on_gpu:

@@ -18,6 +18,9 @@ results (exact fp64 distances, (dist asc, id desc) order, vote tie -> larger lab
                 row/column sub-communicators (MPI_Cart_sub -> dist.new_group), column merge to
                 row 0, results gathered to rank 0.
   serial        bench.debug (B0): KD-tree on rank 0's CPU, other ranks idle.
+  ring          beyond the reference: dataset sharded, queries split, shards
+                rotate around the xGMI ring while each rank merges its queries' running top-k —
+                datasets larger than one GPU's HBM.
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ import numpy as np
 
 from .comm import block_partition, dims_create
 
-STRATEGIES = ("farm", "shard_gather", "shard_reduce", "grid2d", "serial")
+STRATEGIES = ("farm", "shard_gather", "shard_reduce", "grid2d", "serial", "ring")
 
 
 def _torch():
@@ -163,6 +166,16 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
     mode = os.environ.get("KNN_DATA_INGRESS", "allgather") if comm.world > 1 else "h2d"
+    max_rows = int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)
+    if max_rows and N > max_rows:
+        # out-of-core: the replica does not fit the device budget, stream it from the segment
+        with tr.phase("h2d"):
+            Ql = be.tensor(inp.Qx[a:b])
+            kl_h = np.array(inp.k[a:b])
+        with tr.phase("h2d+compute"):
+            d, i, lb, cs = be.knn_streamed(inp.X, inp.labels, (lo, hi), Ql, kl_h, max_rows,
+                                           kstride=kmax)
+        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
     if mode == "allgather":
         with tr.phase("h2d"):
             nc, nd = block_partition(N, comm.world)
@@ -473,5 +486,77 @@ def serial(comm, be, inp, tr, debug=False, **_):
             torch.from_numpy(i))
 
 
+# ============================================================================ ring (beyond-HBM datasets)
+def ring(comm, be, inp, tr, debug=False, **_):
+    """Ring k-NN — the SURVEY.md §5 "long-context" analog (ring-attention pattern over the
+    dataset axis): the dataset is sharded N/P per GPU and never replicated, the queries are split
+    in P blocks, and every rank keeps the running top-k of its own block while the data shards
+    travel one hop per step around the xGMI ring (P - 1 grouped send/recv exchanges, each
+    overlapped with the local screen + exact re-rank of the shard in hand, merged by the K-way
+    merge kernel).  Memory per GPU: two shards + Q/P queries, so datasets up to P x the HBM of
+    one MI355X (288 GB ~ 3.6e10 fp64 values) stay exact, with the farm's query parallelism."""
+    torch = _torch()
+    N, Q, A, lo, hi, kmax, shared = _meta(comm, inp, with_shared=True)
+    P, r = comm.world, comm.rank
+    nc, nd = block_partition(N, P)
+    qc, qd = block_partition(Q, P)
+    mx = max(nc)
+    with tr.phase("h2d"):
+        if shared:  # node-shared segment: every rank copies its shard, its query block, labels
+            cur = torch.zeros((mx, A), dtype=torch.float64, device=be.device)
+            if nc[r]:
+                cur[: nc[r]] = be.tensor(inp.X[nd[r]:nd[r] + nc[r]])
+            Ql = be.tensor(inp.Qx[qd[r]:qd[r] + qc[r]])
+            kl_h = np.array(inp.k[qd[r]:qd[r] + qc[r]], np.int32)
+            lab = be.tensor(inp.labels)
+        else:
+            X = lab = Qx = kd = None
+            if comm.is_root:
+                X, lab, Qx, kd = _root_arrays(be, inp)
+    if not shared:
+        with tr.phase("scatter"):
+            cur = comm.scatter_rows(X, nc, (A,), torch.float64)
+            if cur.shape[0] < mx:
+                cur = torch.cat([cur, torch.zeros((mx - cur.shape[0], A), dtype=torch.float64,
+                                                  device=be.device)])
+            Ql = comm.scatter_rows(Qx, qc, (A,), torch.float64)
+            kl_h = comm.scatter_rows(kd, qc, (), torch.int32).cpu().numpy()
+            lab = comm.bcast(lab, (N,), torch.int32)
+    dr = ir = None
+    nxt = torch.empty_like(cur) if P > 1 else None
+    for step in range(P):
+        src = (r - step) % P  # the shard in hand started on rank src
+        reqs = []
+        if step < P - 1:
+            import torch.distributed as dist
+            ops = [dist.P2POp(dist.isend, cur, (r + 1) % P), dist.P2POp(dist.irecv, nxt, (r - 1) % P)]
+            with tr.phase("ring_post"):
+                reqs = dist.batch_isend_irecv(ops)
+        with tr.phase("compute"):
+            d, i, _, _ = be.knn(cur[: nc[src]], Ql, kl_h, finalize=False, kstride=kmax)
+            i = _offset_ids(i, nd[src])
+            if dr is None:
+                dr, ir = d, i
+            else:
+                dr, ir = be.merge(torch.stack([dr, d]), torch.stack([ir, i]), kl_h, kmax)
+        if reqs:
+            with tr.phase("ring_wait"):
+                for q_ in reqs:
+                    q_.wait()
+            cur, nxt = nxt, cur
+    with tr.phase("finalize"):
+        lb, cs = be.finalize(lab, (lo, hi), dr, ir, kl_h)
+    with tr.phase("gather"):
+        packed = torch.stack([lb.to(torch.int64), cs], dim=1)
+        allp = comm.gather_rows(packed, qc, (2,), torch.int64)
+        dd = ii = None
+        if debug:
+            dd = comm.gather_rows(dr, qc, (kmax,), torch.float64)
+            ii = comm.gather_rows(ir, qc, (kmax,), torch.int32)
+    if not comm.is_root:
+        return None
+    return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii
+
+
 FUNCS = {"farm": farm, "shard_gather": shard_gather, "shard_reduce": shard_reduce,
-         "grid2d": grid2d, "serial": serial}
+         "grid2d": grid2d, "serial": serial, "ring": ring}

@@ -48,14 +48,15 @@ def workload(tmp_path_factory):
     return str(p), _oracle_report(inp)
 
 
-@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "serial"])
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "serial",
+                                      "ring"])
 @pytest.mark.parametrize("np_", [1, 2, 3])
 def test_strategy_matches_oracle(workload, strategy, np_):
     path, expect = workload
     assert _run(path, np_, strategy) == expect
 
 
-@pytest.mark.parametrize("strategy", ["grid2d", "shard_gather", "shard_reduce"])
+@pytest.mark.parametrize("strategy", ["grid2d", "shard_gather", "shard_reduce", "ring"])
 def test_four_and_six_ranks(workload, strategy):
     path, expect = workload
     assert _run(path, 4, strategy) == expect
@@ -85,9 +86,18 @@ def test_shared_ingress_dataset_modes(workload, data_ingress):
     assert _run(path, 3, "farm", env_extra=env) == expect
 
 
+@pytest.mark.parametrize("np_", [1, 2])
+def test_out_of_core_farm(workload, np_):
+    """Dataset larger than the device budget (KNN_MAX_DEVICE_ROWS): streamed from the node-
+    shared segment in 50-row chunks, running top-k lists merged after every chunk."""
+    path, expect = workload
+    env = {"KNN_INGRESS": "shm", "KNN_MAX_DEVICE_ROWS": "50"}
+    assert _run(path, np_, "farm", env_extra=env) == expect
+
+
 def test_shared_ingress_other_strategies(workload):
     path, expect = workload
-    for strategy in ("shard_reduce", "grid2d"):
+    for strategy in ("shard_reduce", "grid2d", "ring"):
         assert _run(path, 2, strategy, env_extra={"KNN_INGRESS": "shm"}) == expect
 
 
@@ -103,14 +113,15 @@ def test_edge_cases(tmp_path):
     p = tmp_path / "edge.in"
     p.write_text(dmlp.to_text(inp))
     expect = _oracle_report(dmlp.parse_input(p.read_text()))
-    for s in ["farm", "shard_gather", "shard_reduce", "grid2d"]:
+    for s in ["farm", "shard_gather", "shard_reduce", "grid2d", "ring"]:
         assert _run(str(p), 4, s) == expect, s
 
 
 def test_debug_output(workload):
     """DEBUG build listing (common.cpp:72-78) from every strategy is identical."""
     path, _ = workload
-    outs = {s: _run(path, 2, s, extra=["--debug"]) for s in ["farm", "shard_reduce", "grid2d"]}
+    outs = {s: _run(path, 2, s, extra=["--debug"])
+            for s in ["farm", "shard_reduce", "grid2d", "ring"]}
     assert len(set(outs.values())) == 1
     first = list(outs.values())[0].decode().splitlines()
     assert first[0].startswith("Label for Query 0 : ")

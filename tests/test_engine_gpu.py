@@ -1,0 +1,64 @@
+"""Python Engine (engine.h API) on one MI355X, in-process (world size 1): every strategy, the
+node-shared ingress, the out-of-core streamed farm and the debug listing print the CPU oracle's
+bytes.  The multi-rank versions of the same paths run on CPU (gloo) in test_distributed.py."""
+import numpy as np
+import pytest
+
+import distributed_machine_learning_project_amd as dmlp
+from distributed_machine_learning_project_amd.ops import knn as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def workload():
+    inp = dmlp.generate(6000, 700, 32, 0.0, 1000.0, 1, 40, 10, seed=31)
+    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+    _, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    return inp, dmlp.format_report(cs), d, i
+
+
+def _engine(strategy, **kw):
+    from distributed_machine_learning_project_amd.parallel.engine import Engine
+    return Engine(strategy, device="gpu", **kw)
+
+
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "ring"])
+def test_strategies_match_oracle(gpu, workload, strategy):
+    inp, expect, _, _ = workload
+    eng = _engine(strategy)
+    out = eng.KNN(inp.params, inp, None)
+    assert bytes(eng.report(out)) == expect
+    eng.close()
+
+
+@pytest.mark.parametrize("max_rows", ["0", "2500"])
+def test_shared_ingress_and_out_of_core(gpu, workload, monkeypatch, max_rows):
+    """Node-shared page-locked segment; with KNN_MAX_DEVICE_ROWS=2500 the dataset is streamed
+    from it in 3 chunks instead of being copied whole."""
+    from distributed_machine_learning_project_amd.utils.shm import share_input
+    inp, expect, _, _ = workload
+    monkeypatch.setenv("KNN_MAX_DEVICE_ROWS", max_rows)
+    eng = _engine("farm")
+    sh = share_input(eng.comm, inp)
+    out = eng.KNN(sh.params, sh, None)
+    assert bytes(eng.report(out)) == expect
+    sh.close()
+    eng.close()
+
+
+def test_debug_listing(gpu, workload):
+    inp, _, d, i = workload
+    eng = _engine("ring", debug=True)
+    out = eng.KNN(inp.params, inp, None)
+    lab, _ = K.finalize_cpu(i, inp.k, inp.labels)
+    assert bytes(eng.report(out)) == dmlp.format_debug(d, i, inp.k, lab)
+    eng.close()

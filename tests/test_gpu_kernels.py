@@ -195,6 +195,22 @@ def test_pipelined_chunks_match(torch_cuda):
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
 
 
+def test_streamed_out_of_core_matches(torch_cuda):
+    """Dataset streamed from pinned host memory in 3 chunks (double-buffered H2D), running
+    top-k lists merged per chunk == the exact CPU path."""
+    torch = torch_cuda
+    inp = dmlp.generate(25000, 3000, 32, 0.0, 1000.0, 1, 30, 10, seed=23)
+    Xp = torch.from_numpy(inp.X).pin_memory().numpy()
+    Qx = torch.from_numpy(inp.Qx).cuda()
+    d, i, lab, cs = K.knn_gpu_streamed(Xp, inp.labels, (0, 10), Qx, inp.k, chunk_rows=9000)
+    torch.cuda.synchronize()
+    d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
 def test_merge_and_finalize(torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(1)
