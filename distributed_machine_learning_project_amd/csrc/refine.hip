@@ -90,10 +90,11 @@ struct RunTopK {
 
 __device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* __restrict__ labels,
                                               int label_lo, int label_hi, int* hist,
-                                              int* out_label, uint64_t* out_cs) {
+                                              int* out_label, uint64_t* out_cs,
+                                              int hist_cap = kHistCap) {
   const int lane = dmlp::lane_id();
   // labels of ids < 0 (padding) are never read
-  const int label = k > 0 ? dmlp::wave_vote(ids, k, labels, label_lo, label_hi, hist, kHistCap) : -1;
+  const int label = k > 0 ? dmlp::wave_vote(ids, k, labels, label_lo, label_hi, hist, hist_cap) : -1;
   if (lane == 0) {
     *out_label = label;
     *out_cs = dmlp::fnv_checksum(label, ids, k);
@@ -116,8 +117,12 @@ struct GroupIn {
   int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
 };
 
-template <int E, bool GROUPS>
-__global__ __launch_bounds__(256) void k_refine(
+// GROUPS = KT of the single-term screen (1 or 2) for group-mode input, 0 otherwise.  The group
+// variant sizes its LDS for k <= 32 (the screen's limit) and labels in [lo, lo + 256) (wider
+// label ranges take wave_vote's counting fallback), so more waves stay resident to hide the
+// gathers that dominate this kernel.
+template <int E, int GROUPS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 : 1))) void k_refine(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int S, int cap,
     const double* __restrict__ X, int A, const double* __restrict__ Qx,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
@@ -126,13 +131,14 @@ __global__ __launch_bounds__(256) void k_refine(
     int* __restrict__ status, const GroupIn gin) {
   constexpr int P = E * 64;
   constexpr int SMAX = 256;
-  constexpr int KMAX = 128;
+  constexpr int KMAX = GROUPS ? 64 : 128;
+  constexpr int HCAP = GROUPS ? 256 : kHistCap;  // >= 256: the key histogram of the global threshold
   __shared__ double s_d[4][P];
   __shared__ int s_i[4][P];
   __shared__ double s_rd[4][KMAX];
   __shared__ int s_ri[4][KMAX];
   __shared__ int s_pre[4][SMAX + 1];
-  __shared__ int s_hist[4][kHistCap];
+  __shared__ int s_hist[4][HCAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wave;
   if (p >= nq) return;
@@ -212,17 +218,15 @@ __global__ __launch_bounds__(256) void k_refine(
     const unsigned tq = __float_as_uint(hq);
     const unsigned kh = (tq ^ ((unsigned)((int)tq >> 31) | 0x80000000u)) & 0xffff0000u;
     // ---- expand surviving groups; keep members whose single-term score reaches hq
-    const int KT = gin.KT;
-    float qf[2 * 32];  // KT <= 2: hi(q') as fp32, k-fragment order
+    constexpr int KT = GROUPS ? GROUPS : 1;  // (dead code for GROUPS == 0)
+    float qf[KT * 32];  // hi(q') as fp32, k-fragment order
 #pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      if (f < KT * 4) {
-        const u32x4 w = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
+    for (int f = 0; f < KT * 4; ++f) {
+      const u32x4 w = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          qf[f * 8 + 2 * e] = __uint_as_float(w[e] << 16);
-          qf[f * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-        }
+      for (int e = 0; e < 4; ++e) {
+        qf[f * 8 + 2 * e] = __uint_as_float(w[e] << 16);
+        qf[f * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
       }
     }
     // one member per lane (4 lanes per group: their fragments are adjacent 16-byte chunks)
@@ -242,8 +246,7 @@ __global__ __launch_bounds__(256) void k_refine(
           const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * 2 * 64) + (pl & 15);
           float sc = gin.xinit[id];
 #pragma unroll
-          for (int kt = 0; kt < 2; ++kt) {
-            if (kt >= KT) break;
+          for (int kt = 0; kt < KT; ++kt) {
             const u32x4* fk = fr + (int64_t)(((pl >> 4) * KT + kt) * 2) * 64;
 #pragma unroll
             for (int kq = 0; kq < 4; ++kq) {
@@ -355,7 +358,8 @@ __global__ __launch_bounds__(256) void k_refine(
   }
   if (labels) {
     dmlp::wave_sync();
-    finalize_wave(res_i, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q);
+    finalize_wave(res_i, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q,
+                  HCAP);
   }
 }
 
@@ -537,7 +541,7 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   // cap is only the id stride per (query, slice).  P = 256 slots cover k + 64 for every screened
   // k (<= 128); a larger P would cut the resident waves that hide the row-gather latency
   if (cap < 1) return -2;
-  hipLaunchKernelGGL((k_refine<4, false>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
+  hipLaunchKernelGGL((k_refine<4, 0>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
                      Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
                      out_label, out_cs, status, GroupIn{});
   DMLP_LAUNCH_CHECK();
@@ -556,9 +560,13 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
   const int64_t n_tiles = (n_points + 63) / 64;
   const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, (int)n_points,
                     (int)((n_tiles + S - 1) / S)};
-  hipLaunchKernelGGL((k_refine<4, true>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride,
-                     labels, label_lo, label_hi, out_label, out_cs, status, gin);
+#define DMLP_REFINE_G(KTV)                                                                     \
+  hipLaunchKernelGGL((k_refine<2, KTV>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
+                     cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
+                     labels, label_lo, label_hi, out_label, out_cs, status, gin)
+  if (KT == 1) DMLP_REFINE_G(1);
+  else DMLP_REFINE_G(2);
+#undef DMLP_REFINE_G
   DMLP_LAUNCH_CHECK();
   return 0;
 }
