@@ -89,6 +89,68 @@ __global__ void k_prep_frag(const double* __restrict__ X, int64_t N, int A,
   frag[f_lo] = vl;
 }
 
+// Fragments + norms in one pass: one thread per (point, 8-attribute group) as in k_prep_frag;
+// the G = 4*KT threads of a point are adjacent lanes, so |x - mu|^2 is a G-lane xor-shuffle
+// reduction and every thread keeps its 8 centred values in registers (the row is read once).
+// G must be a power of two (KT = 1, 2, 4); the wave folds its max norm before the one atomic.
+template <int G>
+__global__ __launch_bounds__(256) void k_prep_frag_norm(const double* __restrict__ X, int64_t N,
+                                                       int A, const double* __restrict__ mu,
+                                                       int64_t n_tiles, uint4* __restrict__ frag,
+                                                       float* __restrict__ xinit,
+                                                       unsigned* __restrict__ xnmax_bits,
+                                                       unsigned* __restrict__ bad) {
+  constexpr int KT = G / 4;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = n_tiles * 64 * G;
+  const bool live = gid < total;
+  const int64_t p = gid / G;
+  const int g = (int)(gid - p * G);
+  const int kt = g >> 2, kg = g & 3;
+  const int64_t t = p >> 6;
+  const int pl = (int)(p & 63);
+  const int rt = pl >> 4, r = pl & 15;
+  const int lane = r + 16 * kg;
+  unsigned short hi[8], lo[8];
+  unsigned badv = 0;
+  double ss = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int a = kt * 32 + kg * 8 + j;
+    double c = 0.0;
+    if (live && p < N && a < A) {
+      c = X[p * A + a] - mu[a];
+      if (!(fabs(c) < kMaxAbs)) { badv = 1; c = 0.0; }
+    }
+    ss += c * c;
+    split_bf16(c, hi[j], lo[j]);
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) ss += __shfl_xor(ss, o);
+  if (badv) atomicOr(bad, 1u);
+  if (live) {
+    const int64_t fbase = t * (int64_t)(4 * KT * 2) * 64;  // in uint4 (16 B) units
+    uint4 vh, vl;
+    vh.x = hi[0] | ((unsigned)hi[1] << 16); vh.y = hi[2] | ((unsigned)hi[3] << 16);
+    vh.z = hi[4] | ((unsigned)hi[5] << 16); vh.w = hi[6] | ((unsigned)hi[7] << 16);
+    vl.x = lo[0] | ((unsigned)lo[1] << 16); vl.y = lo[2] | ((unsigned)lo[3] << 16);
+    vl.z = lo[4] | ((unsigned)lo[5] << 16); vl.w = lo[6] | ((unsigned)lo[7] << 16);
+    frag[fbase + (int64_t)((rt * KT + kt) * 2 + 0) * 64 + lane] = vh;
+    frag[fbase + (int64_t)((rt * KT + kt) * 2 + 1) * 64 + lane] = vl;
+  }
+  // round the max up so the bound stays conservative; padding rows score -inf
+  const float sf = (float)ss;
+  float up = (live && p < N) ? sf * (1.0f + 1.0e-6f) + 1.0e-30f : 0.0f;
+  if (live && g == 0) xinit[p] = p < N ? (float)(-0.5 * ss) : -INFINITY;
+  // block max (non-negative floats order as their bits), one atomic per 256 threads
+  __shared__ unsigned smax;
+  if (threadIdx.x == 0) smax = 0u;
+  __syncthreads();
+  if (g == 0 && up > 0.0f) atomicMax(&smax, __float_as_uint(up));
+  __syncthreads();
+  if (threadIdx.x == 0 && smax) atomicMax(xnmax_bits, smax);
+}
+
 // One thread per point: xinit and the running max norm.
 __global__ void k_prep_norm(const double* __restrict__ X, int64_t N, int A,
                             const double* __restrict__ mu, int64_t n_pad,
@@ -107,6 +169,46 @@ __global__ void k_prep_norm(const double* __restrict__ X, int64_t N, int A,
   const float sf = (float)s;
   const float up = sf * (1.0f + 1.0e-6f) + 1.0e-30f;
   atomicMax(xnmax_bits, __float_as_uint(up));
+}
+
+// One thread per (query, 8-attribute group), G = 4*KT adjacent lanes per query (power of two).
+template <int G>
+__global__ __launch_bounds__(256) void k_prep_queries_g(const double* __restrict__ Qx, int64_t Q,
+                                                       int A, const double* __restrict__ mu,
+                                                       uint4* __restrict__ qhi,
+                                                       uint4* __restrict__ qlo,
+                                                       float* __restrict__ qn,
+                                                       unsigned* __restrict__ bad) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t q = gid / G;
+  const int g = (int)(gid - q * G);
+  const bool live = q < Q;
+  unsigned short hi[8], lo[8];
+  unsigned badv = 0;
+  double ss = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int a = g * 8 + j;
+    double c = 0.0;
+    if (live && a < A) {
+      c = Qx[q * A + a] - mu[a];
+      if (!(fabs(c) < kMaxAbs)) { badv = 1; c = 0.0; }
+    }
+    ss += c * c;
+    split_bf16(c, hi[j], lo[j]);
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) ss += __shfl_xor(ss, o);
+  if (badv) atomicOr(bad, 1u);
+  if (!live) return;
+  uint4 vh, vl;
+  vh.x = hi[0] | ((unsigned)hi[1] << 16); vh.y = hi[2] | ((unsigned)hi[3] << 16);
+  vh.z = hi[4] | ((unsigned)hi[5] << 16); vh.w = hi[6] | ((unsigned)hi[7] << 16);
+  vl.x = lo[0] | ((unsigned)lo[1] << 16); vl.y = lo[2] | ((unsigned)lo[3] << 16);
+  vl.z = lo[4] | ((unsigned)lo[5] << 16); vl.w = lo[6] | ((unsigned)lo[7] << 16);
+  qhi[q * G + g] = vh;
+  qlo[q * G + g] = vl;
+  if (g == 0) qn[q] = (float)ss;
 }
 
 __global__ void k_prep_queries(const double* __restrict__ Qx, int64_t Q, int A,
@@ -156,7 +258,20 @@ extern "C" int dmlp_prep_data(const double* X, int64_t N, int A, const double* m
   if (KT < 1 || A > KT * 32) return -1;
   const int64_t n_tiles = (N + 63) / 64;
   const int64_t total = n_tiles * 64 * KT * 4;
-  if (total > 0) {
+  if (total > 0 && (KT == 1 || KT == 2 || KT == 4)) {
+    const dim3 grid((unsigned)((total + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (KT == 1)
+      hipLaunchKernelGGL(k_prep_frag_norm<4>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
+                         (uint4*)xfrag, xinit, xnmax_bits, bad);
+    else if (KT == 2)
+      hipLaunchKernelGGL(k_prep_frag_norm<8>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
+                         (uint4*)xfrag, xinit, xnmax_bits, bad);
+    else
+      hipLaunchKernelGGL(k_prep_frag_norm<16>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
+                         (uint4*)xfrag, xinit, xnmax_bits, bad);
+    DMLP_LAUNCH_CHECK();
+  } else if (total > 0) {
     const int64_t blocks = (total + 255) / 256;
     hipLaunchKernelGGL(k_prep_frag, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, X,
                        N, A, mu, KT, n_tiles, (uint4*)xfrag, bad);
@@ -173,7 +288,23 @@ extern "C" int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const doubl
                                  void* qhi, void* qlo, float* qn, unsigned* bad, void* stream) {
   if (KT < 1 || A > KT * 32) return -1;
   if (Q <= 0) return 0;
-  hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)Q), dim3(64), 0, (hipStream_t)stream, Qx, Q,
+  hipStream_t st = (hipStream_t)stream;
+  if (KT == 1 || KT == 2 || KT == 4) {
+    const int64_t total = Q * KT * 4;
+    const dim3 grid((unsigned)((total + 255) / 256));
+    if (KT == 1)
+      hipLaunchKernelGGL(k_prep_queries_g<4>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
+                         (uint4*)qlo, qn, bad);
+    else if (KT == 2)
+      hipLaunchKernelGGL(k_prep_queries_g<8>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
+                         (uint4*)qlo, qn, bad);
+    else
+      hipLaunchKernelGGL(k_prep_queries_g<16>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
+                         (uint4*)qlo, qn, bad);
+    DMLP_LAUNCH_CHECK();
+    return 0;
+  }
+  hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)Q), dim3(64), 0, st, Qx, Q,
                      A, mu, KT, (unsigned short*)qhi, (unsigned short*)qlo, qn, bad);
   DMLP_LAUNCH_CHECK();
   return 0;
