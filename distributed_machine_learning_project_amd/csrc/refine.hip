@@ -500,30 +500,53 @@ __global__ void k_fmt_scan_blocks(int64_t* __restrict__ blocksum, int nb) {
   }
 }
 
-__global__ void k_fmt_write(const uint64_t* __restrict__ cs, int nq, int qid_base,
-                            int64_t* __restrict__ off, const int64_t* __restrict__ blocksum,
-                            char* __restrict__ out) {
+// Each block renders its 1024 lines into LDS, then stores the block's byte range with dword
+// stores (bytes only at the two unaligned ends).  The target may be page-locked host memory
+// (the native engine writes the report straight into its output buffer): wide, contiguous
+// stores keep the link busy where per-character stores would not.
+__global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__ cs, int nq,
+                                                   int qid_base, int64_t* __restrict__ off,
+                                                   const int64_t* __restrict__ blocksum,
+                                                   char* __restrict__ out) {
+  __shared__ char txt[1024 * 48 + 4];
   const int i = blockIdx.x * 1024 + threadIdx.x;
-  if (i >= nq) return;
-  const int64_t qid = (int64_t)qid_base + i;
-  const uint64_t v = cs[i];
-  const int len = line_len(qid, v);
-  const int64_t end = blocksum[blockIdx.x] + off[i + 1];
-  int64_t pos = end - len;
-  const char* pre = "Query ";
-  for (int c = 0; c < 6; ++c) out[pos++] = pre[c];
-  char tmp[24];
-  int n = 0;
-  uint64_t t = (uint64_t)qid;
-  do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
-  while (n) out[pos++] = tmp[--n];
-  const char* mid = " checksum: ";
-  for (int c = 0; c < 11; ++c) out[pos++] = mid[c];
-  t = v;
-  do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
-  while (n) out[pos++] = tmp[--n];
-  out[pos++] = '\n';
-  off[i + 1] = end;
+  const int64_t g0 = blocksum[blockIdx.x], g1 = blocksum[blockIdx.x + 1];
+  if (i < nq) {
+    const int64_t qid = (int64_t)qid_base + i;
+    const uint64_t v = cs[i];
+    const int len = line_len(qid, v);
+    const int64_t endl = off[i + 1];  // block-local inclusive end
+    int pos = (int)(endl - len);
+    const char* pre = "Query ";
+    for (int c = 0; c < 6; ++c) txt[pos++] = pre[c];
+    char tmp[24];
+    int n = 0;
+    uint64_t t = (uint64_t)qid;
+    do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
+    while (n) txt[pos++] = tmp[--n];
+    const char* mid = " checksum: ";
+    for (int c = 0; c < 11; ++c) txt[pos++] = mid[c];
+    t = v;
+    do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
+    while (n) txt[pos++] = tmp[--n];
+    txt[pos++] = '\n';
+  }
+  __syncthreads();
+  const int64_t a0 = (g0 + 3) & ~int64_t(3), a1 = std::max(a0, g1 & ~int64_t(3));
+  if (threadIdx.x < 3) {  // unaligned head / tail bytes
+    const int64_t h = g0 + threadIdx.x, tl = a1 + threadIdx.x;
+    if (h < a0 && h < g1) out[h] = txt[h - g0];
+    if (tl < g1 && tl >= a0) out[tl] = txt[tl - g0];
+  }
+  unsigned* o32 = reinterpret_cast<unsigned*>(out + a0);
+  const int nw = (int)((a1 - a0) >> 2), b = (int)(a0 - g0);
+  for (int w = threadIdx.x; w < nw; w += 1024) {
+    const int s = b + 4 * w;
+    o32[w] = (unsigned)(unsigned char)txt[s] | ((unsigned)(unsigned char)txt[s + 1] << 8) |
+             ((unsigned)(unsigned char)txt[s + 2] << 16) |
+             ((unsigned)(unsigned char)txt[s + 3] << 24);
+  }
+  if (i < nq) off[i + 1] += g0;
   if (i == 0) off[0] = 0;
 }
 
