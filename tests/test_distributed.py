@@ -13,7 +13,14 @@ import distributed_machine_learning_project_amd as dmlp
 from distributed_machine_learning_project_amd.ops import reference as ref
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-_port = [29800 + (os.getpid() % 500)]
+
+
+def _free_port():
+    """A port the OS just handed out (safe under pytest-xdist, unlike a counter)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
 
 
 def _oracle_report(inp):
@@ -22,14 +29,13 @@ def _oracle_report(inp):
 
 
 def _run(path, np_, strategy, extra=(), env_extra=None):
-    _port[0] += 1
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     env.update(env_extra or {})
     if np_ == 1:
         cmd = [sys.executable, "-m", "distributed_machine_learning_project_amd.harness"]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
-               str(np_), "--master-addr", "127.0.0.1", "--master-port", str(_port[0]), "-m",
+               str(np_), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
                "distributed_machine_learning_project_amd.harness"]
     cmd += ["--strategy", strategy, "--device", "cpu", "--input", path, *extra]
     r = subprocess.run(cmd, capture_output=True, env=env, timeout=240, cwd=ROOT)
