@@ -22,6 +22,9 @@ _SIGS = {
     "dmlp_center": (i32, [vp, i64, i32, vp, vp]),
     "dmlp_prep_data": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp]),
     "dmlp_prep_queries": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, vp]),
+    "dmlp_host_threads": (i32, []),
+    "dmlp_cpu_center": (None, [vp, i64, i32, vp]),
+    "dmlp_cpu_prep_queries": (i32, [vp, i64, i32, vp, i32, vp, vp]),
     "dmlp_screen_kmax": (i32, [i32]),
     "dmlp_screen_lds_bytes": (i32, [i32, i32]),
     "dmlp_screen_waves": (i32, [i32, i32]),

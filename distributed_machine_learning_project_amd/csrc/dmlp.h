@@ -33,6 +33,14 @@ int dmlp_prep_data(const double* X, int64_t N, int A, const double* mu, int KT, 
 int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT, void* qhi,
                       void* qlo, float* qn, unsigned* bad, void* stream);
 
+// host_prep.cpp: the screen's query operands rendered on the host (persistent thread pool) —
+// mu over the first min(N, 4096) rows like dmlp_center; qhi [Q][KT*32] bf16 bits, qn [Q] fp32.
+// dmlp_cpu_prep_queries returns 1 if some |q - mu| is outside the screen's range.
+int dmlp_host_threads(void);
+void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu);
+int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
+                          uint16_t* qhi, float* qn);
+
 // ---------------------------------------------------------------- device: screen (K2+K3, fused)
 // bf16x3 MFMA screen + per-query streaming threshold + candidate compaction.  Queries are the
 // class list qidx[0..nq); data is split into S slices.  Output: for class position p and slice s,

@@ -1,0 +1,200 @@
+// host_prep.cpp — query preparation on the host, run while the dataset is still crossing PCIe.
+//
+// The single-term screen reads only bf16(q - mu) and |q - mu|^2 of each query; the fp64 query
+// rows are needed later, by the exact re-rank.  Rendering the screen operands here (8.4 MB for
+// the bench shape instead of the 33.5 MB of fp64 rows) lets the screen start once the dataset and
+// these operands have landed, with the fp64 queries copied behind the screen.  mu is the mean of
+// the first min(N, 4096) rows, exactly the rows k_center (prep.hip) uses.
+//
+// The bits match prep.hip: c = q - mu in fp64; hi = bf16_rn(fp32_rn(c)); |c| >= 1e15 or NaN
+// flags the input as outside the screen's range (the caller then takes the device path).
+#include "dmlp.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include <immintrin.h>
+
+namespace {
+
+constexpr double kMaxAbs = 1.0e15;
+
+// Persistent workers: a per-call std::thread spawn (tens of microseconds each) would cost more
+// than the conversion itself.
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int t = 0; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  // f(part, parts) on every worker and the caller; returns when all parts are done
+  void run(const std::function<void(int, int)>& f) {
+    const int parts = size();
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      pending_.store(parts - 1);
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(parts - 1, parts);
+    while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int, int)>* job;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+        job = job_;
+      }
+      (*job)(t, size());
+      pending_.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  const std::function<void(int, int)>* job_ = nullptr;
+  std::atomic<int> pending_{0};
+};
+
+int pool_threads() {
+  if (const char* e = std::getenv("DMLP_HOST_THREADS")) return std::max(1, std::atoi(e));
+  const unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(h ? h : 1u, 8u));
+}
+
+Pool& pool() {
+  static Pool p(pool_threads() - 1);
+  return p;
+}
+
+inline uint16_t bf16_rn(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs only)
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace
+
+extern "C" int dmlp_host_threads(void) { return pool().size(); }
+
+extern "C" void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu) {
+  const int64_t n = std::min<int64_t>(N, 4096);
+  for (int a = 0; a < A; ++a) mu[a] = 0.0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int a = 0; a < A; ++a) mu[a] += X[i * A + a];
+  for (int a = 0; a < A; ++a) mu[a] = n ? mu[a] / (double)n : 0.0;
+}
+
+namespace {
+
+// Portable row: the reference for the AVX2 path's bits (four fixed partial sums for |c|^2).
+int prep_range_scalar(const double* Qx, int64_t q0, int64_t q1, int A, const double* mu, int W,
+                      uint16_t* qhi, float* qn) {
+  int ok = 1;
+  for (int64_t q = q0; q < q1; ++q) {
+    const double* r = Qx + q * A;
+    uint16_t* h = qhi + q * W;
+    double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int a = 0; a < A; ++a) {
+      double c = r[a] - mu[a];
+      if (!(std::fabs(c) < kMaxAbs)) { ok = 0; c = 0.0; }
+      s4[a & 3] += c * c;
+      h[a] = bf16_rn((float)c);
+    }
+    for (int a = A; a < W; ++a) h[a] = 0;
+    qn[q] = (float)((s4[0] + s4[2]) + (s4[1] + s4[3]));
+  }
+  return ok;
+}
+
+// A multiple of 8: 4 doubles per vector, partial sums s4[a & 3] exactly as the scalar row.
+__attribute__((target("avx2"))) int prep_range_avx2(const double* Qx, int64_t q0, int64_t q1,
+                                                     int A, const double* mu, int W,
+                                                     uint16_t* qhi, float* qn) {
+  const __m256d lim = _mm256_set1_pd(kMaxAbs);
+  const __m256d sgn = _mm256_set1_pd(-0.0);
+  const __m256i rnd = _mm256_set1_epi32(0x7fff), one = _mm256_set1_epi32(1);
+  __m256d okv = _mm256_castsi256_pd(_mm256_set1_epi64x(-1));
+  for (int64_t q = q0; q < q1; ++q) {
+    const double* r = Qx + q * A;
+    uint16_t* h = qhi + q * W;
+    __m256d acc = _mm256_setzero_pd();
+    for (int a = 0; a < A; a += 8) {
+      __m256d c0 = _mm256_sub_pd(_mm256_loadu_pd(r + a), _mm256_loadu_pd(mu + a));
+      __m256d c1 = _mm256_sub_pd(_mm256_loadu_pd(r + a + 4), _mm256_loadu_pd(mu + a + 4));
+      const __m256d m0 = _mm256_cmp_pd(_mm256_andnot_pd(sgn, c0), lim, _CMP_LT_OQ);
+      const __m256d m1 = _mm256_cmp_pd(_mm256_andnot_pd(sgn, c1), lim, _CMP_LT_OQ);
+      okv = _mm256_and_pd(okv, _mm256_and_pd(m0, m1));
+      c0 = _mm256_and_pd(c0, m0);
+      c1 = _mm256_and_pd(c1, m1);
+      acc = _mm256_add_pd(acc, _mm256_mul_pd(c0, c0));
+      acc = _mm256_add_pd(acc, _mm256_mul_pd(c1, c1));
+      const __m256 f = _mm256_set_m128(_mm256_cvtpd_ps(c1), _mm256_cvtpd_ps(c0));
+      __m256i u = _mm256_castps_si256(f);
+      u = _mm256_add_epi32(u, _mm256_add_epi32(rnd, _mm256_and_si256(_mm256_srli_epi32(u, 16), one)));
+      u = _mm256_srli_epi32(u, 16);
+      // 8 x u32 -> 8 x u16 (values < 2^16): pack within lanes, then gather the two halves
+      const __m256i p = _mm256_packus_epi32(u, u);
+      const __m256i o = _mm256_permute4x64_epi64(p, 0x08);
+      _mm_storeu_si128((__m128i*)(h + a), _mm256_castsi256_si128(o));
+    }
+    for (int a = A; a < W; ++a) h[a] = 0;
+    alignas(32) double s4[4];
+    _mm256_store_pd(s4, acc);
+    qn[q] = (float)((s4[0] + s4[2]) + (s4[1] + s4[3]));
+  }
+  return _mm256_movemask_pd(okv) == 0xf;
+}
+
+int prep_range_any(const double* Qx, int64_t q0, int64_t q1, int A, const double* mu, int W,
+                   uint16_t* qhi, float* qn) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2 && A % 8 == 0) return prep_range_avx2(Qx, q0, q1, A, mu, W, qhi, qn);
+  return prep_range_scalar(Qx, q0, q1, A, mu, W, qhi, qn);
+}
+
+}  // namespace
+
+// qhi: [Q][KT*32] bf16 bits (zero padded), qn: [Q] fp32 |q - mu|^2.  Returns 1 if some
+// |q - mu| is outside the screen's range (outputs then not usable), else 0.
+extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
+                                     uint16_t* qhi, float* qn) {
+  const int W = KT * 32;
+  std::atomic<int> ok{1};
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    const int64_t q0 = Q * part / parts, q1 = Q * (part + 1) / parts;
+    if (!prep_range_any(Qx, q0, q1, A, mu, W, qhi, qn)) ok.store(0, std::memory_order_relaxed);
+  };
+  if (Q * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+  return ok.load() ? 0 : 1;
+}

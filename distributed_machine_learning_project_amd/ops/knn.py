@@ -137,7 +137,9 @@ class DeviceDataset:
         return (self.N + 63) // 64
 
 
-def prepare_dataset(X, labels=None, label_range=None) -> DeviceDataset:
+def prepare_dataset(X, labels=None, label_range=None, mu=None) -> DeviceDataset:
+    """mu (device f64 [A]), if given, is the centre to use instead of dmlp_center's (the
+    host-prepared query operands of knn_gpu_pipelined were centred on it)."""
     torch = _torch()
     L = _lib.lib()
     X = X.contiguous()
@@ -146,7 +148,9 @@ def prepare_dataset(X, labels=None, label_range=None) -> DeviceDataset:
     KT = max(1, (A + 31) // 32)
     screen_ok = KT <= SCREEN_MAX_KT and N > 0
     dev = X.device
-    mu = torch.empty(max(A, 1), dtype=torch.float64, device=dev)
+    mu_given = mu is not None
+    if not mu_given:
+        mu = torch.empty(max(A, 1), dtype=torch.float64, device=dev)
     xnmax = torch.zeros(1, dtype=torch.int32, device=dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
     n_tiles = (N + 63) // 64
@@ -154,7 +158,8 @@ def prepare_dataset(X, labels=None, label_range=None) -> DeviceDataset:
         xfrag = torch.empty(n_tiles * 64 * KT * 32 * 2, dtype=torch.int16, device=dev)
         xinit = torch.empty(n_tiles * 64, dtype=torch.float32, device=dev)
         s = _stream()
-        _lib.check(L.dmlp_center(_p(X), N, A, _p(mu), s), "center")
+        if not mu_given:
+            _lib.check(L.dmlp_center(_p(X), N, A, _p(mu), s), "center")
         _lib.check(L.dmlp_prep_data(_p(X), N, A, _p(mu), KT, _p(xfrag), _p(xinit), _p(xnmax),
                                     _p(bad), s), "prep_data")
     else:
@@ -231,7 +236,11 @@ class _KnnCall:
     3-term escalation / exact fallback / finalize of the few queries that need it).  The split
     lets knn_gpu_pipelined keep several query chunks in flight on their own streams."""
 
-    def __init__(self, ds, Qx, k_host, finalize=True, exact=False, kstride=None, gpu_share=1.0):
+    def __init__(self, ds, Qx, k_host, finalize=True, exact=False, kstride=None, gpu_share=1.0,
+                 out=None, prepped=None, qx_event=None):
+        """prepped = (qhi, qn) device tensors rendered by the host (dmlp_cpu_prep_queries) with
+        ds.mu; qx_event: the fp64 query rows are only complete once it fires (they are copied
+        behind the screen) — everything that reads Qx waits for it."""
         torch = _torch()
         self.ds = ds
         self.Qx = Qx.contiguous()
@@ -245,15 +254,22 @@ class _KnnCall:
         self.ks = max(1, self.kmax) if kstride is None else kstride
         self.exact = exact
         self.gpu_share = gpu_share
+        self.prepped = prepped
+        self.qx_event = qx_event
         self.want_fin = finalize and ds.labels is not None
         # k > N: pad with (+inf,-1) like bench_2
         self.kk = self.k_host if self.kmax <= ds.N else np.minimum(self.k_host, ds.N)
         dev = self.dev
         self.k_dev = _h2d(self.k_host, dev)
-        self.out_d = torch.full((Q, self.ks), float("inf"), dtype=torch.float64, device=dev)
-        self.out_i = torch.full((Q, self.ks), -1, dtype=torch.int32, device=dev)
-        self.lab = torch.empty(Q, dtype=torch.int32, device=dev) if self.want_fin else None
-        self.cs = torch.empty(Q, dtype=torch.int64, device=dev) if self.want_fin else None
+        if out is not None:  # rows of caller-owned result tensors (pipelined chunks)
+            self.out_d, self.out_i, self.lab, self.cs = out
+            self.out_d.fill_(float("inf"))
+            self.out_i.fill_(-1)
+        else:
+            self.out_d = torch.full((Q, self.ks), float("inf"), dtype=torch.float64, device=dev)
+            self.out_i = torch.full((Q, self.ks), -1, dtype=torch.int32, device=dev)
+            self.lab = torch.empty(Q, dtype=torch.int32, device=dev) if self.want_fin else None
+            self.cs = torch.empty(Q, dtype=torch.int64, device=dev) if self.want_fin else None
         self.status = torch.zeros(Q, dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------------ launch (async)
@@ -283,13 +299,6 @@ class _KnnCall:
             return self
         KT = ds.KT
         dev = self.dev
-        self.qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
-        self.qlo = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
-        self.qn = torch.empty(Q, dtype=torch.float32, device=dev)
-        _lib.check(L.dmlp_prep_queries(_p(self.Qx), Q, A, _p(ds.mu), KT, _p(self.qhi),
-                                       _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
-                   "prep_queries")
-        self.kdev_eff = self.k_dev if kk is self.k_host else _h2d(kk.astype(np.int32), dev)
         # k <= 32 and A <= 64: single-term (x1) or 3-term barrier-free streaming kernel;
         # otherwise the LDS-shared 3-term kernel.  x1 queries whose candidates overflow (data
         # too tight for the single-term bound) escalate to the 3-term screen, and only what
@@ -297,14 +306,39 @@ class _KnnCall:
         x1_ok = SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(KT) > 0
         self.stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
         self.first_a = "x1" if x1_ok else ("stream" if self.stream_ok else "lds")
+        if self.prepped is not None and self.all_a and self.first_a == "x1":
+            self.qhi, self.qn = self.prepped  # x1 reads neither qlo nor the fp64 rows
+            self.qlo = None
+        else:
+            self._prep_on_device()
+        self.kdev_eff = self.k_dev if kk is self.k_host else _h2d(kk.astype(np.int32), dev)
         if self.all_a or len(self.cls_a):
             self._screen_pass(self.cls_a, self.first_a)
         if len(self.cls_b):
             self._screen_pass(self.cls_b, "lds")
         return self
 
+    def _wait_qx(self):
+        if self.qx_event is not None:
+            _torch().cuda.current_stream().wait_event(self.qx_event)
+            self.qx_event = None
+
+    def _prep_on_device(self):
+        torch = _torch()
+        L = _lib.lib()
+        ds, Q, A, KT, dev = self.ds, self.Q, self.A, self.ds.KT, self.dev
+        self._wait_qx()
+        self.qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
+        self.qlo = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
+        self.qn = torch.empty(Q, dtype=torch.float32, device=dev)
+        _lib.check(L.dmlp_prep_queries(_p(self.Qx), Q, A, _p(ds.mu), KT, _p(self.qhi),
+                                       _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
+                   "prep_queries")
+
     def _screen_pass(self, idx, impl):
         torch = _torch()
+        if impl != "x1" and self.qlo is None:
+            self._prep_on_device()  # escalation after a host-prepared x1 pass
         L = _lib.lib()
         ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
         N = ds.N
@@ -339,6 +373,7 @@ class _KnnCall:
                                         _p(self.qhi), _p(self.qn), _p(qidx), _p(self.kdev_eff),
                                         nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                                         _p(cand_ids), _p(cand_cnt), _p(cand_h), s), "screen_x1")
+            self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
                 cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
                 _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, N, _p(qidx), _p(self.kdev_eff), nq,
@@ -357,6 +392,7 @@ class _KnnCall:
                                      _p(self.qhi), _p(self.qlo), _p(self.qn), _p(qidx),
                                      _p(self.kdev_eff), nq, _p(ds.xnmax_bits), _p(ds.bad), er, S,
                                      _p(cand_ids), _p(cand_cnt), s), "screen")
+        self._wait_qx()
         _lib.check(L.dmlp_refine(cap, _p(cand_ids), _p(cand_cnt), S, _p(ds.X), A, _p(self.Qx),
                                  _p(qidx), _p(self.kdev_eff), nq, _p(self.out_d), _p(self.out_i),
                                  self.ks, *fin), "refine")
@@ -377,6 +413,7 @@ class _KnnCall:
                       getattr(self, "qn", None), getattr(self, "kdev_eff", None)):
                 if t is not None:
                     t.record_stream(cur)
+        self._wait_qx()
         n_ovf = n_esc = 0
         if self.screened:
             n_ovf = int(self.status.sum().item())
@@ -426,18 +463,23 @@ class _PinnedArena:
         self.old = []
         self.off = 0
 
-    def put(self, a: np.ndarray):
+    def alloc(self, n: int):
+        """n uninitialised page-locked bytes (torch uint8), valid until the next reset()."""
         torch = _torch()
-        a = np.ascontiguousarray(a)
-        n = a.nbytes
         if self.buf is None or self.off + n > self.buf.numel():
             if self.buf is not None:
                 self.old.append(self.buf)  # in-flight copies may still read it
             self.buf = torch.empty(max(4 << 20, 2 * (self.off + n)), dtype=torch.uint8).pin_memory()
             self.off = 0
         view = self.buf[self.off:self.off + n]
-        view.numpy()[:] = a.view(np.uint8).reshape(-1)
         self.off = (self.off + n + 255) & ~255
+        return view
+
+    def put(self, a: np.ndarray):
+        torch = _torch()
+        a = np.ascontiguousarray(a)
+        view = self.alloc(a.nbytes)
+        view.numpy()[:] = a.view(np.uint8).reshape(-1)
         return view.view(torch.from_numpy(a[:0]).dtype)
 
     def mark(self):
@@ -482,63 +524,101 @@ def _side_stream(name):
 
 
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
-                      chunks: int = 2, finalize: bool = True, exact: bool = False):
-    """Host arrays in (page-locked for real overlap), device results out: the dataset and the
-    query chunks are copied on a copy stream while earlier chunks already screen on their own
-    compute streams, so the H2D of the queries hides behind the MFMA screen (SURVEY.md §7.2
-    step 6, "chunked H2D overlapped with compute").  Same results as prepare_dataset + knn_gpu.
-    Two chunks by default: a process gets 4 hardware queues (main, copy, 2 compute), and more
-    streams than queues share one in order, which serializes their kernels.
+                      chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
+                      mu_rows=None):
+    """Host arrays in (page-locked for real overlap), device results out, with the fp64 query
+    rows copied behind the screen ("H2D overlapped with compute").
+
+    chunks == 1 (default): while the dataset rows cross PCIe, the host renders the screen's
+    query operands (bf16 fragments + norms, host_prep.cpp: 8.4 MB instead of 33.5 MB for the
+    bench shape); the screen starts once the rows and these operands have landed, and only the
+    re-rank waits for the fp64 queries.  chunks > 1: query chunks each screened once they land
+    (measured slower on the bench shape: two half-size screens have a worse tail than one).
+
+    gather(X_dev, lab_dev) -> (X, lab), if given, completes a dataset shard into the replica on
+    the compute stream (the RCCL all-gather ingress) while the queries are still in flight.
+    mu_rows: the dataset's first rows when X_host is a shard (the centre is their mean).
     Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
     torch = _torch()
+    L = _lib.lib()
     dev = torch.device("cuda", torch.cuda.current_device())
     main = torch.cuda.current_stream()
     copy = _side_stream("h2d")
     t_enter = time.perf_counter()
     _ARENA.reset()
-    copy.wait_stream(main)
+    copy.wait_stream(main)  # buffers recycled from the previous call
     Q = len(Q_host)
     A = X_host.shape[1]
+    KT = max(1, (A + 31) // 32)
+    k_host = np.ascontiguousarray(k_host, np.int32)
+    chunks = max(1, min(chunks, Q // 2048 if Q >= 4096 else 1))
+    bounds = [Q * c // chunks for c in range(chunks + 1)]
     with torch.cuda.stream(copy):
         X = torch.from_numpy(np.ascontiguousarray(X_host)).to(dev, non_blocking=True)
         lab = (torch.from_numpy(np.ascontiguousarray(labels_host)).to(dev, non_blocking=True)
                if labels_host is not None else None)
+        ev_x = torch.cuda.Event()
+        ev_x.record(copy)
+    prepped = mu_d = None
+    Qh = np.ascontiguousarray(Q_host, np.float64)
+    if (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and L.dmlp_screen_x1_qw(KT) > 0
+            and len(X_host) > 0 and int(k_host.min()) >= 1 and int(k_host.max()) <= SCREEN_KMAX_A):
+        src = np.ascontiguousarray((X_host if mu_rows is None else mu_rows)[:4096], np.float64)
+        mu_h = np.empty(A, np.float64)
+        L.dmlp_cpu_center(src.ctypes.data, len(src), A, mu_h.ctypes.data)
+        qhi_h = _ARENA.alloc(Q * KT * 64)
+        qn_h = _ARENA.alloc(Q * 4)
+        if L.dmlp_cpu_prep_queries(Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT, qhi_h.data_ptr(),
+                                   qn_h.data_ptr()) == 0:
+            with torch.cuda.stream(copy):
+                qhi = qhi_h.to(dev, non_blocking=True).view(torch.int16)
+                qn = qn_h.to(dev, non_blocking=True).view(torch.float32)
+            prepped = (qhi, qn)
+            mu_d = _h2d(mu_h, dev)
+    ev = []
+    with torch.cuda.stream(copy):
+        ev_p = torch.cuda.Event()
+        ev_p.record(copy)
         Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
-    main.wait_stream(copy)
-    ds = prepare_dataset(X, lab if finalize else None, label_range)
-    for t in (X, Qd) + ((lab,) if lab is not None else ()):
+        for c in range(chunks):
+            a, b = bounds[c], bounds[c + 1]
+            Qd[a:b].copy_(torch.from_numpy(Qh[a:b]), non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(copy)
+            ev.append(e)
+    for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()):
         t.record_stream(main)
-    chunks = max(1, min(chunks, Q // 2048 if Q >= 4096 else 1))
-    bounds = [Q * c // chunks for c in range(chunks + 1)]
+    main.wait_event(ev_x)
+    if gather is not None:
+        X, lab = gather(X, lab)
+    ds = prepare_dataset(X, lab if finalize else None, label_range, mu=mu_d)
+    ks = max(1, int(k_host.max()) if Q else 1) if kstride is None else kstride
+    fin = finalize and ds.labels is not None
+    od = torch.empty((Q, ks), dtype=torch.float64, device=dev)
+    oi = torch.empty((Q, ks), dtype=torch.int32, device=dev)
+    ol = torch.empty(Q, dtype=torch.int32, device=dev) if fin else None
+    oc = torch.empty(Q, dtype=torch.int64, device=dev) if fin else None
     calls = []
     for c in range(chunks):
         a, b = bounds[c], bounds[c + 1]
-        with torch.cuda.stream(copy):
-            Qd[a:b].copy_(torch.from_numpy(np.ascontiguousarray(Q_host[a:b])), non_blocking=True)
-        sc = _side_stream(f"chunk{c}")
-        sc.wait_stream(main)   # dataset prep
-        sc.wait_stream(copy)   # this chunk's queries
-        with torch.cuda.stream(sc):
-            Qd.record_stream(sc)
-            calls.append(_KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, kstride,
-                                  gpu_share=1.0 / chunks).launch())
+        out = (od[a:b], oi[a:b], ol[a:b] if fin else None, oc[a:b] if fin else None)
+        if prepped is not None:
+            main.wait_event(ev_p)  # screen operands landed; the fp64 rows may still be in flight
+            call = _KnnCall(ds, Qd, k_host, finalize, exact, ks, out=out, prepped=prepped,
+                            qx_event=ev[0])
+        else:
+            main.wait_event(ev[c])
+            call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)
+        calls.append(call.launch())
     t_launched = time.perf_counter()
-    results = []
-    for c, call in enumerate(calls):
-        main.wait_stream(_side_stream(f"chunk{c}"))
-        results.append(call.finish())
+    n_fb = sum(call.finish().n_fallback for call in calls)
     _ARENA.mark()
     if _PIPE_DEBUG:
         import sys
         print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms, finish "
-              f"{1e3 * (time.perf_counter() - t_launched):.3f} ms", file=sys.stderr)
-    if chunks == 1:
-        r = results[0]
-        return ds, r.dist, r.ids, r.label, r.checksum, r.n_fallback
-    cat = lambda xs: torch.cat(xs) if xs[0] is not None else None
-    return (ds, cat([r.dist for r in results]), cat([r.ids for r in results]),
-            cat([r.label for r in results]), cat([r.checksum for r in results]),
-            sum(r.n_fallback for r in results))
+              f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host prep "
+              f"{prepped is not None}", file=sys.stderr)
+    return ds, od, oi, ol, oc, n_fb
 
 
 _ENV_APPLIED = [False]

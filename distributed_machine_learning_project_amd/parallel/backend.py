@@ -52,15 +52,22 @@ class Backend:
         return torch.from_numpy(d), torch.from_numpy(i), lab, cs
 
     def knn_host(self, X_host, labels_host, label_range, Q_host, k_host: np.ndarray,
-                 kstride=None):
-        """knn() from host arrays: on the GPU the dataset / query H2D is chunked and overlapped
-        with the screen of earlier chunks (ops.knn.knn_gpu_pipelined).  Returns (dist, ids,
+                 kstride=None, gather=None, mu_rows=None):
+        """knn() from host arrays: on the GPU the query H2D is chunked and overlapped with the
+        screen of earlier chunks (ops.knn.knn_gpu_pipelined).  gather(X, lab) -> (X, lab)
+        completes a dataset shard on the device (all-gather ingress).  Returns (dist, ids,
         label, checksum) like knn()."""
         torch = _torch()
         if self.on_gpu:
             _, d, i, lab, cs, _ = K.knn_gpu_pipelined(X_host, labels_host, label_range, Q_host,
-                                                      k_host, kstride=kstride, exact=self.exact)
+                                                      k_host, kstride=kstride, exact=self.exact,
+                                                      gather=gather, mu_rows=mu_rows)
             return d, i, lab, cs
+        if gather is not None:
+            X, lab = gather(torch.from_numpy(np.ascontiguousarray(X_host)),
+                            torch.from_numpy(np.ascontiguousarray(labels_host)))
+            return self.knn(X, torch.from_numpy(np.ascontiguousarray(Q_host)), k_host,
+                            labels=lab, label_range=label_range, kstride=kstride)
         return self.knn(torch.from_numpy(np.ascontiguousarray(X_host)),
                         torch.from_numpy(np.ascontiguousarray(Q_host)), k_host,
                         labels=torch.from_numpy(np.ascontiguousarray(labels_host)),

@@ -176,25 +176,35 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             d, i, lb, cs = be.knn_streamed(inp.X, inp.labels, (lo, hi), Ql, kl_h, max_rows,
                                            kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
+    pipeline = os.environ.get("KNN_PIPELINE", "1") == "1"
     if mode == "allgather":
+        nc, nd = block_partition(N, comm.world)
+        r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
+        kl_h = np.array(inp.k[a:b])
+
+        def gather(Xs, ls):
+            return (comm.allgather_rows(Xs, nc, (A,), torch.float64),
+                    comm.allgather_rows(ls, nc, (), torch.int32))
+        if pipeline:
+            # this rank's rows and its query chunks on the copy stream; the all-gather and the
+            # screen of the first chunk run while the later chunks are still crossing PCIe
+            with tr.phase("h2d+allgather+compute"):
+                d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
+                                           inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
+                                           mu_rows=inp.X[:4096])
+            return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
         with tr.phase("h2d"):
-            nc, nd = block_partition(N, comm.world)
-            r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
             Xs = be.tensor(inp.X[r0:r1])
             ls = be.tensor(inp.labels[r0:r1])
             Ql = be.tensor(inp.Qx[a:b])
-            kl_h = np.array(inp.k[a:b])
         with tr.phase("allgather_data"):
-            X = comm.allgather_rows(Xs, nc, (A,), torch.float64)
-            lab = comm.allgather_rows(ls, nc, (), torch.int32)
+            X, lab = gather(Xs, ls)
         with tr.phase("compute"):
             d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
     bcast_data = mode == "bcast"
-    if not bcast_data and os.environ.get("KNN_PIPELINE", "0") == "1":
-        # per-GPU H2D chunked and overlapped with the screen of the chunks already resident
-        # (opt-in: measured 4.59 vs 4.22 ms/step on the bench shape — two half-size screens
-        # sharing the GPU cost more than the 0.6 ms of query H2D they hide)
+    if not bcast_data and pipeline:
+        # per-GPU H2D: the query chunks land while the earlier chunks already screen
         with tr.phase("h2d+compute"):
             kl_h = np.array(inp.k[a:b])
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
