@@ -25,6 +25,7 @@ _SIGS = {
     "dmlp_host_threads": (i32, []),
     "dmlp_cpu_center": (None, [vp, i64, i32, vp]),
     "dmlp_cpu_prep_queries": (i32, [vp, i64, i32, vp, i32, vp, vp]),
+    "dmlp_cpu_prep_data": (i32, [vp, i64, i32, vp, i32, vp, vp, vp]),
     "dmlp_screen_kmax": (i32, [i32]),
     "dmlp_screen_lds_bytes": (i32, [i32, i32]),
     "dmlp_screen_waves": (i32, [i32, i32]),
@@ -46,9 +47,9 @@ _SIGS = {
     "dmlp_screen_x1_waves_per_cu": (i32, [i32]),
     "dmlp_screen_x1_min_slices": (i64, [i64]),
     "dmlp_screen_x1_bound": (None, [i32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
-    "dmlp_screen_x1": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
+    "dmlp_screen_x1": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
-    "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i64, vp, vp,
+    "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp,
                                  i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
     "dmlp_set_x1_check": (None, [i32]),

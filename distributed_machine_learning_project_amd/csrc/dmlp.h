@@ -40,6 +40,10 @@ int dmlp_host_threads(void);
 void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu);
 int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
                           uint16_t* qhi, float* qn);
+// The dataset's single-term operands: the hi-only tile image (hl = 1 in dmlp_screen_x1 /
+// dmlp_refine_groups), xinit and the max norm bits.  Returns 1 if outside the screen's range.
+int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
+                       uint16_t* xhi, float* xinit, unsigned* xnmax_bits);
 
 // ---------------------------------------------------------------- device: screen (K2+K3, fused)
 // bf16x3 MFMA screen + per-query streaming threshold + candidate compaction.  Queries are the
@@ -79,7 +83,9 @@ int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);
-int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
+// hl: fragment halves per (step, kt) in xfrag — 2 for prep.hip's hi/lo image, 1 for the hi-only
+// image of dmlp_cpu_prep_data (same for dmlp_refine_groups).
+int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
                    int64_t n_points, const void* qhi, const float* qn, const int* qidx,
                    const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
                    const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
@@ -108,7 +114,7 @@ int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const 
 // exact distances.  status = 1 also when the survivors exceed 256 (pathological ties).
 int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
                        int S, const double* X, int A, const double* Qx, const void* xfrag,
-                       const float* xinit, const void* qhi, int KT, int64_t n_points,
+                       const float* xinit, const void* qhi, int KT, int hl, int64_t n_points,
                        const int* qidx, const int* qk, int nq, double* out_d, int* out_i,
                        int kstride, const int* labels, int label_lo, int label_hi,
                        int* out_label, uint64_t* out_cs, int* status, void* stream);

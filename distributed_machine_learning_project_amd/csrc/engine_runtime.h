@@ -359,9 +359,9 @@ struct LocalKnn {
         int* cc = cand_cnt.get((size_t)nq * S);
         if (impl == 0) {
           float* ch = cand_h.get((size_t)nq * S * 2);
-          DMLPCHK(dmlp_screen_x1(KT, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
+          DMLPCHK(dmlp_screen_x1(KT, 2, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
                                  words.p, words.p + 1, S, ci, cc, ch, st));
-          DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, N,
+          DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, 2, N,
                                      qi, kd, nq, out_d, out_i, kstride, fin ? labels : nullptr,
                                      lab_lo, lab_hi, lab, cs, stat, st));
           return;

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include <immintrin.h>
+#include <sched.h>
 
 namespace {
 
@@ -84,10 +85,15 @@ class Pool {
   std::atomic<int> pending_{0};
 };
 
+// CPUs this process may run on (the affinity mask, not the machine: a GPU box grants each job a
+// share of a 256-thread host), at most 16 — the conversions are bound by memory, not cores.
 int pool_threads() {
   if (const char* e = std::getenv("DMLP_HOST_THREADS")) return std::max(1, std::atoi(e));
-  const unsigned h = std::thread::hardware_concurrency();
-  return (int)std::max(1u, std::min(h ? h : 1u, 8u));
+  cpu_set_t set;
+  int n = 0;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 16));
 }
 
 Pool& pool() {
@@ -196,5 +202,69 @@ extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const d
   };
   if (Q * (int64_t)A < (int64_t)1 << 14) job(0, 1);
   else pool().run(job);
+  return ok.load() ? 0 : 1;
+}
+
+namespace {
+
+// One point's contribution to the hi-only tile image: 8 attributes (one 16-byte fragment chunk)
+// per (kt, kg), |c|^2 in fp64.  The chunk of point p = t*64 + rt*16 + r, attributes kt*32 + kg*8
+// .. +7, sits at uint4 index ((t*4 + rt)*KT + kt)*64 + kg*16 + r (prep.hip's layout, lo dropped).
+int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, const double* mu,
+                    int KT, uint16_t* xhi, float* xinit, float* nmax) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  const int W = KT * 32;
+  int ok = 1;
+  float mx = 0.0f;
+  alignas(32) uint16_t h[128];
+  alignas(32) float qn1[1];
+  for (int64_t p = p0; p < p1; ++p) {
+    float ssf;
+    if (p < N) {
+      if (avx2 && A % 8 == 0) {
+        if (!prep_range_avx2(X + p * A, 0, 1, A, mu, W, h, qn1)) ok = 0;
+      } else {
+        if (!prep_range_scalar(X + p * A, 0, 1, A, mu, W, h, qn1)) ok = 0;
+      }
+      ssf = qn1[0];
+      xinit[p] = -0.5f * ssf;
+      const float up = ssf * (1.0f + 1.0e-6f) + 1.0e-30f;
+      mx = std::max(mx, up);
+    } else {
+      std::memset(h, 0, sizeof(uint16_t) * W);
+      xinit[p] = -INFINITY;
+    }
+    const int64_t t = p >> 6;
+    const int pl = (int)(p & 63), rt = pl >> 4, r = pl & 15;
+    for (int kt = 0; kt < KT; ++kt)
+      for (int kg = 0; kg < 4; ++kg)
+        std::memcpy(xhi + ((((t * 4 + rt) * KT + kt) * 64 + kg * 16 + r) * 8), h + kt * 32 + kg * 8, 16);
+  }
+  *nmax = mx;
+  return ok;
+}
+
+}  // namespace
+
+// Dataset screen operands on the host: xhi = prep.hip's tile image with the lo halves dropped
+// ([n_tiles][4][KT][64] x 16 B, what the single-term screen and the group refine read),
+// xinit[n_tiles*64] = -|x - mu|^2 / 2 (fp32; -inf for padding rows), *xnmax_bits = the rounded-up
+// max |x - mu|^2 (fp32 bits).  Returns 1 if some |x - mu| is outside the screen's range.
+extern "C" int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
+                                  uint16_t* xhi, float* xinit, unsigned* xnmax_bits) {
+  const int64_t n_pad = ((N + 63) / 64) * 64;
+  std::atomic<int> ok{1};
+  std::vector<float> mx(64, 0.0f);
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    // whole tiles per part
+    const int64_t nt = n_pad / 64;
+    const int64_t p0 = nt * part / parts * 64, p1 = nt * (part + 1) / parts * 64;
+    if (!prep_data_range(X, N, p0, p1, A, mu, KT, xhi, xinit, &mx[part])) ok.store(0);
+  };
+  if (N * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+  float m = 0.0f;
+  for (float v : mx) m = std::max(m, v);
+  std::memcpy(xnmax_bits, &m, 4);
   return ok.load() ? 0 : 1;
 }

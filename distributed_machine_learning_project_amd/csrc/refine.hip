@@ -109,10 +109,11 @@ __device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* 
 // any summation order obeys the same error bound) is >= h.  Only survivors get exact distances.
 struct GroupIn {
   const float* cand_h;    // [nq * S][2]: slice threshold, query eps
-  const u32x4* xfrag;     // prep.hip tile image (hi at hl = 0)
+  const u32x4* xfrag;     // tile image (hi first; hl = 2: prep.hip's hi/lo, 1: hi only)
   const float* xinit;     // -|x'|^2/2 per point
   const bf16x8* qhi;      // [Q][KT*4] query hi fragments
   int KT;
+  int hl;
   int n_points;
   int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
 };
@@ -243,11 +244,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
         if (e >= kh && id < gin.n_points) {
           const int64_t t = id >> 6;
           const int pl = id & 63;
-          const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * 2 * 64) + (pl & 15);
+          const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * gin.hl * 64) + (pl & 15);
           float sc = gin.xinit[id];
 #pragma unroll
           for (int kt = 0; kt < KT; ++kt) {
-            const u32x4* fk = fr + (int64_t)(((pl >> 4) * KT + kt) * 2) * 64;
+            const u32x4* fk = fr + (int64_t)(((pl >> 4) * KT + kt) * gin.hl) * 64;
 #pragma unroll
             for (int kq = 0; kq < 4; ++kq) {
               const u32x4 w = fk[16 * kq];
@@ -574,14 +575,15 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
 extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt,
                                   const float* cand_h, int S, const double* X, int A,
                                   const double* Qx, const void* xfrag, const float* xinit,
-                                  const void* qhi, int KT, int64_t n_points, const int* qidx,
+                                  const void* qhi, int KT, int hl, int64_t n_points, const int* qidx,
                                   const int* qk, int nq, double* out_d, int* out_i, int kstride,
                                   const int* labels, int label_lo, int label_hi, int* out_label,
                                   uint64_t* out_cs, int* status, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256 || cap < 1 || KT < 1 || KT > 2 || n_points > 0x7fffffff) return -1;
+  if (hl != 1 && hl != 2) return -1;
   const int64_t n_tiles = (n_points + 63) / 64;
-  const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, (int)n_points,
+  const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
                     (int)((n_tiles + S - 1) / S)};
 #define DMLP_REFINE_G(KTV)                                                                     \
   hipLaunchKernelGGL((k_refine<2, KTV>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \

@@ -43,7 +43,6 @@ struct X1Cfg {
   // SUB - CHECK entries (CHECK more appends always fit) and keeps at most SUB - CHECK of them
   static constexpr int CAPE = 4 * (SUB - CHECK);  // group entries a column may keep
   static constexpr int IDCAP = 4 * (SUB - 1);  // group-id stride per (query, slice), any CHECK
-  static constexpr int FRAGS = 4 * KT * 2;      // 1 KiB fragments per 64-point tile (hi, lo)
   static constexpr int SBUF = NCOL * CP * 4;
   static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4;
   static constexpr int D = DEPTH;               // register-ring depth (steps in flight)
@@ -66,7 +65,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
     const unsigned* __restrict__ bad, float r1, float r2, int S, int tiles_per_slice,
-    int n_qblocks, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
+    int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
     float* __restrict__ cand_h) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
   constexpr int CT = C::CT;
@@ -131,11 +130,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       lflag[col] = 0;
     }
   }
-  // slice-local buffer resources: step j's fragments sit at j * KT * 2 KiB (hi at +0, lo at
-  // +1 KiB per kt) and its -|x|^2/2 at j * 64 B, so the ring loads need no address arithmetic
-  // beyond one scalar offset; prefetches past the slice read zeros instead of faulting
+  // slice-local buffer resources: step j's fragments sit at j * KT * hl KiB (hi at +0, lo — when
+  // the image carries it (hl = 2) — at +1 KiB per kt) and its -|x|^2/2 at j * 64 B, so the ring
+  // loads need no address arithmetic beyond one scalar offset; prefetches past the slice read
+  // zeros instead of faulting
+  const int ks = hl * 1024;          // bytes between kt fragments of a step
+  const int frags = 4 * KT * hl;     // 1 KiB fragments per 64-point tile
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(xfrag + (int64_t)t0 * (C::FRAGS * 64)), (short)0, nt * C::FRAGS * 64 * 16, 0x00020000);
+      (void*)(xfrag + (int64_t)t0 * (frags * 64)), (short)0, nt * frags * 64 * 16, 0x00020000);
   const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
 
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   do {                                                                                          \
     _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
       A[R][kt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(              \
-          xr, lane * 16 + kt * 2048, (J) * (KT * 2048), 0));                                    \
+          xr, lane * 16 + kt * ks, (J) * (KT * ks), 0));                                        \
     Xi[R] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ir, kg * 16, (J) * 64, 0)); \
   } while (0)
 #define DMLP_MFMA(R, AB)                                                                        \
@@ -363,7 +365,7 @@ int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
 int g_x1_check = 2;
 
 template <int KT, int SUB, int DEPTH, int CHECK>
-int launch_x1(const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
+int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, int S,
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream) {
@@ -376,7 +378,7 @@ int launch_x1(const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_
   hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, S, tps,          \
-                     n_qblocks, cand_ids, cand_cnt, cand_h)
+                     n_qblocks, hl, cand_ids, cand_cnt, cand_h)
   switch (g_x1_mode) {
     case 1: DMLP_X1_LAUNCH(1); break;
     case 8: DMLP_X1_LAUNCH(8); break;
@@ -424,7 +426,7 @@ extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
   return 0;
 }
 
-extern "C" int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xinit,
+extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit,
                               int64_t n_tiles, int64_t n_points, const void* qhi, const float* qn,
                               const int* qidx, const int* qk, int nq, int kmax,
                               const unsigned* xnmax_bits, const unsigned* bad, int S,
@@ -433,10 +435,11 @@ extern "C" int dmlp_screen_x1(int KT, int A, const void* xfrag, const float* xin
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 || n_points > n_tiles * 64) return -1;
   if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
   if (kmax > 32 || KT < 1 || KT > 2 || A > KT * 32) return -3;
+  if (hl != 1 && hl != 2) return -1;
   float r1, r2;
   dmlp_screen_x1_bound(A, &r1, &r2);
   hipStream_t st = (hipStream_t)stream;
-#define DMLP_X1_ARGS xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
+#define DMLP_X1_ARGS hl, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
                      r2, S, cand_ids, cand_cnt, cand_h, st
   const int sub = x1_sub(kmax);
   if (KT == 1 && sub == 16) {  // A/B variants of the bench shape: fill-check period

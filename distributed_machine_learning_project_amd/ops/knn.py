@@ -123,6 +123,24 @@ class DeviceDataset:
     xnmax_bits: "object"   # torch i32 [1] (fp32 bits)
     bad: "object"          # torch i32 [1]
     screen_ok: bool
+    hl: int = 2            # fragment halves in xfrag: 2 = prep.hip's hi/lo, 1 = host hi-only image
+
+    def ensure_full_frags(self):
+        """The 3-term screens read the lo halves too: render prep.hip's hi/lo image on the device
+        from the (landed) fp64 rows when the dataset arrived as the host's hi-only image."""
+        if self.hl == 2 or not self.screen_ok:
+            return
+        torch = _torch()
+        L = _lib.lib()
+        dev = self.X.device
+        n_tiles = self.n_tiles
+        xfrag = torch.empty(n_tiles * 64 * self.KT * 32 * 2, dtype=torch.int16, device=dev)
+        xinit = torch.empty(n_tiles * 64, dtype=torch.float32, device=dev)
+        xnmax = torch.zeros(1, dtype=torch.int32, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L.dmlp_prep_data(_p(self.X), self.N, self.A, _p(self.mu), self.KT, _p(xfrag),
+                                    _p(xinit), _p(xnmax), _p(bad), _stream()), "prep_data")
+        self.xfrag, self.xinit, self.xnmax_bits, self.bad, self.hl = xfrag, xinit, xnmax, bad, 2
 
     @property
     def N(self):
@@ -369,17 +387,20 @@ class _KnnCall:
                _p(self.cs), _p(self.status), s)
         if impl == "x1":
             cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
-            _lib.check(L.dmlp_screen_x1(KT, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
+            _lib.check(L.dmlp_screen_x1(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
                                         _p(self.qhi), _p(self.qn), _p(qidx), _p(self.kdev_eff),
                                         nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                                         _p(cand_ids), _p(cand_cnt), _p(cand_h), s), "screen_x1")
             self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
                 cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
-                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, N, _p(qidx), _p(self.kdev_eff), nq,
+                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, ds.hl, N, _p(qidx), _p(self.kdev_eff), nq,
                 _p(self.out_d), _p(self.out_i), self.ks, *fin), "refine_groups")
             self._keep = (qidx, cand_ids, cand_cnt, cand_h)
             return
+        if ds.hl != 2:
+            self._wait_qx()  # the device image is rendered from the fp64 rows
+            ds.ensure_full_frags()
         er = eps_rel(A)
         if impl == "stream":
             _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
@@ -525,19 +546,21 @@ def _side_stream(name):
 
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
                       chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
-                      mu_rows=None):
-    """Host arrays in (page-locked for real overlap), device results out, with the fp64 query
-    rows copied behind the screen ("H2D overlapped with compute").
+                      mu_rows=None, X_full_host=None):
+    """Host arrays in (page-locked for real overlap), device results out, with the fp64 rows
+    copied behind the screen ("H2D overlapped with compute").
 
-    chunks == 1 (default): while the dataset rows cross PCIe, the host renders the screen's
-    query operands (bf16 fragments + norms, host_prep.cpp: 8.4 MB instead of 33.5 MB for the
-    bench shape); the screen starts once the rows and these operands have landed, and only the
-    re-rank waits for the fp64 queries.  chunks > 1: query chunks each screened once they land
-    (measured slower on the bench shape: two half-size screens have a worse tail than one).
+    chunks == 1 (default): the host renders the single-term screen's operands — the dataset's
+    hi-only bf16 tile image + norms and the queries' bf16 fragments + norms (host_prep.cpp:
+    15.7 MB instead of the 59 MB of fp64 rows for the bench shape).  The screen starts once they
+    have landed; the fp64 dataset and query rows (and the labels) cross PCIe behind the screen,
+    and only the exact re-rank waits for them.  chunks > 1: query chunks each screened once they
+    land (measured slower on the bench shape: two half-size screens have a worse tail than one).
 
-    gather(X_dev, lab_dev) -> (X, lab), if given, completes a dataset shard into the replica on
-    the compute stream (the RCCL all-gather ingress) while the queries are still in flight.
-    mu_rows: the dataset's first rows when X_host is a shard (the centre is their mean).
+    gather(X_dev, lab_dev) -> (X, lab), if given, completes a dataset shard into the replica (the
+    RCCL all-gather ingress); it is issued on the copy stream, so it too runs behind the screen.
+    X_full_host: the whole dataset when X_host is a shard (the host renders the full screen
+    image from it); mu_rows: the dataset's first rows (the centre is their mean).
     Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
     torch = _torch()
     L = _lib.lib()
@@ -553,32 +576,50 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     k_host = np.ascontiguousarray(k_host, np.int32)
     chunks = max(1, min(chunks, Q // 2048 if Q >= 4096 else 1))
     bounds = [Q * c // chunks for c in range(chunks + 1)]
-    with torch.cuda.stream(copy):
-        X = torch.from_numpy(np.ascontiguousarray(X_host)).to(dev, non_blocking=True)
-        lab = (torch.from_numpy(np.ascontiguousarray(labels_host)).to(dev, non_blocking=True)
-               if labels_host is not None else None)
-        ev_x = torch.cuda.Event()
-        ev_x.record(copy)
-    prepped = mu_d = None
+    Xf = X_host if X_full_host is None else X_full_host
+    N = len(Xf)
     Qh = np.ascontiguousarray(Q_host, np.float64)
-    if (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and L.dmlp_screen_x1_qw(KT) > 0
-            and len(X_host) > 0 and int(k_host.min()) >= 1 and int(k_host.max()) <= SCREEN_KMAX_A):
-        src = np.ascontiguousarray((X_host if mu_rows is None else mu_rows)[:4096], np.float64)
+    host_ops = (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
+                and L.dmlp_screen_x1_qw(KT) > 0 and int(k_host.min()) >= 1
+                and int(k_host.max()) <= min(SCREEN_KMAX_A, N))
+    dsops = prepped = mu_d = None
+    if host_ops:
+        src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
         mu_h = np.empty(A, np.float64)
         L.dmlp_cpu_center(src.ctypes.data, len(src), A, mu_h.ctypes.data)
-        qhi_h = _ARENA.alloc(Q * KT * 64)
-        qn_h = _ARENA.alloc(Q * 4)
-        if L.dmlp_cpu_prep_queries(Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT, qhi_h.data_ptr(),
-                                   qn_h.data_ptr()) == 0:
-            with torch.cuda.stream(copy):
-                qhi = qhi_h.to(dev, non_blocking=True).view(torch.int16)
-                qn = qn_h.to(dev, non_blocking=True).view(torch.float32)
-            prepped = (qhi, qn)
+        n_tiles = (N + 63) // 64
+        Xc = np.ascontiguousarray(Xf, np.float64)
+        xhi_h = _ARENA.alloc(n_tiles * 64 * KT * 64)
+        xin_h = _ARENA.alloc(n_tiles * 64 * 4)
+        xnm_h = _ARENA.alloc(4)
+        if L.dmlp_cpu_prep_data(Xc.ctypes.data, N, A, mu_h.ctypes.data, KT, xhi_h.data_ptr(),
+                                xin_h.data_ptr(), xnm_h.data_ptr()) == 0:
             mu_d = _h2d(mu_h, dev)
-    ev = []
+            with torch.cuda.stream(copy):
+                dsops = (xhi_h.to(dev, non_blocking=True).view(torch.int16),
+                         xin_h.to(dev, non_blocking=True).view(torch.float32),
+                         xnm_h.to(dev, non_blocking=True).view(torch.int32))
+            qhi_h = _ARENA.alloc(Q * KT * 64)
+            qn_h = _ARENA.alloc(Q * 4)
+            if L.dmlp_cpu_prep_queries(Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT,
+                                       qhi_h.data_ptr(), qn_h.data_ptr()) == 0:
+                with torch.cuda.stream(copy):
+                    prepped = (qhi_h.to(dev, non_blocking=True).view(torch.int16),
+                               qn_h.to(dev, non_blocking=True).view(torch.float32))
+        if dsops is None or prepped is None:
+            dsops = prepped = mu_d = None  # outside the screen's range: the device path decides
     with torch.cuda.stream(copy):
         ev_p = torch.cuda.Event()
         ev_p.record(copy)
+        X = torch.from_numpy(np.ascontiguousarray(X_host)).to(dev, non_blocking=True)
+        lab = (torch.from_numpy(np.ascontiguousarray(labels_host, np.int32)).to(
+            dev, non_blocking=True) if labels_host is not None else None)
+        if dsops is not None and gather is not None:
+            X, lab = gather(X, lab)  # RCCL all-gather behind the screen
+        ev_x = torch.cuda.Event()
+        ev_x.record(copy)
+    ev = []
+    with torch.cuda.stream(copy):
         Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
         for c in range(chunks):
             a, b = bounds[c], bounds[c + 1]
@@ -586,13 +627,23 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             e = torch.cuda.Event()
             e.record(copy)
             ev.append(e)
-    for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()):
+    for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()) + (dsops or ()):
         t.record_stream(main)
-    main.wait_event(ev_x)
-    if gather is not None:
-        X, lab = gather(X, lab)
-    ds = prepare_dataset(X, lab if finalize else None, label_range, mu=mu_d)
     ks = max(1, int(k_host.max()) if Q else 1) if kstride is None else kstride
+    if dsops is not None:
+        # the screen operands are on their way; X / labels / Qd complete with ev[-1]
+        if lab is not None and finalize:
+            lo, hi = label_range
+            lab_ds = lab
+        else:
+            lo, hi, lab_ds = 0, 1, None
+        ds = DeviceDataset(X, lab_ds, lo, hi, KT, mu_d, dsops[0], dsops[1], dsops[2],
+                           torch.zeros(1, dtype=torch.int32, device=dev), True, hl=1)
+    else:
+        main.wait_event(ev_x)
+        if gather is not None:
+            X, lab = gather(X, lab)
+        ds = prepare_dataset(X, lab if finalize else None, label_range, mu=mu_d)
     fin = finalize and ds.labels is not None
     od = torch.empty((Q, ks), dtype=torch.float64, device=dev)
     oi = torch.empty((Q, ks), dtype=torch.int32, device=dev)
@@ -605,7 +656,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         if prepped is not None:
             main.wait_event(ev_p)  # screen operands landed; the fp64 rows may still be in flight
             call = _KnnCall(ds, Qd, k_host, finalize, exact, ks, out=out, prepped=prepped,
-                            qx_event=ev[0])
+                            qx_event=ev[-1])
         else:
             main.wait_event(ev[c])
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)
@@ -616,7 +667,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     if _PIPE_DEBUG:
         import sys
         print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms, finish "
-              f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host prep "
+              f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host ops "
               f"{prepped is not None}", file=sys.stderr)
     return ds, od, oi, ol, oc, n_fb
 

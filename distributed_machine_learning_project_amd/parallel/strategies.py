@@ -191,7 +191,7 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             with tr.phase("h2d+allgather+compute"):
                 d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
                                            inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
-                                           mu_rows=inp.X[:4096])
+                                           mu_rows=inp.X[:4096], X_full_host=inp.X)
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
         with tr.phase("h2d"):
             Xs = be.tensor(inp.X[r0:r1])

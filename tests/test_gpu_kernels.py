@@ -199,6 +199,62 @@ def test_pipelined_chunks_match(torch_cuda, chunks, kmin):
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
 
 
+@pytest.mark.parametrize("case", ["escalate", "slices", "ragged"])
+def test_pipelined_host_image_paths(torch_cuda, case, monkeypatch):
+    """The host's hi-only dataset image (hl = 1) through the x1 screen and group refine:
+    tight 1-D data escalates to the 3-term screen (device hi/lo image rendered on demand from
+    the fp64 rows), few queries split the data into many slices, and A = 40 / N % 64 != 0
+    exercises KT = 2 and a ragged last tile."""
+    torch = torch_cuda
+    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    if case == "escalate":
+        monkeypatch.setattr(K, "NUM_CUS", 1)
+        inp = dmlp.generate(20000, 100, 1, 0.0, 1000.0, 8, 16, 4, seed=2)
+    elif case == "slices":
+        inp = dmlp.generate(60000, 64, 32, 0.0, 1000.0, 1, 32, 10, seed=4)
+    else:
+        inp = dmlp.generate(9001, 700, 40, -100.0, 100.0, 1, 30, 7, seed=6)
+    Xp = torch.from_numpy(inp.X).pin_memory().numpy()
+    Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, int(inp.labels.max()) + 1),
+                                                 Qp, inp.k)
+    torch.cuda.synchronize()
+    if case != "escalate":
+        assert ds.hl == 1
+    d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
+def test_host_data_image_matches_device(torch_cuda):
+    """dmlp_cpu_prep_data's hi-only image == the hi halves of prep.hip's hi/lo image; xinit and
+    the max norm agree to fp32 rounding of differently ordered fp64 sums."""
+    torch = torch_cuda
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    inp = dmlp.generate(5000, 10, 40, -50.0, 1000.0, 1, 8, 10, seed=5)
+    N, A, KT = 5000, 40, 2
+    n_tiles = (N + 63) // 64
+    mu = np.empty(A)
+    L.dmlp_cpu_center(inp.X.ctypes.data, N, A, mu.ctypes.data)
+    img = np.zeros(n_tiles * 64 * KT * 32, np.uint16)
+    xin_h = np.zeros(n_tiles * 64, np.float32)
+    nm_h = np.zeros(1, np.uint32)
+    assert L.dmlp_cpu_prep_data(inp.X.ctypes.data, N, A, mu.ctypes.data, KT, img.ctypes.data,
+                                xin_h.ctypes.data, nm_h.ctypes.data) == 0
+    ds = K.prepare_dataset(torch.from_numpy(inp.X).cuda(), mu=torch.from_numpy(mu).cuda())
+    torch.cuda.synchronize()
+    dev = ds.xfrag.cpu().numpy().view(np.uint16).reshape(n_tiles, 4, KT, 2, 64 * 8)
+    np.testing.assert_array_equal(dev[:, :, :, 0].reshape(-1), img)
+    np.testing.assert_allclose(ds.xinit.cpu().numpy()[:N], xin_h[:N], rtol=1e-6)
+    assert np.isneginf(ds.xinit.cpu().numpy()[N:]).all()
+    np.testing.assert_allclose(ds.xnmax_bits.cpu().numpy().view(np.float32),
+                               nm_h.view(np.float32), rtol=1e-6)
+
+
 def test_host_prep_matches_device_prep(torch_cuda):
     """dmlp_cpu_prep_queries renders the same bf16 fragments as the device prep (qn within
     fp64 summation order, rounded to fp32)."""

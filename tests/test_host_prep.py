@@ -46,3 +46,49 @@ def test_cpu_prep_queries_flags_range():
     Qx[1234, 5] = np.nan
     assert L.dmlp_cpu_prep_queries(Qx.ctypes.data, 5000, A, mu.ctypes.data, 1, hh.ctypes.data,
                                    qn.ctypes.data) == 1
+
+
+def _hi_image_ref(X, mu, KT):
+    """prep.hip's tile image with the lo halves dropped: uint16 [n_tiles][4][KT][64 lanes][8],
+    lane = r + 16 * kg holds attributes kt*32 + kg*8 .. +7 of point t*64 + rt*16 + r."""
+    N, A = X.shape
+    n_tiles = (N + 63) // 64
+    c = np.zeros((n_tiles * 64, KT * 32))
+    c[:N, :A] = X - mu
+    h = _bf16_ref(c)  # zero rows / columns render as 0
+    img = h.reshape(n_tiles, 4, 16, KT, 4, 8)          # t, rt, r, kt, kg, j
+    return img.transpose(0, 1, 3, 4, 2, 5).reshape(-1)  # t, rt, kt, kg, r, j
+
+
+@pytest.mark.parametrize("N,A", [(6000, 32), (1000, 40), (130, 7), (4097, 64)])
+def test_cpu_prep_data_image(N, A):
+    L = _lib.lib()
+    rng = np.random.default_rng(N + A)
+    X = rng.uniform(-1000, 1000, (N, A))
+    KT = (A + 31) // 32
+    mu = np.empty(A)
+    L.dmlp_cpu_center(X.ctypes.data, N, A, mu.ctypes.data)
+    n_tiles = (N + 63) // 64
+    img = np.full(n_tiles * 64 * KT * 32, 7, np.uint16)
+    xinit = np.zeros(n_tiles * 64, np.float32)
+    nmax = np.zeros(1, np.uint32)
+    assert L.dmlp_cpu_prep_data(X.ctypes.data, N, A, mu.ctypes.data, KT, img.ctypes.data,
+                                xinit.ctypes.data, nmax.ctypes.data) == 0
+    np.testing.assert_array_equal(img, _hi_image_ref(X, mu, KT))
+    ss = ((X - mu) ** 2).sum(1)
+    np.testing.assert_allclose(xinit[:N], -0.5 * ss, rtol=1e-6)
+    assert np.isneginf(xinit[N:]).all()
+    m = nmax.view(np.float32)[0]
+    assert ss.max() * (1 + 5e-7) <= m <= ss.max() * (1 + 3e-6)
+
+
+def test_cpu_prep_data_flags_range():
+    L = _lib.lib()
+    X = np.ones((3000, 32))
+    X[2999, 31] = np.inf
+    mu = np.zeros(32)
+    img = np.zeros(3008 * 32, np.uint16)
+    xinit = np.zeros(3008, np.float32)
+    nmax = np.zeros(1, np.uint32)
+    assert L.dmlp_cpu_prep_data(X.ctypes.data, 3000, 32, mu.ctypes.data, 1, img.ctypes.data,
+                                xinit.ctypes.data, nmax.ctypes.data) == 1

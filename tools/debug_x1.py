@@ -38,7 +38,7 @@ def run(name, inp):
     ci = torch.empty(Q * S * cap, dtype=torch.int32, device="cuda")
     cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
     ch = torch.empty(Q * S * 2, dtype=torch.float32, device="cuda")
-    _lib.check(L.dmlp_screen_x1(KT, A, ds.xfrag.data_ptr(), ds.xinit.data_ptr(), ds.n_tiles, ds.N,
+    _lib.check(L.dmlp_screen_x1(KT, 2, A, ds.xfrag.data_ptr(), ds.xinit.data_ptr(), ds.n_tiles, ds.N,
                                 qhi.data_ptr(), qn.data_ptr(), qidx.data_ptr(), kd.data_ptr(), Q,
                                 kmax, ds.xnmax_bits.data_ptr(), ds.bad.data_ptr(), S,
                                 ci.data_ptr(), cc.data_ptr(), ch.data_ptr(), s), "x1")
@@ -98,7 +98,7 @@ def refine_check():
         ci = torch.zeros(Q * S * cap, dtype=torch.int32, device="cuda")
         cc = torch.empty(Q * S, dtype=torch.int32, device="cuda")
         ch = torch.empty(Q * S * 2, dtype=torch.float32, device="cuda")
-        _lib.check(L.dmlp_screen_x1(KT, A, P(ds.xfrag), P(ds.xinit), ds.n_tiles, ds.N, P(qhi), P(qn),
+        _lib.check(L.dmlp_screen_x1(KT, 2, A, P(ds.xfrag), P(ds.xinit), ds.n_tiles, ds.N, P(qhi), P(qn),
                                     P(qidx), P(kd), Q, 16, P(ds.xnmax_bits), P(ds.bad), S, P(ci),
                                     P(cc), P(ch), s), "x1")
         od = torch.full((Q, 16), float("inf"), dtype=torch.float64, device="cuda")
@@ -107,7 +107,7 @@ def refine_check():
         cs = torch.empty(Q, dtype=torch.int64, device="cuda")
         st = torch.zeros(Q, dtype=torch.int32, device="cuda")
         _lib.check(L.dmlp_refine_groups(cap, P(ci), P(cc), P(ch), S, P(ds.X), A, P(Qx), P(ds.xfrag),
-                                        P(ds.xinit), P(qhi), KT, ds.N, P(qidx), P(kd), Q, P(od),
+                                        P(ds.xinit), P(qhi), KT, 2, ds.N, P(qidx), P(kd), Q, P(od),
                                         P(oi), 16, P(lab), 0, 10, P(lb), P(cs), P(st), s), "rg")
         torch.cuda.synchronize()
         c = cc.cpu().numpy().reshape(Q, S)
