@@ -26,6 +26,10 @@ _SIGS = {
     "dmlp_cpu_center": (None, [vp, i64, i32, vp]),
     "dmlp_cpu_prep_queries": (i32, [vp, i64, i32, vp, i32, vp, vp]),
     "dmlp_cpu_prep_data": (i32, [vp, i64, i32, vp, i32, vp, vp, vp]),
+    "dmlp_d2h_async": (i32, [vp, vp, i64, vp]),
+    "dmlp_cpu_prep_data_tiles": (i32, [vp, i64, i32, vp, i32, i64, i64, vp, vp, vp]),
+    "dmlp_host_ops_h2d": (i32, [vp, i64, vp, i64, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                vp, i32, vp]),
     "dmlp_screen_kmax": (i32, [i32]),
     "dmlp_screen_lds_bytes": (i32, [i32, i32]),
     "dmlp_screen_waves": (i32, [i32, i32]),

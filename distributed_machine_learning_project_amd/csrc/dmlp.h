@@ -44,6 +44,18 @@ int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, 
 // dmlp_refine_groups), xinit and the max norm bits.  Returns 1 if outside the screen's range.
 int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
                        uint16_t* xhi, float* xinit, unsigned* xnmax_bits);
+// Async device->host copy on `stream` (dst: page-locked or host-registered memory).
+int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream);
+int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu, int KT,
+                             int64_t t0, int64_t t1, uint16_t* xhi, float* xinit, float* nmax);
+// Both operand sets rendered in `chunks` slices each (data first), every slice copied to the
+// device on `stream` (hipMemcpyAsync from the page-locked *_h buffers) as soon as it is ready,
+// so the host conversion overlaps PCIe.  Returns 0, or | 1 (data) / | 2 (queries) when some
+// value is outside the screen's range (then those device operands are not usable).
+int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, int A,
+                      const double* mu, int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
+                      uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d, void* xnm_d,
+                      void* qhi_d, void* qn_d, int chunks, void* stream);
 
 // ---------------------------------------------------------------- device: screen (K2+K3, fused)
 // bf16x3 MFMA screen + per-query streaming threshold + candidate compaction.  Queries are the

@@ -30,7 +30,9 @@ namespace {
 constexpr double kMaxAbs = 1.0e15;
 
 // Persistent workers: a per-call std::thread spawn (tens of microseconds each) would cost more
-// than the conversion itself.
+// than the conversion itself.  After a job a worker spins ~100 us on the generation counter
+// before it sleeps on the condition variable, so back-to-back jobs (the chunked host-ops
+// pipeline dispatches one per PCIe slice) start in about a microsecond instead of a futex wake.
 class Pool {
  public:
   explicit Pool(int n) {
@@ -40,7 +42,7 @@ class Pool {
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
-      ++gen_;
+      gen_.fetch_add(1);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
@@ -49,38 +51,45 @@ class Pool {
   // f(part, parts) on every worker and the caller; returns when all parts are done
   void run(const std::function<void(int, int)>& f) {
     const int parts = size();
-    {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &f;
-      pending_.store(parts - 1);
-      ++gen_;
+    job_ = &f;
+    pending_.store(parts - 1, std::memory_order_relaxed);
+    gen_.fetch_add(1);  // seq_cst: a worker either sees it or is counted in sleepers_
+    if (sleepers_.load() > 0) {
+      { std::lock_guard<std::mutex> g(m_); }
+      cv_.notify_all();
     }
-    cv_.notify_all();
     f(parts - 1, parts);
-    while (pending_.load(std::memory_order_acquire) != 0) std::this_thread::yield();
+    while (pending_.load(std::memory_order_acquire) != 0) _mm_pause();
   }
 
  private:
   void loop(int t) {
-    uint64_t seen = 0;
+    uint64_t seen = 0;  // gen_ starts at 0: a job dispatched before this thread ran is not missed
     for (;;) {
-      const std::function<void(int, int)>* job;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        job = job_;
+      uint64_t g = gen_.load(std::memory_order_acquire);
+      for (int spin = 0; g == seen && spin < 40000; ++spin) {
+        _mm_pause();
+        g = gen_.load(std::memory_order_acquire);
       }
-      (*job)(t, size());
+      if (g == seen) {
+        std::unique_lock<std::mutex> lk(m_);
+        sleepers_.fetch_add(1);
+        cv_.wait(lk, [&] { return gen_.load() != seen; });
+        sleepers_.fetch_sub(1);
+        g = gen_.load();
+      }
+      seen = g;
+      if (stop_) return;
+      (*job_)(t, size());
       pending_.fetch_sub(1, std::memory_order_release);
     }
   }
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> sleepers_{0};
+  std::atomic<bool> stop_{false};
   const std::function<void(int, int)>* job_ = nullptr;
   std::atomic<int> pending_{0};
 };
@@ -114,10 +123,17 @@ extern "C" int dmlp_host_threads(void) { return pool().size(); }
 
 extern "C" void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu) {
   const int64_t n = std::min<int64_t>(N, 4096);
-  for (int a = 0; a < A; ++a) mu[a] = 0.0;
-  for (int64_t i = 0; i < n; ++i)
-    for (int a = 0; a < A; ++a) mu[a] += X[i * A + a];
-  for (int a = 0; a < A; ++a) mu[a] = n ? mu[a] / (double)n : 0.0;
+  // column sums in a local block: accumulating in place would reload / store mu[a] on every
+  // row (the compiler cannot rule out mu aliasing X)
+  for (int a0 = 0; a0 < A; a0 += 64) {
+    const int w = std::min(64, A - a0);
+    double acc[64] = {0.0};
+    for (int64_t i = 0; i < n; ++i) {
+      const double* r = X + i * A + a0;
+      for (int a = 0; a < w; ++a) acc[a] += r[a];
+    }
+    for (int a = 0; a < w; ++a) mu[a0 + a] = n ? acc[a] / (double)n : 0.0;
+  }
 }
 
 namespace {
@@ -246,25 +262,35 @@ int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, c
 
 }  // namespace
 
-// Dataset screen operands on the host: xhi = prep.hip's tile image with the lo halves dropped
-// ([n_tiles][4][KT][64] x 16 B, what the single-term screen and the group refine read),
-// xinit[n_tiles*64] = -|x - mu|^2 / 2 (fp32; -inf for padding rows), *xnmax_bits = the rounded-up
-// max |x - mu|^2 (fp32 bits).  Returns 1 if some |x - mu| is outside the screen's range.
-extern "C" int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
-                                  uint16_t* xhi, float* xinit, unsigned* xnmax_bits) {
-  const int64_t n_pad = ((N + 63) / 64) * 64;
+// Dataset screen operands on the host for tiles [t0, t1) of the image: xhi = prep.hip's tile
+// image with the lo halves dropped ([n_tiles][4][KT][64] x 16 B, what the single-term screen and
+// the group refine read), xinit[n_tiles*64] = -|x - mu|^2 / 2 (fp32; -inf for padding rows),
+// *nmax = the rounded-up max |x - mu|^2 over these tiles (fp32).  The buffers are the whole
+// image's (tile offsets are applied here).  Returns 1 if some |x - mu| is outside the screen's
+// range.
+extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu,
+                                        int KT, int64_t t0, int64_t t1, uint16_t* xhi,
+                                        float* xinit, float* nmax) {
   std::atomic<int> ok{1};
-  std::vector<float> mx(64, 0.0f);
+  float mx[64] = {0.0f};
   std::function<void(int, int)> job = [&](int part, int parts) {
-    // whole tiles per part
-    const int64_t nt = n_pad / 64;
-    const int64_t p0 = nt * part / parts * 64, p1 = nt * (part + 1) / parts * 64;
+    const int64_t nt = t1 - t0;
+    const int64_t p0 = (t0 + nt * part / parts) * 64, p1 = (t0 + nt * (part + 1) / parts) * 64;
     if (!prep_data_range(X, N, p0, p1, A, mu, KT, xhi, xinit, &mx[part])) ok.store(0);
   };
-  if (N * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  if ((t1 - t0) * 64 * (int64_t)A < (int64_t)1 << 14) job(0, 1);
   else pool().run(job);
   float m = 0.0f;
   for (float v : mx) m = std::max(m, v);
-  std::memcpy(xnmax_bits, &m, 4);
+  *nmax = m;
   return ok.load() ? 0 : 1;
+}
+
+// The whole image; *xnmax_bits = the max as fp32 bits.
+extern "C" int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
+                                  uint16_t* xhi, float* xinit, unsigned* xnmax_bits) {
+  float m = 0.0f;
+  const int bad = dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, 0, (N + 63) / 64, xhi, xinit, &m);
+  std::memcpy(xnmax_bits, &m, 4);
+  return bad;
 }

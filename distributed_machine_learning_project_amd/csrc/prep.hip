@@ -13,6 +13,10 @@
 #include "dmlp.h"
 #include "dmlp_device.h"
 #include <float.h>
+#include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <chrono>
 
 namespace {
 
@@ -326,4 +330,64 @@ extern "C" int dmlp_host_register(void* p, int64_t bytes) {
 extern "C" int dmlp_host_unregister(void* p) {
   if (!p) return 0;
   return (int)hipHostUnregister(p);
+}
+
+extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, int A,
+                                 const double* mu, int KT, uint16_t* xhi_h, float* xin_h,
+                                 unsigned* xnm_h, uint16_t* qhi_h, float* qn_h, void* xhi_d,
+                                 void* xin_d, void* xnm_d, void* qhi_d, void* qn_d, int chunks,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n_tiles = (N + 63) / 64;
+  const int64_t W = (int64_t)KT * 32;  // bf16 per row / point
+  static const bool dbg = getenv("DMLP_HOST_OPS_DEBUG") != nullptr;
+  double tl[32];
+  int nt = 0;
+  auto now = [] {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  const double t_start = dbg ? now() : 0.0;
+  auto mark = [&] { if (dbg && nt < 32) tl[nt++] = now() - t_start; };
+  chunks = chunks < 1 ? 1 : chunks;
+  int rc = 0;
+  float m = 0.0f;
+  auto h2d = [&](void* d, const void* h, int64_t bytes) {
+    if (bytes > 0 && hipMemcpyAsync(d, h, (size_t)bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+      rc |= 4;
+  };
+  for (int c = 0; c < chunks; ++c) {
+    const int64_t t0 = n_tiles * c / chunks, t1 = n_tiles * (c + 1) / chunks;
+    if (t1 <= t0) continue;
+    float mc = 0.0f;
+    if (dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, t0, t1, xhi_h, xin_h, &mc)) rc |= 1;
+    m = mc > m ? mc : m;
+    mark();
+    h2d((char*)xhi_d + t0 * 64 * W * 2, xhi_h + t0 * 64 * W, (t1 - t0) * 64 * W * 2);
+    h2d((float*)xin_d + t0 * 64, xin_h + t0 * 64, (t1 - t0) * 64 * 4);
+  }
+  memcpy(xnm_h, &m, 4);
+  h2d(xnm_d, xnm_h, 4);
+  for (int c = 0; c < chunks; ++c) {
+    const int64_t q0 = Q * c / chunks, q1 = Q * (c + 1) / chunks;
+    if (q1 <= q0) continue;
+    if (dmlp_cpu_prep_queries(Qx + q0 * A, q1 - q0, A, mu, KT, qhi_h + q0 * W, qn_h + q0)) rc |= 2;
+    mark();
+    h2d((char*)qhi_d + q0 * W * 2, qhi_h + q0 * W, (q1 - q0) * W * 2);
+    h2d((float*)qn_d + q0, qn_h + q0, (q1 - q0) * 4);
+  }
+  mark();
+  if (dbg) {
+    fprintf(stderr, "[dmlp-hostops] threads %d us:", dmlp_host_threads());
+    for (int i = 0; i < nt; ++i) fprintf(stderr, " %.1f", tl[i]);
+    fprintf(stderr, "\n");
+  }
+  return rc;
+}
+
+extern "C" int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (bytes <= 0) return 0;
+  const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost,
+                                      (hipStream_t)stream);
+  return e == hipSuccess ? 0 : -(int)e;
 }

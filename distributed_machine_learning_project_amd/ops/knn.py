@@ -33,6 +33,9 @@ SCREEN_MAX_KT = 4       # A <= 128 on the screen path
 NUM_CUS = 256
 # "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
 SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
+# slices of the host-rendered screen operands, each copied as soon as it is converted (1: measured
+# best on the bench shape — every extra slice costs ~20 us of copy-API time on the host)
+HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "1"))
 
 
 def eps_rel(A: int) -> float:
@@ -436,6 +439,7 @@ class _KnnCall:
                     t.record_stream(cur)
         self._wait_qx()
         n_ovf = n_esc = 0
+        self.cs_modified = False  # set when work after launch() rewrites labels / checksums
         if self.screened:
             n_ovf = int(self.status.sum().item())
             if n_ovf and self.first_a == "x1":
@@ -443,6 +447,7 @@ class _KnnCall:
                 esc = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
                 n_esc = len(esc)
                 if n_esc:
+                    self.cs_modified = True
                     self._screen_pass(esc, "stream" if self.stream_ok else "lds")
                     n_ovf = int(self.status.sum().item())
         fb = (np.empty(0, np.int64) if self.all_a
@@ -450,12 +455,14 @@ class _KnnCall:
         if n_ovf:
             fb = np.union1d(fb, np.nonzero(self.status.cpu().numpy())[0])
         if len(fb):
+            self.cs_modified = True
             _fallback_exact(ds, self.Qx, fb, kk, self.out_d, self.out_i)
         if self.want_fin and (len(fb) or self.kmin < 1 or self.kmax > N):
             # queries not (correctly) finalized by refine: fallback ones, k == 0, and k > N
             # (the checksum then also covers the (+inf, -1) padding, as the CPU path does)
             rest = np.union1d(fb, np.nonzero((kk < 1) | (self.k_host > N))[0]).astype(np.int32)
             if len(rest):
+                self.cs_modified = True
                 ridx = _h2d(rest, dev)
                 _lib.check(L.dmlp_finalize(_p(self.out_d), _p(self.out_i), self.ks,
                                            _p(self.k_dev), _p(ridx), len(rest), _p(ds.labels),
@@ -546,7 +553,7 @@ def _side_stream(name):
 
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
                       chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
-                      mu_rows=None, X_full_host=None):
+                      mu_rows=None, X_full_host=None, report=None):
     """Host arrays in (page-locked for real overlap), device results out, with the fp64 rows
     copied behind the screen ("H2D overlapped with compute").
 
@@ -561,6 +568,11 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     RCCL all-gather ingress); it is issued on the copy stream, so it too runs behind the screen.
     X_full_host: the whole dataset when X_host is a shard (the host renders the full screen
     image from it); mu_rows: the dataset's first rows (the centre is their mean).
+    report: {"qid_base": b[, "dst": page-locked uint8 numpy view of >= 48 Q + 64 bytes]} renders
+    the report lines right behind the re-rank, before the one host sync (and, with "dst", copies
+    the 48-byte-per-line bound of it there too); on return report["valid"] says whether nothing
+    rewrote the checksums afterwards (escalation / fallback), report["text"] = (device bytes,
+    pinned int64 byte count) and report["copied"] whether dst already holds them.
     Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
     torch = _torch()
     L = _lib.lib()
@@ -587,27 +599,29 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
         mu_h = np.empty(A, np.float64)
         L.dmlp_cpu_center(src.ctypes.data, len(src), A, mu_h.ctypes.data)
+        mu_d = _h2d(mu_h, dev)
         n_tiles = (N + 63) // 64
         Xc = np.ascontiguousarray(Xf, np.float64)
-        xhi_h = _ARENA.alloc(n_tiles * 64 * KT * 64)
-        xin_h = _ARENA.alloc(n_tiles * 64 * 4)
-        xnm_h = _ARENA.alloc(4)
-        if L.dmlp_cpu_prep_data(Xc.ctypes.data, N, A, mu_h.ctypes.data, KT, xhi_h.data_ptr(),
-                                xin_h.data_ptr(), xnm_h.data_ptr()) == 0:
-            mu_d = _h2d(mu_h, dev)
-            with torch.cuda.stream(copy):
-                dsops = (xhi_h.to(dev, non_blocking=True).view(torch.int16),
-                         xin_h.to(dev, non_blocking=True).view(torch.float32),
-                         xnm_h.to(dev, non_blocking=True).view(torch.int32))
-            qhi_h = _ARENA.alloc(Q * KT * 64)
-            qn_h = _ARENA.alloc(Q * 4)
-            if L.dmlp_cpu_prep_queries(Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT,
-                                       qhi_h.data_ptr(), qn_h.data_ptr()) == 0:
-                with torch.cuda.stream(copy):
-                    prepped = (qhi_h.to(dev, non_blocking=True).view(torch.int16),
-                               qn_h.to(dev, non_blocking=True).view(torch.float32))
-        if dsops is None or prepped is None:
-            dsops = prepped = mu_d = None  # outside the screen's range: the device path decides
+        hb = [_ARENA.alloc(n) for n in (n_tiles * 64 * KT * 64, n_tiles * 64 * 4, 4, Q * KT * 64,
+                                        Q * 4)]
+        with torch.cuda.stream(copy):
+            xhi = torch.empty(n_tiles * 64 * KT * 32, dtype=torch.int16, device=dev)
+            xin = torch.empty(n_tiles * 64, dtype=torch.float32, device=dev)
+            xnm = torch.empty(1, dtype=torch.int32, device=dev)
+            qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
+            qn = torch.empty(Q, dtype=torch.float32, device=dev)
+        # host conversion of each slice overlaps the PCIe copy of the previous one
+        t_ops = time.perf_counter()
+        rc = L.dmlp_host_ops_h2d(Xc.ctypes.data, N, Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT,
+                                 *[b.data_ptr() for b in hb], _p(xhi), _p(xin), _p(xnm), _p(qhi),
+                                 _p(qn), HOST_OPS_CHUNKS, copy.cuda_stream)
+        t_ops = time.perf_counter() - t_ops
+        if rc & 4:
+            raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
+        if rc == 0:
+            dsops, prepped = (xhi, xin, xnm), (qhi, qn)
+        else:
+            mu_d = None  # outside the screen's range: the device path decides
     with torch.cuda.stream(copy):
         ev_p = torch.cuda.Event()
         ev_p.record(copy)
@@ -661,14 +675,27 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             main.wait_event(ev[c])
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)
         calls.append(call.launch())
+    spec = None
+    if report is not None and fin and Q > 0:
+        spec = format_report_dev_async(oc, report.get("qid_base", 0))
+        dst = report.get("dst")
+        if dst is not None and len(dst) >= L.dmlp_format_bound(Q):
+            _lib.check(L.dmlp_d2h_async(dst.ctypes.data, _p(spec[0]), L.dmlp_format_bound(Q),
+                                        _stream()), "d2h report")
+            report["copied"] = True
+        else:
+            report["copied"] = False
     t_launched = time.perf_counter()
     n_fb = sum(call.finish().n_fallback for call in calls)
+    if report is not None:
+        report["valid"] = spec is not None and not any(c.cs_modified for c in calls)
+        report["text"] = spec
     _ARENA.mark()
     if _PIPE_DEBUG:
         import sys
         print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms, finish "
               f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host ops "
-              f"{prepped is not None}", file=sys.stderr)
+              f"{prepped is not None} ({1e3 * t_ops if host_ops else 0:.3f} ms)", file=sys.stderr)
     return ds, od, oi, ol, oc, n_fb
 
 
@@ -796,6 +823,21 @@ def finalize_gpu(ds_labels, label_range, dist, ids, k_dev):
                                         label_range[0], label_range[1], _p(lab), _p(cs),
                                         _stream()), "finalize")
     return lab, cs
+
+
+def format_report_dev_async(cs, qid_base: int = 0):
+    """format_report_dev without the host sync: (device uint8 text, pinned int64 [1] byte count
+    valid once the current stream has reached this point)."""
+    torch = _torch()
+    L = _lib.lib()
+    cs = cs.contiguous()
+    nq = cs.numel()
+    off = torch.empty(L.dmlp_format_scratch(nq), dtype=torch.int64, device=cs.device)
+    out = torch.empty(L.dmlp_format_bound(nq), dtype=torch.uint8, device=cs.device)
+    _lib.check(L.dmlp_format_report(_p(cs), nq, qid_base, _p(off), _p(out), _stream()), "format")
+    n_h = _ARENA.alloc(8).view(torch.int64)
+    n_h.copy_(off[nq:nq + 1], non_blocking=True)
+    return out, n_h
 
 
 def format_report_dev(cs, qid_base: int = 0):

@@ -177,6 +177,11 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
                                            kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
     pipeline = os.environ.get("KNN_PIPELINE", "1") == "1"
+    # the report lines are rendered right behind the re-rank (and, on one rank, copied straight
+    # into the segment's output region) before the call's one host sync
+    rep = {"qid_base": a}
+    if comm.world == 1 and not debug:
+        rep["dst"] = inp.out
     if mode == "allgather":
         nc, nd = block_partition(N, comm.world)
         r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
@@ -191,8 +196,10 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             with tr.phase("h2d+allgather+compute"):
                 d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
                                            inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
-                                           mu_rows=inp.X[:4096], X_full_host=inp.X)
-            return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
+                                           mu_rows=inp.X[:4096], X_full_host=inp.X,
+                                           report=rep)
+            return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug,
+                                     rep)
         with tr.phase("h2d"):
             Xs = be.tensor(inp.X[r0:r1])
             ls = be.tensor(inp.labels[r0:r1])
@@ -208,8 +215,8 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
         with tr.phase("h2d+compute"):
             kl_h = np.array(inp.k[a:b])
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax)
-        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
+                                       kstride=kmax, report=rep)
+        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, rep)
     with tr.phase("h2d"):
         X = lab = None
         if not bcast_data or comm.is_root:
@@ -226,12 +233,12 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
 
 
-def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug):
+def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, report=None):
     torch = _torch()
     text = None
     if not debug:
         with tr.phase("report"):
-            text = _shared_egress(comm, be, inp, cs, a)
+            text = _shared_egress(comm, be, inp, cs, a, report)
     with tr.phase("gather"):
         packed = torch.stack([lb.to(torch.int64), cs], dim=1)
         allp = comm.gather_rows(packed, counts, (2,), torch.int64)
@@ -244,11 +251,18 @@ def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug):
     return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii, text
 
 
-def _shared_egress(comm, be, inp, cs, qid_base):
+def _shared_egress(comm, be, inp, cs, qid_base, report=None):
     """Every rank renders its block's report lines and copies them straight into the shared
-    segment's output region at its byte offset; rank 0 gets a view of the whole report."""
+    segment's output region at its byte offset; rank 0 gets a view of the whole report.
+    report: knn_gpu_pipelined's speculative rendering (used when still valid)."""
     torch = _torch()
-    if be.on_gpu:
+    if be.on_gpu and report is not None and report.get("valid"):
+        dev_text, n_h = report["text"]
+        n = int(n_h[0])
+        if report.get("copied"):  # one rank: the text already sits at offset 0
+            comm.barrier()
+            return memoryview(inp.out)[:n].toreadonly() if comm.is_root else None
+    elif be.on_gpu:
         from ..ops import knn as K
         dev_text, n = K.format_report_dev(cs, qid_base)
     else:
