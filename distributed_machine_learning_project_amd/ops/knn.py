@@ -258,7 +258,7 @@ class _KnnCall:
     lets knn_gpu_pipelined keep several query chunks in flight on their own streams."""
 
     def __init__(self, ds, Qx, k_host, finalize=True, exact=False, kstride=None, gpu_share=1.0,
-                 out=None, prepped=None, qx_event=None):
+                 out=None, prepped=None, qx_event=None, k_range=None):
         """prepped = (qhi, qn) device tensors rendered by the host (dmlp_cpu_prep_queries) with
         ds.mu; qx_event: the fp64 query rows are only complete once it fires (they are copied
         behind the screen) — everything that reads Qx waits for it."""
@@ -270,8 +270,11 @@ class _KnnCall:
         self.dev = self.Qx.device
         self.k_host = np.ascontiguousarray(k_host, np.int32)
         Q = self.Q
-        self.kmin = int(self.k_host.min()) if Q else 0
-        self.kmax = int(self.k_host.max()) if Q else 0
+        if k_range is not None and Q:  # (lower bound of min k, upper bound of max k)
+            self.kmin, self.kmax = int(k_range[0]), int(k_range[1])
+        else:
+            self.kmin = int(self.k_host.min()) if Q else 0
+            self.kmax = int(self.k_host.max()) if Q else 0
         self.ks = max(1, self.kmax) if kstride is None else kstride
         self.exact = exact
         self.gpu_share = gpu_share
@@ -553,7 +556,7 @@ def _side_stream(name):
 
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
                       chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
-                      mu_rows=None, X_full_host=None, report=None):
+                      mu_rows=None, X_full_host=None, report=None, k_range=None):
     """Host arrays in (page-locked for real overlap), device results out, with the fp64 rows
     copied behind the screen ("H2D overlapped with compute").
 
@@ -573,6 +576,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     the 48-byte-per-line bound of it there too); on return report["valid"] says whether nothing
     rewrote the checksums afterwards (escalation / fallback), report["text"] = (device bytes,
     pinned int64 byte count) and report["copied"] whether dst already holds them.
+    k_range: (a lower bound of the smallest k, an upper bound of the largest k), e.g. from a
+    segment header, instead of scanning k_host (bounds only steer the dispatch).
     Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
     torch = _torch()
     L = _lib.lib()
@@ -591,9 +596,11 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     Xf = X_host if X_full_host is None else X_full_host
     N = len(Xf)
     Qh = np.ascontiguousarray(Q_host, np.float64)
+    if Q and k_range is None:
+        k_range = (int(k_host.min()), int(k_host.max()))
     host_ops = (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
-                and L.dmlp_screen_x1_qw(KT) > 0 and int(k_host.min()) >= 1
-                and int(k_host.max()) <= min(SCREEN_KMAX_A, N))
+                and L.dmlp_screen_x1_qw(KT) > 0 and k_range[0] >= 1
+                and k_range[1] <= min(SCREEN_KMAX_A, N))
     dsops = prepped = mu_d = None
     if host_ops:
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
@@ -643,7 +650,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             ev.append(e)
     for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()) + (dsops or ()):
         t.record_stream(main)
-    ks = max(1, int(k_host.max()) if Q else 1) if kstride is None else kstride
+    ks = max(1, k_range[1] if Q else 1) if kstride is None else kstride
     if dsops is not None:
         # the screen operands are on their way; X / labels / Qd complete with ev[-1]
         if lab is not None and finalize:
@@ -670,7 +677,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         if prepped is not None:
             main.wait_event(ev_p)  # screen operands landed; the fp64 rows may still be in flight
             call = _KnnCall(ds, Qd, k_host, finalize, exact, ks, out=out, prepped=prepped,
-                            qx_event=ev[-1])
+                            qx_event=ev[-1], k_range=k_range)
         else:
             main.wait_event(ev[c])
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)

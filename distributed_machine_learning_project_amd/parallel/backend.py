@@ -52,7 +52,8 @@ class Backend:
         return torch.from_numpy(d), torch.from_numpy(i), lab, cs
 
     def knn_host(self, X_host, labels_host, label_range, Q_host, k_host: np.ndarray,
-                 kstride=None, gather=None, mu_rows=None, X_full_host=None, report=None):
+                 kstride=None, gather=None, mu_rows=None, X_full_host=None, report=None,
+                 k_range=None):
         """knn() from host arrays: on the GPU the query H2D is chunked and overlapped with the
         screen of earlier chunks (ops.knn.knn_gpu_pipelined).  gather(X, lab) -> (X, lab)
         completes a dataset shard on the device (all-gather ingress).  Returns (dist, ids,
@@ -62,7 +63,8 @@ class Backend:
             _, d, i, lab, cs, _ = K.knn_gpu_pipelined(X_host, labels_host, label_range, Q_host,
                                                       k_host, kstride=kstride, exact=self.exact,
                                                       gather=gather, mu_rows=mu_rows,
-                                                      X_full_host=X_full_host, report=report)
+                                                      X_full_host=X_full_host, report=report,
+                                                      k_range=k_range)
             return d, i, lab, cs
         if gather is not None:
             X, lab = gather(torch.from_numpy(np.ascontiguousarray(X_host)),

@@ -58,9 +58,13 @@ def _meta(comm, inp, with_shared=False):
     if comm.is_root:
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
-        lo = int(inp.labels.min()) if N else 0
-        hi = int(inp.labels.max()) + 1 if N else 1
-        kmax = max(1, int(inp.k.max())) if Q else 1
+        if getattr(inp, "shared", False):  # written once with the segment (utils/shm.py)
+            lo, hi, _, kmax = inp.summary
+            kmax = max(1, kmax) if Q else 1
+        else:
+            lo = int(inp.labels.min()) if N else 0
+            hi = int(inp.labels.max()) + 1 if N else 1
+            kmax = max(1, int(inp.k.max())) if Q else 1
         vals = [N, Q, A, lo, hi, kmax, int(bool(getattr(inp, "shared", False)))]
     else:
         vals = None
@@ -185,7 +189,7 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     if mode == "allgather":
         nc, nd = block_partition(N, comm.world)
         r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
-        kl_h = np.array(inp.k[a:b])
+        kl_h = inp.k[a:b]  # read-only view of the segment
 
         def gather(Xs, ls):
             return (comm.allgather_rows(Xs, nc, (A,), torch.float64),
@@ -197,7 +201,7 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
                 d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
                                            inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
                                            mu_rows=inp.X[:4096], X_full_host=inp.X,
-                                           report=rep)
+                                           report=rep, k_range=inp.summary[2:])
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug,
                                      rep)
         with tr.phase("h2d"):
@@ -213,9 +217,9 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     if not bcast_data and pipeline:
         # per-GPU H2D: the query chunks land while the earlier chunks already screen
         with tr.phase("h2d+compute"):
-            kl_h = np.array(inp.k[a:b])
+            kl_h = inp.k[a:b]  # read-only view of the segment
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax, report=rep)
+                                       kstride=kmax, report=rep, k_range=inp.summary[2:])
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, rep)
     with tr.phase("h2d"):
         X = lab = None
@@ -239,6 +243,8 @@ def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, r
     if not debug:
         with tr.phase("report"):
             text = _shared_egress(comm, be, inp, cs, a, report)
+    if comm.world == 1:
+        return lb, cs, d if debug else None, i if debug else None, text
     with tr.phase("gather"):
         packed = torch.stack([lb.to(torch.int64), cs], dim=1)
         allp = comm.gather_rows(packed, counts, (2,), torch.int64)

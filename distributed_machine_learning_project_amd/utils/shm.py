@@ -14,7 +14,8 @@ Egress is symmetric: with the static farm each rank renders the report lines of 
 block on its GPU and copies them over its own PCIe link into the segment's output region at its
 byte offset, so rank 0 ends up holding the whole report in host memory without a funnel.
 
-Layout: 64-byte header (magic, N, Q, A), then labels i32[N], k i32[Q], X f64[N*A],
+Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — the summary every
+KNN call needs, computed once when the segment is written), then labels i32[N], k i32[Q], X f64[N*A],
 Qx f64[Q*A], out u8[48*Q + 64] (report text), each section 4096-byte aligned.
 """
 from __future__ import annotations
@@ -72,8 +73,21 @@ class SharedInput(KNNInput):
         s.k[:] = inp.k
         s.X[:] = inp.X
         s.Qx[:] = inp.Qx
+        s.refresh_summary()
         mm.flush()
         return s
+
+    def refresh_summary(self):
+        """Recompute the header summary (call after writing the arrays in place)."""
+        N, Q = len(self.labels), len(self.k)
+        np.frombuffer(self._mm, np.int64, 4, 32)[:] = [
+            int(self.labels.min()) if N else 0, int(self.labels.max()) + 1 if N else 1,
+            int(self.k.min()) if Q else 0, int(self.k.max()) if Q else 0]
+
+    @property
+    def summary(self):
+        """(label lo, label hi (exclusive), k min, k max) from the header."""
+        return tuple(int(v) for v in np.frombuffer(self._mm, np.int64, 4, 32))
 
     @staticmethod
     def attach(path: str) -> "SharedInput":

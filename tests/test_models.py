@@ -73,3 +73,24 @@ def test_classifier_gpu_matches_oracle():
     for q in range(0, 500, 37):
         np.testing.assert_array_equal(i[q, :k[q]], res[q][1])
         np.testing.assert_array_equal(d[q, :k[q]], res[q][0])
+
+
+def test_shared_segment_summary(tmp_path):
+    """The node-shared segment's header carries (label lo, label hi, k min, k max), written once
+    with the arrays and read by every KNN call instead of scanning them."""
+    import numpy as np
+    from distributed_machine_learning_project_amd.utils.io import generate
+    from distributed_machine_learning_project_amd.utils.shm import SharedInput
+    inp = generate(500, 300, 4, 0.0, 10.0, 2, 9, 5, seed=3)
+    s = SharedInput.create(inp, directory=str(tmp_path))
+    try:
+        assert s.summary == (int(inp.labels.min()), int(inp.labels.max()) + 1,
+                             int(inp.k.min()), int(inp.k.max()))
+        t = SharedInput.attach(s.path)
+        assert t.summary == s.summary
+        s.k[7] = 31
+        s.refresh_summary()
+        assert t.summary[3] == 31
+        np.testing.assert_array_equal(t.X, inp.X)
+    finally:
+        s.close()
