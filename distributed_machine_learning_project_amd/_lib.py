@@ -56,6 +56,15 @@ _SIGS = {
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp,
                                  i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
+    "dmlp_screen_x2_kmax": (i32, []),
+    "dmlp_screen_x2_qw": (i32, [i32]),
+    "dmlp_screen_x2_cap": (i32, [i32]),
+    "dmlp_screen_x2_waves_per_cu": (i32, [i32]),
+    "dmlp_set_x2_mode": (None, [i32]),
+    "dmlp_x2_debug_counters": (i32, [vp, i32]),
+    "dmlp_set_x2_pw": (None, [i32]),
+    "dmlp_screen_x2": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
+                             vp, vp, vp, vp]),
     "dmlp_set_x1_check": (None, [i32]),
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
@@ -78,6 +87,7 @@ _SIGS = {
     "dmlp_cpu_merge": (i32, [vp, vp, i32, i64, i32, vp, i64, vp, vp, i32]),
     "dmlp_kdtree_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp]),
     "dmlp_cpu_format_report": (i64, [vp, i64, i64, vp]),
+    "dmlp_cpu_i32_range": (None, [vp, i64, i32p, i32p]),
     "dmlp_cpu_format_debug": (i64, [vp, vp, i32, vp, vp, i64, vp, i64]),
     "dmlp_parse_header": (i32, [vp, i64, i64p, i64p, i32p, i64p]),
     "dmlp_parse_body": (i64, [vp, i64, i64, i64, i64, i32, vp, vp, vp, vp, i32]),
@@ -111,6 +121,17 @@ def lib():
         fn.argtypes = args
     _lib = h
     return h
+
+
+def i32_range(a) -> tuple[int, int]:
+    """(min, max) of an int32 numpy array (one native pass); (0, -1) when empty."""
+    import numpy as np
+    a = np.ascontiguousarray(a, np.int32)
+    if a.size == 0:
+        return 0, -1
+    lo, hi = C.c_int(), C.c_int()
+    lib().dmlp_cpu_i32_range(a.ctypes.data, a.size, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
 
 
 def check(rc: int, what: str):

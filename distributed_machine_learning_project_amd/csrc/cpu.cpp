@@ -1,3 +1,4 @@
+#include <cstdint>
 // cpu.cpp — host implementations: exact brute-force k-NN, serial KD-tree (bench.debug analog),
 // top-k merge, vote/checksum, report formatting and the multi-threaded input parser.
 //
@@ -363,6 +364,45 @@ extern "C" int64_t dmlp_parse_body(const char* buf, int64_t len, int64_t body_of
   });
   const int64_t b = bad.load();
   return b ? -b : 0;
+}
+
+// [min, max] of an int32 array in one pass (the label range and k bounds every KNN call scans:
+// engine.cpp:27-35 broadcasts the sizes, the vote needs the label range).  n == 0: lo > hi.
+__attribute__((target("avx2"))) static void i32_range_avx2(const int* a, int64_t n, int* lo,
+                                                           int* hi);
+extern "C" void dmlp_cpu_i32_range(const int* a, int64_t n, int* lo, int* hi) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) return i32_range_avx2(a, n, lo, hi);
+  int mn = INT32_MAX, mx = INT32_MIN;
+  int64_t i = 0;
+  int m4[8], x4[8];
+  for (int j = 0; j < 8; ++j) { m4[j] = INT32_MAX; x4[j] = INT32_MIN; }
+  for (; i + 8 <= n; i += 8)  // 8 independent lanes: vectorised by the compiler
+    for (int j = 0; j < 8; ++j) {
+      m4[j] = a[i + j] < m4[j] ? a[i + j] : m4[j];
+      x4[j] = a[i + j] > x4[j] ? a[i + j] : x4[j];
+    }
+  for (int j = 0; j < 8; ++j) { mn = m4[j] < mn ? m4[j] : mn; mx = x4[j] > mx ? x4[j] : mx; }
+  for (; i < n; ++i) { mn = a[i] < mn ? a[i] : mn; mx = a[i] > mx ? a[i] : mx; }
+  *lo = mn;
+  *hi = mx;
+}
+
+__attribute__((target("avx2"))) static void i32_range_avx2(const int* a, int64_t n, int* lo,
+                                                           int* hi) {
+  int mn = INT32_MAX, mx = INT32_MIN;
+  int64_t i = 0;
+  int m4[8], x4[8];
+  for (int j = 0; j < 8; ++j) { m4[j] = INT32_MAX; x4[j] = INT32_MIN; }
+  for (; i + 8 <= n; i += 8)
+    for (int j = 0; j < 8; ++j) {
+      m4[j] = a[i + j] < m4[j] ? a[i + j] : m4[j];
+      x4[j] = a[i + j] > x4[j] ? a[i + j] : x4[j];
+    }
+  for (int j = 0; j < 8; ++j) { mn = m4[j] < mn ? m4[j] : mn; mx = x4[j] > mx ? x4[j] : mx; }
+  for (; i < n; ++i) { mn = a[i] < mn ? a[i] : mn; mx = a[i] > mx ? a[i] : mx; }
+  *lo = mn;
+  *hi = mx;
 }
 
 extern "C" const char* dmlp_version(void) { return "dmlp 0.1.0 (gfx950)"; }

@@ -28,6 +28,7 @@
 namespace {
 
 constexpr double kMaxAbs = 1.0e15;
+constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch of the data prep
 
 // Persistent workers: a per-call std::thread spawn (tens of microseconds each) would cost more
 // than the conversion itself.  After a job a worker spins ~100 us on the generation counter
@@ -36,6 +37,8 @@ constexpr double kMaxAbs = 1.0e15;
 class Pool {
  public:
   explicit Pool(int n) {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus_ = std::max(1, (int)CPU_COUNT(&set));
     for (int t = 0; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
   }
   ~Pool() {
@@ -59,15 +62,22 @@ class Pool {
       cv_.notify_all();
     }
     f(parts - 1, parts);
-    while (pending_.load(std::memory_order_acquire) != 0) _mm_pause();
+    for (int spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
+      if (spin < 4096) _mm_pause();
+      else std::this_thread::yield();  // a preempted worker: give it the CPU
+    }
   }
 
  private:
+  bool oversubscribed() const { return (int)th_.size() + 1 > cpus_; }
   void loop(int t) {
     uint64_t seen = 0;  // gen_ starts at 0: a job dispatched before this thread ran is not missed
     for (;;) {
       uint64_t g = gen_.load(std::memory_order_acquire);
-      for (int spin = 0; g == seen && spin < 40000; ++spin) {
+      // spin only while the pool fits the CPUs it may use: oversubscribed workers would burn
+      // the time slices of the threads they wait for
+      const int spins = oversubscribed() ? 0 : 40000;
+      for (int spin = 0; g == seen && spin < spins; ++spin) {
         _mm_pause();
         g = gen_.load(std::memory_order_acquire);
       }
@@ -92,17 +102,26 @@ class Pool {
   std::atomic<bool> stop_{false};
   const std::function<void(int, int)>* job_ = nullptr;
   std::atomic<int> pending_{0};
+  int cpus_ = 1 << 30;
 };
 
 // CPUs this process may run on (the affinity mask, not the machine: a GPU box grants each job a
-// share of a 256-thread host), at most 16 — the conversions are bound by memory, not cores.
+// share of a 256-thread host), divided among the ranks of the node that share that mask
+// (LOCAL_WORLD_SIZE, set by torchrun / the MPI launchers), at most 16 — the conversions are bound
+// by memory, not cores.  DMLP_HOST_THREADS overrides (clamped to [1, 16]).
 int pool_threads() {
-  if (const char* e = std::getenv("DMLP_HOST_THREADS")) return std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("DMLP_HOST_THREADS"))
+    return std::max(1, std::min(std::atoi(e), kMaxPool));
   cpu_set_t set;
   int n = 0;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
   if (n <= 0) n = (int)std::thread::hardware_concurrency();
-  return std::max(1, std::min(n, 16));
+  int local = 1;
+  for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"})
+    if (const char* e = std::getenv(v)) { local = std::max(1, std::atoi(e)); break; }
+  // ranks pinned to disjoint CPU sets see only their own share; a shared mask is split
+  if (local > 1 && n >= 2 * local) n /= local;
+  return std::max(1, std::min(n, kMaxPool));
 }
 
 Pool& pool() {
@@ -272,7 +291,7 @@ extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const
                                         int KT, int64_t t0, int64_t t1, uint16_t* xhi,
                                         float* xinit, float* nmax) {
   std::atomic<int> ok{1};
-  float mx[64] = {0.0f};
+  float mx[kMaxPool] = {0.0f};  // one slot per pool part (pool().size() <= kMaxPool)
   std::function<void(int, int)> job = [&](int part, int parts) {
     const int64_t nt = t1 - t0;
     const int64_t p0 = (t0 + nt * part / parts) * 64, p1 = (t0 + nt * (part + 1) / parts) * 64;

@@ -58,13 +58,11 @@ def _meta(comm, inp, with_shared=False):
     if comm.is_root:
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
-        if getattr(inp, "shared", False):  # written once with the segment (utils/shm.py)
-            lo, hi, _, kmax = inp.summary
-            kmax = max(1, kmax) if Q else 1
-        else:
-            lo = int(inp.labels.min()) if N else 0
-            hi = int(inp.labels.max()) + 1 if N else 1
-            kmax = max(1, int(inp.k.max())) if Q else 1
+        # scanned inside every call, like the reference engines' own passes over the input
+        from .. import _lib
+        lmin, lmax = _lib.i32_range(inp.labels)
+        lo, hi = (lmin, lmax + 1) if N else (0, 1)
+        kmax = max(1, _lib.i32_range(inp.k)[1]) if Q else 1
         vals = [N, Q, A, lo, hi, kmax, int(bool(getattr(inp, "shared", False)))]
     else:
         vals = None
@@ -72,6 +70,12 @@ def _meta(comm, inp, with_shared=False):
     if out[6] and not getattr(inp, "shared", False):
         raise RuntimeError("rank 0 passed a node-shared input but this rank has none mapped")
     return out if with_shared else out[:6]
+
+
+def _lib_range(k):
+    from .. import _lib
+    lo, hi = _lib.i32_range(k)
+    return (lo, hi) if len(k) else (0, 0)
 
 
 def _k_host(comm, k_dev_or_none, Q):
@@ -189,7 +193,8 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     if mode == "allgather":
         nc, nd = block_partition(N, comm.world)
         r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
-        kl_h = inp.k[a:b]  # read-only view of the segment
+        kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
+        k_range = _lib_range(kl_h)  # this rank's own k bounds steer its dispatch
 
         def gather(Xs, ls):
             return (comm.allgather_rows(Xs, nc, (A,), torch.float64),
@@ -201,7 +206,7 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
                 d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
                                            inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
                                            mu_rows=inp.X[:4096], X_full_host=inp.X,
-                                           report=rep, k_range=inp.summary[2:])
+                                           report=rep, k_range=k_range)
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug,
                                      rep)
         with tr.phase("h2d"):
@@ -217,9 +222,9 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     if not bcast_data and pipeline:
         # per-GPU H2D: the query chunks land while the earlier chunks already screen
         with tr.phase("h2d+compute"):
-            kl_h = inp.k[a:b]  # read-only view of the segment
+            kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax, report=rep, k_range=inp.summary[2:])
+                                       kstride=kmax, report=rep, k_range=_lib_range(kl_h))
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, rep)
     with tr.phase("h2d"):
         X = lab = None

@@ -14,9 +14,9 @@ Egress is symmetric: with the static farm each rank renders the report lines of 
 block on its GPU and copies them over its own PCIe link into the segment's output region at its
 byte offset, so rank 0 ends up holding the whole report in host memory without a funnel.
 
-Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — the summary every
-KNN call needs, computed once when the segment is written), then labels i32[N], k i32[Q], X f64[N*A],
-Qx f64[Q*A], out u8[48*Q + 64] (report text), each section 4096-byte aligned.
+Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — a summary for tools;
+the KNN strategies re-scan the labels and k inside every timed call), then labels i32[N],
+k i32[Q], X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), each section 4096-byte aligned.
 """
 from __future__ import annotations
 

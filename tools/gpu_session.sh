@@ -1,0 +1,74 @@
+#!/bin/bash
+# Maintained GPU entry point (one gpurun call = one session).  Every GPU step runs under its own
+# time limit and the session stops at the first failing step.
+#
+#   gpurun --timeout 900 -- bash tools/gpu_session.sh <tag> <task> [<task> ...]
+#
+# tasks:
+#   tests      pytest -m gpu (the round-end GPU tier)
+#   bench      python bench.py (defaults: 1 GPU, headline config)
+#   verify     python bench.py --verify (every report line vs the exact CPU path)
+#   prof       rocprofv3 --kernel-trace --stats over a short bench run (kernel split)
+#   timeline   rocprofv3 kernel + memory-copy trace of the last steps (tools/timeline.py)
+#   pmc        one --pmc pass per counter group over the screen + refine (tools/pmc_summary.py)
+#   engine     native knn_engine: every strategy vs the CPU oracle bytes (tools/engine_check.sh)
+#   sweep      bench sweep over N / A / k (profiles/ sweep table)
+#   exact      bench.py --exact (fp64-only path)
+#   harness    bench.py --harness native (knn_engine through the reference contract)
+set -u
+TAG=${1:?tag}
+shift
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name seconds cmd...  (stdout+stderr to $OUT/name.log)
+  local name=$1 secs=$2
+  shift 2
+  echo "[session] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ne 0 ]; then echo "[session] $name failed rc=$rc"; exit $rc; fi
+}
+for task in "$@"; do
+  case "$task" in
+    tests)
+      step tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+          --timeout-method thread ;;
+    bench)
+      step bench 300 python bench.py ;;
+    verify)
+      step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
+    exact)
+      step exact 300 python bench.py --exact --steps 5 --warmup 1 ;;
+    prof)
+      step prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+          -- python3 bench.py --steps 10 --warmup 2 --no-busbw
+      find "$OUT/prof" -name '*kernel_stats.csv' -exec sh -c 'head -12 "$1" | cut -c1-200' _ {} \; ;;
+    timeline)
+      step timeline 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/tl" -o run \
+          --output-format csv -- python3 bench.py --steps 4 --warmup 2 --no-busbw
+      python3 tools/timeline.py "$OUT/tl" 7 > "$OUT/timeline.txt"; tail -40 "$OUT/timeline.txt" ;;
+    pmc)
+      n=0
+      for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+               "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM" \
+               "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum" \
+               "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        n=$((n + 1))
+        # counters only: no trace domains beside --pmc
+        step pmc$n 120 rocprofv3 --kernel-trace --pmc $C -d "$OUT/pmc$n" -o run --output-format csv \
+            -- python3 tools/quick_gpu_bench.py --q 131072 --iters 2 --check 0
+      done
+      python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
+    engine)
+      step engine 400 bash tools/engine_check.sh "$OUT/engine" ;;
+    sweep)
+      step sweep 900 python3 tools/bench_sweep.py --out "$OUT/sweep.jsonl" ;;
+    harness)
+      step harness 600 python bench.py --harness native ;;
+    *)
+      echo "unknown task $task"; exit 2 ;;
+  esac
+done
