@@ -47,6 +47,7 @@ _SIGS = {
     "dmlp_screen_debug_counters": (i32, [vp, i32]),
     "dmlp_screen_x1_kmax": (i32, []),
     "dmlp_screen_x1_qw": (i32, [i32]),
+    "dmlp_screen_x1_cols": (i32, [i32, i32]),
     "dmlp_screen_x1_cap": (i32, [i32]),
     "dmlp_screen_x1_waves_per_cu": (i32, [i32]),
     "dmlp_screen_x1_min_slices": (i64, [i64]),
@@ -65,7 +66,7 @@ _SIGS = {
     "dmlp_set_x2_pw": (None, [i32]),
     "dmlp_screen_x2": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
-    "dmlp_set_x1_check": (None, [i32]),
+    "dmlp_set_x1_ct": (None, [i32]),
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
                           vp, vp]),

@@ -91,6 +91,7 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
 // overflow) and cand_h[2] = {slice threshold, query eps} — consumed by dmlp_refine_groups.
 int dmlp_screen_x1_kmax(void);
 int dmlp_screen_x1_qw(int KT);
+int dmlp_screen_x1_cols(int KT, int kmax);
 int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
@@ -120,7 +121,7 @@ int dmlp_screen_x2(int KT, int hl, int A, const void* xfrag, const float* xinit,
                    const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
                    void* stream);
 
-void dmlp_set_x1_check(int steps);
+void dmlp_set_x1_ct(int ct);
 int dmlp_x1_debug_counters(unsigned long long* out, int reset);
 // Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off,
 // sub-buffer depth (8 / 16, 0 = automatic).

@@ -350,7 +350,7 @@ struct LocalKnn {
         for (int q : idx) kcls = std::max(kcls, kk[q]);
         const int cap = impl == 0 ? dmlp_screen_x1_cap(kcls)
                         : impl == 1 ? dmlp_screen_stream_cap(kcls) : (kcls <= 32 ? 128 : 256);
-        const int S = impl == 0 ? slices_stream(nq, dmlp_screen_x1_qw(KT), nt,
+        const int S = impl == 0 ? slices_stream(nq, dmlp_screen_x1_cols(KT, kcls), nt,
                                                 dmlp_screen_x1_waves_per_cu(kcls),
                                                 dmlp_screen_x1_min_slices(nt))
                       : impl == 1 ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))

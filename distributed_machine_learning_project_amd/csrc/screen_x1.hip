@@ -29,12 +29,13 @@
 
 namespace {
 
-int g_x1_mode = 0;  // profiling: 1 no candidate path, 8 event counters (g_x1_dbg)
+// profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 8 event counters (g_x1_dbg)
+int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
 
-template <int KT, int SUB, int DEPTH, int CHECK>
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV>
 struct X1Cfg {
-  static constexpr int CT = 4;                  // MFMA column tiles per wave
+  static constexpr int CT = CTV;                // MFMA column tiles per wave (4 or 8)
   static constexpr int NCOL = 16 * CT;          // queries per wave (= workgroup)
   // column pitch in entries: 4 interleaved sub-buffers + 4 pad slots; 68 = 4 (mod 64) puts the
   // 64 lanes of an append (16 columns x 4 sub-buffers, same fill) on 64 distinct banks
@@ -59,17 +60,18 @@ __device__ __forceinline__ unsigned unord32(unsigned o) {
   return o ^ ((o >> 31) ? 0x80000000u : 0xffffffffu);
 }
 
-template <int KT, int SUB, int DEPTH, int CHECK, int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_screen_x1(
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32) ? 1 : 2))) void k_screen_x1(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
     const unsigned* __restrict__ bad, float r1, float r2, int S, int tiles_per_slice,
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
     float* __restrict__ cand_h) {
-  using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   constexpr int CT = C::CT;
   constexpr int D = C::D;
+  constexpr int NH = C::NCOL / 64;  // columns per lane in the lane-owns-column phases
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned* const sbuf = (unsigned*)smem;                    // [col][CP] interleaved entries
   int* const lcnt = (int*)(smem + C::SBUF);                  // [col][m] counts
@@ -102,7 +104,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const int pbase = qb * C::NCOL;
 
   if (*bad) {
-    if (lane < C::NCOL && pbase + lane < nq) cand_cnt[(int64_t)(pbase + lane) * S + s] = -1;
+    for (int col = lane; col < C::NCOL; col += 64)
+      if (pbase + col < nq) cand_cnt[(int64_t)(pbase + col) * S + s] = -1;
     return;
   }
   const float xnmax = __uint_as_float(*xnmax_bits);
@@ -149,7 +152,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = (int)(addr[ct] - (lim[ct] - (SUB - CHECK) * 16)) >> 4;
     dmlp::wave_sync();
-    const int j = lane;
+#pragma unroll 1
+    for (int hb = 0; hb < NH; ++hb) {
+    const int j = lane + 64 * hb;
     unsigned* const colbuf = sbuf + j * C::CP;
     const int4 n4 = *(const int4*)(lcnt + j * 4);
     const int nm[4] = {n4.x, n4.y, n4.z, n4.w};
@@ -234,15 +239,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       *(int4*)(lcnt + j * 4) = nn;
       lh[j] = ovf ? INFINITY : hc;
       lflag[j] = ovf ? 1 : 0;
-      dmlp::wave_sync();
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * lcnt[(ct * 16 + c) * 4 + kg];
-        h[ct] = lh[ct * 16 + c];
-      }
-      // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
-      // pending after the conditional call and drains lgkmcnt at every following step
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     } else {
       // kept entries out as (ordered 16-bit key << 16 | slice-relative group index): the refine
       // takes the k-th largest key over ALL slices of the query (a global threshold, as tight as
@@ -262,6 +258,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         cand_h[2 * ((int64_t)p * S + s)] = hc;       // this slice's final threshold
         cand_h[2 * ((int64_t)p * S + s) + 1] = epc;  // the query's error bound
       }
+    }
+    }  // column halves
+    if (!final_pass) {
+      dmlp::wave_sync();
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * lcnt[(ct * 16 + c) * 4 + kg];
+        h[ct] = lh[ct * 16 + c];
+      }
+      // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
+      // pending after the conditional call and drains lgkmcnt at every following step
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     }
   };
 
@@ -340,7 +348,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const int j = j0 + r;  // D = 4: j < nsteps (nsteps % 4 == 0); D = 8: guarded epilogue
         DMLP_MFMA(r, r & 1);
         DMLP_LOAD(j + D, r);
-        if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
+        if (MODE & 2) {  // ablation: keep every MFMA result alive, no epilogue at all
+          _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[r & 1][ct]));
+        } else if (j > 0) {
+          DMLP_EPILOGUE((r + 1) & 1, j - 1);
+        }
         if (r % CHECK == CHECK - 1) DMLP_CHECK();
       }
     }
@@ -362,25 +374,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
 int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
 
-int g_x1_check = 2;
+// column tiles per wave of the SUB = 16 (k <= 16) variants.  8 (128 queries per wave, one wave
+// per SIMD) halves the vector-memory instructions per MFMA — the 4-tile kernel keeps the texture
+// addresser ~75 % busy (TA_TA_BUSY, profiles/r2b_screen_x1_ta_pmc.txt) — but measured 2.39 ms
+// against 1.38 ms on the bench shape: without a partner wave nothing covers the in-order epilogue.
+// Kept as an A/B switch (DMLP_X1_CT=8).  SUB = 32 always uses 4.
+int g_x1_ct = 4;
+int x1_ct(int kmax) { return x1_sub(kmax) == 16 ? g_x1_ct : 4; }
 
-template <int KT, int SUB, int DEPTH, int CHECK>
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV>
 int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, int S,
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream) {
-  using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
   const int64_t grid = (int64_t)n_qblocks * S;
   if (grid <= 0) return 0;
 #define DMLP_X1_LAUNCH(M)                                                                      \
-  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
+  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, S, tps,          \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h)
   switch (g_x1_mode) {
     case 1: DMLP_X1_LAUNCH(1); break;
+    case 2: DMLP_X1_LAUNCH(2); break;
     case 8: DMLP_X1_LAUNCH(8); break;
     default: DMLP_X1_LAUNCH(0); break;
   }
@@ -406,15 +425,22 @@ extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
 }
 extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
 extern "C" int dmlp_screen_x1_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
+// queries per wave (= workgroup) of the variant that serves kmax
+extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
+  return (KT == 1 || KT == 2) ? 16 * x1_ct(kmax) : 0;
+}
 // group ids per (query, slice) (refine expands each to its 4 members)
 extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
-// resident workgroups (= waves) per CU, LDS-bound: 19.5 KiB (SUB 16) / 36.3 KiB (SUB 32)
-extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }
+// resident workgroups (= waves) per CU: LDS-bound at 19.5 KiB (SUB 16, 4 tiles) / 36.3 KiB
+// (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
+extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {
+  return x1_sub(kmax) == 16 ? (x1_ct(kmax) == 8 ? 4 : 8) : 4;
+}
 // a slice must stay below 2^16 4-row groups (16-bit group index in an entry)
 extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles + 4095) / 4096; }
 extern "C" void dmlp_set_x1_mode(int mode) { g_x1_mode = mode; }
-// steps between fill checks (1, 2, 4) of the KT = 1, k <= 16 variant (A/B)
-extern "C" void dmlp_set_x1_check(int c) { g_x1_check = (c == 1 || c == 4) ? c : 2; }
+// column tiles per wave of the k <= 16 variants (4 or 8; A/B)
+extern "C" void dmlp_set_x1_ct(int ct) { g_x1_ct = ct == 4 ? 4 : 8; }
 extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_dbg), sizeof(g_x1_dbg));
   if (e != hipSuccess) return -(int)e;
@@ -442,12 +468,12 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
 #define DMLP_X1_ARGS hl, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
                      r2, S, cand_ids, cand_cnt, cand_h, st
   const int sub = x1_sub(kmax);
-  if (KT == 1 && sub == 16) {  // A/B variants of the bench shape: fill-check period
-    if (g_x1_check == 1) return launch_x1<1, 16, 4, 1>(DMLP_X1_ARGS);
-    if (g_x1_check == 4) return launch_x1<1, 16, 4, 4>(DMLP_X1_ARGS);
-    return launch_x1<1, 16, 4, 2>(DMLP_X1_ARGS);
+  const int ct = x1_ct(kmax);
+  if (KT == 1) {
+    if (sub == 32) return launch_x1<1, 32, 4, 2, 4>(DMLP_X1_ARGS);
+    return ct == 8 ? launch_x1<1, 16, 4, 2, 8>(DMLP_X1_ARGS) : launch_x1<1, 16, 4, 2, 4>(DMLP_X1_ARGS);
   }
-  if (KT == 1) return launch_x1<1, 32, 4, 2>(DMLP_X1_ARGS);
-  return sub == 16 ? launch_x1<2, 16, 4, 2>(DMLP_X1_ARGS) : launch_x1<2, 32, 4, 2>(DMLP_X1_ARGS);
+  if (sub == 32) return launch_x1<2, 32, 4, 2, 4>(DMLP_X1_ARGS);
+  return ct == 8 ? launch_x1<2, 16, 4, 2, 8>(DMLP_X1_ARGS) : launch_x1<2, 16, 4, 2, 4>(DMLP_X1_ARGS);
 #undef DMLP_X1_ARGS
 }

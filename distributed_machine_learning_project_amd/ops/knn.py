@@ -387,7 +387,7 @@ class _KnnCall:
                                       int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
         elif impl == "x1":
             cap = L.dmlp_screen_x1_cap(kcls)
-            S = _choose_slices_stream(nq, L.dmlp_screen_x1_qw(KT), ds.n_tiles,
+            S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), ds.n_tiles,
                                       L.dmlp_screen_x1_waves_per_cu(kcls),
                                       int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
         elif impl == "stream":
@@ -726,8 +726,8 @@ def _apply_env_switches(L):
     if not _ENV_APPLIED[0]:
         if os.environ.get("DMLP_STREAM_GROUPS", "1") == "0":
             L.dmlp_set_stream_groups(0)
-        if os.environ.get("DMLP_X1_CHECK"):
-            L.dmlp_set_x1_check(int(os.environ["DMLP_X1_CHECK"]))
+        if os.environ.get("DMLP_X1_CT"):
+            L.dmlp_set_x1_ct(int(os.environ["DMLP_X1_CT"]))
         if os.environ.get("DMLP_X2_PW"):
             L.dmlp_set_x2_pw(int(os.environ["DMLP_X2_PW"]))
         if os.environ.get("DMLP_STREAM_SUB"):
