@@ -364,33 +364,204 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
   }
 }
 
-// Sequential k-way merge, one thread per query (lists are short and already sorted).
-__global__ void k_merge(const double* __restrict__ in_d, const int* __restrict__ in_i, int L,
-                        int64_t list_stride, int kin, const int* __restrict__ qk, int nq,
-                        double* __restrict__ out_d, int* __restrict__ out_i, int kout) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+// K-way merge of L sorted top-k lists per query (K4: bench_2's custom MPI_Op / bench_1's root
+// merge), one wave per query, no sequential head scan: every element's output position is its
+// rank in the union, i.e. its index in its own list plus, for every other list, the number of
+// entries ordered before it (a binary search over that list's real prefix; ties between lists
+// go to the lower list index).  The ranks of the real elements are therefore exactly
+// 0 .. total-1; each element with rank < k is stored once, and slots [total, k) get the
+// (+inf, -1) padding.  Padding entries (id < 0) form a suffix of each list.
+__global__ __launch_bounds__(256) void k_merge(const double* __restrict__ in_d,
+                                               const int* __restrict__ in_i, int L,
+                                               int64_t list_stride, int kin,
+                                               const int* __restrict__ qk, int nq,
+                                               double* __restrict__ out_d, int* __restrict__ out_i,
+                                               int kout) {
+  __shared__ int s_cnt[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + wave;
   if (q >= nq) return;
-  const int k = qk[q];
-  constexpr int LMAX = 64;
-  int head[LMAX];
-  for (int l = 0; l < L; ++l) head[l] = 0;
+  int k = qk[q];
+  k = k < kout ? k : kout;
   const int lim = k < kin ? k : kin;
-  for (int o = 0; o < k; ++o) {
-    int best = -1;
-    double bd = INFINITY;
-    int bi = -1;
-    for (int l = 0; l < L; ++l) {
-      if (head[l] >= lim) continue;
-      const int64_t off = l * list_stride + (int64_t)q * kin + head[l];
-      const int ii = in_i[off];
-      if (ii < 0) continue;  // padding
-      const double dd = in_d[off];
-      if (best < 0 || dmlp::key_less(dd, ii, bd, bi)) { best = l; bd = dd; bi = ii; }
+  const int64_t qo = (int64_t)q * kin;
+  int* cnt = s_cnt[wave];
+  // real prefix length of each list (first padding entry, by binary search)
+  for (int l = lane; l < L; l += 64) {
+    const int* ids = in_i + l * list_stride + qo;
+    int lo = 0, n = lim;
+    while (n > 0) {
+      const int h = n >> 1;
+      if (ids[lo + h] >= 0) { lo += h + 1; n -= h + 1; } else { n = h; }
     }
-    if (best < 0) { bd = INFINITY; bi = -1; }
-    else head[best]++;
-    out_d[(int64_t)q * kout + o] = bd;
-    out_i[(int64_t)q * kout + o] = bi;
+    cnt[l] = lo;
+  }
+  dmlp::wave_sync();
+  int total = 0;
+  for (int l = 0; l < L; ++l) total += cnt[l];
+  for (int t = lane; t < L * lim; t += 64) {
+    const int l = t / lim, p = t - l * lim;
+    if (p >= cnt[l]) continue;
+    const int64_t off = l * list_stride + qo + p;
+    const double d = in_d[off];
+    const int id = in_i[off];
+    int rank = p;
+    for (int m = 0; m < L && rank < k; ++m) {
+      if (m == l) continue;
+      const double* md = in_d + m * list_stride + qo;
+      const int* mi = in_i + m * list_stride + qo;
+      // equal keys (only when the caller's lists overlap) order by list index, as a sequential
+      // merge that scans the lists in order would: count entries <= the key in earlier lists
+      const bool before = m < l;
+      int lo = 0, n = cnt[m];
+      while (n > 0) {
+        const int h = n >> 1;
+        const bool lt = before ? !dmlp::key_less(d, id, md[lo + h], mi[lo + h])
+                               : dmlp::key_less(md[lo + h], mi[lo + h], d, id);
+        if (lt) { lo += h + 1; n -= h + 1; } else { n = h; }
+      }
+      rank += lo;
+    }
+    if (rank < k) {
+      out_d[(int64_t)q * kout + rank] = d;
+      out_i[(int64_t)q * kout + rank] = id;
+    }
+  }
+  for (int o = total + lane; o < k; o += 64) {
+    out_d[(int64_t)q * kout + o] = INFINITY;
+    out_i[(int64_t)q * kout + o] = -1;
+  }
+}
+
+// Merge-path form of the same K4 merge for lists that fit in LDS (2 x L x kout entries):
+// one wave per query stages the L real prefixes in LDS, then merges adjacent pairs level by
+// level (log2 L levels, ties to the lower list index, i.e. the earlier pair member — the same
+// order as the rank kernel).  Every output element of a pair merge finds its co-rank (how many
+// of its predecessors come from the first list) by one binary search, so a lane does
+// ceil(pairs x k / 64) searches of log2 k probes per level, all in LDS.
+__global__ __launch_bounds__(256) void k_merge_path(const double* __restrict__ in_d,
+                                                   const int* __restrict__ in_i, int L,
+                                                   int64_t list_stride, int kin,
+                                                   const int* __restrict__ qk, int nq,
+                                                   double* __restrict__ out_d,
+                                                   int* __restrict__ out_i, int kout, int lcap) {
+  extern __shared__ __attribute__((aligned(16))) char smem_all[];
+  __shared__ int s_cnt_all[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x * (blockDim.x >> 6) + wave;  // one query per wave
+  if (q >= nq) return;
+  char* const smem = smem_all + (size_t)wave * 2 * L * lcap * (sizeof(double) + sizeof(int));
+  int (*s_cnt)[64] = s_cnt_all[wave];
+  int k = qk[q];
+  k = k < kout ? k : kout;
+  const int lim = k < kin ? k : kin;
+  double* bd[2] = {(double*)smem, (double*)smem + (size_t)L * lcap};
+  int* bi[2] = {(int*)((double*)smem + 2 * (size_t)L * lcap),
+                (int*)((double*)smem + 2 * (size_t)L * lcap) + (size_t)L * lcap};
+  const int64_t qo = (int64_t)q * kin;
+  // t / d for the small flat indices below by a float reciprocal (exact: t < 2^16, +0.5 margin)
+  auto divq = [](int t, float inv) { return (int)(((float)t + 0.5f) * inv); };
+  // stage the L prefixes (all loads of a lane issued back to back), then each list's real
+  // prefix length by a binary search for its first padding id
+  const float inv_lim = 1.0f / (float)(lim > 0 ? lim : 1);
+  for (int t0 = 0; t0 < L * lim; t0 += 256) {  // 4 loads in flight per lane, then the stores
+    double dv[4];
+    int iv[4], dst[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = t0 + 64 * u + lane;
+      dst[u] = -1;
+      if (t < L * lim) {
+        const int l = divq(t, inv_lim), p = t - l * lim;
+        const int64_t off = l * list_stride + qo + p;
+        dv[u] = in_d[off];
+        iv[u] = in_i[off];
+        dst[u] = l * lcap + p;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (dst[u] >= 0) { bd[0][dst[u]] = dv[u]; bi[0][dst[u]] = iv[u]; }
+  }
+  dmlp::wave_sync();
+  for (int l = lane; l < L; l += 64) {
+    const int* ids = bi[0] + l * lcap;
+    int lo = 0, n = lim;
+    while (n > 0) {
+      const int h = n >> 1;
+      if (ids[lo + h] >= 0) { lo += h + 1; n -= h + 1; } else { n = h; }
+    }
+    s_cnt[0][l] = lo;
+  }
+  dmlp::wave_sync();
+  const float inv_k = 1.0f / (float)(k > 0 ? k : 1);
+  int cur = 0, Lc = L;
+  while (Lc > 1) {
+    const int Ln = (Lc + 1) >> 1;
+    const double* sd = bd[cur];
+    const int* si = bi[cur];
+    double* dd = bd[cur ^ 1];
+    int* di = bi[cur ^ 1];
+    // lane-contiguous output ranges over the flattened (pair, position) space: one co-rank
+    // search per pair segment, then a sequential merge of the segment from register heads
+    const int tot = Ln * k;
+    const int chunk = (tot + 63) >> 6;
+    int t = lane * chunk;
+    const int tend = t + chunk < tot ? t + chunk : tot;
+    while (t < tend) {
+      const int pr = divq(t, inv_k), o0 = t - pr * k;
+      const int oend = o0 + (tend - t) < k ? o0 + (tend - t) : k;
+      t += oend - o0;
+      const int la = 2 * pr, lb = la + 1;
+      const int ca = s_cnt[cur][la];
+      const double* ad = sd + la * lcap;
+      const int* ai = si + la * lcap;
+      double* od = dd + pr * lcap;
+      int* oi = di + pr * lcap;
+      if (lb >= Lc) {
+        for (int o = o0; o < oend && o < ca; ++o) { od[o] = ad[o]; oi[o] = ai[o]; }
+        continue;
+      }
+      const int cb = s_cnt[cur][lb];
+      const int m = ca + cb < oend ? ca + cb : oend;
+      if (o0 >= m) continue;
+      const double* b_d = sd + lb * lcap;
+      const int* b_i = si + lb * lcap;
+      // co-rank of o0: the smallest i with NOT (a[i] precedes b[o0 - i - 1]); a first on ties
+      int lo = o0 > cb ? o0 - cb : 0, hi = o0 < ca ? o0 : ca;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const int j = o0 - mid - 1;
+        if (!dmlp::key_less(b_d[j], b_i[j], ad[mid], ai[mid])) lo = mid + 1; else hi = mid;
+      }
+      int i = lo, j = o0 - lo;
+      double xa = i < ca ? ad[i] : 0.0, xb = j < cb ? b_d[j] : 0.0;
+      int ia = i < ca ? ai[i] : 0, ib = j < cb ? b_i[j] : 0;
+      for (int o = o0; o < m; ++o) {
+        const bool take_a = i < ca && (j >= cb || !dmlp::key_less(xb, ib, xa, ia));
+        if (take_a) {
+          od[o] = xa; oi[o] = ia;
+          if (++i < ca) { xa = ad[i]; ia = ai[i]; }
+        } else {
+          od[o] = xb; oi[o] = ib;
+          if (++j < cb) { xb = b_d[j]; ib = b_i[j]; }
+        }
+      }
+    }
+    if (lane < Ln) {
+      const int la = 2 * lane, lb = la + 1;
+      const int c = s_cnt[cur][la] + (lb < Lc ? s_cnt[cur][lb] : 0);
+      s_cnt[cur ^ 1][lane] = c < k ? c : k;
+    }
+    dmlp::wave_sync();
+    cur ^= 1;
+    Lc = Ln;
+  }
+  const int total = s_cnt[cur][0];
+  for (int o = lane; o < k; o += 64) {
+    const bool real = o < total;
+    out_d[(int64_t)q * kout + o] = real ? bd[cur][o] : INFINITY;
+    out_i[(int64_t)q * kout + o] = real ? bi[cur][o] : -1;
   }
 }
 
@@ -611,8 +782,17 @@ extern "C" int dmlp_merge(const double* in_d, const int* in_i, int L, int64_t li
                           void* stream) {
   if (nq <= 0) return 0;
   if (L < 1 || L > 64) return -1;
-  hipLaunchKernelGGL(k_merge, dim3((nq + 127) / 128), dim3(128), 0, (hipStream_t)stream, in_d,
-                     in_i, L, list_stride, kin, qk, nq, out_d, out_i, kout);
+  const int lcap = std::max(1, kout);  // a merged list holds up to k <= kout entries
+  const size_t lds = 2 * (size_t)L * lcap * (sizeof(double) + sizeof(int));
+  if (lds <= 48 * 1024) {  // LDS-resident merge path (P <= 8 lists of k <= 256, ...)
+    const int w = lds <= 12 * 1024 ? 4 : 1;  // queries (waves) per workgroup
+    hipLaunchKernelGGL(k_merge_path, dim3((nq + w - 1) / w), dim3(64 * w), lds * w,
+                       (hipStream_t)stream, in_d, in_i, L, list_stride, kin, qk, nq, out_d, out_i,
+                       kout, lcap);
+  } else {
+    hipLaunchKernelGGL(k_merge, dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, in_d,
+                       in_i, L, list_stride, kin, qk, nq, out_d, out_i, kout);
+  }
   DMLP_LAUNCH_CHECK();
   return 0;
 }

@@ -347,6 +347,31 @@ def test_merge_and_finalize(torch_cuda):
     np.testing.assert_array_equal(cs_c, cs_g.cpu().numpy().view(np.uint64))
 
 
+@pytest.mark.parametrize("Lists,kin,kout", [(8, 16, 16), (8, 128, 128), (3, 40, 64), (64, 4, 8)])
+def test_merge_rank_shapes(torch_cuda, Lists, kin, kout):
+    """K4 merge at shard-merge shapes: disjoint ids, padded (+inf, -1) suffixes of random length,
+    per-query k in [0, kout] (bench_2 @0xbc70 custom op semantics via merge_cpu)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(Lists * 1000 + kin)
+    Q = 777
+    d = np.sort(rng.integers(0, 400, size=(Lists, Q, kin)).astype(np.float64), axis=2)
+    ids = rng.permutation(Lists * Q * kin).reshape(Lists, Q, kin).astype(np.int32)
+    for l in range(Lists):
+        for q in range(Q):
+            o = np.lexsort((-ids[l, q], d[l, q]))
+            d[l, q], ids[l, q] = d[l, q][o], ids[l, q][o]
+            npad = int(rng.integers(0, kin + 1)) if rng.random() < 0.3 else 0
+            if npad:
+                d[l, q, kin - npad:] = np.inf
+                ids[l, q, kin - npad:] = -1
+    k = rng.integers(0, kout + 1, size=Q).astype(np.int32)
+    dc, ic = K.merge_cpu(d, ids, k, kout=kout)
+    kd = torch.from_numpy(k).cuda()
+    dg, ig = K.merge_gpu(torch.from_numpy(d).cuda(), torch.from_numpy(ids).cuda(), kd, kout)
+    np.testing.assert_array_equal(ic, ig.cpu().numpy())
+    np.testing.assert_array_equal(dc, dg.cpu().numpy())
+
+
 def test_format_report_gpu(torch_cuda):
     torch = torch_cuda
     rng = np.random.default_rng(2)
