@@ -108,13 +108,13 @@ def main(argv=None):
     # max over ranks
     el = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
     if world > 1:
-        import torch.distributed as dist
+        from distributed_machine_learning_project_amd.parallel import dist_api as dist
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms = elapsed / max(1, a.steps) * 1e3
 
     extra = {}
-    if world > 1 and comm.on_gpu and not a.no_busbw:
+    if world > 1 and comm.backend == "nccl" and not a.no_busbw:
         extra["allreduce_busbw_GBps"] = round(_allreduce_busbw(comm), 1)
     if a.verify and comm.is_root:
         import hashlib

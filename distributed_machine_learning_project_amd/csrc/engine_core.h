@@ -157,20 +157,124 @@ class KnnCore {
  private:
   template <typename T>
   static ncclDataType_t nty();
+  // Data plane.  RCCL over xGMI; with KNN_DATA_PLANE=host (Runtime::host_plane, a test mode
+  // that lets several ranks share one GPU, which RCCL refuses) every transfer is staged through
+  // host memory and carried by blocking MPI point-to-point calls in the same order, so the
+  // strategies' offsets, trees and merge kernels run unchanged on the real kernels.  Every
+  // point-to-point transfer is also logged (peer, bytes) for the KNN_P2P_CHECK matching check.
+  void grp_start() {
+    if (!rt_.host_plane) grp_start();
+  }
+  void grp_end() {
+    if (!rt_.host_plane) grp_end();
+  }
   template <typename T>
   void snd(const T* p, int64_t n, int peer) {
-    NCCLCHK(ncclSend(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
-    sent_ += n * (int64_t)sizeof(T);
+    const int64_t bytes = n * (int64_t)sizeof(T);
+    p2p_log_.push_back({1, peer, bytes});
+    sent_ += bytes;
+    if (!rt_.host_plane) {
+      NCCLCHK(ncclSend(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+      return;
+    }
+    std::vector<char> h(bytes);
+    HIPCHK(hipMemcpyAsync(h.data(), p, bytes, hipMemcpyDeviceToHost, rt_.stream));
+    rt_.sync();
+    mpi_bytes(h.data(), bytes, peer, true);
   }
   template <typename T>
   void rcv(T* p, int64_t n, int peer) {
-    NCCLCHK(ncclRecv(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+    const int64_t bytes = n * (int64_t)sizeof(T);
+    p2p_log_.push_back({0, peer, bytes});
+    if (!rt_.host_plane) {
+      NCCLCHK(ncclRecv(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+      return;
+    }
+    std::vector<char> h(bytes);
+    mpi_bytes(h.data(), bytes, peer, false);
+    HIPCHK(hipMemcpyAsync(p, h.data(), bytes, hipMemcpyHostToDevice, rt_.stream));
+    rt_.sync();  // h dies here
   }
   template <typename T>
   void bcast(T* p, int64_t n) {
-    NCCLCHK(ncclBroadcast(p, p, n, nty<T>(), 0, rt_.nccl, rt_.stream));
-    if (rt_.rank == 0) sent_ += n * (int64_t)sizeof(T) * (rt_.world - 1);
+    const int64_t bytes = n * (int64_t)sizeof(T);
+    if (rt_.rank == 0) sent_ += bytes * (rt_.world - 1);
+    if (!rt_.host_plane) {
+      NCCLCHK(ncclBroadcast(p, p, n, nty<T>(), 0, rt_.nccl, rt_.stream));
+      return;
+    }
+    std::vector<char> h(bytes);
+    if (rt_.rank == 0) {
+      HIPCHK(hipMemcpyAsync(h.data(), p, bytes, hipMemcpyDeviceToHost, rt_.stream));
+      rt_.sync();
+    }
+    for (int64_t o = 0; o < bytes; o += kMpiChunk)
+      MPI_Bcast(h.data() + o, (int)std::min<int64_t>(kMpiChunk, bytes - o), MPI_BYTE, 0,
+                MPI_COMM_WORLD);
+    if (rt_.rank != 0) {
+      HIPCHK(hipMemcpyAsync(p, h.data(), bytes, hipMemcpyHostToDevice, rt_.stream));
+      rt_.sync();
+    }
   }
+  static constexpr int64_t kMpiChunk = int64_t(1) << 30;
+  static void mpi_bytes(char* p, int64_t bytes, int peer, bool send) {
+    for (int64_t o = 0; o < bytes; o += kMpiChunk) {
+      const int c = (int)std::min<int64_t>(kMpiChunk, bytes - o);
+      if (send) MPI_Send(p + o, c, MPI_BYTE, peer, 77, MPI_COMM_WORLD);
+      else MPI_Recv(p + o, c, MPI_BYTE, peer, 77, MPI_COMM_WORLD, MPI_STATUS_IGNORE);
+    }
+  }
+
+ public:
+  struct P2PEntry {
+    int64_t send, peer, bytes;
+  };
+  std::vector<P2PEntry> p2p_log_;
+  // KNN_P2P_CHECK: every rank's ordered (send/recv, peer, bytes) log goes to rank 0, which checks
+  // that the sends from a to b and the receives at b from a are the same sequence of sizes (a
+  // mismatched ncclSend/ncclRecv pair hangs or corrupts; this catches it on any host, even
+  // with the host-staged plane).  Returns the number of matched messages; throws on mismatch.
+  int64_t check_p2p() {
+    const int P = rt_.world;
+    std::vector<int64_t> flat;
+    for (const auto& e : p2p_log_) { flat.push_back(e.send); flat.push_back(e.peer); flat.push_back(e.bytes); }
+    int n = (int)flat.size();
+    std::vector<int> counts(P), displs(P);
+    MPI_Gather(&n, 1, MPI_INT, counts.data(), 1, MPI_INT, 0, MPI_COMM_WORLD);
+    std::vector<int64_t> all;
+    if (rt_.rank == 0) {
+      int tot = 0;
+      for (int r = 0; r < P; ++r) { displs[r] = tot; tot += counts[r]; }
+      all.resize(std::max(1, tot));
+    }
+    MPI_Gatherv(flat.data(), n, MPI_INT64_T, all.data(), counts.data(), displs.data(),
+                MPI_INT64_T, 0, MPI_COMM_WORLD);
+    int64_t matched = 0;
+    if (rt_.rank == 0) {
+      // seq[a][b] = sizes a sent to b; got[b][a] = sizes b received from a
+      std::vector<std::vector<std::vector<int64_t>>> seq(P, std::vector<std::vector<int64_t>>(P)),
+          got(P, std::vector<std::vector<int64_t>>(P));
+      for (int r = 0; r < P; ++r)
+        for (int i = 0; i < counts[r]; i += 3) {
+          const int64_t* e = all.data() + displs[r] + i;
+          if (e[1] < 0 || e[1] >= P) throw std::runtime_error("p2p check: bad peer");
+          (e[0] ? seq[r][e[1]] : got[r][e[1]]).push_back(e[2]);
+        }
+      for (int a = 0; a < P; ++a)
+        for (int b = 0; b < P; ++b) {
+          if (seq[a][b] != got[b][a])
+            throw std::runtime_error("p2p check: rank " + std::to_string(a) + " -> " +
+                                     std::to_string(b) + ": " + std::to_string(seq[a][b].size()) +
+                                     " sends vs " + std::to_string(got[b][a].size()) +
+                                     " receives (or sizes differ)");
+          matched += (int64_t)seq[a][b].size();
+        }
+    }
+    p2p_log_.clear();
+    return matched;
+  }
+
+ private:
 
   void warmup() {
     // load every kernel once (module load + first-launch costs stay outside the timed region)
@@ -283,14 +387,14 @@ class KnnCore {
       bcast(Xd, N_ * A_);
       bcast(Ld, N_);
       // static query blocks: one direct xGMI hop per rank
-      NCCLCHK(ncclGroupStart());
+      grp_start();
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r)
           if (cnt[r]) snd(Qall + off[r] * A_, cnt[r] * A_, r);
       } else if (cnt[rt_.rank]) {
         rcv(Qall, cnt[rt_.rank] * A_, 0);
       }
-      NCCLCHK(ncclGroupEnd());
+      grp_end();
     }
     trace.mark("distribute");
     const int64_t nl = cnt[rt_.rank];
@@ -301,7 +405,7 @@ class KnnCore {
     local_knn(Xd, N_, Qall, nl, kl.data(), dd, ii, Ld, lb, cs);
     trace.mark("compute");
     if (P > 1) {  // gather (label, checksum [, lists]) to rank 0 in rank order
-      NCCLCHK(ncclGroupStart());
+      grp_start();
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r) {
           if (!cnt[r]) continue;
@@ -320,7 +424,7 @@ class KnnCore {
           snd(ii, nl * kmax_, 0);
         }
       }
-      NCCLCHK(ncclGroupEnd());
+      grp_end();
     }
     trace.mark("gather");
     if (rt_.rank == 0) render(out, cs, lb, dd, ii);
@@ -348,14 +452,14 @@ class KnnCore {
     if (rt_.rank == 0) k = in->k;
     MPI_Bcast(k.data(), (int)Q_, MPI_INT, 0, MPI_COMM_WORLD);
     if (P > 1) {
-      NCCLCHK(ncclGroupStart());  // MPI_Scatterv of the shards -> direct sends
+      grp_start();  // MPI_Scatterv of the shards -> direct sends
       if (rt_.rank == 0) {
         for (int r = 1; r < P; ++r)
           if (cnt[r]) snd(Xd + off[r] * A_, cnt[r] * A_, r);
       } else if (nl) {
         rcv(Xd, nl * A_, 0);
       }
-      NCCLCHK(ncclGroupEnd());
+      grp_end();
       bcast(Qd, Q_ * A_);
     }
     trace.mark("distribute");
@@ -370,7 +474,7 @@ class KnnCore {
     if (P > 1 && !tree) {  // bench_1: ONE batched gather of all lists, K-way merge at the root
       double* all_d = dall_.get(rt_.rank == 0 ? L * P : 1);
       int* all_i = iall_.get(rt_.rank == 0 ? L * P : 1);
-      NCCLCHK(ncclGroupStart());
+      grp_start();
       if (rt_.rank == 0) {
         HIPCHK(hipMemcpyAsync(all_d, dd, L * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(all_i, ii, L * 4, hipMemcpyDeviceToDevice, st));
@@ -382,26 +486,26 @@ class KnnCore {
         snd(dd, L, 0);
         snd(ii, L, 0);
       }
-      NCCLCHK(ncclGroupEnd());
+      grp_end();
       if (rt_.rank == 0) DMLPCHK(dmlp_merge(all_d, all_i, P, L, kmax_, kd, (int)Q_, dd, ii, kmax_, st));
     } else if (P > 1) {  // bench_2/3: binomial tree, pairwise merge at every receiving rank
       double* sd = stage_d_.get(2 * L);
       int* si = stage_i_.get(2 * L);
       for (int step = 1; step < P; step *= 2) {
         if (rt_.rank % (2 * step) == step) {
-          NCCLCHK(ncclGroupStart());
+          grp_start();
           snd(dd, L, rt_.rank - step);
           snd(ii, L, rt_.rank - step);
-          NCCLCHK(ncclGroupEnd());
+          grp_end();
           break;
         }
         if (rt_.rank % (2 * step) == 0 && rt_.rank + step < P) {
           HIPCHK(hipMemcpyAsync(sd, dd, L * 8, hipMemcpyDeviceToDevice, st));
           HIPCHK(hipMemcpyAsync(si, ii, L * 4, hipMemcpyDeviceToDevice, st));
-          NCCLCHK(ncclGroupStart());
+          grp_start();
           rcv(sd + L, L, rt_.rank + step);
           rcv(si + L, L, rt_.rank + step);
-          NCCLCHK(ncclGroupEnd());
+          grp_end();
           DMLPCHK(dmlp_merge(sd, si, 2, L, kmax_, kd, (int)Q_, dd, ii, kmax_, st));
         }
       }
@@ -448,7 +552,7 @@ class KnnCore {
     if (root) k = in->k;
     MPI_Bcast(k.data(), (int)Q_, MPI_INT, 0, MPI_COMM_WORLD);
     if (P > 1) {
-      NCCLCHK(ncclGroupStart());
+      grp_start();
       if (root) {
         for (int r = 1; r < P; ++r) {
           const int rr = r / C, cc = r % C;
@@ -461,7 +565,7 @@ class KnnCore {
         if (qc[col]) rcv(Qd, qc[col] * A_, 0);
         if (row == 0 && N_) rcv(Ld, N_, 0);
       }
-      NCCLCHK(ncclGroupEnd());
+      grp_end();
     }
     trace.mark("distribute");
     const int64_t nq = qc[col];
@@ -481,18 +585,18 @@ class KnnCore {
         int* all_i = iall_.get(L * R);
         HIPCHK(hipMemcpyAsync(all_d, dd, L * 8, hipMemcpyDeviceToDevice, st));
         HIPCHK(hipMemcpyAsync(all_i, ii, L * 4, hipMemcpyDeviceToDevice, st));
-        NCCLCHK(ncclGroupStart());
+        grp_start();
         for (int r = 1; r < R; ++r) {
           rcv(all_d + r * L, L, r * C + col);
           rcv(all_i + r * L, L, r * C + col);
         }
-        NCCLCHK(ncclGroupEnd());
+        grp_end();
         DMLPCHK(dmlp_merge(all_d, all_i, R, L, kmax_, kd, (int)nq, dd, ii, kmax_, st));
       } else {
-        NCCLCHK(ncclGroupStart());
+        grp_start();
         snd(dd, L, col);
         snd(ii, L, col);
-        NCCLCHK(ncclGroupEnd());
+        grp_end();
       }
     }
     trace.mark("merge");
@@ -501,7 +605,7 @@ class KnnCore {
       uint64_t* cs = cs_.get((root ? Q_ : nq) + 1);
       DMLPCHK(dmlp_finalize(dd, ii, kmax_, kd, nullptr, (int)nq, Ld, lo_, hi_, lb, cs, st));
       if (C > 1) {  // row-0 gather of (label, checksum [, lists]) in query order
-        NCCLCHK(ncclGroupStart());
+        grp_start();
         if (root) {
           for (int c = 1; c < C; ++c) {
             if (!qc[c]) continue;
@@ -520,7 +624,7 @@ class KnnCore {
             snd(ii, L, 0);
           }
         }
-        NCCLCHK(ncclGroupEnd());
+        grp_end();
       }
       trace.mark("gather");
       if (root) render(out, cs, lb, dd, ii);

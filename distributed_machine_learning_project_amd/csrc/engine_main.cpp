@@ -70,7 +70,12 @@ int main(int argc, char** argv) {
                    (long long)std::chrono::duration_cast<std::chrono::milliseconds>(t1 - t0).count());
       total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     }
-    // after the timed region: per-phase trace (KNN_TRACE=1) and the metrics sidecar
+    // after the timed region: the send/recv matching check (KNN_P2P_CHECK=1), per-phase trace
+    // (KNN_TRACE=1) and the metrics sidecar
+    if (getenv("KNN_P2P_CHECK") && std::string(getenv("KNN_P2P_CHECK")) == "1") {
+      const int64_t m = eng.check_p2p();
+      if (rt.rank == 0) std::fprintf(stderr, "[knn_engine] p2p check OK: %lld matched messages\n", (long long)m);
+    }
     const auto phases = eng.trace.finish();
     int64_t bytes = 0;
     MPI_Reduce(&eng.sent_, &bytes, 1, MPI_INT64_T, MPI_SUM, 0, MPI_COMM_WORLD);

@@ -120,6 +120,9 @@ struct Runtime {
   hipStream_t stream = nullptr;
 
   bool gpu = false;
+  // KNN_DATA_PLANE=host: no RCCL communicator; KnnCore stages transfers through host memory
+  // and MPI (several ranks may then share one GPU — test mode)
+  bool host_plane = getenv("KNN_DATA_PLANE") && std::string(getenv("KNN_DATA_PLANE")) == "host";
 
   void init(bool need_gpu = true) {
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
@@ -137,7 +140,7 @@ struct Runtime {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     reserve_arenas();
-    if (world > 1) {
+    if (world > 1 && !host_plane) {
       ncclUniqueId id;
       if (rank == 0) NCCLCHK(ncclGetUniqueId(&id));
       MPI_Bcast(&id, sizeof(id), MPI_BYTE, 0, MPI_COMM_WORLD);

@@ -94,18 +94,21 @@ class Comm:
             dev = torch.device("cuda", torch.cuda.current_device())
         else:
             dev = torch.device("cpu")
-        backend = "nccl" if use_gpu else "gloo"
+        # DMLP_DATA_PLANE=host: gloo over host-staged copies of the device tensors (dist_api.py)
+        # so that several ranks can share one GPU — a test mode; RCCL is the MI355X data plane
+        staged = use_gpu and os.environ.get("DMLP_DATA_PLANE", "") == "host"
+        backend = "nccl" if use_gpu and not staged else "gloo"
         here = False
         if world > 1 and not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29511")
             kw = {}
-            if use_gpu:
+            if backend == "nccl":
                 kw["device_id"] = dev
             with quiet_stdout():
                 dist.init_process_group(backend, rank=rank, world_size=world,
                                         timeout=datetime.timedelta(seconds=timeout_s), **kw)
-                if not use_gpu:
+                if backend == "gloo":
                     dist.barrier()
             here = True
         elif dist.is_initialized():
@@ -114,7 +117,7 @@ class Comm:
         return Comm(rank, world, local_rank, dev, backend, here)
 
     def finalize(self):
-        import torch.distributed as dist
+        from . import dist_api as dist
         if self.initialized_here and dist.is_initialized():
             dist.destroy_process_group()
 
@@ -129,11 +132,8 @@ class Comm:
     # ------------------------------------------------------------------ primitives
     def barrier(self):
         if self.world > 1:
-            import torch.distributed as dist
-            if self.on_gpu:
-                dist.barrier(device_ids=[self.device.index])
-            else:
-                dist.barrier()
+            from . import dist_api as dist
+            dist.barrier(device_ids=[self.device.index] if self.on_gpu else None)
 
     def sync(self):
         if self.on_gpu:
@@ -144,7 +144,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return list(vals)
-        import torch.distributed as dist
+        from . import dist_api as dist
         n = len(vals) if vals is not None else n
         t = torch.zeros(n, dtype=torch.int64, device=self.device)
         if self.is_root:
@@ -157,7 +157,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return [list(vals)]
-        import torch.distributed as dist
+        from . import dist_api as dist
         t = torch.tensor(list(vals), dtype=torch.int64, device=self.device)
         out = torch.empty(self.world * t.numel(), dtype=torch.int64, device=self.device)
         dist.all_gather_into_tensor(out, t)
@@ -170,7 +170,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return t
-        import torch.distributed as dist
+        from . import dist_api as dist
         if not self.is_root:
             t = torch.empty(shape, dtype=dtype, device=self.device)
         if t.numel():
@@ -182,7 +182,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return t[: counts[0]]
-        import torch.distributed as dist
+        from . import dist_api as dist
         mx = max(counts)
         out = torch.empty((mx, *row_shape), dtype=dtype, device=self.device)
         if mx == 0:
@@ -207,7 +207,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return t
-        import torch.distributed as dist
+        from . import dist_api as dist
         mx = max(counts)
         if mx == 0:
             return torch.empty((0, *row_shape), dtype=dtype, device=self.device)
@@ -227,7 +227,7 @@ class Comm:
         torch = _torch()
         if self.world == 1:
             return t
-        import torch.distributed as dist
+        from . import dist_api as dist
         mx = max(counts)
         src = torch.zeros((mx, *row_shape), dtype=dtype, device=self.device)
         if t is not None and t.shape[0]:
@@ -239,18 +239,18 @@ class Comm:
         return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
     def send(self, t, dst):
-        import torch.distributed as dist
+        from . import dist_api as dist
         dist.send(t.contiguous(), dst)
 
     def recv(self, shape, dtype, src):
         torch = _torch()
-        import torch.distributed as dist
+        from . import dist_api as dist
         t = torch.empty(shape, dtype=dtype, device=self.device)
         dist.recv(t, src)
         return t
 
     def new_group(self, ranks):
-        import torch.distributed as dist
+        from . import dist_api as dist
         if self.world == 1:
             return None
         with quiet_stdout():

@@ -150,7 +150,7 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
                 dbg_i[a:b] = i
     with tr.phase("reduce"):
         if comm.world > 1:
-            import torch.distributed as dist
+            from . import dist_api as dist
             dist.reduce(out, 0, op=dist.ReduceOp.SUM)
             if debug:
                 dist.reduce(dbg_d, 0, op=dist.ReduceOp.SUM)
@@ -329,7 +329,7 @@ def shard_gather(comm, be, inp, tr, debug=False, **_):
     with tr.phase("gather"):
         P = comm.world
         if P > 1:
-            import torch.distributed as dist
+            from . import dist_api as dist
             bd = [torch.empty_like(d) for _ in range(P)] if comm.is_root else None
             bi = [torch.empty_like(i) for _ in range(P)] if comm.is_root else None
             dist.gather(d.contiguous(), bd, dst=0)
@@ -394,7 +394,7 @@ class GridGroups:
 def _grp_scatter(comm, t, counts, row_shape, dtype, group, ranks, src_idx=0):
     """MPI_Scatterv inside a sub-communicator (equal-size padded chunks)."""
     torch = _torch()
-    import torch.distributed as dist
+    from . import dist_api as dist
     me = ranks.index(comm.rank)
     mx = max(counts)
     out = torch.empty((mx, *row_shape), dtype=dtype, device=be_device(comm))
@@ -416,7 +416,7 @@ def _grp_scatter(comm, t, counts, row_shape, dtype, group, ranks, src_idx=0):
 
 def _grp_bcast(comm, t, shape, dtype, group, ranks, src_idx=0):
     torch = _torch()
-    import torch.distributed as dist
+    from . import dist_api as dist
     if len(ranks) == 1:
         return t
     if ranks.index(comm.rank) != src_idx:
@@ -432,7 +432,7 @@ def be_device(comm):
 
 def grid2d(comm, be, inp, tr, groups=None, debug=False, **_):
     torch = _torch()
-    import torch.distributed as dist
+    from . import dist_api as dist
     g = groups or GridGroups(comm)
     N, Q, A, lo, hi, kmax = _meta(comm, inp)
     dcounts, ddispl = block_partition(N, g.R)   # data over grid rows (engine.cpp:62-63)
@@ -563,7 +563,7 @@ def ring(comm, be, inp, tr, debug=False, **_):
         src = (r - step) % P  # the shard in hand started on rank src
         reqs = []
         if step < P - 1:
-            import torch.distributed as dist
+            from . import dist_api as dist
             ops = [dist.P2POp(dist.isend, cur, (r + 1) % P), dist.P2POp(dist.irecv, nxt, (r - 1) % P)]
             with tr.phase("ring_post"):
                 reqs = dist.batch_isend_irecv(ops)

@@ -123,7 +123,7 @@ class SharedInput(KNNInput):
 def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedInput:
     """Collective: rank 0 places `inp` in a node-shared segment, every rank maps it.  Single
     node only (all ranks must see the same /dev/shm)."""
-    import torch.distributed as dist
+    from ..parallel import dist_api as dist
     path = None
     s = None
     if comm.is_root:
@@ -131,7 +131,7 @@ def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedIn
         path = s.path
     if comm.world > 1:
         obj = [path]
-        dist.broadcast_object_list(obj, 0, device=comm.device if comm.on_gpu else None)
+        dist.broadcast_object_list(obj, 0, device=comm.device if comm.backend == "nccl" else None)
         path = obj[0]
         if not comm.is_root:
             s = SharedInput.attach(path)

@@ -1,0 +1,91 @@
+"""Multi-rank GPU data plane on ONE MI355X (SURVEY.md §4 level 4).
+
+Several ranks share cuda:0, which RCCL refuses, so the data plane is host-staged: gloo over
+host copies of the device tensors in the Python front end (DMLP_DATA_PLANE=host,
+parallel/dist_api.py) and blocking MPI point-to-point over host copies in knn_engine
+(KNN_DATA_PLANE=host, engine_core.h).  Everything else is the production multi-rank code on the
+real HIP kernels: partitions, offsets, the x1 / 3-term screens, K4 merge kernels, the binomial
+tree, the ring, the grid's column merge, the dynamic farm.  Output bytes must equal the NumPy
+fp64 oracle's; knn_engine additionally checks that every send has a matching receive of the
+same size (KNN_P2P_CHECK=1, logged per rank and compared on rank 0).
+References: bench_2 @0xc844 (tree reduce), engine.cpp:283-309 (grid merge), bench_4 @0xd80c.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+import distributed_machine_learning_project_amd as dmlp
+from distributed_machine_learning_project_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPIEXEC = "/opt/conda/bin/mpiexec"
+ENGINE = os.path.join(ROOT, "distributed_machine_learning_project_amd", "knn_engine")
+
+
+def _port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def case(tmp_path_factory):
+    """k in 1..40: the single-term x1 class (k <= 32) and the 3-term LDS class in one input."""
+    d = tmp_path_factory.mktemp("mr")
+    txt = dmlp.generate_text(3000, 301, 16, 0, 1000, 1, 40, 5, seed=11)
+    p = d / "mr.in"
+    p.write_text(txt)
+    inp = dmlp.parse_input(txt)
+    _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    return str(p), ref.report_lines(cs).encode()
+
+
+def _python(path, np_, strategy, env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLP_DATA_PLANE="host", OMP_NUM_THREADS="2")
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(np_), "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m",
+           "distributed_machine_learning_project_amd.harness", "--strategy", strategy,
+           "--device", "gpu", "--input", path]
+    r = subprocess.run(cmd, capture_output=True, env=env, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "ring"])
+@pytest.mark.parametrize("np_", [2, 3])
+def test_python_front_end(case, strategy, np_):
+    path, expect = case
+    assert _python(path, np_, strategy) == expect
+
+
+def test_python_dynamic_farm_and_shm_ingress(case):
+    path, expect = case
+    assert _python(path, 3, "farm", {"KNN_SCHEDULE": "dynamic"}) == expect
+    assert _python(path, 2, "farm", {"KNN_INGRESS": "shm"}) == expect
+
+
+def _native(path, np_, strategy, extra=()):
+    if not os.path.exists(ENGINE):
+        pytest.skip("knn_engine not built")
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("no mpiexec")
+    env = dict(os.environ, KNN_DATA_PLANE="host", KNN_P2P_CHECK="1", KNN_POOL_MB="256",
+               KNN_HOST_POOL_MB="64")
+    cmd = [MPIEXEC, "-n", str(np_), ENGINE, "--strategy", strategy, "--input", path, *extra]
+    r = subprocess.run(cmd, capture_output=True, env=env, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"p2p check OK" in r.stderr, r.stderr.decode()[-2000:]
+    return r.stdout
+
+
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d"])
+@pytest.mark.parametrize("np_", [2, 3])
+def test_native_front_end(case, strategy, np_):
+    path, expect = case
+    assert _native(path, np_, strategy) == expect
