@@ -406,3 +406,10 @@ __attribute__((target("avx2"))) static void i32_range_avx2(const int* a, int64_t
 }
 
 extern "C" const char* dmlp_version(void) { return "dmlp 0.1.0 (gfx950)"; }
+
+// Sequentially consistent fetch-and-add on a 64-bit word that several processes map (the
+// node-shared segment's work counter, utils/shm.py): the dynamic farm's chunk claim.
+extern "C" int64_t dmlp_atomic_fetch_add_i64(int64_t* p, int64_t v) {
+  return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
+}
+extern "C" void dmlp_atomic_store_i64(int64_t* p, int64_t v) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }

@@ -103,15 +103,25 @@ inline Input parse(const std::vector<char>& buf) {
 
 class KnnCore {
  public:
-  KnnCore(Runtime& rt, std::string strategy, bool debug, bool exact)
-      : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact) {
+  KnnCore(Runtime& rt, std::string strategy, bool debug, bool exact, bool dynamic = false)
+      : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact), dynamic_(dynamic) {
     lk_.st = rt_.stream;
     lk_.rt = &rt_;
     trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
         strategy_ != "serial" && strategy_ != "grid2d")
       throw std::runtime_error("unknown strategy " + strategy_);
+    if (dynamic_ && (strategy_ != "farm" || debug_))
+      throw std::runtime_error("--schedule dynamic needs --strategy farm (and no --debug)");
+    if (dynamic_) {
+      // the chunk counter: one int64 in an MPI window on rank 0 (collective, untimed)
+      MPI_Win_allocate(rt_.rank == 0 ? sizeof(int64_t) : 0, sizeof(int64_t), MPI_INFO_NULL,
+                       MPI_COMM_WORLD, &ctr_base_, &ctr_win_);
+    }
     if (rt_.gpu) warmup();
+  }
+  ~KnnCore() {
+    if (ctr_win_ != MPI_WIN_NULL) MPI_Win_free(&ctr_win_);
   }
 
   // Engine::KNN — called on every rank; rank 0 holds `in` and receives `out`.
@@ -132,7 +142,7 @@ class KnnCore {
     N_ = meta[0]; Q_ = meta[1]; A_ = (int)meta[2];
     lo_ = (int)meta[3]; hi_ = (int)meta[4]; kmax_ = (int)meta[5];
     if (strategy_ == "serial") return serial(in, out);
-    if (strategy_ == "farm") return farm(in, out);
+    if (strategy_ == "farm") return dynamic_ ? farm_dynamic(in, out) : farm(in, out);
     if (strategy_ == "grid2d") return grid2d(in, out);
     return sharded(in, out, strategy_ == "shard_reduce");
   }
@@ -140,7 +150,10 @@ class KnnCore {
  private:
   Runtime& rt_;
   std::string strategy_;
-  bool debug_, exact_;
+  bool debug_, exact_, dynamic_;
+  MPI_Win ctr_win_ = MPI_WIN_NULL;
+  int64_t* ctr_base_ = nullptr;
+  DevBuf<int64_t> res_;
   LocalKnn lk_;
   int64_t N_ = 0, Q_ = 0;
   int A_ = 0, lo_ = 0, hi_ = 1, kmax_ = 1;
@@ -432,6 +445,97 @@ class KnnCore {
     rt_.sync();
   }
 
+  // ---------------------------------------------------------------- dynamic farm (bench_4)
+  // bench_4's master hands out work per query on request (@0xd80c Recv ANY_SOURCE -> @0xd986
+  // Send).  Here no rank is a master: every rank holds the replicated dataset and all queries
+  // (broadcast over xGMI), claims query chunks with an MPI-3 atomic fetch-and-add on a counter
+  // in rank 0's window (passive target, no progress thread on rank 0 needed), writes each
+  // chunk's (label, checksum) into its own zero-initialised full-length arrays, and one sum
+  // reduce (each element non-zero on exactly one rank) lands every result on rank 0.
+  int64_t claim() {
+    const int64_t one = 1;
+    int64_t got = 0;
+    MPI_Win_lock(MPI_LOCK_SHARED, 0, 0, ctr_win_);
+    MPI_Fetch_and_op(&one, &got, MPI_INT64_T, 0, 0, MPI_SUM, ctr_win_);
+    MPI_Win_unlock(0, ctr_win_);
+    return got;
+  }
+  template <typename T>
+  void reduce_sum_to_root(T* p, int64_t n, MPI_Datatype mt, ncclDataType_t nt) {
+    if (!rt_.host_plane) {
+      NCCLCHK(ncclReduce(p, p, n, nt, ncclSum, 0, rt_.nccl, rt_.stream));
+      return;
+    }
+    std::vector<T> h(n), r(rt_.rank == 0 ? n : 0);
+    HIPCHK(hipMemcpyAsync(h.data(), p, n * sizeof(T), hipMemcpyDeviceToHost, rt_.stream));
+    rt_.sync();
+    MPI_Reduce(h.data(), r.data(), (int)n, mt, MPI_SUM, 0, MPI_COMM_WORLD);
+    if (rt_.rank == 0) {
+      HIPCHK(hipMemcpyAsync(p, r.data(), n * sizeof(T), hipMemcpyHostToDevice, rt_.stream));
+      rt_.sync();
+    }
+  }
+  void farm_dynamic(Input* in, Output* out) {
+    const int P = rt_.world;
+    hipStream_t st = rt_.stream;
+    double* Xd = X_.get(N_ * A_ + 1);
+    int* Ld = lab_.get(N_ + 1);
+    double* Qd = Qx_.get(Q_ * A_ + 1);
+    if (rt_.rank == 0) {
+      HIPCHK(hipMemcpyAsync(Xd, in->X.data(), N_ * A_ * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Qd, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
+      // zero the counter for this call (exclusive epoch on our own window)
+      const int64_t zero = 0;
+      MPI_Win_lock(MPI_LOCK_EXCLUSIVE, 0, 0, ctr_win_);
+      MPI_Put(&zero, 1, MPI_INT64_T, 0, 0, 1, MPI_INT64_T, ctr_win_);
+      MPI_Win_unlock(0, ctr_win_);
+    }
+    trace.mark("h2d");
+    std::vector<int> k(Q_);
+    if (rt_.rank == 0) k = in->k;
+    MPI_Bcast(k.data(), (int)Q_, MPI_INT, 0, MPI_COMM_WORLD);  // also orders the reset first
+    if (P > 1) {
+      bcast(Xd, N_ * A_);
+      bcast(Ld, N_);
+      bcast(Qd, Q_ * A_);
+    }
+    trace.mark("distribute");
+    int* lb = labout_.get(Q_ + 1);
+    uint64_t* cs = cs_.get(Q_ + 1);
+    HIPCHK(hipMemsetAsync(lb, 0, Q_ * sizeof(int), st));
+    HIPCHK(hipMemsetAsync(cs, 0, Q_ * sizeof(uint64_t), st));
+    const char* e = getenv("KNN_CHUNKS_PER_RANK");
+    const int per_rank = std::max(1, e ? std::atoi(e) : 4);
+    const int64_t nchunks = std::max<int64_t>(1, std::min<int64_t>(Q_, (int64_t)P * per_rank));
+    const int64_t csz = (Q_ + nchunks - 1) / nchunks;
+    double* dd = d_.get(std::max<int64_t>(1, csz) * kmax_);
+    int* ii = ids_.get(std::max<int64_t>(1, csz) * kmax_);
+    int64_t done = 0;
+    for (;;) {
+      const int64_t c = claim();
+      if (c >= nchunks) break;
+      const int64_t a = c * csz, b = std::min<int64_t>(Q_, a + csz);
+      if (a >= b) continue;
+      local_knn(Xd, N_, Qd + a * A_, b - a, k.data() + a, dd, ii, Ld, lb + a, cs + a);
+      done += b - a;
+    }
+    chunks_done_ = done;
+    trace.mark("compute");
+    if (P > 1) {
+      reduce_sum_to_root(lb, Q_, MPI_INT, ncclInt32);
+      reduce_sum_to_root(cs, Q_, MPI_UINT64_T, ncclUint64);
+    }
+    trace.mark("reduce");
+    if (rt_.rank == 0) render(out, cs, lb, dd, ii);
+    trace.mark("report");
+    rt_.sync();
+  }
+
+ public:
+  int64_t chunks_done_ = 0;  // queries this rank computed in the last dynamic call
+
+ private:
   // ---------------------------------------------------------------- shard_gather / shard_reduce
   void sharded(Input* in, Output* out, bool tree) {
     const int P = rt_.world;

@@ -2,7 +2,7 @@
 // (common.cpp:81-135) and Engine::KNN (engine.h:10-11) in native C++.
 //
 //   mpirun -np P ./knn_engine [--strategy farm|shard_gather|shard_reduce|grid2d|serial] [--debug]
-//          [--exact] [--input FILE] < input
+//          [--exact] [--schedule static|dynamic] [--input FILE] < input
 //
 // Process model: one MPI rank per GPU (MPI only bootstraps and carries tiny host-side control
 // messages: sizes, per-query k, the RCCL unique id); the data plane is RCCL over xGMI; every
@@ -21,12 +21,14 @@ int main(int argc, char** argv) {
   std::string strategy = getenv("KNN_STRATEGY") ? getenv("KNN_STRATEGY") : "farm";
   bool debug = false, exact = getenv("KNN_EXACT") && std::string(getenv("KNN_EXACT")) == "1";
   const char* input = "-";
+  bool dynamic = getenv("KNN_SCHEDULE") && std::string(getenv("KNN_SCHEDULE")) == "dynamic";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--strategy" && i + 1 < argc) strategy = argv[++i];
     else if (a == "--debug") debug = true;
     else if (a == "--exact") exact = true;
     else if (a == "--input" && i + 1 < argc) input = argv[++i];
+    else if (a == "--schedule" && i + 1 < argc) dynamic = std::string(argv[++i]) == "dynamic";
   }
   Runtime rt;
   int rc = 0;
@@ -41,7 +43,7 @@ int main(int argc, char** argv) {
       in = parse(read_all(input));
     }
     MPI_Barrier(MPI_COMM_WORLD);
-    KnnCore eng(rt, strategy, debug, exact);
+    KnnCore eng(rt, strategy, debug, exact, dynamic);
     Output out;
     auto t0 = std::chrono::steady_clock::now();
     eng.trace.begin();
@@ -76,6 +78,9 @@ int main(int argc, char** argv) {
       const int64_t m = eng.check_p2p();
       if (rt.rank == 0) std::fprintf(stderr, "[knn_engine] p2p check OK: %lld matched messages\n", (long long)m);
     }
+    if (dynamic && getenv("KNN_TRACE") && std::string(getenv("KNN_TRACE")) != "0")
+      std::fprintf(stderr, "[dmlp-trace] rank %d dynamic farm: %lld queries\n", rt.rank,
+                   (long long)eng.chunks_done_);
     const auto phases = eng.trace.finish();
     int64_t bytes = 0;
     MPI_Reduce(&eng.sent_, &bytes, 1, MPI_INT64_T, MPI_SUM, 0, MPI_COMM_WORLD);

@@ -36,10 +36,14 @@ constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch 
 // pipeline dispatches one per PCIe slice) start in about a microsecond instead of a futex wake.
 class Pool {
  public:
-  explicit Pool(int n) {
+  // The worker count is fixed before any worker starts: workers read it (size(),
+  // oversubscribed()) while the constructor is still spawning — reading th_.size() there raced
+  // with the vector's growth (found by the TSan driver, tests/native/host_prep_driver.cpp).
+  explicit Pool(int n) : n_(n > 0 ? n : 0) {
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus_ = std::max(1, (int)CPU_COUNT(&set));
-    for (int t = 0; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+    th_.reserve(n_);
+    for (int t = 0; t < n_; ++t) th_.emplace_back([this, t] { loop(t); });
   }
   ~Pool() {
     {
@@ -50,7 +54,7 @@ class Pool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  int size() const { return (int)th_.size() + 1; }
+  int size() const { return n_ + 1; }
   // f(part, parts) on every worker and the caller; returns when all parts are done
   void run(const std::function<void(int, int)>& f) {
     const int parts = size();
@@ -69,7 +73,7 @@ class Pool {
   }
 
  private:
-  bool oversubscribed() const { return (int)th_.size() + 1 > cpus_; }
+  bool oversubscribed() const { return n_ + 1 > cpus_; }
   void loop(int t) {
     uint64_t seen = 0;  // gen_ starts at 0: a job dispatched before this thread ran is not missed
     for (;;) {
@@ -94,6 +98,7 @@ class Pool {
       pending_.fetch_sub(1, std::memory_order_release);
     }
   }
+  const int n_;
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_;

@@ -91,6 +91,9 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
     N, Q, A, lo, hi, kmax, shared = _meta(comm, inp, with_shared=True)
     if shared and schedule == "static":
         return _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug)
+    if shared and not debug:
+        return _farm_dynamic_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, call_id,
+                                    chunks_per_rank)
     with tr.phase("h2d"):
         X = lab = Qx = kd = None
         if shared:  # dynamic schedule over a node-shared segment: per-rank dataset H2D
@@ -158,6 +161,46 @@ def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, deb
     if not comm.is_root:
         return None
     return out[:, 0].to(torch.int32), out[:, 1].contiguous(), dbg_d, dbg_i
+
+
+def _farm_dynamic_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, call_id, chunks_per_rank):
+    """Dynamic farm over the node-shared segment (bench_4's master/worker hand-out, @0xd80c
+    Recv ANY_SOURCE -> @0xd986 Send, without a master rank or a server round trip): query
+    chunks are claimed with an atomic fetch-and-add on a counter word in the shared mapping,
+    each rank copies its claimed chunk straight from the segment to its GPU and writes the
+    chunk's (label, checksum) rows back into the segment's results region; one barrier, and
+    rank 0 holds every result.  The two counters alternate by call: at the start of call c
+    rank 0 zeroes the one call c - 1 used (every rank finished with it — the call ended with a
+    barrier) while the ranks claim from the other."""
+    import os
+    torch = _torch()
+    slot = call_id & 1
+    if comm.is_root:
+        inp.reset_counter(slot ^ 1)
+    per_rank = int(os.environ.get("KNN_CHUNKS_PER_RANK", chunks_per_rank))
+    nchunks = max(1, min(Q, comm.world * max(1, per_rank)))
+    csz = (Q + nchunks - 1) // nchunks
+    with tr.phase("h2d"):
+        X, lab = be.tensor(inp.X), be.tensor(inp.labels)
+    res = torch.from_numpy(inp.res)  # host view of the shared results rows
+    with tr.phase("compute"):
+        while True:
+            c = inp.claim(slot)
+            if c >= nchunks:
+                break
+            a, b = c * csz, min(Q, (c + 1) * csz)
+            if a >= b:
+                continue
+            kc = inp.k[a:b]
+            d, i, lb, cs = be.knn(X, be.tensor(inp.Qx[a:b]), kc, labels=lab,
+                                  label_range=(lo, hi), kstride=kmax)
+            res[a:b].copy_(torch.stack([lb.to(torch.int64), cs], dim=1))  # D2H into the segment
+    comm.barrier()
+    if not comm.is_root:
+        return None
+    with tr.phase("collect"):
+        out = be.tensor(inp.res)
+    return out[:, 0].to(torch.int32), out[:, 1].contiguous(), None, None
 
 
 def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):

@@ -15,8 +15,10 @@ block on its GPU and copies them over its own PCIe link into the segment's outpu
 byte offset, so rank 0 ends up holding the whole report in host memory without a funnel.
 
 Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — a summary for tools;
-the KNN strategies re-scan the labels and k inside every timed call), then labels i32[N],
-k i32[Q], X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), each section 4096-byte aligned.
+the KNN strategies re-scan the labels and k inside every timed call), two int64 work counters at
+byte 64 (the dynamic farm's chunk claims, alternating per call), then labels i32[N], k i32[Q],
+X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), res i64[2*Q] (the dynamic farm's
+(label, checksum) per query), each section 4096-byte aligned.
 """
 from __future__ import annotations
 
@@ -39,7 +41,7 @@ def _layout(N, Q, A):
     off = {}
     o = _ALIGN
     for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A),
-                         ("out", 48 * Q + 64)):
+                         ("out", 48 * Q + 64), ("res", 16 * Q)):
         off[name] = o
         o += _up(max(nbytes, 1))
     return off, o
@@ -57,6 +59,8 @@ class SharedInput(KNNInput):
         Qx = np.frombuffer(mm, np.float64, Q * A, off["Qx"]).reshape(Q, A)
         super().__init__(labels, X, k, Qx)
         self.out = np.frombuffer(mm, np.uint8, 48 * Q + 64, off["out"])
+        self.res = np.frombuffer(mm, np.int64, 2 * Q, off["res"]).reshape(Q, 2)
+        self.counters = np.frombuffer(mm, np.int64, 2, 64)
         self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
         self._pinned = False
 
@@ -83,6 +87,16 @@ class SharedInput(KNNInput):
         np.frombuffer(self._mm, np.int64, 4, 32)[:] = [
             int(self.labels.min()) if N else 0, int(self.labels.max()) + 1 if N else 1,
             int(self.k.min()) if Q else 0, int(self.k.max()) if Q else 0]
+
+    def claim(self, slot: int) -> int:
+        """Atomically take the next work item from counter `slot` (0 or 1): 0, 1, 2, ... across
+        every process that maps the segment (a fetch-and-add on shared memory, no server)."""
+        from .. import _lib
+        return int(_lib.lib().dmlp_atomic_fetch_add_i64(self.counters.ctypes.data + 8 * slot, 1))
+
+    def reset_counter(self, slot: int):
+        from .. import _lib
+        _lib.lib().dmlp_atomic_store_i64(self.counters.ctypes.data + 8 * slot, 0)
 
     @property
     def summary(self):

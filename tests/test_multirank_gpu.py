@@ -70,6 +70,15 @@ def test_python_dynamic_farm_and_shm_ingress(case):
     assert _python(path, 2, "farm", {"KNN_INGRESS": "shm"}) == expect
 
 
+@pytest.mark.parametrize("np_", [2, 3])
+def test_python_dynamic_farm_shared_counter(case, np_):
+    """Chunks claimed by an atomic fetch-and-add in the node-shared segment (utils/shm.py),
+    results written back into it; 7 chunks per rank so ranks interleave."""
+    path, expect = case
+    env = {"KNN_INGRESS": "shm", "KNN_SCHEDULE": "dynamic", "KNN_CHUNKS_PER_RANK": "7"}
+    assert _python(path, np_, "farm", env) == expect
+
+
 def _native(path, np_, strategy, extra=()):
     if not os.path.exists(ENGINE):
         pytest.skip("knn_engine not built")
@@ -89,3 +98,18 @@ def _native(path, np_, strategy, extra=()):
 def test_native_front_end(case, strategy, np_):
     path, expect = case
     assert _native(path, np_, strategy) == expect
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_native_dynamic_farm(case, np_):
+    """knn_engine --schedule dynamic: chunks claimed by MPI_Fetch_and_op on rank 0's window."""
+    path, expect = case
+    env_save = os.environ.get("KNN_CHUNKS_PER_RANK")
+    os.environ["KNN_CHUNKS_PER_RANK"] = "7"
+    try:
+        assert _native(path, np_, "farm", ("--schedule", "dynamic")) == expect
+    finally:
+        if env_save is None:
+            os.environ.pop("KNN_CHUNKS_PER_RANK")
+        else:
+            os.environ["KNN_CHUNKS_PER_RANK"] = env_save

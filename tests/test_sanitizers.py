@@ -1,4 +1,5 @@
-"""Host-code sanitizers (ASan+UBSan, TSan) over csrc/cpu.cpp via tests/native/host_driver.cpp."""
+"""Host-code sanitizers (ASan+UBSan, TSan) over csrc/cpu.cpp (tests/native/host_driver.cpp) and
+csrc/host_prep.cpp's worker pool + conversions (tests/native/host_prep_driver.cpp)."""
 import os
 import shutil
 import subprocess
@@ -14,3 +15,4 @@ def test_host_sanitizers(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("host driver: OK") == 2
+    assert r.stdout.count("host prep driver: OK") == 3
