@@ -62,7 +62,13 @@ def main(argv=None):
                     help="compare a SHA-256 digest of the WHOLE rank-0 report (every query line) "
                          "with the CPU oracle's (C++ fp64 brute force, outside the timed region)")
     ap.add_argument("--no-busbw", action="store_true")
+    ap.add_argument("--harness", default="python", choices=["python", "native"],
+                    help="native: time the reference-contract binary (knn_engine: parse untimed, "
+                         "'Time taken' = KNN + report + barrier, common.cpp:121-131) at this "
+                         "config AND at BASELINE.md's Q = 1000, one process per run")
     a = ap.parse_args(argv)
+    if a.harness == "native":
+        return _bench_native(a)
 
     import numpy as np
     import torch
@@ -166,6 +172,78 @@ def main(argv=None):
     if a.ingress == "shm":
         inp.close()
     eng.close()
+
+
+def _bench_native(a):
+    """knn_engine through the reference's harness contract: the input text is written once
+    (untimed), then each run is a fresh `mpiexec -n P knn_engine --input F` process that parses
+    (untimed), builds the engine (untimed warm-up) and times KNN + report + barrier; the
+    KNN_METRICS sidecar carries that time with microsecond resolution ("Time taken" on stderr is
+    whole milliseconds).  --steps runs per config (median reported), --warmup runs discarded.
+    Rank 0's stdout is checked byte-for-byte against the Python engine's CPU oracle for Q = 1000."""
+    import json as _json
+    import statistics
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    from distributed_machine_learning_project_amd import build
+    from distributed_machine_learning_project_amd.utils.io import generate, to_text
+
+    exe = build.build_engine()
+    P = max(1, a.gpus)
+    kmin = a.k if a.kmin is None else a.kmin
+    kmax = max(kmin, a.k if a.kmax is None else a.kmax)
+    steps = a.steps if a.steps != 200 else 5  # one process per run: 5 by default
+    res = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for tag, q in (("bench", a.q_per_gpu * P), ("q1000", 1000)):
+            inp = generate(a.n_data, q, a.attrs, 0.0, 1000.0, kmin, kmax, a.labels, seed=42)
+            path = os.path.join(td, f"{tag}.in")
+            with open(path, "w") as f:
+                f.write(to_text(inp))
+            times, out0 = [], None
+            for r in range(a.warmup + steps):
+                met = os.path.join(td, f"{tag}_{r}.json")
+                env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy)
+                cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [
+                    str(exe), "--input", path]
+                if a.schedule == "dynamic":
+                    cmd += ["--schedule", "dynamic"]
+                pr = subprocess.run(cmd, capture_output=True, env=env, timeout=600)
+                if pr.returncode != 0:
+                    raise RuntimeError(pr.stderr.decode()[-2000:])
+                if r >= a.warmup:
+                    with open(met) as f:
+                        times.append(float(_json.load(f)["time_ms"]))
+                out0 = pr.stdout
+            entry = {"Q": q, "time_ms_median": round(statistics.median(times), 3),
+                     "time_ms_min": round(min(times), 3), "runs": len(times)}
+            if tag == "q1000":
+                from distributed_machine_learning_project_amd.ops import knn as K
+                from distributed_machine_learning_project_amd.utils.io import format_report
+                _, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+                _, cs = K.finalize_cpu(i, inp.k, inp.labels)
+                entry["verify_ok"] = bytes(out0) == format_report(cs)
+            res[tag] = entry
+    ms = res["bench"]["time_ms_median"]
+    Q = res["bench"]["Q"]
+    value = Q / (ms / 1e3)
+    line = {
+        "metric": "samples/sec (whole node) on bench_4", "value": round(value, 1),
+        "unit": "queries/s", "n_gpus": P, "steps": steps, "warmup": a.warmup,
+        "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_QPS, 1), "dtype": "fp64",
+        "harness": "native knn_engine (reference contract: Time taken = KNN + report + barrier)",
+        "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",
+        "config": {"model": f"bench_4 exact k-NN classifier N={a.n_data} A={a.attrs} "
+                            f"k={a.k if kmin == kmax else f'{kmin}-{kmax}'} labels={a.labels}",
+                   "global_batch": Q, "seq_len": a.attrs,
+                   "parallelism": f"{a.strategy}{P}", "num_data": a.n_data},
+        "q1000": res["q1000"], "bench_runs": res["bench"],
+    }
+    print(json.dumps(line), flush=True)
 
 
 def _allreduce_busbw(comm, nbytes=256 << 20, iters=10):

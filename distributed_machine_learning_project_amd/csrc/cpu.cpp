@@ -8,6 +8,8 @@
 // separate mulsd/addsd exactly as the reference's SSE2 code does (engine.cpp:12-18).
 #include "dmlp.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
@@ -390,16 +392,27 @@ extern "C" void dmlp_cpu_i32_range(const int* a, int64_t n, int* lo, int* hi) {
 
 __attribute__((target("avx2"))) static void i32_range_avx2(const int* a, int64_t n, int* lo,
                                                            int* hi) {
-  int mn = INT32_MAX, mx = INT32_MIN;
+  // four independent min/max chains of 8 lanes (32 ints per iteration): load-bound
+  __m256i mn0 = _mm256_set1_epi32(INT32_MAX), mn1 = mn0, mn2 = mn0, mn3 = mn0;
+  __m256i mx0 = _mm256_set1_epi32(INT32_MIN), mx1 = mx0, mx2 = mx0, mx3 = mx0;
   int64_t i = 0;
-  int m4[8], x4[8];
-  for (int j = 0; j < 8; ++j) { m4[j] = INT32_MAX; x4[j] = INT32_MIN; }
-  for (; i + 8 <= n; i += 8)
-    for (int j = 0; j < 8; ++j) {
-      m4[j] = a[i + j] < m4[j] ? a[i + j] : m4[j];
-      x4[j] = a[i + j] > x4[j] ? a[i + j] : x4[j];
-    }
-  for (int j = 0; j < 8; ++j) { mn = m4[j] < mn ? m4[j] : mn; mx = x4[j] > mx ? x4[j] : mx; }
+  for (; i + 32 <= n; i += 32) {
+    const __m256i v0 = _mm256_loadu_si256((const __m256i*)(a + i));
+    const __m256i v1 = _mm256_loadu_si256((const __m256i*)(a + i + 8));
+    const __m256i v2 = _mm256_loadu_si256((const __m256i*)(a + i + 16));
+    const __m256i v3 = _mm256_loadu_si256((const __m256i*)(a + i + 24));
+    mn0 = _mm256_min_epi32(mn0, v0); mx0 = _mm256_max_epi32(mx0, v0);
+    mn1 = _mm256_min_epi32(mn1, v1); mx1 = _mm256_max_epi32(mx1, v1);
+    mn2 = _mm256_min_epi32(mn2, v2); mx2 = _mm256_max_epi32(mx2, v2);
+    mn3 = _mm256_min_epi32(mn3, v3); mx3 = _mm256_max_epi32(mx3, v3);
+  }
+  mn0 = _mm256_min_epi32(_mm256_min_epi32(mn0, mn1), _mm256_min_epi32(mn2, mn3));
+  mx0 = _mm256_max_epi32(_mm256_max_epi32(mx0, mx1), _mm256_max_epi32(mx2, mx3));
+  alignas(32) int m8[8], x8[8];
+  _mm256_store_si256((__m256i*)m8, mn0);
+  _mm256_store_si256((__m256i*)x8, mx0);
+  int mn = INT32_MAX, mx = INT32_MIN;
+  for (int j = 0; j < 8; ++j) { mn = m8[j] < mn ? m8[j] : mn; mx = x8[j] > mx ? x8[j] : mx; }
   for (; i < n; ++i) { mn = a[i] < mn ? a[i] : mn; mx = a[i] > mx ? a[i] : mx; }
   *lo = mn;
   *hi = mx;

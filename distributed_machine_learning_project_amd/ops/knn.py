@@ -290,14 +290,23 @@ class _KnnCall:
         self.k_dev = _h2d(self.k_host, dev)
         if out is not None:  # rows of caller-owned result tensors (pipelined chunks)
             self.out_d, self.out_i, self.lab, self.cs = out
-            self.out_d.fill_(float("inf"))
-            self.out_i.fill_(-1)
         else:
-            self.out_d = torch.full((Q, self.ks), float("inf"), dtype=torch.float64, device=dev)
-            self.out_i = torch.full((Q, self.ks), -1, dtype=torch.int32, device=dev)
+            self.out_d = torch.empty((Q, self.ks), dtype=torch.float64, device=dev)
+            self.out_i = torch.empty((Q, self.ks), dtype=torch.int32, device=dev)
             self.lab = torch.empty(Q, dtype=torch.int32, device=dev) if self.want_fin else None
             self.cs = torch.empty(Q, dtype=torch.int64, device=dev) if self.want_fin else None
-        self.status = torch.zeros(Q, dtype=torch.int32, device=dev)
+        self.status = torch.empty(Q, dtype=torch.int32, device=dev)
+        self._filled = False
+
+    def _fill_outputs(self):
+        """(+inf, -1) padding of the result rows and a zero status, issued once, right before the
+        first kernel that writes results — i.e. after the first screen is already queued, so
+        these fills are not on the screen's critical path."""
+        if not self._filled:
+            self.out_d.fill_(float("inf"))
+            self.out_i.fill_(-1)
+            self.status.zero_()
+            self._filled = True
 
     # ------------------------------------------------------------------ launch (async)
     def launch(self):
@@ -409,6 +418,7 @@ class _KnnCall:
                           nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                           _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
                        "screen_x2" if use_x2 else "screen_x1")
+            self._fill_outputs()
             self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
                 cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
@@ -419,6 +429,7 @@ class _KnnCall:
         if ds.hl != 2:
             self._wait_qx()  # the device image is rendered from the fp64 rows
             ds.ensure_full_frags()
+        self._fill_outputs()
         er = eps_rel(A)
         if impl == "stream":
             _lib.check(L.dmlp_screen_stream(KT, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
@@ -453,6 +464,7 @@ class _KnnCall:
                 if t is not None:
                     t.record_stream(cur)
         self._wait_qx()
+        self._fill_outputs()  # no screen ran (exact / fallback-only calls)
         n_ovf = n_esc = 0
         self.cs_modified = False  # set when work after launch() rewrites labels / checksums
         if self.screened:

@@ -65,7 +65,7 @@ for task in "$@"; do
     engine)
       step engine 400 bash tools/engine_check.sh "$OUT/engine" ;;
     sweep)
-      step sweep 900 python3 tools/bench_sweep.py --out "$OUT/sweep.jsonl" ;;
+      step sweep 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep.jsonl" --timeout 170 ;;
     harness)
       step harness 600 python bench.py --harness native ;;
     *)
