@@ -75,6 +75,8 @@ _SIGS = {
     "dmlp_exact_rows": (i32, [vp, i64, i32, vp, vp, i32, vp, i64, vp]),
     "dmlp_fallback_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select_kmax": (i32, []),
+    "dmlp_exact_topk_kmax": (i32, []),
+    "dmlp_exact_topk": (i32, [vp, i64, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp]),
     "dmlp_fallback_select_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select": (i32, [vp, i64, i32, vp, vp, vp, i32, vp, i64, vp, vp, i32, vp]),
     "dmlp_fallback_topk": (i32, [vp, i64, i32, vp, vp, vp, i32, vp, i64, vp, vp, i32, vp]),

@@ -164,6 +164,12 @@ int dmlp_fallback_topk(const double* X, int64_t N, int A, const double* Qx, cons
 // exact distance bits + an LDS bitonic sort of the survivors (rows with larger k are skipped;
 // callers send those to dmlp_fallback_topk).  Workspace: dmlp_fallback_select_bytes(nb, N).
 int dmlp_fallback_select_kmax(void);
+// Fused streaming exact top-k (exact.hip), k <= dmlp_exact_topk_kmax(): no workspace, no
+// distance rows; kmax bounds the k of these queries.
+int dmlp_exact_topk_kmax(void);
+int dmlp_exact_topk(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
+                    const int* qk, int nb, int kmax, double* out_d, int* out_i, int kstride,
+                    void* stream);
 int64_t dmlp_fallback_select_bytes(int nb, int64_t N);
 int dmlp_fallback_select(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
                          const int* qk, int nb, void* ws, int64_t ws_bytes, double* out_d,

@@ -413,12 +413,23 @@ struct LocalKnn {
     }
     if (!f.empty()) {
       std::sort(f.begin(), f.end());
-      // k <= 2048: radix select over exact rows; larger k: rows + segmented sort
-      std::vector<int> small, big;
-      const int ksel = dmlp_fallback_select_kmax();
-      for (int q : f) (kk[q] <= ksel ? small : big).push_back(q);
+      // k <= 64: fused streaming exact kernel (exact.hip); k <= 2048: radix select over exact
+      // rows; larger k: rows + segmented sort
+      std::vector<int> fused, small, big;
+      const int kf = dmlp_exact_topk_kmax(), ksel = dmlp_fallback_select_kmax();
+      int kfmax = 0;
+      for (int q : f) {
+        if (kk[q] <= kf) { fused.push_back(q); kfmax = std::max(kfmax, kk[q]); }
+        else (kk[q] <= ksel ? small : big).push_back(q);
+      }
       int* qi = qidx_f.get(f.size());
       size_t base = 0;
+      if (!fused.empty()) {
+        HIPCHK(hipMemcpyAsync(qi, fused.data(), fused.size() * sizeof(int), hipMemcpyHostToDevice, st));
+        DMLPCHK(dmlp_exact_topk(X, N, A, Qx, qi, kd, (int)fused.size(), kfmax, out_d, out_i,
+                                kstride, st));
+        base += fused.size();
+      }
       for (int pass = 0; pass < 2; ++pass) {
         const std::vector<int>& v = pass == 0 ? small : big;
         if (v.empty()) continue;

@@ -1,0 +1,260 @@
+// exact.hip — fused streaming exact top-k (k <= 64): fp64 distances in the reference's order
+// (engine.cpp:12-18: left to right over the attributes, each subtraction, product and sum
+// separately rounded — no FMA) and the per-query selection in ONE pass, with no Q x N distance
+// rows in HBM (fallback.hip writes every row, then radix-selects it: ~5 HBM passes per row).
+//
+// Workgroup = 256 threads = 64 queries; the data stream is tiled by 128 points.  Thread
+// (tx = tid & 15, ty = tid >> 4) owns the 4 x 8 micro-tile of queries ty + 16 i and points
+// tx + 16 j of the tile (query and point chunks of 16 attributes staged in LDS), so a query's
+// 16 threads all sit in ONE wave: every query's candidate buffer is wave-private and needs no
+// workgroup barrier.  After a tile, its distances are offered in 8 rounds (one point column
+// j per round, <= 16 candidates per query): a distance is appended iff it is <= the query's
+// current threshold T (the k-th best so far; points arrive in increasing id order, so a later
+// point equal to T — larger id — ranks before it under (dist asc, id desc) and must be kept).
+// Before a round, if some buffer of the wave could overflow, the wave compacts: every entry's
+// rank among its query's buffer (key_less, exact order), the best k rewritten in sorted order,
+// T = the k-th.  At the end one compaction sorts every buffer and the first k go out.
+#include "dmlp.h"
+#include "dmlp_device.h"
+#include <math.h>
+
+namespace {
+
+constexpr int QB = 64;   // queries per workgroup
+constexpr int PJ = 8;    // points per thread per tile (micro-tile 4 queries x PJ points)
+constexpr int PT = 16 * PJ;  // points per tile
+constexpr int AC = 16;   // attributes per LDS chunk (small staging: 2 workgroups per CU)
+constexpr int AS = AC + 2;   // LDS row stride in doubles: 16-byte aligned rows (b128 reads)
+
+template <int CB>
+struct ExactCfg {
+  static constexpr int STG = (QB + PT) * AS * 8;             // Qs + Xs chunk staging
+  static constexpr int BUF = QB * CB * (8 + 4) + QB * 4 + QB * 8;  // entries + counts + T
+  static constexpr int LDS = STG + BUF;
+};
+
+// Compact every row of wave `wave` that holds more than its k entries (final: every row, and
+// write the sorted first k out).  Rows of wave w: ty in [4w, 4w + 4) x i -> 16 rows.  Rare
+// (a few times per query), so it is an out-of-line call: inlined at every offer round it
+// would inflate the hot loop's register allocation.
+template <int CB>
+__device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restrict__ bi,
+                                          int* __restrict__ cnt, double* __restrict__ thr,
+                                          const int* __restrict__ qidx,
+                                          const int* __restrict__ qk, int nb, int64_t N, int q0,
+                                          int wave, int lane, bool final_pass,
+                                          double* __restrict__ out_d, int* __restrict__ out_i,
+                                          int kstride) {
+  for (int s = 0; s < 16; ++s) {
+    const int r = (4 * wave + (s & 3)) + 16 * (s >> 2);
+    const int n = cnt[r];
+    const int q = q0 + r;
+    int k = 0;
+    if (q < nb) {
+      k = qk[qidx[q]];
+      if ((int64_t)k > N) k = (int)N;
+    }
+    if (!final_pass && n <= k) continue;
+    double* rd = bd + r * CB;
+    int* ri = bi + r * CB;
+    // ranks of this lane's entries (lane, lane + 64) under (dist asc, id desc)
+    double ed[2];
+    int ei[2], rk[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = lane + 64 * h;
+      rk[h] = 1 << 30;
+      if (e < n) {
+        ed[h] = rd[e];
+        ei[h] = ri[e];
+        int c = 0;
+        for (int j = 0; j < n; ++j) c += dmlp::key_less(rd[j], ri[j], ed[h], ei[h]) ? 1 : 0;
+        rk[h] = c;
+      }
+    }
+    dmlp::wave_sync();  // every lane has read the buffer before any rewrite
+    const int kept = n < k ? n : k;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (rk[h] < kept) {
+        if (final_pass) {
+          out_d[(int64_t)qidx[q] * kstride + rk[h]] = ed[h];
+          out_i[(int64_t)qidx[q] * kstride + rk[h]] = ei[h];
+        } else {
+          rd[rk[h]] = ed[h];
+          ri[rk[h]] = ei[h];
+        }
+      }
+    }
+    dmlp::wave_sync();
+    if (lane == 0) {
+      cnt[r] = kept;
+      thr[r] = (!final_pass && kept == k && k > 0) ? rd[k - 1] : INFINITY;
+    }
+    dmlp::wave_sync();
+  }
+}
+
+template <int CB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_exact_topk(const double* __restrict__ X, int64_t N, int A,
+                                                    const double* __restrict__ Qx,
+                                                    const int* __restrict__ qidx,
+                                                    const int* __restrict__ qk, int nb,
+                                                    double* __restrict__ out_d,
+                                                    int* __restrict__ out_i, int kstride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double (*Qs)[AS] = (double (*)[AS])smem;
+  double (*Xs)[AS] = (double (*)[AS])(smem + QB * AS * 8);
+  double* const bd = (double*)(smem + ExactCfg<CB>::STG);          // [QB][CB]
+  int* const bi = (int*)(bd + QB * CB);                              // [QB][CB]
+  int* const cnt = bi + QB * CB;                                     // [QB]
+  double* const thr = (double*)(cnt + QB);                           // [QB]
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int q0 = blockIdx.x * QB;
+  // this thread's rows: ty + 16 i; per-row k (0 for rows past nb)
+  int kq[4];
+  double tq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = ty + 16 * i;
+    kq[i] = q0 + r < nb ? qk[qidx[q0 + r]] : 0;
+    if ((int64_t)kq[i] > N) kq[i] = (int)N;
+    tq[i] = INFINITY;
+  }
+  if (tid < QB) { cnt[tid] = 0; thr[tid] = INFINITY; }
+  __syncthreads();
+
+  // staging is software-pipelined: the next (tile, chunk)'s elements are loaded into registers
+  // while the current chunk computes, so no wave waits on global memory at the barriers
+  constexpr int NQ = QB * AC / 256, NX = PT * AC / 256;
+  double qr[NQ], xr[NX];
+  auto fetch = [&](int64_t p0, int a0) __attribute__((always_inline)) {
+    const int ac = A - a0 < AC ? A - a0 : AC;
+#pragma unroll
+    for (int u = 0; u < NQ; ++u) {
+      const int e = tid + 256 * u, r = e / AC, a = e % AC;
+      const int qi = q0 + r;
+      qr[u] = (qi < nb && a < ac) ? Qx[(int64_t)qidx[qi] * A + a0 + a] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int e = tid + 256 * u, r = e / AC, a = e % AC;
+      const int64_t pi = p0 + r;
+      xr[u] = (pi < N && a < ac) ? X[pi * A + a0 + a] : 0.0;
+    }
+  };
+  fetch(0, 0);
+  for (int64_t p0 = 0; p0 < N; p0 += PT) {
+    double acc[4][PJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < PJ; ++j) acc[i][j] = 0.0;
+    for (int a0 = 0; a0 < A; a0 += AC) {
+      const int ac = A - a0 < AC ? A - a0 : AC;
+      __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+      for (int u = 0; u < NQ; ++u) Qs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = qr[u];
+#pragma unroll
+      for (int u = 0; u < NX; ++u) Xs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = xr[u];
+      __syncthreads();
+      {
+        int64_t np = p0;
+        int na = a0 + AC;
+        if (na >= A) { na = 0; np = p0 + PT; }
+        if (np < N) fetch(np, na);
+      }
+      // two attributes per step: 16-byte LDS reads; the sums stay in attribute order
+      int a = 0;
+      for (; a + 1 < ac; a += 2) {
+        double2 qv[4], xv[PJ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qv[i] = *(const double2*)&Qs[ty + 16 * i][a];
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) xv[j] = *(const double2*)&Xs[tx + 16 * j][a];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < PJ; ++j) {
+            const double d0 = __dsub_rn(qv[i].x, xv[j].x);
+            acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(d0, d0));
+            const double d1 = __dsub_rn(qv[i].y, xv[j].y);
+            acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(d1, d1));
+          }
+      }
+      if (a < ac) {  // odd attribute count: the last one alone
+        double qv[4], xv[PJ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qv[i] = Qs[ty + 16 * i][a];
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) xv[j] = Xs[tx + 16 * j][a];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < PJ; ++j) {
+            const double d0 = __dsub_rn(qv[i], xv[j]);
+            acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(d0, d0));
+          }
+      }
+    }
+    // offer the tile's distances, one point column per round (<= 16 per query per round)
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      bool full = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) full |= cnt[ty + 16 * i] > CB - 16;
+      if (__ballot(full)) {
+        compact_rows<CB>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, false, out_d, out_i,
+                         kstride);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tq[i] = thr[ty + 16 * i];
+      }
+      const int64_t p = p0 + tx + 16 * j;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (p < N && kq[i] > 0 && acc[i][j] <= tq[i]) {
+          const int r = ty + 16 * i;
+          const int pos = atomicAdd(&cnt[r], 1);
+          bd[r * CB + pos] = acc[i][j];
+          bi[r * CB + pos] = (int)p;
+        }
+      }
+      dmlp::wave_sync();
+    }
+  }
+  compact_rows<CB>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, true, out_d, out_i,
+                   kstride);
+}
+
+template <int CB>
+int launch_exact(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
+                 const int* qk, int nb, double* out_d, int* out_i, int kstride, hipStream_t st) {
+  const int lds = ExactCfg<CB>::LDS;
+  static const bool attr = hipFuncSetAttribute((const void*)&k_exact_topk<CB>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               lds) == hipSuccess;
+  if (!attr) return -5;
+  hipLaunchKernelGGL((k_exact_topk<CB>), dim3((unsigned)((nb + QB - 1) / QB)), dim3(256), lds, st,
+                     X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int dmlp_exact_topk_kmax(void) { return 64; }
+
+// Exact top-k (k <= 64, clamped to N) of queries qidx[0..nb), sorted by (dist asc, id desc) into
+// out_*[q * kstride + j], j < k (slots past min(k, N) untouched).  kmax: an upper bound of the
+// k of these queries (selects the buffer size).  No workspace.
+extern "C" int dmlp_exact_topk(const double* X, int64_t N, int A, const double* Qx,
+                               const int* qidx, const int* qk, int nb, int kmax, double* out_d,
+                               int* out_i, int kstride, void* stream) {
+  if (nb <= 0 || N <= 0) return 0;
+  if (N > 0x7fffffff || A < 1 || kmax > 64) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  if (kmax <= 16) return launch_exact<48>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  if (kmax <= 32) return launch_exact<64>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  return launch_exact<128>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+}

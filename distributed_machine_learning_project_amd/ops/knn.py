@@ -757,6 +757,15 @@ def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d
     dev = Qx.device
     s = _stream()
     kdev = _h2d(np.ascontiguousarray(kk, np.int32), dev)
+    # k <= 64: the fused streaming kernel (exact.hip: no distance rows, no workspace)
+    kf = L.dmlp_exact_topk_kmax() if os.environ.get("DMLP_EXACT_FUSED", "1") != "0" else 0
+    fused = fb[kk[fb] <= kf]
+    if len(fused):
+        qidx = _h2d(fused.astype(np.int32), dev)
+        _lib.check(L.dmlp_exact_topk(_p(ds.X), N, A, _p(Qx), _p(qidx), _p(kdev), len(fused),
+                                     int(kk[fused].max()), _p(out_d), _p(out_i), out_d.shape[1],
+                                     s), "exact_topk")
+    fb = fb[kk[fb] > kf]
     ksel = L.dmlp_fallback_select_kmax()
     small = fb[kk[fb] <= ksel]
     big = fb[kk[fb] > ksel]
