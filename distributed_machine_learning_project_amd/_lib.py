@@ -76,6 +76,7 @@ _SIGS = {
     "dmlp_fallback_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select_kmax": (i32, []),
     "dmlp_exact_topk_kmax": (i32, []),
+    "dmlp_exact_topk_kmax_for": (i32, [i64]),
     "dmlp_exact_topk": (i32, [vp, i64, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp]),
     "dmlp_fallback_select_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select": (i32, [vp, i64, i32, vp, vp, vp, i32, vp, i64, vp, vp, i32, vp]),

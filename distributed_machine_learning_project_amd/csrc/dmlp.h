@@ -167,6 +167,7 @@ int dmlp_fallback_select_kmax(void);
 // Fused streaming exact top-k (exact.hip), k <= dmlp_exact_topk_kmax(): no workspace, no
 // distance rows; kmax bounds the k of these queries.
 int dmlp_exact_topk_kmax(void);
+int dmlp_exact_topk_kmax_for(int64_t N);  // dispatch policy: fused vs rows + select
 int dmlp_exact_topk(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
                     const int* qk, int nb, int kmax, double* out_d, int* out_i, int kstride,
                     void* stream);

@@ -413,10 +413,10 @@ struct LocalKnn {
     }
     if (!f.empty()) {
       std::sort(f.begin(), f.end());
-      // k <= 64: fused streaming exact kernel (exact.hip); k <= 2048: radix select over exact
-      // rows; larger k: rows + segmented sort
+      // k <= dmlp_exact_topk_kmax_for(N) (64, or 256 for large N): fused streaming exact kernel
+      // (exact.hip); k <= 2048: radix select over exact rows; larger k: rows + segmented sort
       std::vector<int> fused, small, big;
-      const int kf = dmlp_exact_topk_kmax(), ksel = dmlp_fallback_select_kmax();
+      const int kf = dmlp_exact_topk_kmax_for(N), ksel = dmlp_fallback_select_kmax();
       int kfmax = 0;
       for (int q : f) {
         if (kk[q] <= kf) { fused.push_back(q); kfmax = std::max(kfmax, kk[q]); }

@@ -1,13 +1,13 @@
-// exact.hip — fused streaming exact top-k (k <= 64): fp64 distances in the reference's order
+// exact.hip — fused streaming exact top-k (k <= 256): fp64 distances in the reference's order
 // (engine.cpp:12-18: left to right over the attributes, each subtraction, product and sum
 // separately rounded — no FMA) and the per-query selection in ONE pass, with no Q x N distance
 // rows in HBM (fallback.hip writes every row, then radix-selects it: ~5 HBM passes per row).
 //
-// Workgroup = 256 threads = 64 queries; the data stream is tiled by 128 points.  Thread
-// (tx = tid & 15, ty = tid >> 4) owns the 4 x 8 micro-tile of queries ty + 16 i and points
-// tx + 16 j of the tile (query and point chunks of 16 attributes staged in LDS), so a query's
+// Workgroup = 256 threads = QB queries (64; 16 for k > 64); the data stream is tiled by 16 PJ
+// points.  Thread (tx = tid & 15, ty = tid >> 4) owns the (QB/16) x PJ micro-tile of queries
+// ty + 16 i and points tx + 16 j of the tile (query and point chunks staged in LDS), so a query's
 // 16 threads all sit in ONE wave: every query's candidate buffer is wave-private and needs no
-// workgroup barrier.  After a tile, its distances are offered in 8 rounds (one point column
+// workgroup barrier.  After a tile, its distances are offered in PJ rounds (one point column
 // j per round, <= 16 candidates per query): a distance is appended iff it is <= the query's
 // current threshold T (the k-th best so far; points arrive in increasing id order, so a later
 // point equal to T — larger id — ranks before it under (dist asc, id desc) and must be kept).
@@ -20,24 +20,29 @@
 
 namespace {
 
-constexpr int QB = 64;   // queries per workgroup
-constexpr int PJ = 8;    // points per thread per tile (micro-tile 4 queries x PJ points)
-constexpr int PT = 16 * PJ;  // points per tile
-constexpr int AC = 16;   // attributes per LDS chunk (small staging: 2 workgroups per CU)
-constexpr int AS = AC + 2;   // LDS row stride in doubles: 16-byte aligned rows (b128 reads)
-
-template <int CB>
-struct ExactCfg {
-  static constexpr int STG = (QB + PT) * AS * 8;             // Qs + Xs chunk staging
-  static constexpr int BUF = QB * CB * (8 + 4) + QB * 4 + QB * 8;  // entries + counts + T
+// QB queries per workgroup (RI = QB / 16 rows per thread), PJ points per thread per tile
+// (tile = 16 PJ points), CB candidate slots per query, AC attributes per LDS chunk.
+template <int QB_, int PJ_, int CB_, int AC_>
+struct Ex {
+  static constexpr int QB = QB_, PJ = PJ_, PT = 16 * PJ_, CB = CB_, AC = AC_;
+  static constexpr int AS = AC + 2;   // LDS row stride in doubles: 16-byte aligned rows (b128)
+  static constexpr int RI = QB / 16;  // rows (queries) per thread
+  static constexpr int EPL = (CB + 63) / 64;  // buffer entries per lane in a compaction
+  static constexpr int NQ = (QB * AC + 255) / 256, NX = (PT * AC + 255) / 256;
+  static constexpr int STG = (QB + PT) * AS * 8;                    // Qs + Xs chunk staging
+  static constexpr int BUF = QB * CB * (8 + 4) + QB * 4 + QB * 8;   // entries + counts + T
   static constexpr int LDS = STG + BUF;
 };
+using ExK16 = Ex<64, 8, 48, 16>;    // k <= 16: 2 workgroups per CU
+using ExK32 = Ex<64, 8, 64, 16>;
+using ExK64 = Ex<64, 8, 128, 16>;
+using ExK256 = Ex<16, 16, 384, 8>;  // k <= 256: 16 queries per workgroup, 384-slot buffers
 
 // Compact every row of wave `wave` that holds more than its k entries (final: every row, and
-// write the sorted first k out).  Rows of wave w: ty in [4w, 4w + 4) x i -> 16 rows.  Rare
+// write the sorted first k out).  Rows of wave w: ty in [4w, 4w + 4) x i -> 4 RI rows.  Rare
 // (a few times per query), so it is an out-of-line call: inlined at every offer round it
 // would inflate the hot loop's register allocation.
-template <int CB>
+template <class C>
 __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restrict__ bi,
                                           int* __restrict__ cnt, double* __restrict__ thr,
                                           const int* __restrict__ qidx,
@@ -45,7 +50,8 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
                                           int wave, int lane, bool final_pass,
                                           double* __restrict__ out_d, int* __restrict__ out_i,
                                           int kstride) {
-  for (int s = 0; s < 16; ++s) {
+  constexpr int CB = C::CB, EPL = C::EPL;
+  for (int s = 0; s < 4 * C::RI; ++s) {
     const int r = (4 * wave + (s & 3)) + 16 * (s >> 2);
     const int n = cnt[r];
     const int q = q0 + r;
@@ -57,11 +63,11 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
     if (!final_pass && n <= k) continue;
     double* rd = bd + r * CB;
     int* ri = bi + r * CB;
-    // ranks of this lane's entries (lane, lane + 64) under (dist asc, id desc)
-    double ed[2];
-    int ei[2], rk[2];
+    // ranks of this lane's entries (lane + 64 h) under (dist asc, id desc)
+    double ed[EPL];
+    int ei[EPL], rk[EPL];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < EPL; ++h) {
       const int e = lane + 64 * h;
       rk[h] = 1 << 30;
       if (e < n) {
@@ -75,7 +81,7 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
     dmlp::wave_sync();  // every lane has read the buffer before any rewrite
     const int kept = n < k ? n : k;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < EPL; ++h) {
       if (rk[h] < kept) {
         if (final_pass) {
           out_d[(int64_t)qidx[q] * kstride + rk[h]] = ed[h];
@@ -95,17 +101,19 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
   }
 }
 
-template <int CB>
+template <class C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_exact_topk(const double* __restrict__ X, int64_t N, int A,
                                                     const double* __restrict__ Qx,
                                                     const int* __restrict__ qidx,
                                                     const int* __restrict__ qk, int nb,
                                                     double* __restrict__ out_d,
                                                     int* __restrict__ out_i, int kstride) {
+  constexpr int QB = C::QB, PJ = C::PJ, PT = C::PT, CB = C::CB, AC = C::AC, AS = C::AS;
+  constexpr int RI = C::RI, NQ = C::NQ, NX = C::NX;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double (*Qs)[AS] = (double (*)[AS])smem;
   double (*Xs)[AS] = (double (*)[AS])(smem + QB * AS * 8);
-  double* const bd = (double*)(smem + ExactCfg<CB>::STG);          // [QB][CB]
+  double* const bd = (double*)(smem + C::STG);                       // [QB][CB]
   int* const bi = (int*)(bd + QB * CB);                              // [QB][CB]
   int* const cnt = bi + QB * CB;                                     // [QB]
   double* const thr = (double*)(cnt + QB);                           // [QB]
@@ -113,10 +121,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int lane = tid & 63, wave = tid >> 6;
   const int q0 = blockIdx.x * QB;
   // this thread's rows: ty + 16 i; per-row k (0 for rows past nb)
-  int kq[4];
-  double tq[4];
+  int kq[RI];
+  double tq[RI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RI; ++i) {
     const int r = ty + 16 * i;
     kq[i] = q0 + r < nb ? qk[qidx[q0 + r]] : 0;
     if ((int64_t)kq[i] > N) kq[i] = (int)N;
@@ -127,7 +135,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   // staging is software-pipelined: the next (tile, chunk)'s elements are loaded into registers
   // while the current chunk computes, so no wave waits on global memory at the barriers
-  constexpr int NQ = QB * AC / 256, NX = PT * AC / 256;
   double qr[NQ], xr[NX];
   auto fetch = [&](int64_t p0, int a0) __attribute__((always_inline)) {
     const int ac = A - a0 < AC ? A - a0 : AC;
@@ -135,29 +142,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int u = 0; u < NQ; ++u) {
       const int e = tid + 256 * u, r = e / AC, a = e % AC;
       const int qi = q0 + r;
-      qr[u] = (qi < nb && a < ac) ? Qx[(int64_t)qidx[qi] * A + a0 + a] : 0.0;
+      qr[u] = (e < QB * AC && qi < nb && a < ac) ? Qx[(int64_t)qidx[qi] * A + a0 + a] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < NX; ++u) {
       const int e = tid + 256 * u, r = e / AC, a = e % AC;
       const int64_t pi = p0 + r;
-      xr[u] = (pi < N && a < ac) ? X[pi * A + a0 + a] : 0.0;
+      xr[u] = (e < PT * AC && pi < N && a < ac) ? X[pi * A + a0 + a] : 0.0;
     }
   };
   fetch(0, 0);
   for (int64_t p0 = 0; p0 < N; p0 += PT) {
-    double acc[4][PJ];
+    double acc[RI][PJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < RI; ++i)
 #pragma unroll
       for (int j = 0; j < PJ; ++j) acc[i][j] = 0.0;
     for (int a0 = 0; a0 < A; a0 += AC) {
       const int ac = A - a0 < AC ? A - a0 : AC;
       __syncthreads();  // the previous chunk's reads are done
 #pragma unroll
-      for (int u = 0; u < NQ; ++u) Qs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = qr[u];
+      for (int u = 0; u < NQ; ++u)
+        if (tid + 256 * u < QB * AC) Qs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = qr[u];
 #pragma unroll
-      for (int u = 0; u < NX; ++u) Xs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = xr[u];
+      for (int u = 0; u < NX; ++u)
+        if (tid + 256 * u < PT * AC) Xs[(tid + 256 * u) / AC][(tid + 256 * u) % AC] = xr[u];
       __syncthreads();
       {
         int64_t np = p0;
@@ -168,13 +177,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       // two attributes per step: 16-byte LDS reads; the sums stay in attribute order
       int a = 0;
       for (; a + 1 < ac; a += 2) {
-        double2 qv[4], xv[PJ];
+        double2 qv[RI], xv[PJ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) qv[i] = *(const double2*)&Qs[ty + 16 * i][a];
+        for (int i = 0; i < RI; ++i) qv[i] = *(const double2*)&Qs[ty + 16 * i][a];
 #pragma unroll
         for (int j = 0; j < PJ; ++j) xv[j] = *(const double2*)&Xs[tx + 16 * j][a];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < RI; ++i)
 #pragma unroll
           for (int j = 0; j < PJ; ++j) {
             const double d0 = __dsub_rn(qv[i].x, xv[j].x);
@@ -184,13 +193,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
           }
       }
       if (a < ac) {  // odd attribute count: the last one alone
-        double qv[4], xv[PJ];
+        double qv[RI], xv[PJ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) qv[i] = Qs[ty + 16 * i][a];
+        for (int i = 0; i < RI; ++i) qv[i] = Qs[ty + 16 * i][a];
 #pragma unroll
         for (int j = 0; j < PJ; ++j) xv[j] = Xs[tx + 16 * j][a];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < RI; ++i)
 #pragma unroll
           for (int j = 0; j < PJ; ++j) {
             const double d0 = __dsub_rn(qv[i], xv[j]);
@@ -203,16 +212,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int j = 0; j < PJ; ++j) {
       bool full = false;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) full |= cnt[ty + 16 * i] > CB - 16;
+      for (int i = 0; i < RI; ++i) full |= cnt[ty + 16 * i] > CB - 16;
       if (__ballot(full)) {
-        compact_rows<CB>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, false, out_d, out_i,
+        compact_rows<C>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, false, out_d, out_i,
                          kstride);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tq[i] = thr[ty + 16 * i];
+        for (int i = 0; i < RI; ++i) tq[i] = thr[ty + 16 * i];
       }
       const int64_t p = p0 + tx + 16 * j;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < RI; ++i) {
         if (p < N && kq[i] > 0 && acc[i][j] <= tq[i]) {
           const int r = ty + 16 * i;
           const int pos = atomicAdd(&cnt[r], 1);
@@ -223,38 +232,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       dmlp::wave_sync();
     }
   }
-  compact_rows<CB>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, true, out_d, out_i,
+  compact_rows<C>(bd, bi, cnt, thr, qidx, qk, nb, N, q0, wave, lane, true, out_d, out_i,
                    kstride);
 }
 
-template <int CB>
+template <class C>
 int launch_exact(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
                  const int* qk, int nb, double* out_d, int* out_i, int kstride, hipStream_t st) {
-  const int lds = ExactCfg<CB>::LDS;
-  static const bool attr = hipFuncSetAttribute((const void*)&k_exact_topk<CB>,
+  const int lds = C::LDS;
+  static const bool attr = hipFuncSetAttribute((const void*)&k_exact_topk<C>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                lds) == hipSuccess;
   if (!attr) return -5;
-  hipLaunchKernelGGL((k_exact_topk<CB>), dim3((unsigned)((nb + QB - 1) / QB)), dim3(256), lds, st,
-                     X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride);
+  hipLaunchKernelGGL((k_exact_topk<C>), dim3((unsigned)((nb + C::QB - 1) / C::QB)), dim3(256),
+                     lds, st, X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride);
   DMLP_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace
 
-extern "C" int dmlp_exact_topk_kmax(void) { return 64; }
+extern "C" int dmlp_exact_topk_kmax(void) { return 256; }
+// The largest k the fused kernel should take for a dataset of N points.  For k in (64, 256] its
+// rank-based compactions of 384-slot buffers cost about as much as the distances when N is
+// small (N = 1e5, k = 200: 93.6 ms vs 23.5 ms for rows + radix select), and win once the
+// rows' HBM traffic grows (N = 1e6: 260 vs 756 ms; N = 1e7: 1.5 s vs > 170 s).
+extern "C" int dmlp_exact_topk_kmax_for(int64_t N) { return N >= (int64_t(1) << 19) ? 256 : 64; }
 
-// Exact top-k (k <= 64, clamped to N) of queries qidx[0..nb), sorted by (dist asc, id desc) into
+// Exact top-k (k <= 256, clamped to N) of queries qidx[0..nb), sorted by (dist asc, id desc) into
 // out_*[q * kstride + j], j < k (slots past min(k, N) untouched).  kmax: an upper bound of the
 // k of these queries (selects the buffer size).  No workspace.
 extern "C" int dmlp_exact_topk(const double* X, int64_t N, int A, const double* Qx,
                                const int* qidx, const int* qk, int nb, int kmax, double* out_d,
                                int* out_i, int kstride, void* stream) {
   if (nb <= 0 || N <= 0) return 0;
-  if (N > 0x7fffffff || A < 1 || kmax > 64) return -1;
+  if (N > 0x7fffffff || A < 1 || kmax > 256) return -1;
   hipStream_t st = (hipStream_t)stream;
-  if (kmax <= 16) return launch_exact<48>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
-  if (kmax <= 32) return launch_exact<64>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
-  return launch_exact<128>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  if (kmax <= 16) return launch_exact<ExK16>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  if (kmax <= 32) return launch_exact<ExK32>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  if (kmax <= 64) return launch_exact<ExK64>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  return launch_exact<ExK256>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
 }

@@ -757,8 +757,11 @@ def _fallback_exact(ds: DeviceDataset, Qx, fb: np.ndarray, kk: np.ndarray, out_d
     dev = Qx.device
     s = _stream()
     kdev = _h2d(np.ascontiguousarray(kk, np.int32), dev)
-    # k <= 64: the fused streaming kernel (exact.hip: no distance rows, no workspace)
-    kf = L.dmlp_exact_topk_kmax() if os.environ.get("DMLP_EXACT_FUSED", "1") != "0" else 0
+    # the fused streaming kernel (exact.hip: no distance rows, no workspace) for k <= 64, and for
+    # k <= 256 once N is large enough that the rows' HBM traffic dominates
+    mode = os.environ.get("DMLP_EXACT_FUSED", "1")  # 0: never, 2: for every k it supports
+    kf = 0 if mode == "0" else (L.dmlp_exact_topk_kmax() if mode == "2"
+                                else L.dmlp_exact_topk_kmax_for(N))
     fused = fb[kk[fb] <= kf]
     if len(fused):
         qidx = _h2d(fused.astype(np.int32), dev)

@@ -138,6 +138,24 @@ def test_exact_mode(torch_cuda):
     assert_same(r, refs)
 
 
+@pytest.mark.parametrize("N,Q,A,kmin,kmax,lo,hi", [
+    (3000, 130, 32, 1, 16, 0, 1000),       # k <= 16 variant, two workgroups' worth of queries
+    (4097, 70, 7, 17, 64, -5, 5),          # k in (16, 64], odd A, ragged last tile
+    (5000, 40, 33, 65, 256, 0, 1000),      # the 16-query, 384-slot variant
+    (700, 33, 3, 200, 256, 0, 2),          # heavy exact ties (3 attrs in {0, 1, 2}); k near N/3
+    (300, 20, 16, 250, 256, 0, 1000),      # k close to N
+])
+def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, monkeypatch):
+    """exact.hip (the --exact path and the fallback for k <= 256) == the CPU path, bit for bit:
+    every variant, ties broken by larger id, per-query k mixed within a workgroup.  Forced for
+    every k (DMLP_EXACT_FUSED=2): at these small N the dispatch would pick rows + select for
+    k > 64."""
+    monkeypatch.setenv("DMLP_EXACT_FUSED", "2")
+    inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 5, seed=N + A)
+    r, refs = run_both(torch_cuda, inp, exact=True)
+    assert_same(r, refs)
+
+
 def test_many_slices_small_q(torch_cuda):
     inp = dmlp.generate(200000, 8, 32, 0.0, 1000.0, 16, 16, 10, seed=8)
     r, refs = run_both(torch_cuda, inp)

@@ -27,10 +27,12 @@ def main():
     ap.add_argument("--ns", default="100000,1000000,10000000")
     ap.add_argument("--attrs", default="32,128")
     ap.add_argument("--ks", default="16,1-64,200")
+    ap.add_argument("--exact", action="store_true", help="bench.py --exact (fp64-only path)")
+    ap.add_argument("--append", action="store_true", help="append to --out")
     a = ap.parse_args()
     rows = []
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
-    with open(a.out, "w") as f:
+    with open(a.out, "a" if a.append else "w") as f:
         for n in (int(x) for x in a.ns.split(",")):
             for attrs in (int(x) for x in a.attrs.split(",")):
                 for ks in a.ks.split(","):
@@ -40,9 +42,9 @@ def main():
                     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--n-data", str(n),
                            "--attrs", str(attrs), "--k", str(kmin), "--kmin", str(kmin),
                            "--kmax", str(kmax), "--q-per-gpu", str(a.q), "--steps", str(steps),
-                           "--warmup", str(warm), "--no-busbw"]
+                           "--warmup", str(warm), "--no-busbw"] + (["--exact"] if a.exact else [])
                     t0 = time.time()
-                    rec = {"sweep": {"N": n, "A": attrs, "k": ks}}
+                    rec = {"sweep": {"N": n, "A": attrs, "k": ks, "exact": a.exact}}
                     try:
                         r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout,
                                            cwd=ROOT)

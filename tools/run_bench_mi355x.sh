@@ -1,7 +1,8 @@
 #!/bin/bash
 # MI355X counterpart of the reference's run_bench.sh: CONFIG 1-4 run the matching strategy on
 # 1/2/4/8 GPUs of one node (one MPI rank per GPU), CONFIG debug runs the serial KD-tree on the
-# CPU; every run is checked byte-for-byte against the serial oracle and the "Time taken" lines
+# CPU; every run (debug: the GPU farm's DEBUG listing) is checked byte-for-byte against the serial
+# oracle (a mismatch fails the script) and the "Time taken" lines
 # are compared like run_bench.sh:29-72.  Inputs are generated (the reference's inputs.zip is
 # absent) and cached under inputs/.
 #
@@ -27,34 +28,39 @@ gen() {  # name N Q A kmin kmax
 gen input1 100000 20000 32 1 32
 gen input2 200000 40000 32 1 64
 gen input3 100000 100000 32 16 16
-run() {  # config strategy gpus input
-  local cfg=$1 strat=$2 np=$3 in=inputs/$4.in
-  if [[ ! -f outputs/ref_$4.out ]]; then
-    timeout 3000 distributed_machine_learning_project_amd/knn_engine --strategy serial < $in \
-        > outputs/ref_$4.out 2> outputs/ref_$4.err
+run() {  # config strategy gpus input [--debug]
+  local cfg=$1 strat=$2 np=$3 in=inputs/$4.in dbg=${5:-}
+  local ref=outputs/ref_$4${dbg:+_debug}
+  if [[ ! -f $ref.out ]]; then
+    timeout 3000 distributed_machine_learning_project_amd/knn_engine --strategy serial $dbg < $in \
+        > $ref.out 2> $ref.err
   fi
+  local launch=(/opt/conda/bin/mpiexec -n $np)
+  [[ $np -eq 1 ]] && launch=()
   if [[ "$IMPL" == "native" ]]; then
-    timeout 300 /opt/conda/bin/mpiexec -n $np distributed_machine_learning_project_amd/knn_engine \
-        --strategy $strat < $in > outputs/tmp_$cfg.out 2> outputs/tmp_$cfg.err
+    timeout 300 "${launch[@]}" distributed_machine_learning_project_amd/knn_engine \
+        --strategy $strat $dbg < $in > outputs/tmp_$cfg.out 2> outputs/tmp_$cfg.err
   else
     timeout 300 python3 -m torch.distributed.run --nnodes 1 --nproc-per-node $np \
         --master-addr 127.0.0.1 --master-port $((29500 + np)) \
-        -m distributed_machine_learning_project_amd.harness --strategy $strat --input $in \
+        -m distributed_machine_learning_project_amd.harness --strategy $strat --input $in $dbg \
         > outputs/tmp_$cfg.out 2> outputs/tmp_$cfg.err
   fi
   local ref_t eng_t
-  ref_t=$(grep -oP 'Time taken:\s*\K[0-9]+' outputs/ref_$4.err)
+  ref_t=$(grep -oP 'Time taken:\s*\K[0-9]+' $ref.err)
   eng_t=$(grep -oP 'Time taken:\s*\K[0-9]+' outputs/tmp_$cfg.err)
   echo "=== CONFIG $cfg: $strat on $np GPU(s), $4 ==="
   echo "Serial KD-tree time: ${ref_t} ms"
   echo "Engine time:         ${eng_t} ms"
-  if cmp -s outputs/ref_$4.out outputs/tmp_$cfg.out; then echo "Output: identical"; else echo "Output: MISMATCH"; fi
+  if cmp -s $ref.out outputs/tmp_$cfg.out; then echo "Output: identical"; else echo "Output: MISMATCH"; return 1; fi
 }
 case "$CONFIG" in
   1) run 1 shard_gather 1 input1 ;;
   2) run 2 shard_reduce 2 input2 ;;
   3) run 3 shard_reduce 4 input2 ;;
   4) run 4 farm 8 input3 ;;
-  debug) timeout 3000 distributed_machine_learning_project_amd/knn_engine --strategy serial --debug < inputs/input1.in | head -20 ;;
+  # DEBUG listing (common.cpp:72-78): the GPU farm's listing byte-compared with the serial
+  # KD-tree's (bench.debug), like the other configs
+  debug) run debug farm 1 input1 --debug ;;
   all) for c in 1 2 3 4; do "$0" $c "$IMPL"; done ;;
 esac
