@@ -29,7 +29,8 @@
 
 namespace {
 
-// profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 8 event counters (g_x1_dbg)
+// profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
+// wrong results, timing only), 8 event counters (g_x1_dbg)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
 
@@ -45,7 +46,10 @@ struct X1Cfg {
   static constexpr int CAPE = 4 * (SUB - CHECK);  // group entries a column may keep
   static constexpr int IDCAP = 4 * (SUB - 1);  // group-id stride per (query, slice), any CHECK
   static constexpr int SBUF = NCOL * CP * 4;
-  static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4;
+  // + a 512-byte ring of two 4-step windows of the rows' -|x'|^2/2 (the MFMA C operand): the
+  // ring loads read it with ds_read_b128 instead of a 16-byte-per-lane buffer load per step
+  static constexpr int XRING = 512;
+  static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4 + XRING;
   static constexpr int D = DEPTH;               // register-ring depth (steps in flight)
 };
 
@@ -282,12 +286,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
       A[R][kt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(              \
           xr, lane * 16 + kt * ks, (J) * (KT * ks), 0));                                        \
-    Xi[R] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ir, kg * 16, (J) * 64, 0)); \
+    if (!(MODE & 4))                                                                            \
+      Xi[R] = *(__attribute__((address_space(3))) const f32x4*)(size_t)(                        \
+          xrb + (((J) >> 2) & 1) * 256 + ((J) & 3) * 64 + kg * 16);                             \
   } while (0)
 #define DMLP_MFMA(R, AB)                                                                        \
   do {                                                                                          \
     _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
-      acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][0], bh[ct][0], Xi[R], 0, 0, 0); \
+      acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][0], bh[ct][0],                 \
+                                                            (MODE & 4) ? f32x4{0, 0, 0, 0} : Xi[R], 0, 0, 0); \
       _Pragma("unroll") for (int kt = 1; kt < KT; ++kt)                                         \
         acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][kt], bh[ct][kt], acc[AB][ct], 0, 0, 0); \
     }                                                                                           \
@@ -334,7 +341,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   } while (0)
 
   unsigned long long trig = 0;  // wave-uniform: some lane's sub-buffer passed its limit
+  // The C-operand ring: window w (steps 4w .. 4w + 3, 64 floats) sits in LDS slot w & 1; lane L
+  // moves float L of a window (one dword per lane, 4 steps ahead of its first read).  16 lanes
+  // read each 16-byte row group (an LDS broadcast), so the per-step norm traffic leaves the
+  // texture path — which the fragment loads keep busy (profiles/r2b_screen_x1_ta_pmc.txt).
+  static_assert(D == 4, "the C-operand ring assumes a 4-deep fragment ring");
+  const unsigned xrb = C::LDS - C::XRING;  // LDS byte offset of the ring
+  float xw = 0.0f;                          // the next window's float of this lane
+  auto xwin = [&](int w) __attribute__((always_inline)) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ir, lane * 4, w * 256, 0));
+  };
   if (nsteps > 0) {
+    if (!(MODE & 4)) {
+      *(__attribute__((address_space(3))) float*)(size_t)(xrb + lane * 4) = xwin(0);
+      xw = xwin(1);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the ring reads stay after it
+    }
     // prologue in the loop's issue order (A, Xi per step), so the waitcnt at the loop head is
     // the steady-state vmcnt(2 * (D - 1)), not a merge with a reordered prologue
 #pragma unroll
@@ -347,6 +369,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       for (int r = 0; r < D; ++r) {
         const int j = j0 + r;  // D = 4: j < nsteps (nsteps % 4 == 0); D = 8: guarded epilogue
         DMLP_MFMA(r, r & 1);
+        if (r == 0 && !(MODE & 4)) {
+          // window j0/4 + 1 (steps j0 + 4 .. j0 + 7) into the slot window j0/4 - 1 used (every
+          // read of it is done: those steps were loaded into the register ring already)
+          *(__attribute__((address_space(3))) float*)(size_t)(
+              xrb + (((j0 >> 2) + 1) & 1) * 256 + lane * 4) = xw;
+          xw = xwin((j0 >> 2) + 2);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
         DMLP_LOAD(j + D, r);
         if (MODE & 2) {  // ablation: keep every MFMA result alive, no epilogue at all
           _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[r & 1][ct]));
@@ -400,6 +430,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
   switch (g_x1_mode) {
     case 1: DMLP_X1_LAUNCH(1); break;
     case 2: DMLP_X1_LAUNCH(2); break;
+    case 4: DMLP_X1_LAUNCH(4); break;
+    case 6: DMLP_X1_LAUNCH(6); break;
     case 8: DMLP_X1_LAUNCH(8); break;
     default: DMLP_X1_LAUNCH(0); break;
   }
