@@ -54,8 +54,7 @@ _SIGS = {
     "dmlp_screen_x1_bound": (None, [i32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "dmlp_screen_x1": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
-    "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp,
-                                 i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp]),
+    "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
     "dmlp_screen_x2_kmax": (i32, []),
     "dmlp_screen_x2_qw": (i32, [i32]),
@@ -70,8 +69,7 @@ _SIGS = {
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
                           vp, vp]),
-    "dmlp_refine": (i32, [i32, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, i32, i32,
-                          vp, vp, vp, vp]),
+    "dmlp_refine": (i32, [i32, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_exact_rows": (i32, [vp, i64, i32, vp, vp, i32, vp, i64, vp]),
     "dmlp_fallback_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select_kmax": (i32, []),

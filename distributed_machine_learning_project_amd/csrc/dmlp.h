@@ -132,12 +132,13 @@ void dmlp_set_stream_sub(int sub);
 // ---------------------------------------------------------------- device: exact refine (K2 exact + K3 + K6)
 // Exact fp64 distances of the candidates, exact top-k under (dist asc, id desc).
 // Writes out_d/out_i[q*kstride + i], i < k_q (rest untouched).  status[q] = 1 if the query
-// overflowed and must take the exact fallback path, else 0.  If labels != NULL the vote and
+// overflowed and must take the exact fallback path, else 0 (and *ovf_count, if given, grows by
+// one per overflowed query: a running total).  Slots [k_q, kstride) get (+inf, -1).  If labels != NULL the vote and
 // checksum are fused (out_label[q], out_cs[q]); label_lo/label_hi give the label range.
 int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const double* X,
                 int A, const double* Qx, const int* qidx, const int* qk, int nq, double* out_d,
                 int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
-                int* out_label, uint64_t* out_cs, int* status, void* stream);
+                int* out_label, uint64_t* out_cs, int* status, int* ovf_count, void* stream);
 // Same for the single-term screen's group output: members of each group whose single-term score
 // (recomputed from xfrag / xinit / qhi, KT <= 2) reaches the (query, slice) threshold cand_h get
 // exact distances.  status = 1 also when the survivors exceed 256 (pathological ties).
@@ -146,7 +147,7 @@ int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const 
                        const float* xinit, const void* qhi, int KT, int hl, int64_t n_points,
                        const int* qidx, const int* qk, int nq, double* out_d, int* out_i,
                        int kstride, const int* labels, int label_lo, int label_hi,
-                       int* out_label, uint64_t* out_cs, int* status, void* stream);
+                       int* out_label, uint64_t* out_cs, int* status, int* ovf_count, void* stream);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

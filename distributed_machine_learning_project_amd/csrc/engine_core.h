@@ -509,10 +509,9 @@ class KnnCore {
     int* lb = labout_.get(Q_);
     uint64_t* cs = cs_.get(Q_);
     int* stat = f_st_.get(Q_);
-    HIPCHK(hipMemsetAsync(ii, 0xff, (size_t)Q_ * kmax_ * sizeof(int), st));
-    DMLPCHK(dmlp_fill_f64(dd, Q_ * kmax_, INFINITY, st));
+    // (the refine writes every row's padding and status itself: no fill passes)
     DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, qi, kd,
-                               (int)Q_, dd, ii, kmax_, Ld, lo_, hi_, lb, cs, stat, st));
+                               (int)Q_, dd, ii, kmax_, Ld, lo_, hi_, lb, cs, stat, nullptr, st));
     trace.mark("refine");
     std::vector<int> sh(Q_);
     HIPCHK(hipMemcpyAsync(sh.data(), stat, Q_ * 4, hipMemcpyDeviceToHost, st));

@@ -378,7 +378,7 @@ struct LocalKnn {
                                  words.p, words.p + 1, S, ci, cc, ch, st));
           DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, 2, N,
                                      qi, kd, nq, out_d, out_i, kstride, fin ? labels : nullptr,
-                                     lab_lo, lab_hi, lab, cs, stat, st));
+                                     lab_lo, lab_hi, lab, cs, stat, nullptr, st));
           return;
         }
         if (impl == 1)
@@ -388,7 +388,7 @@ struct LocalKnn {
           DMLPCHK(dmlp_screen(KT, cap, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,
                               words.p, words.p + 1, er, S, ci, cc, st));
         DMLPCHK(dmlp_refine(cap, ci, cc, S, X, A, Qx, qi, kd, nq, out_d, out_i, kstride,
-                            fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, st));
+                            fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, nullptr, st));
       };
       const int first_a = x1 ? 0 : (qw > 0 ? 1 : 2);
       if (!a.empty()) pass(a, first_a, qidx_a);

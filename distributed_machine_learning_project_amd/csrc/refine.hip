@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
     int* __restrict__ out_i, int kstride, const int* __restrict__ labels, int label_lo,
     int label_hi, int* __restrict__ out_label, uint64_t* __restrict__ out_cs,
-    int* __restrict__ status, const GroupIn gin) {
+    int* __restrict__ status, int* __restrict__ ovf_count, const GroupIn gin) {
   constexpr int P = E * 64;
   constexpr int SMAX = 256;
   constexpr int KMAX = GROUPS ? 64 : 128;
@@ -160,8 +160,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
     }
   }
   ovf = __shfl(ovf ? 1 : 0, 0) != 0;
+  // the (+inf, -1) padding of slots [k, kstride) is written here, so callers need no fill pass
+  // (slots [0, k) of a query handed back below are written by its escalation / exact path)
+  for (int i = k + lane; i < kstride; i += 64) {
+    out_d[(int64_t)q * kstride + i] = INFINITY;
+    out_i[(int64_t)q * kstride + i] = -1;
+  }
   if (ovf) {
-    if (lane == 0) status[q] = 1;
+    if (lane == 0) {
+      status[q] = 1;
+      if (ovf_count) atomicAdd(ovf_count, 1);  // running total: the host reads 4 bytes
+    }
     return;
   }
   if (lane == 0) status[q] = 0;
@@ -269,7 +278,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
     }
     if (nm > P) {
       // pathological ties: hand the query back (x1 overflow -> 3-term screen escalation)
-      if (lane == 0) status[q] = 1;
+      if (lane == 0) {
+        status[q] = 1;
+        if (ovf_count) atomicAdd(ovf_count, 1);
+      }
       return;
     }
     M = nm;
@@ -728,7 +740,7 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
                            const double* X, int A, const double* Qx, const int* qidx,
                            const int* qk, int nq, double* out_d, int* out_i, int kstride,
                            const int* labels, int label_lo, int label_hi, int* out_label,
-                           uint64_t* out_cs, int* status, void* stream) {
+                           uint64_t* out_cs, int* status, int* ovf_count, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256) return -1;
   const dim3 grid((nq + 3) / 4), block(256);
@@ -738,7 +750,7 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   if (cap < 1) return -2;
   hipLaunchKernelGGL((k_refine<4, 0>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
                      Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
-                     out_label, out_cs, status, GroupIn{});
+                     out_label, out_cs, status, ovf_count, GroupIn{});
   DMLP_LAUNCH_CHECK();
   return 0;
 }
@@ -749,7 +761,7 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
                                   const void* qhi, int KT, int hl, int64_t n_points, const int* qidx,
                                   const int* qk, int nq, double* out_d, int* out_i, int kstride,
                                   const int* labels, int label_lo, int label_hi, int* out_label,
-                                  uint64_t* out_cs, int* status, void* stream) {
+                                  uint64_t* out_cs, int* status, int* ovf_count, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256 || cap < 1 || KT < 1 || KT > 2 || n_points > 0x7fffffff) return -1;
   if (hl != 1 && hl != 2) return -1;
@@ -759,7 +771,7 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
 #define DMLP_REFINE_G(KTV)                                                                     \
   hipLaunchKernelGGL((k_refine<2, KTV>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
-                     labels, label_lo, label_hi, out_label, out_cs, status, gin)
+                     labels, label_lo, label_hi, out_label, out_cs, status, ovf_count, gin)
   if (KT == 1) DMLP_REFINE_G(1);
   else DMLP_REFINE_G(2);
 #undef DMLP_REFINE_G

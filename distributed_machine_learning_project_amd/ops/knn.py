@@ -297,6 +297,8 @@ class _KnnCall:
             self.cs = torch.empty(Q, dtype=torch.int64, device=dev) if self.want_fin else None
         self.status = torch.empty(Q, dtype=torch.int32, device=dev)
         self._filled = False
+        self._ovf = _ovf_counters(dev)
+        self._ovf_slot = self._ovf.slot()
 
     def _fill_outputs(self):
         """(+inf, -1) padding of the result rows and a zero status, issued once, right before the
@@ -409,7 +411,7 @@ class _KnnCall:
         cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
         cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
         fin = (_p(ds.labels) if self.want_fin else None, ds.label_lo, ds.label_hi, _p(self.lab),
-               _p(self.cs), _p(self.status), s)
+               _p(self.cs), _p(self.status), self._ovf.ptr(self._ovf_slot), s)
         if impl == "x1":
             cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
             fn = L.dmlp_screen_x2 if use_x2 else L.dmlp_screen_x1
@@ -418,6 +420,10 @@ class _KnnCall:
                           nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                           _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
                        "screen_x2" if use_x2 else "screen_x1")
+            if idx is None:
+                # every query goes through this refine: it writes each row's (+inf, -1) padding
+                # and each status itself, so no fill pass at all
+                self._filled = True
             self._fill_outputs()
             self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
@@ -468,7 +474,9 @@ class _KnnCall:
         n_ovf = n_esc = 0
         self.cs_modified = False  # set when work after launch() rewrites labels / checksums
         if self.screened:
-            n_ovf = int(self.status.sum().item())
+            # the refine kernels count overflowed queries into this call's counter slot: one
+            # 4-byte read (and the call's one host sync) instead of a reduce over the status
+            n_ovf = self._ovf.read(self._ovf_slot, self.stream)
             if n_ovf and self.first_a == "x1":
                 st = self.status.cpu().numpy()
                 esc = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
@@ -476,7 +484,7 @@ class _KnnCall:
                 if n_esc:
                     self.cs_modified = True
                     self._screen_pass(esc, "stream" if self.stream_ok else "lds")
-                    n_ovf = int(self.status.sum().item())
+                    n_ovf = self._ovf.read(self._ovf_slot, self.stream)
         fb = (np.empty(0, np.int64) if self.all_a
               else np.nonzero(~self.on_screen & (kk >= 1))[0])
         if n_ovf:
@@ -497,6 +505,50 @@ class _KnnCall:
                                            _stream()), "finalize")
         return DeviceResult(self.out_d, self.out_i, self.lab, self.cs, self.k_host,
                             int(len(fb)), int(n_esc))
+
+
+class _OvfCounters:
+    """Per-device running counters of overflowed queries (refine.hip atomically adds one per
+    handed-back query).  Each call owns a slot (round robin over 256, far more than the calls
+    ever in flight); the host keeps the value it last read per slot, so nothing is zeroed."""
+
+    SLOTS = 256
+
+    def __init__(self, dev):
+        torch = _torch()
+        self.dev_t = torch.zeros(self.SLOTS, dtype=torch.int32, device=dev)
+        self.host = torch.zeros(self.SLOTS, dtype=torch.int32).pin_memory()
+        self.seen = [0] * self.SLOTS
+        self.next = 0
+
+    def slot(self):
+        i = self.next
+        self.next = (i + 1) % self.SLOTS
+        return i
+
+    def ptr(self, i):
+        return self.dev_t.data_ptr() + 4 * i
+
+    def read(self, i, stream):
+        """Overflows counted in slot i since the last read (synchronizes `stream`)."""
+        torch = _torch()
+        with torch.cuda.stream(stream):
+            self.host[i:i + 1].copy_(self.dev_t[i:i + 1], non_blocking=True)
+        stream.synchronize()
+        v = int(self.host[i])
+        d, self.seen[i] = v - self.seen[i], v
+        return d
+
+
+_OVF = {}
+
+
+def _ovf_counters(dev):
+    key = str(dev)
+    c = _OVF.get(key)
+    if c is None:
+        c = _OVF[key] = _OvfCounters(dev)
+    return c
 
 
 class _PinnedArena:
