@@ -107,7 +107,8 @@ def build_engine(force: bool = False) -> Path | None:
     for s in srcs:  # host-only C++ against the HIP runtime / RCCL / MPI headers
         o = BUILD / (s.name + ".o")
         _run(["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
-              f"-I{CSRC}", f"-I{MPI_HOME}/include", f"-I{ROCM}/include", "-c", str(s), "-o", str(o)])
+              "-Werror=return-type", f"-I{CSRC}", f"-I{MPI_HOME}/include", f"-I{ROCM}/include",
+              "-c", str(s), "-o", str(o)])
         objs.append(str(o))
     # MPICH lives in the conda prefix next to an old libstdc++: never put that directory on the
     # link/run path (ROCm needs the system libstdc++).  Link libmpi by its own path through a

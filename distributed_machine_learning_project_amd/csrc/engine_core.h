@@ -110,7 +110,7 @@ class KnnCore {
     total_h_.resize(1);
     trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
-        strategy_ != "serial" && strategy_ != "grid2d")
+        strategy_ != "serial" && strategy_ != "grid2d" && strategy_ != "ring")
       throw std::runtime_error("unknown strategy " + strategy_);
     if (dynamic_ && (strategy_ != "farm" || debug_))
       throw std::runtime_error("--schedule dynamic needs --strategy farm (and no --debug)");
@@ -125,6 +125,9 @@ class KnnCore {
     if (ctr_win_ != MPI_WIN_NULL) MPI_Win_free(&ctr_win_);
     if (ev_rows_) (void)hipEventDestroy(ev_rows_);
     if (wake_st_) (void)hipStreamDestroy(wake_st_);
+    if (ring_ev_) (void)hipEventDestroy(ring_ev_);
+    if (ring_done_) (void)hipEventDestroy(ring_done_);
+    if (ring_st_) (void)hipStreamDestroy(ring_st_);
     if (side_) (void)hipStreamDestroy(side_);
   }
 
@@ -166,6 +169,7 @@ class KnnCore {
     if (strategy_ == "serial") return serial(in, out);
     if (strategy_ == "farm") return dynamic_ ? farm_dynamic(in, out) : farm(in, out);
     if (strategy_ == "grid2d") return grid2d(in, out);
+    if (strategy_ == "ring") return ring(in, out);
     return sharded(in, out, strategy_ == "shard_reduce");
   }
 
@@ -201,37 +205,56 @@ class KnnCore {
   // strategies' offsets, trees and merge kernels run unchanged on the real kernels.  Every
   // point-to-point transfer is also logged (peer, bytes) for the KNN_P2P_CHECK matching check.
   void grp_start() {
-    if (!rt_.host_plane) grp_start();
+    if (!rt_.host_plane) NCCLCHK(ncclGroupStart());
   }
   void grp_end() {
-    if (!rt_.host_plane) grp_end();
+    if (!rt_.host_plane) NCCLCHK(ncclGroupEnd());
   }
+  // (st: the stream the transfer is ordered on; default the engine stream)
   template <typename T>
-  void snd(const T* p, int64_t n, int peer) {
+  void snd(const T* p, int64_t n, int peer, hipStream_t st = nullptr) {
+    if (!st) st = rt_.stream;
     const int64_t bytes = n * (int64_t)sizeof(T);
     p2p_log_.push_back({1, peer, bytes});
     sent_ += bytes;
     if (!rt_.host_plane) {
-      NCCLCHK(ncclSend(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+      NCCLCHK(ncclSend(p, n, nty<T>(), peer, rt_.nccl, st));
       return;
     }
     std::vector<char> h(bytes);
-    HIPCHK(hipMemcpyAsync(h.data(), p, bytes, hipMemcpyDeviceToHost, rt_.stream));
-    rt_.sync();
+    HIPCHK(hipMemcpyAsync(h.data(), p, bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     mpi_bytes(h.data(), bytes, peer, true);
   }
   template <typename T>
-  void rcv(T* p, int64_t n, int peer) {
+  void rcv(T* p, int64_t n, int peer, hipStream_t st = nullptr) {
+    if (!st) st = rt_.stream;
     const int64_t bytes = n * (int64_t)sizeof(T);
     p2p_log_.push_back({0, peer, bytes});
     if (!rt_.host_plane) {
-      NCCLCHK(ncclRecv(p, n, nty<T>(), peer, rt_.nccl, rt_.stream));
+      NCCLCHK(ncclRecv(p, n, nty<T>(), peer, rt_.nccl, st));
       return;
     }
     std::vector<char> h(bytes);
     mpi_bytes(h.data(), bytes, peer, false);
-    HIPCHK(hipMemcpyAsync(p, h.data(), bytes, hipMemcpyHostToDevice, rt_.stream));
-    rt_.sync();  // h dies here
+    HIPCHK(hipMemcpyAsync(p, h.data(), bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // h dies here
+  }
+  // One ring exchange: send `cur` to the next rank, receive the previous rank's into `nxt`.  In
+  // host-staged mode the blocking MPI pair is ordered by rank parity so it cannot deadlock.
+  template <typename T>
+  void ring_exchange(const T* cur, T* nxt, int64_t n, hipStream_t st) {
+    const int P = rt_.world, r = rt_.rank;
+    const int to = (r + 1) % P, from = (r + P - 1) % P;
+    if (!rt_.host_plane) {
+      grp_start();
+      snd(cur, n, to, st);
+      rcv(nxt, n, from, st);
+      grp_end();
+      return;
+    }
+    if (r % 2 == 0) { snd(cur, n, to, st); rcv(nxt, n, from, st); }
+    else { rcv(nxt, n, from, st); snd(cur, n, to, st); }
   }
   template <typename T>
   void bcast(T* p, int64_t n) {
@@ -315,6 +338,10 @@ class KnnCore {
  private:
 
   void warmup() {
+    // the RCCL group wrappers run here once, on every run: an empty ncclGroupStart/End pair is
+    // valid at any world size, so a single-GPU test exercises the code the multi-GPU path uses
+    grp_start();
+    grp_end();
     (void)dmlp_host_threads();  // the host conversion pool's threads start here, untimed
     wake_d2h();                 // creates its stream and runs its first copy, untimed
     if (wake_st_) HIPCHK(hipStreamSynchronize(wake_st_));
@@ -884,6 +911,140 @@ class KnnCore {
       if (root) render(out, cs, lb, dd, ii);
       trace.mark("report");
     }
+    rt_.sync();
+  }
+
+  // ---------------------------------------------------------------- ring
+  // The long-context analog (parallel/strategies.py ring): the dataset is sharded N/P per GPU and
+  // never replicated, the queries are split in P blocks, and every rank keeps the running top-k
+  // of its block while the shards travel one hop per step around the ring.  Each exchange runs
+  // on a side stream while the local screen + exact re-rank of the shard in hand runs on the
+  // engine stream; the running and new lists are merged by the K-way merge kernel.  Memory per
+  // GPU: two shards + Q/P queries.
+  DevBuf<double> ring_a_, ring_b_, ring_d_;
+  DevBuf<int> ring_i_;
+  hipStream_t ring_st_ = nullptr;
+  hipEvent_t ring_ev_ = nullptr, ring_done_ = nullptr;
+  void ring(Input* in, Output* out) {
+    const int P = rt_.world, r = rt_.rank;
+    std::vector<int64_t> nc, nd, qc, qd;
+    block_partition(N_, P, nc, nd);
+    block_partition(Q_, P, qc, qd);
+    const int64_t mx = *std::max_element(nc.begin(), nc.end());
+    hipStream_t st = rt_.stream;
+    if (P > 1 && !ring_st_) {
+      HIPCHK(hipStreamCreateWithFlags(&ring_st_, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ring_ev_, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&ring_done_, hipEventDisableTiming));
+    }
+    double* cur = ring_a_.get(mx * A_ + 1);
+    double* nxt = ring_b_.get(mx * A_ + 1);
+    const int64_t nq = qc[r];
+    double* Qd = Qx_.get((r == 0 ? Q_ : nq) * A_ + 1);
+    int* Ld = lab_.get(N_ + 1);
+    double* Xall = r == 0 ? X_.get(N_ * A_ + 1) : nullptr;
+    if (r == 0) {
+      HIPCHK(hipMemcpyAsync(Xall, in->X.data(), N_ * A_ * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Qd, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
+      if (nc[0]) HIPCHK(hipMemcpyAsync(cur, Xall, nc[0] * A_ * 8, hipMemcpyDeviceToDevice, st));
+    }
+    trace.mark("h2d");
+    std::vector<int> kl(std::max<int64_t>(1, nq)), sc(P), so(P);
+    for (int i = 0; i < P; ++i) { sc[i] = (int)qc[i]; so[i] = (int)qd[i]; }
+    MPI_Scatterv(r == 0 ? in->k.data() : nullptr, sc.data(), so.data(), MPI_INT, kl.data(), sc[r],
+                 MPI_INT, 0, MPI_COMM_WORLD);
+    if (P > 1) {
+      grp_start();  // shards and query blocks: one direct hop each from the root
+      if (r == 0) {
+        for (int t = 1; t < P; ++t) {
+          if (nc[t]) snd(Xall + nd[t] * A_, nc[t] * A_, t);
+          if (qc[t]) snd(Qd + qd[t] * A_, qc[t] * A_, t);
+        }
+      } else {
+        if (nc[r]) rcv(cur, nc[r] * A_, 0);
+        if (nq) rcv(Qd, nq * A_, 0);
+      }
+      grp_end();
+      bcast(Ld, N_);  // the vote needs every label
+    }
+    trace.mark("distribute");
+    const int64_t L = std::max<int64_t>(1, nq) * kmax_;
+    double* sd = ring_d_.get(2 * L);  // [running | this shard's] lists, merged in place below
+    int* si = ring_i_.get(2 * L);
+    double* dd = d_.get(L);
+    int* ii = ids_.get(L);
+    int* kd = kd_.get(std::max<int64_t>(1, nq));
+    if (nq) HIPCHK(hipMemcpyAsync(kd, kl.data(), nq * 4, hipMemcpyHostToDevice, st));
+    bool have = false;
+    for (int step = 0; step < P; ++step) {
+      const int src = (r + P - step) % P;  // the shard in hand started on rank src
+      if (step < P - 1) {
+        // the exchange reads cur / fills nxt on the side stream, concurrently with the compute
+        HIPCHK(hipEventRecord(ring_ev_, st));  // cur complete (received / staged) on st
+        HIPCHK(hipStreamWaitEvent(ring_st_, ring_ev_, 0));
+        ring_exchange(cur, nxt, mx * A_, ring_st_);
+        HIPCHK(hipEventRecord(ring_done_, ring_st_));
+      }
+      if (nq && nc[src]) {
+        double* od = have ? sd + L : sd;
+        int* oi = have ? si + L : si;
+        local_knn(cur, nc[src], Qd, nq, kl.data(), od, oi, nullptr, nullptr, nullptr);
+        DMLPCHK(dmlp_offset_ids(oi, L, (int)nd[src], st));
+        if (have) {
+          DMLPCHK(dmlp_merge(sd, si, 2, L, kmax_, kd, (int)nq, dd, ii, kmax_, st));
+          HIPCHK(hipMemcpyAsync(sd, dd, L * 8, hipMemcpyDeviceToDevice, st));
+          HIPCHK(hipMemcpyAsync(si, ii, L * 4, hipMemcpyDeviceToDevice, st));
+        }
+        have = true;
+      }
+      if (step < P - 1) {
+        HIPCHK(hipStreamWaitEvent(st, ring_done_, 0));  // nxt landed; cur free to overwrite
+        std::swap(cur, nxt);
+      }
+    }
+    if (nq && !have) {  // no data at all (N == 0): padding lists
+      HIPCHK(hipMemsetAsync(si, 0xff, L * 4, st));
+      DMLPCHK(dmlp_fill_f64(sd, L, INFINITY, st));
+    }
+    trace.mark("compute");
+    int* lb = labout_.get((r == 0 ? Q_ : nq) + 1);
+    uint64_t* cs = cs_.get((r == 0 ? Q_ : nq) + 1);
+    if (nq)
+      DMLPCHK(dmlp_finalize(sd, si, kmax_, kd, nullptr, (int)nq, Ld, lo_, hi_, lb, cs, st));
+    if (P > 1) {  // (label, checksum [, lists]) to rank 0 in query order
+      double* gd = r == 0 ? dall_.get(Q_ * kmax_ + 1) : nullptr;
+      int* gi = r == 0 ? iall_.get(Q_ * kmax_ + 1) : nullptr;
+      if (r == 0 && debug_ && nq) {
+        HIPCHK(hipMemcpyAsync(gd, sd, nq * kmax_ * 8, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpyAsync(gi, si, nq * kmax_ * 4, hipMemcpyDeviceToDevice, st));
+      }
+      grp_start();
+      if (r == 0) {
+        for (int t = 1; t < P; ++t) {
+          if (!qc[t]) continue;
+          rcv(lb + qd[t], qc[t], t);
+          rcv(cs + qd[t], qc[t], t);
+          if (debug_) {
+            rcv(gd + qd[t] * kmax_, qc[t] * kmax_, t);
+            rcv(gi + qd[t] * kmax_, qc[t] * kmax_, t);
+          }
+        }
+      } else if (nq) {
+        snd(lb, nq, 0);
+        snd(cs, nq, 0);
+        if (debug_) {
+          snd(sd, nq * kmax_, 0);
+          snd(si, nq * kmax_, 0);
+        }
+      }
+      grp_end();
+      trace.mark("gather");
+      if (r == 0) render(out, cs, lb, gd, gi);
+    } else {
+      render(out, cs, lb, sd, si);
+    }
+    trace.mark("report");
     rt_.sync();
   }
 

@@ -93,7 +93,7 @@ def _native(path, np_, strategy, extra=()):
     return r.stdout
 
 
-@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d"])
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "ring"])
 @pytest.mark.parametrize("np_", [2, 3])
 def test_native_front_end(case, strategy, np_):
     path, expect = case
@@ -113,3 +113,14 @@ def test_native_dynamic_farm(case, np_):
             os.environ.pop("KNN_CHUNKS_PER_RANK")
         else:
             os.environ["KNN_CHUNKS_PER_RANK"] = env_save
+
+
+def test_native_ring_debug_listing(case):
+    """knn_engine --strategy ring --debug (lists gathered to rank 0) == the serial listing."""
+    path, _ = case
+    ring = _native(path, 3, "ring", ("--debug",))
+    env = dict(os.environ)
+    r = subprocess.run([ENGINE, "--strategy", "serial", "--debug", "--input", path],
+                       capture_output=True, env=env, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    assert ring == r.stdout

@@ -23,7 +23,7 @@ for name, args in [("a", (20000, 3000, 32, 0, 1000, 1, 200, 10)), ("b", (5000, 7
 PY
 rc=0
 for f in a b c d; do
-  for s in farm shard_gather shard_reduce grid2d serial; do
+  for s in farm shard_gather shard_reduce grid2d ring serial; do
     timeout -k 10 120 $E --strategy $s --input $OUT/$f.in > $OUT/$f.$s.out 2> $OUT/$f.$s.err; r=$?
     if [ $r -ne 0 ]; then echo "FAIL rc=$r $f $s"; cat $OUT/$f.$s.err; exit $r; fi
     if cmp -s $OUT/$f.$s.out $OUT/$f.expect; then echo "OK $f $s $(cat $OUT/$f.$s.err)"; else echo "MISMATCH $f $s"; rc=1; fi

@@ -10,7 +10,7 @@ import sys
 
 
 def family(name: str) -> str:
-    for key in ("k_screen", "k_refine", "k_merge", "k_exact", "k_fmt"):
+    for key in ("k_screen", "k_refine", "k_merge", "k_exact_topk", "k_exact", "k_fmt"):
         if key in name:
             return key
     return "other"
