@@ -128,6 +128,11 @@ class KnnCore {
     if (ring_ev_) (void)hipEventDestroy(ring_ev_);
     if (ring_done_) (void)hipEventDestroy(ring_done_);
     if (ring_st_) (void)hipStreamDestroy(ring_st_);
+    for (int b = 0; b < 2; ++b) {
+      if (ooc_ready_[b]) (void)hipEventDestroy(ooc_ready_[b]);
+      if (ooc_free_[b]) (void)hipEventDestroy(ooc_free_[b]);
+    }
+    if (ooc_st_) (void)hipStreamDestroy(ooc_st_);
     if (side_) (void)hipStreamDestroy(side_);
   }
 
@@ -551,8 +556,130 @@ class KnnCore {
   int64_t qi_len_ = 0;
 
   // ---------------------------------------------------------------- farm (bench_4)
+  // ---------------------------------------------------------------- out-of-core farm
+  // KNN_MAX_DEVICE_ROWS=R with N > R (SURVEY.md §5 "datasets beyond HBM"; Python twin:
+  // ops/knn.py knn_gpu_streamed): the dataset never sits whole on a GPU.  Rank 0 streams it
+  // from host memory in R-row chunks, double-buffered — the H2D of chunk c + 1 runs on a side
+  // stream while chunk c is screened and re-ranked — each chunk is broadcast to the other ranks,
+  // every rank screens its query block against it and merges the chunk's lists into its
+  // running top-k (K-way merge kernel); labels, vote and checksum once at the end.
+  int64_t ooc_rows_ = getenv("KNN_MAX_DEVICE_ROWS") ? std::atoll(getenv("KNN_MAX_DEVICE_ROWS")) : 0;
+  DevBuf<double> ooc_buf_[2];
+  hipStream_t ooc_st_ = nullptr;
+  hipEvent_t ooc_ready_[2] = {nullptr, nullptr}, ooc_free_[2] = {nullptr, nullptr};
+  void farm_ooc(Input* in, Output* out) {
+    const int P = rt_.world, r = rt_.rank;
+    hipStream_t st = rt_.stream;
+    if (!ooc_st_) {
+      HIPCHK(hipStreamCreateWithFlags(&ooc_st_, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        HIPCHK(hipEventCreateWithFlags(&ooc_ready_[b], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ooc_free_[b], hipEventDisableTiming));
+      }
+    }
+    std::vector<int64_t> cnt, off;
+    block_partition(Q_, P, cnt, off);
+    const int64_t nl = cnt[r];
+    const int64_t R = ooc_rows_, nchunks = (N_ + R - 1) / R;
+    int* Ld = lab_.get(N_);
+    double* Qall = Qx_.get((r == 0 ? Q_ : nl) * A_ + 1);
+    double* buf[2] = {ooc_buf_[0].get(R * A_), ooc_buf_[1].get(R * A_)};
+    auto h2d_chunk = [&](int64_t c) {
+      const int64_t a = c * R, n = std::min(R, N_ - a);
+      const int b = (int)(c & 1);
+      if (c >= 2) HIPCHK(hipStreamWaitEvent(ooc_st_, ooc_free_[b], 0));  // chunk c - 2 done
+      HIPCHK(hipMemcpyAsync(buf[b], in->X.data() + a * A_, n * A_ * 8, hipMemcpyHostToDevice,
+                            ooc_st_));
+      HIPCHK(hipEventRecord(ooc_ready_[b], ooc_st_));
+    };
+    if (r == 0) {
+      HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(Qall, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, st));
+      h2d_chunk(0);
+    }
+    std::vector<int> kl(std::max<int64_t>(1, nl)), sc(P), so(P);
+    for (int t = 0; t < P; ++t) { sc[t] = (int)cnt[t]; so[t] = (int)off[t]; }
+    MPI_Scatterv(r == 0 ? in->k.data() : nullptr, sc.data(), so.data(), MPI_INT, kl.data(), sc[r],
+                 MPI_INT, 0, MPI_COMM_WORLD);
+    if (P > 1) {
+      bcast(Ld, N_);
+      grp_start();
+      if (r == 0) {
+        for (int t = 1; t < P; ++t)
+          if (cnt[t]) snd(Qall + off[t] * A_, cnt[t] * A_, t);
+      } else if (nl) {
+        rcv(Qall, nl * A_, 0);
+      }
+      grp_end();
+    }
+    trace.mark("distribute");
+    const int64_t L = std::max<int64_t>(1, nl) * kmax_;
+    double* sd = ring_d_.get(2 * L);  // [running | this chunk's] lists
+    int* si = ring_i_.get(2 * L);
+    double* dd = d_.get(std::max<int64_t>(L, r == 0 ? Q_ * kmax_ : 1));
+    int* ii = ids_.get(std::max<int64_t>(L, r == 0 ? Q_ * kmax_ : 1));
+    int* kd = kd_.get(std::max<int64_t>(1, nl));
+    if (nl) HIPCHK(hipMemcpyAsync(kd, kl.data(), nl * 4, hipMemcpyHostToDevice, st));
+    for (int64_t c = 0; c < nchunks; ++c) {
+      const int64_t a = c * R, n = std::min(R, N_ - a);
+      const int b = (int)(c & 1);
+      if (r == 0) {
+        if (c + 1 < nchunks) h2d_chunk(c + 1);  // the next chunk crosses PCIe meanwhile
+        HIPCHK(hipStreamWaitEvent(st, ooc_ready_[b], 0));
+      }
+      if (P > 1) bcast(buf[b], n * A_);
+      if (nl) {
+        double* od = c ? sd + L : sd;
+        int* oi = c ? si + L : si;
+        local_knn(buf[b], n, Qall, nl, kl.data(), od, oi, nullptr, nullptr, nullptr);
+        DMLPCHK(dmlp_offset_ids(oi, L, (int)a, st));
+        if (c) {
+          DMLPCHK(dmlp_merge(sd, si, 2, L, kmax_, kd, (int)nl, dd, ii, kmax_, st));
+          HIPCHK(hipMemcpyAsync(sd, dd, L * 8, hipMemcpyDeviceToDevice, st));
+          HIPCHK(hipMemcpyAsync(si, ii, L * 4, hipMemcpyDeviceToDevice, st));
+        }
+      }
+      HIPCHK(hipEventRecord(ooc_free_[b], st));
+    }
+    trace.mark("compute");
+    int* lb = labout_.get((r == 0 ? Q_ : nl) + 1);
+    uint64_t* cs = cs_.get((r == 0 ? Q_ : nl) + 1);
+    if (nl) DMLPCHK(dmlp_finalize(sd, si, kmax_, kd, nullptr, (int)nl, Ld, lo_, hi_, lb, cs, st));
+    if (r == 0 && nl) {  // rank 0's own lists at the head of the gathered arrays
+      HIPCHK(hipMemcpyAsync(dd, sd, nl * kmax_ * 8, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(ii, si, nl * kmax_ * 4, hipMemcpyDeviceToDevice, st));
+    }
+    if (P > 1) {
+      grp_start();
+      if (r == 0) {
+        for (int t = 1; t < P; ++t) {
+          if (!cnt[t]) continue;
+          rcv(lb + off[t], cnt[t], t);
+          rcv(cs + off[t], cnt[t], t);
+          if (debug_) {
+            rcv(dd + off[t] * kmax_, cnt[t] * kmax_, t);
+            rcv(ii + off[t] * kmax_, cnt[t] * kmax_, t);
+          }
+        }
+      } else if (nl) {
+        snd(lb, nl, 0);
+        snd(cs, nl, 0);
+        if (debug_) {
+          snd(sd, nl * kmax_, 0);
+          snd(si, nl * kmax_, 0);
+        }
+      }
+      grp_end();
+    }
+    trace.mark("gather");
+    if (r == 0) render(out, cs, lb, dd, ii);
+    trace.mark("report");
+    rt_.sync();
+  }
+
   void farm(Input* in, Output* out) {
     const int P = rt_.world;
+    if (ooc_rows_ > 0 && N_ > ooc_rows_) return farm_ooc(in, out);
     if (P == 1 && fast_ && farm_fast(in, out)) return;
     std::vector<int64_t> cnt, off;
     block_partition(Q_, P, cnt, off);

@@ -79,13 +79,14 @@ def test_python_dynamic_farm_shared_counter(case, np_):
     assert _python(path, np_, "farm", env) == expect
 
 
-def _native(path, np_, strategy, extra=()):
+def _native(path, np_, strategy, extra=(), env_extra=None):
     if not os.path.exists(ENGINE):
         pytest.skip("knn_engine not built")
     if not os.path.exists(MPIEXEC):
         pytest.skip("no mpiexec")
     env = dict(os.environ, KNN_DATA_PLANE="host", KNN_P2P_CHECK="1", KNN_POOL_MB="256",
                KNN_HOST_POOL_MB="64")
+    env.update(env_extra or {})
     cmd = [MPIEXEC, "-n", str(np_), ENGINE, "--strategy", strategy, "--input", path, *extra]
     r = subprocess.run(cmd, capture_output=True, env=env, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr.decode()[-3000:]
@@ -124,3 +125,17 @@ def test_native_ring_debug_listing(case):
                        capture_output=True, env=env, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     assert ring == r.stdout
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3])
+def test_native_out_of_core_farm(case, np_):
+    """KNN_MAX_DEVICE_ROWS=700 (N=3000 -> 5 chunks): rank 0 streams double-buffered chunks,
+    each broadcast; running lists merged per chunk; == oracle bytes (and the DEBUG listing)."""
+    path, expect = case
+    env = {"KNN_MAX_DEVICE_ROWS": "700"}
+    assert _native(path, np_, "farm", env_extra=env) == expect
+    if np_ == 2:
+        dbg = _native(path, 2, "farm", ("--debug",), env_extra=env)
+        r = subprocess.run([ENGINE, "--strategy", "serial", "--debug", "--input", path],
+                           capture_output=True, timeout=180, cwd=ROOT)
+        assert dbg == r.stdout
