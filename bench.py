@@ -62,12 +62,12 @@ def main(argv=None):
                     help="compare a SHA-256 digest of the WHOLE rank-0 report (every query line) "
                          "with the CPU oracle's (C++ fp64 brute force, outside the timed region)")
     ap.add_argument("--no-busbw", action="store_true")
-    ap.add_argument("--harness", default="python", choices=["python", "native"],
+    ap.add_argument("--harness", default="python", choices=["python", "native", "dropin"],
                     help="native: time the reference-contract binary (knn_engine: parse untimed, "
                          "'Time taken' = KNN + report + barrier, common.cpp:121-131) at this "
                          "config AND at BASELINE.md's Q = 1000, one process per run")
     a = ap.parse_args(argv)
-    if a.harness == "native":
+    if a.harness in ("native", "dropin"):
         return _bench_native(a)
 
     import numpy as np
@@ -191,7 +191,16 @@ def _bench_native(a):
     from distributed_machine_learning_project_amd import build
     from distributed_machine_learning_project_amd.utils.io import generate, to_text
 
-    exe = build.build_engine()
+    dropin = a.harness == "dropin"
+    if dropin:
+        # engine.h + dropin_engine.cpp linked with a harness that keeps the reference's contract
+        # (tests/native/mini_harness.cpp: common.cpp's parse / timing / reportResult through cout)
+        exe = build.build_dropin(os.path.join(ROOT, "tests", "native", "mini_harness.cpp"),
+                                 out=os.path.join(ROOT, "distributed_machine_learning_project_amd",
+                                                  "_build", "engine_dropin"),
+                                 extra_flags=['-DDMLP_COMMON_HEADER="contract_types.h"'])
+    else:
+        exe = build.build_engine()
     P = max(1, a.gpus)
     kmin = a.k if a.kmin is None else a.kmin
     kmax = max(kmin, a.k if a.kmax is None else a.kmax)
@@ -207,16 +216,24 @@ def _bench_native(a):
             for r in range(a.warmup + steps):
                 met = os.path.join(td, f"{tag}_{r}.json")
                 env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy)
-                cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [
-                    str(exe), "--input", path]
-                if a.schedule == "dynamic":
-                    cmd += ["--schedule", "dynamic"]
-                pr = subprocess.run(cmd, capture_output=True, env=env, timeout=600)
+                cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [str(exe)]
+                if not dropin:
+                    cmd += ["--input", path]
+                    if a.schedule == "dynamic":
+                        cmd += ["--schedule", "dynamic"]
+                with open(path, "rb") as fin:
+                    pr = subprocess.run(cmd, stdin=fin if dropin else None, capture_output=True,
+                                        env=env, timeout=600)
                 if pr.returncode != 0:
                     raise RuntimeError(pr.stderr.decode()[-2000:])
                 if r >= a.warmup:
-                    with open(met) as f:
-                        times.append(float(_json.load(f)["time_ms"]))
+                    if dropin:  # the harness prints whole milliseconds only
+                        import re as _re
+                        m = _re.search(rb"Time taken: (\d+) ms", pr.stderr)
+                        times.append(float(m.group(1)))
+                    else:
+                        with open(met) as f:
+                            times.append(float(_json.load(f)["time_ms"]))
                 out0 = pr.stdout
             entry = {"Q": q, "time_ms_median": round(statistics.median(times), 3),
                      "time_ms_min": round(min(times), 3), "runs": len(times)}
@@ -235,7 +252,9 @@ def _bench_native(a):
         "unit": "queries/s", "n_gpus": P, "steps": steps, "warmup": a.warmup,
         "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / BASELINE_QPS, 1), "dtype": "fp64",
-        "harness": "native knn_engine (reference contract: Time taken = KNN + report + barrier)",
+        "harness": ("engine.h drop-in under the reference harness contract (AoS pack + KNN + "
+                    "reportResult via cout + barrier; whole ms)" if dropin else
+                    "native knn_engine (reference contract: Time taken = KNN + report + barrier)"),
         "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",
         "config": {"model": f"bench_4 exact k-NN classifier N={a.n_data} A={a.attrs} "
                             f"k={a.k if kmin == kmax else f'{kmin}-{kmax}'} labels={a.labels}",

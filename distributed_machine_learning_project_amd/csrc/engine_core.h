@@ -391,7 +391,7 @@ class KnnCore {
       HIPCHK(hipMemcpyAsync(pg.data(), db, pg.size(), hipMemcpyDeviceToHost, rt_.stream));
       rt_.sync();
     }
-    if (rt_.world == 1 && fast_ && !debug_ && !exact_) {
+    if (rt_.world == 1 && fast_ && !exact_) {
       // the single-GPU fast path once on a tiny input: its side stream, event, staging and
       // device buffers, the host pool's first job and the first copies on the side stream are
       // all paid here (measured ~16 ms of first-use cost otherwise)
@@ -474,8 +474,9 @@ class KnnCore {
   hipEvent_t ev_rows_ = nullptr;
 
   bool farm_fast(Input* in, Output* out) {
-    if (rt_.world != 1 || debug_ || exact_ || !in || N_ == 0 || Q_ == 0 || Q_ > (1 << 30))
-      return false;
+    // (debug_ = lists mode — the engine.h drop-in hands every list to the harness's reportResult
+    // — is served too: render() then copies the lists and labels instead of the report text)
+    if (rt_.world != 1 || exact_ || !in || N_ == 0 || Q_ == 0 || Q_ > (1 << 30)) return false;
     const int KT = std::max(1, (A_ + 31) / 32);
     if (dmlp_screen_x1_qw(KT) <= 0 || kmax_ > 32 || kmax_ > N_) return false;
     if (*std::min_element(in->k.begin(), in->k.end()) < 1) return false;
