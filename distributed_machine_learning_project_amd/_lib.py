@@ -118,7 +118,8 @@ def lib():
         if not LIB_PATH.exists():
             raise NativeLibraryMissing(
                 f"{LIB_PATH} not built; run `python -m distributed_machine_learning_project_amd.build`")
-    h = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    # DMLP_LIB: an alternative build of the same library (kernel A/B runs on one box)
+    h = C.CDLL(os.environ.get("DMLP_LIB") or str(LIB_PATH), mode=C.RTLD_GLOBAL)
     for name, (res, args) in _SIGS.items():
         fn = getattr(h, name)
         fn.restype = res

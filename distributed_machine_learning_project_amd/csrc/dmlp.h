@@ -142,6 +142,7 @@ int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const 
 // Same for the single-term screen's group output: members of each group whose single-term score
 // (recomputed from xfrag / xinit / qhi, KT <= 2) reaches the (query, slice) threshold cand_h get
 // exact distances.  status = 1 also when the survivors exceed 256 (pathological ties).
+// qidx may be null: query p is row p (the all-queries pass).
 int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
                        int S, const double* X, int A, const double* Qx, const void* xfrag,
                        const float* xinit, const void* qhi, int KT, int hl, int64_t n_points,

@@ -36,7 +36,9 @@ __device__ __forceinline__ double exact_dist(const double* __restrict__ q,
 
 // (dist asc, id desc) total order.
 __device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
-  return da < db || (da == db && ia > ib);
+  // no short circuit: in the unrolled rank loops a branch per term became per-iteration
+  // control flow whose flags the compiler spilled to scratch
+  return (da < db) | ((da == db) & (ia > ib));
 }
 
 // Bitonic sort of E*64 (dist,id) keys held E per lane (element index r*64 + lane), ascending
@@ -161,9 +163,11 @@ __device__ __forceinline__ unsigned long long lanemask_lt() {
 
 // Majority vote over the labels of ids[0..k) (ids < 0 skipped), tie -> larger label, none -> -1
 // (engine.cpp:319-332).  One wave.  `hist` is a per-wave LDS scratch of hist_cap ints used when
-// the label range [label_lo, label_hi) is small; otherwise an O(k^2/64) count.
-__device__ __forceinline__ int wave_vote(const int* ids, int k, const int* __restrict__ labels,
-                                         int label_lo, int label_hi, int* hist, int hist_cap) {
+// the label range [label_lo, label_hi) is small; otherwise an O(k^2/64) count.  lab(i, id)
+// returns the label of entry i (a gather from the label table, or labels carried in LDS).
+template <class LabFn>
+__device__ __forceinline__ int wave_vote_by(const int* ids, int k, LabFn lab, int label_lo,
+                                            int label_hi, int* hist, int hist_cap) {
   const int lane = lane_id();
   long long best = -1;  // (count << 32) | (label ^ 0x80000000)
   const int range = label_hi - label_lo;
@@ -172,7 +176,7 @@ __device__ __forceinline__ int wave_vote(const int* ids, int k, const int* __res
     wave_sync();
     for (int i = lane; i < k; i += 64) {
       const int id = ids[i];
-      if (id >= 0) atomicAdd(&hist[labels[id] - label_lo], 1);
+      if (id >= 0) atomicAdd(&hist[lab(i, id) - label_lo], 1);
     }
     wave_sync();
     for (int i = lane; i < range; i += 64) {
@@ -187,11 +191,11 @@ __device__ __forceinline__ int wave_vote(const int* ids, int k, const int* __res
     for (int i = lane; i < k; i += 64) {
       const int id = ids[i];
       if (id < 0) continue;
-      const int li = labels[id];
+      const int li = lab(i, id);
       int c = 0;
       for (int j = 0; j < k; ++j) {
         const int jd = ids[j];
-        c += (jd >= 0 && labels[jd] == li);
+        c += (jd >= 0 && lab(j, jd) == li);
       }
       const long long key = ((long long)c << 32) | (long long)((unsigned)li ^ 0x80000000u);
       best = key > best ? key : best;
@@ -205,6 +209,12 @@ __device__ __forceinline__ int wave_vote(const int* ids, int k, const int* __res
   wave_sync();
   if (best < 0) return -1;
   return (int)((unsigned)(best & 0xffffffffll) ^ 0x80000000u);
+}
+
+__device__ __forceinline__ int wave_vote(const int* ids, int k, const int* __restrict__ labels,
+                                         int label_lo, int label_hi, int* hist, int hist_cap) {
+  return wave_vote_by(ids, k, [&](int, int id) { return labels[id]; }, label_lo, label_hi, hist,
+                      hist_cap);
 }
 
 __device__ __forceinline__ uint64_t fnv_checksum(int label, const int* ids, int k) {

@@ -543,7 +543,7 @@ class KnnCore {
     uint64_t* cs = cs_.get(Q_);
     int* stat = f_st_.get(Q_);
     // (the refine writes every row's padding and status itself: no fill passes)
-    DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, qi, kd,
+    DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, nullptr, kd,
                                (int)Q_, dd, ii, kmax_, Ld, lo_, hi_, lb, cs, stat, nullptr, st));
     trace.mark("refine");
     std::vector<int> sh(Q_);

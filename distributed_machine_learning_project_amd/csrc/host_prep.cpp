@@ -30,6 +30,15 @@ namespace {
 constexpr double kMaxAbs = 1.0e15;
 constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch of the data prep
 
+// pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN, default 40000)
+int spin_budget() {
+  static const int v = [] {
+    const char* e = std::getenv("DMLP_POOL_SPIN");
+    return e ? std::max(0, std::atoi(e)) : 40000;
+  }();
+  return v;
+}
+
 // Persistent workers: a per-call std::thread spawn (tens of microseconds each) would cost more
 // than the conversion itself.  After a job a worker spins ~100 us on the generation counter
 // before it sleeps on the condition variable, so back-to-back jobs (the chunked host-ops
@@ -80,7 +89,7 @@ class Pool {
       uint64_t g = gen_.load(std::memory_order_acquire);
       // spin only while the pool fits the CPUs it may use: oversubscribed workers would burn
       // the time slices of the threads they wait for
-      const int spins = oversubscribed() ? 0 : 40000;
+      const int spins = oversubscribed() ? 0 : spin_budget();
       for (int spin = 0; g == seen && spin < spins; ++spin) {
         _mm_pause();
         g = gen_.load(std::memory_order_acquire);

@@ -8,6 +8,8 @@
 //  * k_merge    : K-way merge of sorted per-shard top-k lists — the device analog of bench_2's
 //                 user MPI_Op (@0xbc70) and bench_1's root sort (@0xdae6); RCCL has no user
 //                 reductions, so strategies call this between send/recv rounds (K4).
+//                 L <= 8 lists: k_merge_seq (one lane per query, heads in registers);
+//                 more: k_merge_path (LDS merge path) or the rank kernel.
 //  * k_finalize : vote (max count, tie -> larger label; engine.cpp:319-332) + FNV-1a checksum
 //                 (common.cpp:59-70) of sorted lists.
 //  * k_exact_rows: full exact distance rows (fallback for k > screen kmax, overflowing queries,
@@ -143,9 +145,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wave;
   if (p >= nq) return;
-  const int q = __builtin_amdgcn_readfirstlane(qidx[p]);
+  // qidx == nullptr: every query in order (no dependent index load at the head of the chain)
+  const int q = qidx ? __builtin_amdgcn_readfirstlane(qidx[p]) : p;
   const int k = __builtin_amdgcn_readfirstlane(qk[q]);
   const int* cnt = cand_cnt + (int64_t)p * S;
+  // group mode: everything that depends only on (p, q) is requested here, in one batch, instead
+  // of one dependent latency after another (this kernel is bound by its chain of gathers)
+  constexpr int KTG = GROUPS ? GROUPS : 1;
+  u32x4 qraw[KTG * 4];
+  float g_eps = 0.0f, g_h1 = 0.0f;
+  unsigned ebuf = 0;  // S == 1: entry `lane` of the query's single slice
+  if (GROUPS) {
+    if (KTG == 1) {  // (KT = 2: 32 registers held this long would spill; loaded at first use)
+#pragma unroll
+      for (int f = 0; f < KTG * 4; ++f)
+        qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KTG * 4 + f]);
+    }
+    g_eps = gin.cand_h[2 * (int64_t)p * S + 1];
+    g_h1 = gin.cand_h[2 * (int64_t)p];
+    if (S == 1 && lane < cap) ebuf = (unsigned)cand_ids[(int64_t)p * cap + lane];
+  }
   // prefix of candidate counts over slices (S <= SMAX)
   int* pre = s_pre[wave];
   bool ovf = false;
@@ -202,8 +221,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
       return (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
     };
     int* hist = s_hist[wave];
-    const float eps = gin.cand_h[2 * (int64_t)p * S + 1];
-    float hq = S == 1 ? gin.cand_h[2 * (int64_t)p] : -INFINITY;  // one slice: already global
+    const float eps = g_eps;
+    float hq = S == 1 ? g_h1 : -INFINITY;  // one slice: already global
     if (S > 1 && M >= k && k >= 1) {
       int above = 0;
       int b1 = -1, b2 = -1;
@@ -229,26 +248,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
     const unsigned kh = (tq ^ ((unsigned)((int)tq >> 31) | 0x80000000u)) & 0xffff0000u;
     // ---- expand surviving groups; keep members whose single-term score reaches hq
     constexpr int KT = GROUPS ? GROUPS : 1;  // (dead code for GROUPS == 0)
-    float qf[KT * 32];  // hi(q') as fp32, k-fragment order
+    // hi(q') stays packed (two bf16 per dword, 16 VGPRs per KT): unpacked at each use — a
+    // 32-float copy would push this 64-register kernel into scratch spills
+    if (KT != 1) {
 #pragma unroll
-    for (int f = 0; f < KT * 4; ++f) {
-      const u32x4 w = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        qf[f * 8 + 2 * e] = __uint_as_float(w[e] << 16);
-        qf[f * 8 + 2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-      }
+      for (int f = 0; f < KT * 4; ++f)
+        qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
     }
-    // one member per lane (4 lanes per group: their fragments are adjacent 16-byte chunks)
+    // one member per lane (4 lanes per group: their fragments are adjacent 16-byte chunks).
+    // Entries are fetched 64 groups at a time, one per lane, and dealt to the member lanes by
+    // a shuffle: each 64-member step then waits on one gather (the fragments), not two.
     int nm = 0;
     for (int j0 = 0; j0 < 4 * M; j0 += 64) {
       const int jm = j0 + lane;
       const int g = jm >> 2;
+      if ((j0 & 255) == 0 && (S > 1 || j0 > 0)) {  // S == 1: block 0 was fetched up front
+        const int gg = (j0 >> 2) + lane;
+        ebuf = 0;
+        if (gg < M) {
+          const int lo = slice_of(gg);
+          ebuf = (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (gg - pre[lo])];
+        }
+      }
+      const unsigned e = (unsigned)__shfl((int)ebuf, g & 63);
       int id = 0;
       bool keep = false;
       if (g < M) {
         const int lo = slice_of(g);
-        const unsigned e = (unsigned)cand_ids[((int64_t)p * S + lo) * cap + (g - pre[lo])];
         id = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4 + (jm & 3);
         if (e >= kh && id < gin.n_points) {
           const int64_t t = id >> 6;
@@ -263,8 +289,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
               const u32x4 w = fk[16 * kq];
 #pragma unroll
               for (int q2 = 0; q2 < 4; ++q2) {
-                sc += qf[(kt * 4 + kq) * 8 + 2 * q2] * __uint_as_float(w[q2] << 16);
-                sc += qf[(kt * 4 + kq) * 8 + 2 * q2 + 1] * __uint_as_float(w[q2] & 0xffff0000u);
+                const unsigned qw = qraw[kt * 4 + kq][q2];
+                sc += __uint_as_float(qw << 16) * __uint_as_float(w[q2] << 16);
+                sc += __uint_as_float(qw & 0xffff0000u) * __uint_as_float(w[q2] & 0xffff0000u);
               }
             }
           }
@@ -289,6 +316,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
   }
   const double* res_d;
   const int* res_i;
+  // group mode: each candidate's label is gathered beside its row and travels with it (in the
+  // slice-prefix scratch, dead after the member filter), so the vote reads LDS, not a final
+  // dependent gather.  cl: candidates' labels [P], rl: the top-k's labels [KMAX].
+  const bool carry = GROUPS && labels != nullptr;
+  int* const cl = s_pre[wave];
+  int* const rl = s_pre[wave] + P;
+  static_assert(!GROUPS || P + KMAX <= SMAX + 1, "label scratch must fit the prefix array");
+  bool carried = false;
   if (M <= P && k <= KMAX) {
     // rank select: keys are unique (distinct ids), so rank(i) = #{j : key_j < key_i} places
     // every member of the top-k directly at its sorted position.
@@ -297,9 +332,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
     for (int j = lane; j < M; j += 64) {
       double dv; int id;
       cand(j, dv, id);
+      if (carry) cl[j] = labels[id];
       cd[j] = dv;
       if (!GROUPS) ci[j] = id;
     }
+    carried = carry;
     for (int i = lane; i < k; i += 64) { s_rd[wave][i] = INFINITY; s_ri[wave][i] = -1; }
     dmlp::wave_sync();
     int Ms = M;
@@ -311,6 +348,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
       const double di = cd[lane];
       const int ii = ci[lane];
       int rank = 0;
+#pragma unroll 32
       for (int j = 0; j < 64; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
       const unsigned long long hit = __ballot(rank == k - 1);
       const int src = __ffsll((long long)hit) - 1;
@@ -321,11 +359,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
       for (int j0 = 0; j0 < M; j0 += 64) {
         const int j = j0 + lane;
         double dj = INFINITY;
-        int ij = -1;
+        int ij = -1, lj = 0;
         bool keep = false;
         if (j < M) {
           dj = cd[j];
           ij = ci[j];
+          if (carry) lj = cl[j];
           keep = !dmlp::key_less(td, ti, dj, ij);  // key_j <= bound
         }
         const unsigned long long km = __ballot(keep);
@@ -334,6 +373,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
           const int pos = kept + __popcll(km & dmlp::lanemask_lt());
           cd[pos] = dj;
           ci[pos] = ij;
+          if (carry) cl[pos] = lj;
         }
         kept += __popcll(km);
       }
@@ -344,8 +384,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
       const double di = cd[i];
       const int ii = ci[i];
       int rank = 0;
+#pragma unroll 32
       for (int j = 0; j < Ms; ++j) rank += dmlp::key_less(cd[j], ci[j], di, ii) ? 1 : 0;
-      if (rank < k) { s_rd[wave][rank] = di; s_ri[wave][rank] = ii; }
+      if (rank < k) {
+        s_rd[wave][rank] = di;
+        s_ri[wave][rank] = ii;
+        if (carry) rl[rank] = cl[i];
+      }
     }
     dmlp::wave_sync();
     res_d = s_rd[wave];
@@ -371,8 +416,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
   }
   if (labels) {
     dmlp::wave_sync();
-    finalize_wave(res_i, k, labels, label_lo, label_hi, s_hist[wave], out_label + q, out_cs + q,
-                  HCAP);
+    if (carried) {
+      const int label = k > 0 ? dmlp::wave_vote_by(res_i, k, [&](int i, int) { return rl[i]; },
+                                                   label_lo, label_hi, s_hist[wave], HCAP)
+                              : -1;
+      if (lane == 0) {
+        out_label[q] = label;
+        out_cs[q] = dmlp::fnv_checksum(label, res_i, k);
+      }
+    } else {
+      finalize_wave(res_i, k, labels, label_lo, label_hi, s_hist[wave], out_label + q,
+                    out_cs + q, HCAP);
+    }
   }
 }
 
@@ -574,6 +629,81 @@ __global__ __launch_bounds__(256) void k_merge_path(const double* __restrict__ i
     const bool real = o < total;
     out_d[(int64_t)q * kout + o] = real ? bd[cur][o] : INFINITY;
     out_i[(int64_t)q * kout + o] = real ? bi[cur][o] : -1;
+  }
+}
+
+// Register-resident sequential form for few lists (L <= 8): one LANE per query, the L list
+// heads in registers, one output per iteration (the smallest head under (dist asc, id desc);
+// equal keys go to the lower list index: a later list must be strictly smaller to win), then
+// one load refills the list it came from.  No LDS, no co-rank searches, no wave-wide
+// synchronisation: 64 queries per wave, and the per-query work is k selections of L heads —
+// the merge-path kernel spends a whole wave per query.  Padding entries (id < 0) end a list;
+// slots [total, kout) get the (+inf, -1) padding, so callers need no fill pass.
+template <int L>
+__global__ __launch_bounds__(256) void k_merge_seq(const double* __restrict__ in_d,
+                                                  const int* __restrict__ in_i,
+                                                  int64_t list_stride, int kin,
+                                                  const int* __restrict__ qk, int nq,
+                                                  double* __restrict__ out_d,
+                                                  int* __restrict__ out_i, int kout) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  int k = qk[q];
+  k = k < kout ? k : kout;
+  k = k > 0 ? k : 0;
+  const int lim = k < kin ? k : kin;
+  const int64_t qo = (int64_t)q * kin;
+  double hd[L];
+  int hi[L], pos[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    pos[l] = 0;
+    hd[l] = INFINITY;
+    hi[l] = -1;
+    if (lim > 0) {
+      hd[l] = in_d[l * list_stride + qo];
+      hi[l] = in_i[l * list_stride + qo];
+    }
+  }
+  double* const od = out_d + (int64_t)q * kout;
+  int* const oi = out_i + (int64_t)q * kout;
+  int o = 0;
+  for (; o < k; ++o) {
+    int b = -1;
+    double bd = INFINITY;
+    int bi = -1;
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const bool better = hi[l] >= 0 && (b < 0 || dmlp::key_less(hd[l], hi[l], bd, bi));
+      b = better ? l : b;
+      bd = better ? hd[l] : bd;
+      bi = better ? hi[l] : bi;
+    }
+    if (b < 0) break;  // every list exhausted
+    od[o] = bd;
+    oi[o] = bi;
+    int pb = 0;
+#pragma unroll
+    for (int l = 0; l < L; ++l) pb = l == b ? pos[l] : pb;
+    ++pb;
+    double nd = INFINITY;
+    int ni = -1;
+    if (pb < lim) {
+      const int64_t off = b * list_stride + qo + pb;
+      nd = in_d[off];
+      ni = in_i[off];
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      const bool t = l == b;
+      pos[l] = t ? pb : pos[l];
+      hd[l] = t ? nd : hd[l];
+      hi[l] = t ? ni : hi[l];
+    }
+  }
+  for (; o < kout; ++o) {
+    od[o] = INFINITY;
+    oi[o] = -1;
   }
 }
 
@@ -796,7 +926,20 @@ extern "C" int dmlp_merge(const double* in_d, const int* in_i, int L, int64_t li
   if (L < 1 || L > 64) return -1;
   const int lcap = std::max(1, kout);  // a merged list holds up to k <= kout entries
   const size_t lds = 2 * (size_t)L * lcap * (sizeof(double) + sizeof(int));
-  if (lds <= 48 * 1024) {  // LDS-resident merge path (P <= 8 lists of k <= 256, ...)
+  if (L <= 8) {  // one lane per query, heads in registers (writes every slot of [0, kout))
+    const dim3 g((nq + 255) / 256), b(256);
+    hipStream_t st = (hipStream_t)stream;
+#define DMLP_MERGE_SEQ(LV)                                                                     \
+  case LV:                                                                                     \
+    hipLaunchKernelGGL(k_merge_seq<LV>, g, b, 0, st, in_d, in_i, list_stride, kin, qk, nq, out_d, \
+                       out_i, kout);                                                           \
+    break;
+    switch (L) {
+      DMLP_MERGE_SEQ(1) DMLP_MERGE_SEQ(2) DMLP_MERGE_SEQ(3) DMLP_MERGE_SEQ(4)
+      DMLP_MERGE_SEQ(5) DMLP_MERGE_SEQ(6) DMLP_MERGE_SEQ(7) DMLP_MERGE_SEQ(8)
+    }
+#undef DMLP_MERGE_SEQ
+  } else if (lds <= 48 * 1024) {  // LDS-resident merge path (P <= 8 lists of k <= 256, ...)
     const int w = lds <= 12 * 1024 ? 4 : 1;  // queries (waves) per workgroup
     hipLaunchKernelGGL(k_merge_path, dim3((nq + w - 1) / w), dim3(64 * w), lds * w,
                        (hipStream_t)stream, in_d, in_i, L, list_stride, kin, qk, nq, out_d, out_i,

@@ -428,7 +428,8 @@ class _KnnCall:
             self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
                 cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
-                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, ds.hl, N, _p(qidx), _p(self.kdev_eff), nq,
+                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, ds.hl, N,
+                _p(qidx) if idx is not None else None, _p(self.kdev_eff), nq,
                 _p(self.out_d), _p(self.out_i), self.ks, *fin), "refine_groups")
             self._keep = (qidx, cand_ids, cand_cnt, cand_h)
             return
@@ -904,8 +905,12 @@ def merge_gpu(lists_d, lists_i, k_dev, kout: int):
     Ld = lists_d.contiguous()
     Li = lists_i.contiguous()
     Lc, Q, kin = Ld.shape
-    out_d = torch.full((Q, kout), float("inf"), dtype=torch.float64, device=Ld.device)
-    out_i = torch.full((Q, kout), -1, dtype=torch.int32, device=Ld.device)
+    if Lc <= 8:  # the register merge writes every slot, padding included
+        out_d = torch.empty((Q, kout), dtype=torch.float64, device=Ld.device)
+        out_i = torch.empty((Q, kout), dtype=torch.int32, device=Ld.device)
+    else:
+        out_d = torch.full((Q, kout), float("inf"), dtype=torch.float64, device=Ld.device)
+        out_i = torch.full((Q, kout), -1, dtype=torch.int32, device=Ld.device)
     _lib.check(_lib.lib().dmlp_merge(_p(Ld), _p(Li), Lc, Q * kin, kin, _p(k_dev), Q, _p(out_d),
                                      _p(out_i), kout, _stream()), "merge")
     return out_d, out_i

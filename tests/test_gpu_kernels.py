@@ -365,7 +365,8 @@ def test_merge_and_finalize(torch_cuda):
     np.testing.assert_array_equal(cs_c, cs_g.cpu().numpy().view(np.uint64))
 
 
-@pytest.mark.parametrize("Lists,kin,kout", [(8, 16, 16), (8, 128, 128), (3, 40, 64), (64, 4, 8)])
+@pytest.mark.parametrize("Lists,kin,kout", [(8, 16, 16), (8, 128, 128), (3, 40, 64), (64, 4, 8),
+                                             (2, 24, 32), (1, 8, 12), (12, 16, 16)])
 def test_merge_rank_shapes(torch_cuda, Lists, kin, kout):
     """K4 merge at shard-merge shapes: disjoint ids, padded (+inf, -1) suffixes of random length,
     per-query k in [0, kout] (bench_2 @0xbc70 custom op semantics via merge_cpu)."""

@@ -15,6 +15,8 @@
 #   sweep      bench sweep over N / A / k (profiles/ sweep table)
 #   exact      bench.py --exact (fp64-only path)
 #   harness    bench.py --harness native (knn_engine through the reference contract)
+#   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
+#   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
 set -u
 TAG=${1:?tag}
 shift
@@ -68,6 +70,13 @@ for task in "$@"; do
       step sweep 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep.jsonl" --timeout 170 ;;
     harness)
       step harness 600 python bench.py --harness native ;;
+    merge)
+      step merge 300 rocprofv3 --kernel-trace --stats -d "$OUT/merge" -o run --output-format csv \
+          -- python3 tools/merge_bench.py --p 8 --q 131072 --ks 16,128
+      find "$OUT/merge" -name '*kernel_stats.csv' -exec sh -c 'head -8 "$1" | cut -c1-160' _ {} \; ;;
+    hostprof)
+      step hostprof 300 python tools/host_profile.py --steps 100
+      DMLP_PIPE_DEBUG=1 step pipedebug 120 python bench.py --steps 5 --warmup 2 --no-busbw ;;
     *)
       echo "unknown task $task"; exit 2 ;;
   esac
