@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -123,6 +124,21 @@ class Pool {
 // share of a 256-thread host), divided among the ranks of the node that share that mask
 // (LOCAL_WORLD_SIZE, set by torchrun / the MPI launchers), at most 16 — the conversions are bound
 // by memory, not cores.  DMLP_HOST_THREADS overrides (clamped to [1, 16]).
+// CPUs' worth of time the cgroup grants (cgroup v2 cpu.max "quota period"; 0 = unlimited or
+// unknown).  A container can see a 256-CPU affinity mask with a 16-CPU quota: sizing the pool by
+// the mask alone would let spinning workers run the quota out and get the whole process throttled.
+int cgroup_cpus() {
+  FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r");
+  if (!f) return 0;
+  char quota[32] = {0};
+  long period = 0;
+  const int got = std::fscanf(f, "%31s %ld", quota, &period);
+  std::fclose(f);
+  if (got != 2 || period <= 0 || std::strcmp(quota, "max") == 0) return 0;
+  const long q = std::atol(quota);
+  return q > 0 ? (int)std::max(1L, q / period) : 0;
+}
+
 int pool_threads() {
   if (const char* e = std::getenv("DMLP_HOST_THREADS"))
     return std::max(1, std::min(std::atoi(e), kMaxPool));
@@ -130,6 +146,7 @@ int pool_threads() {
   int n = 0;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
   if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  if (const int c = cgroup_cpus()) n = std::min(n, c);
   int local = 1;
   for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"})
     if (const char* e = std::getenv(v)) { local = std::max(1, std::atoi(e)); break; }
