@@ -695,7 +695,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
             qn = torch.empty(Q, dtype=torch.float32, device=dev)
         # host conversion of each slice overlaps the PCIe copy of the previous one
-        t_ops = time.perf_counter()
+        t_ops = t_ops0 = time.perf_counter()
         rc = L.dmlp_host_ops_h2d(Xc.ctypes.data, N, Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT,
                                  *[b.data_ptr() for b in hb], _p(xhi), _p(xin), _p(xnm), _p(qhi),
                                  _p(qn), HOST_OPS_CHUNKS, copy.cuda_stream)
@@ -777,7 +777,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     _ARENA.mark()
     if _PIPE_DEBUG:
         import sys
-        print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms, finish "
+        print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms (before host ops "
+              f"{1e3 * (t_ops0 - t_enter) if host_ops else 0:.3f} ms), finish "
               f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host ops "
               f"{prepped is not None} ({1e3 * t_ops if host_ops else 0:.3f} ms)", file=sys.stderr)
     return ds, od, oi, ol, oc, n_fb
