@@ -56,6 +56,13 @@ int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, i
                       const double* mu, int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d, void* xnm_d,
                       void* qhi_d, void* qn_d, int chunks, void* stream);
+// Same, the dataset part restricted to tiles [t0, t1) (device image pointers at tile t0's slot;
+// *xnm = +inf when the range is outside the screen's range): the per-rank shard of a sharded render.
+int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1, const double* Qx,
+                            int64_t Q, int A, const double* mu, int KT, uint16_t* xhi_h,
+                            float* xin_h, unsigned* xnm_h, uint16_t* qhi_h, float* qn_h,
+                            void* xhi_d, void* xin_d, void* xnm_d, void* qhi_d, void* qn_d,
+                            int chunks, void* stream);
 
 // ---------------------------------------------------------------- device: screen (K2+K3, fused)
 // bf16x3 MFMA screen + per-query streaming threshold + candidate compaction.  Queries are the

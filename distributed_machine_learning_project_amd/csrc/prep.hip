@@ -332,13 +332,21 @@ extern "C" int dmlp_host_unregister(void* p) {
   return (int)hipHostUnregister(p);
 }
 
-extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, int A,
-                                 const double* mu, int KT, uint16_t* xhi_h, float* xin_h,
-                                 unsigned* xnm_h, uint16_t* qhi_h, float* qn_h, void* xhi_d,
-                                 void* xin_d, void* xnm_d, void* qhi_d, void* qn_d, int chunks,
-                                 void* stream) {
+// Host render + H2D of the screen operands, the dataset part restricted to tiles [t0, t1): host
+// staging is indexed by absolute tile (the whole image's layout), the device image destinations
+// xhi_d / xin_d point at the slot of tile t0 (a per-rank shard buffer that a collective then
+// completes).  *xnm_d gets this range's max norm; if the range holds data outside the screen's
+// range (return bit 1) it gets +inf instead, so a max-reduce over ranks tells every rank.
+extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1,
+                                       const double* Qx, int64_t Q, int A, const double* mu,
+                                       int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
+                                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d,
+                                       void* xnm_d, void* qhi_d, void* qn_d, int chunks,
+                                       void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t n_tiles = (N + 63) / 64;
+  t0 = t0 < 0 ? 0 : (t0 > n_tiles ? n_tiles : t0);
+  t1 = t1 < t0 ? t0 : (t1 > n_tiles ? n_tiles : t1);
   const int64_t W = (int64_t)KT * 32;  // bf16 per row / point
   static const bool dbg = getenv("DMLP_HOST_OPS_DEBUG") != nullptr;
   double tl[32];
@@ -357,15 +365,16 @@ extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, i
       rc |= 4;
   };
   for (int c = 0; c < chunks; ++c) {
-    const int64_t t0 = n_tiles * c / chunks, t1 = n_tiles * (c + 1) / chunks;
-    if (t1 <= t0) continue;
+    const int64_t a = t0 + (t1 - t0) * c / chunks, b = t0 + (t1 - t0) * (c + 1) / chunks;
+    if (b <= a) continue;
     float mc = 0.0f;
-    if (dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, t0, t1, xhi_h, xin_h, &mc)) rc |= 1;
+    if (dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, a, b, xhi_h, xin_h, &mc)) rc |= 1;
     m = mc > m ? mc : m;
     mark();
-    h2d((char*)xhi_d + t0 * 64 * W * 2, xhi_h + t0 * 64 * W, (t1 - t0) * 64 * W * 2);
-    h2d((float*)xin_d + t0 * 64, xin_h + t0 * 64, (t1 - t0) * 64 * 4);
+    h2d((char*)xhi_d + (a - t0) * 64 * W * 2, xhi_h + a * 64 * W, (b - a) * 64 * W * 2);
+    h2d((float*)xin_d + (a - t0) * 64, xin_h + a * 64, (b - a) * 64 * 4);
   }
+  if (rc & 1) m = INFINITY;
   memcpy(xnm_h, &m, 4);
   h2d(xnm_d, xnm_h, 4);
   for (int c = 0; c < chunks; ++c) {
@@ -378,11 +387,22 @@ extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, i
   }
   mark();
   if (dbg) {
-    fprintf(stderr, "[dmlp-hostops] threads %d us:", dmlp_host_threads());
+    fprintf(stderr, "[dmlp-hostops] threads %d tiles [%lld, %lld) us:", dmlp_host_threads(),
+            (long long)t0, (long long)t1);
     for (int i = 0; i < nt; ++i) fprintf(stderr, " %.1f", tl[i]);
     fprintf(stderr, "\n");
   }
   return rc;
+}
+
+// The whole image (tiles [0, n_tiles)).
+extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, int A,
+                                 const double* mu, int KT, uint16_t* xhi_h, float* xin_h,
+                                 unsigned* xnm_h, uint16_t* qhi_h, float* qn_h, void* xhi_d,
+                                 void* xin_d, void* xnm_d, void* qhi_d, void* qn_d, int chunks,
+                                 void* stream) {
+  return dmlp_host_ops_h2d_tiles(X, N, 0, (N + 63) / 64, Qx, Q, A, mu, KT, xhi_h, xin_h, xnm_h,
+                                 qhi_h, qn_h, xhi_d, xin_d, xnm_d, qhi_d, qn_d, chunks, stream);
 }
 
 extern "C" int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream) {

@@ -633,7 +633,8 @@ def _side_stream(name):
 
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
                       chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
-                      mu_rows=None, X_full_host=None, report=None, k_range=None):
+                      mu_rows=None, X_full_host=None, report=None, k_range=None,
+                      image_shard=None):
     """Host arrays in (page-locked for real overlap), device results out, with the fp64 rows
     copied behind the screen ("H2D overlapped with compute").
 
@@ -655,6 +656,11 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     pinned int64 byte count) and report["copied"] whether dst already holds them.
     k_range: (a lower bound of the smallest k, an upper bound of the largest k), e.g. from a
     segment header, instead of scanning k_host (bounds only steer the dispatch).
+    image_shard: (rank, world, allgather(out, chunk), allreduce_max(t)) — every rank renders
+    only its 1/world of the dataset's screen image (host memory reads and CPU time per rank drop
+    by world) and one all-gather over xGMI completes the image before the screen; the max norm
+    is max-reduced (+inf from a rank whose rows are outside the screen's range: every rank then
+    takes the device path's exact fallbacks together, no rank-dependent branch).
     Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
     torch = _torch()
     L = _lib.lib()
@@ -688,22 +694,46 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         Xc = np.ascontiguousarray(Xf, np.float64)
         hb = [_ARENA.alloc(n) for n in (n_tiles * 64 * KT * 64, n_tiles * 64 * 4, 4, Q * KT * 64,
                                         Q * 4)]
+        sh = image_shard if image_shard is not None and image_shard[1] > 1 else None
+        if sh is not None:
+            tpr = (n_tiles + sh[1] - 1) // sh[1]  # tiles per rank (the last ranks' tails pad)
+            t0 = min(sh[0] * tpr, n_tiles)
+            t1 = min(t0 + tpr, n_tiles)
+        else:
+            tpr, t0, t1 = n_tiles, 0, n_tiles
         with torch.cuda.stream(copy):
-            xhi = torch.empty(n_tiles * 64 * KT * 32, dtype=torch.int16, device=dev)
-            xin = torch.empty(n_tiles * 64, dtype=torch.float32, device=dev)
+            W = 64 * KT * 32
+            xhi = torch.empty((n_tiles if sh is None else sh[1] * tpr) * W, dtype=torch.int16,
+                              device=dev)
+            xin = torch.empty((n_tiles if sh is None else sh[1] * tpr) * 64, dtype=torch.float32,
+                              device=dev)
+            xhi_c, xin_c = ((xhi, xin) if sh is None else
+                            (torch.empty(tpr * W, dtype=torch.int16, device=dev),
+                             torch.empty(tpr * 64, dtype=torch.float32, device=dev)))
             xnm = torch.empty(1, dtype=torch.int32, device=dev)
             qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
             qn = torch.empty(Q, dtype=torch.float32, device=dev)
         # host conversion of each slice overlaps the PCIe copy of the previous one
         t_ops = t_ops0 = time.perf_counter()
-        rc = L.dmlp_host_ops_h2d(Xc.ctypes.data, N, Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT,
-                                 *[b.data_ptr() for b in hb], _p(xhi), _p(xin), _p(xnm), _p(qhi),
-                                 _p(qn), HOST_OPS_CHUNKS, copy.cuda_stream)
+        rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data, Q, A,
+                                       mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
+                                       _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
+                                       HOST_OPS_CHUNKS, copy.cuda_stream)
         t_ops = time.perf_counter() - t_ops
         if rc & 4:
             raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
+        bad_d = None
+        if sh is not None:
+            # every rank runs these collectives whatever its own rc (no divergent branch)
+            with torch.cuda.stream(copy):
+                sh[2](xhi.view(torch.int32), xhi_c.view(torch.int32))  # (no 16-bit int in RCCL)
+                sh[2](xin, xin_c)
+                sh[3](xnm)
+                # +inf (0x7f800000) from any rank: rows outside the screen's range somewhere
+                bad_d = (xnm >= 0x7f800000).to(torch.int32)
+            rc &= ~1  # the data verdict is the reduced one, on the device
         if rc == 0:
-            dsops, prepped = (xhi, xin, xnm), (qhi, qn)
+            dsops, prepped = (xhi, xin, xnm, bad_d), (qhi, qn)
         else:
             mu_d = None  # outside the screen's range: the device path decides
     with torch.cuda.stream(copy):
@@ -726,7 +756,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             e.record(copy)
             ev.append(e)
     for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()) + (dsops or ()):
-        t.record_stream(main)
+        if t is not None:
+            t.record_stream(main)
     ks = max(1, k_range[1] if Q else 1) if kstride is None else kstride
     if dsops is not None:
         # the screen operands are on their way; X / labels / Qd complete with ev[-1]
@@ -736,7 +767,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         else:
             lo, hi, lab_ds = 0, 1, None
         ds = DeviceDataset(X, lab_ds, lo, hi, KT, mu_d, dsops[0], dsops[1], dsops[2],
-                           torch.zeros(1, dtype=torch.int32, device=dev), True, hl=1)
+                           dsops[3] if dsops[3] is not None
+                           else torch.zeros(1, dtype=torch.int32, device=dev), True, hl=1)
     else:
         main.wait_event(ev_x)
         if gather is not None:

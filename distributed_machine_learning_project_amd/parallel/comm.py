@@ -221,6 +221,23 @@ class Comm:
             return out
         return torch.cat([out[r * mx:r * mx + c] for r, c in enumerate(counts)])
 
+    def allgather_into(self, out, chunk):
+        """out = the concatenation of every rank's equal-size `chunk` in rank order (one RCCL
+        all-gather; out and chunk are flat device tensors, out.numel() = world * chunk.numel())."""
+        if self.world == 1:
+            out.copy_(chunk)
+            return out
+        from . import dist_api as dist
+        dist.all_gather_into_tensor(out, chunk)
+        return out
+
+    def allreduce_max_(self, t):
+        """In-place elementwise max over ranks."""
+        if self.world > 1:
+            from . import dist_api as dist
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+
     def gather_rows(self, t, counts, row_shape, dtype):
         """Gather row blocks to rank 0 in rank order (MPI_Gatherv); returns the concatenation on
         rank 0 and None elsewhere."""

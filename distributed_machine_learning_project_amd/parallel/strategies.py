@@ -246,10 +246,17 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             # this rank's rows and its query chunks on the copy stream; the all-gather and the
             # screen of the first chunk run while the later chunks are still crossing PCIe
             with tr.phase("h2d+allgather+compute"):
+                # KNN_IMAGE_SHARD=0: every rank renders the whole screen image (A/B)
+                shard_img = (os.environ.get("KNN_IMAGE_SHARD", "1") == "1"
+                             and comm.on_gpu and comm.world > 1)
                 d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
                                            inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
                                            mu_rows=inp.X[:4096], X_full_host=inp.X,
-                                           report=rep, k_range=k_range)
+                                           report=rep, k_range=k_range,
+                                           image_shard=(comm.rank, comm.world,
+                                                        comm.allgather_into,
+                                                        comm.allreduce_max_)
+                                           if shard_img else None)
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug,
                                      rep)
         with tr.phase("h2d"):

@@ -139,3 +139,34 @@ def test_native_out_of_core_farm(case, np_):
         r = subprocess.run([ENGINE, "--strategy", "serial", "--debug", "--input", path],
                            capture_output=True, timeout=180, cwd=ROOT)
         assert dbg == r.stdout
+
+
+@pytest.fixture(scope="module")
+def case_x1(tmp_path_factory):
+    """k in 1..32 (every query on the single-term screen, so the host-ops pipeline runs) and
+    N = 3000 -> 47 tiles: uneven per-rank image shards at np 2 and 3.  Plus the same input with
+    one point outside the screen's range (|x| > 1e15) in the LAST rank's shard."""
+    d = tmp_path_factory.mktemp("mrx1")
+    inp = dmlp.parse_input(dmlp.generate_text(3000, 301, 16, 0, 1000, 1, 32, 5, seed=12))
+    out = []
+    for tag, big in (("ok", False), ("bad", True)):
+        if big:
+            inp.X[2990, 3] = 3.0e15
+        p = d / f"{tag}.in"
+        p.write_text(dmlp.to_text(inp))
+        _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+        out.append((str(p), ref.report_lines(cs).encode()))
+    return out
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_python_sharded_image_render(case_x1, np_):
+    """Static farm over the node-shared segment: each rank renders 1/np of the screen image on
+    the host and one all-gather completes it (KNN_IMAGE_SHARD=1, the default), == oracle bytes
+    and == the whole-image-per-rank render; with out-of-range data in one shard every rank
+    takes the fallback together (max-reduced +inf norm, no divergent collective)."""
+    (path, expect), (bad_path, bad_expect) = case_x1
+    env = {"KNN_INGRESS": "shm"}
+    assert _python(path, np_, "farm", env) == expect
+    assert _python(path, np_, "farm", dict(env, KNN_IMAGE_SHARD="0")) == expect
+    assert _python(bad_path, np_, "farm", env) == bad_expect
