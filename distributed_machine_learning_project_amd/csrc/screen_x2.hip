@@ -78,7 +78,10 @@ struct X2Cfg {
   static constexpr int OFF_X = W * SB_WAVE;               // xinit ring [RING][32] fp32
   static constexpr int OFF_A = OFF_X + RING * 128;        // A ring [RING][STEPB]
   static constexpr int OFF_F = OFF_A + RING * STEPB;       // compaction-event flags [3]
-  static constexpr int LDS = PW ? SB_WAVE : OFF_F + 16;
+  // per-wave form: + a C-operand ring of two 4-step windows (4 x 32 rows of -|x'|^2/2 each),
+  // stored in the C/D register layout so a lane's 16 C values are one 64-byte broadcast read
+  static constexpr int XRW = 2 * 4 * 128;
+  static constexpr int LDS = PW ? SB_WAVE + XRW : OFF_F + 16;
   static constexpr int LDB = 8 * KT;                      // staged bytes per lane and phase
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(CAPE <= kX2IdCap, "id stride");
@@ -470,20 +473,39 @@ __global__ __launch_bounds__(PW ? 64 : 512) __attribute__((amdgpu_waves_per_eu(2
       for (int ks = 0; ks < KS; ++ks)
         vg[ks] = 16 * ((((c >> 4) * KT + (ks >> 1)) * hl) * 64 + (2 * (ks & 1) + hh) * 16 + (c & 15));
       // lane 16 g + i reads row (i & 3) + 8 (i >> 2) + 4 hh: C/D register i of its half
-      const int xd = 4 * ((lane & 3) + 8 * ((lane >> 2) & 3) + 4 * hh);
       struct OpsW {
         bf16x8 a[KS];
-        float xv;
       };
       auto read_w = [&](int j, OpsW& o) __attribute__((always_inline)) {
         const int jj = j < nsteps ? j : nsteps - 1;  // past the end: re-read (never used)
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
           o.a[ks] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xrw, vg[ks], jj * STEPG, 0));
-        o.xv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(irw, xd, jj * 128, 0));
       };
-      auto mfma_w = [&](const OpsW& o, f32x16(&ac)[T]) __attribute__((always_inline)) {
-        const f32x16 cn = c_block(o.xv);
+      // C ring: window w = steps 4w .. 4w + 3 (128 row terms) in LDS slot w & 1; lane L moves
+      // row terms L and L + 64 of a window, one window ahead of its first read (no VALU: the
+      // DPP broadcast of one value per lane into the 16-register C block cost 16 VALU per step)
+      const unsigned xrb = (unsigned)C::SB_WAVE;  // LDS byte offset of the ring
+      auto xpos = [](int f) {  // byte offset of window row term f in its slot
+        const int sw = f >> 5, r = f & 31;
+        return sw * 128 + ((r >> 2) & 1) * 64 + ((r & 3) + 4 * (r >> 3)) * 4;
+      };
+      const unsigned xp0 = (unsigned)xpos(lane), xp1 = (unsigned)xpos(lane + 64);
+      auto xload = [&](int win, float& v0, float& v1) __attribute__((always_inline)) {
+        v0 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(irw, lane * 4, win * 512, 0));
+        v1 = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(irw, lane * 4 + 256, win * 512, 0));
+      };
+      auto xstore = [&](int win, float v0, float v1) __attribute__((always_inline)) {
+        const unsigned base = xrb + (unsigned)(win & 1) * 512u;
+        *(__attribute__((address_space(3))) float*)(size_t)(base + xp0) = v0;
+        *(__attribute__((address_space(3))) float*)(size_t)(base + xp1) = v1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the ring reads stay after it
+      };
+      auto cread = [&](int j) __attribute__((always_inline)) {
+        return *(__attribute__((address_space(3))) const f32x16*)(size_t)(
+            xrb + (unsigned)((j >> 2) & 1) * 512u + (unsigned)(j & 3) * 128u + (unsigned)hh * 64u);
+      };
+      auto mfma_w = [&](const OpsW& o, const f32x16& cn, f32x16(&ac)[T]) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < T; ++t) {
           ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.a[0], bq[t][0], cn, 0, 0, 0);
@@ -492,16 +514,29 @@ __global__ __launch_bounds__(PW ? 64 : 512) __attribute__((amdgpu_waves_per_eu(2
             ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o.a[ks], bq[t][ks], ac[t], 0, 0, 0);
         }
       };
+      float xw0, xw1;
+      {
+        float v0, v1;
+        xload(0, v0, v1);
+        xstore(0, v0, v1);
+      }
+      xload(1, xw0, xw1);
       OpsW ring[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) read_w(r, ring[r]);
+      f32x16 cn = cread(0);  // one block live: read after the previous step's epilogue
       const unsigned long long tl0 = (MODE & 8) ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll 1
       for (int j0 = 0; j0 < nsteps; j0 += 4) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = j0 + r;
-          if (j < nsteps) mfma_w(ring[r], acc[r & 1]);
+          if (r == 0) {
+            // window j0/4 + 1 into the slot window j0/4 - 1 used (all its reads are done)
+            xstore((j0 >> 2) + 1, xw0, xw1);
+            xload((j0 >> 2) + 2, xw0, xw1);
+          }
+          if (j < nsteps) mfma_w(ring[r], cn, acc[r & 1]);
           read_w(j + 4, ring[r]);
           if (j > 0 && j - 1 < nsteps) epilogue(j - 1, acc[(r + 1) & 1]);
           if (r & 1) {  // every 2 steps (LIMN leaves room for 2 steps of appends)
@@ -512,6 +547,7 @@ __global__ __launch_bounds__(PW ? 64 : 512) __attribute__((amdgpu_waves_per_eu(2
             }
             trig = 0;
           }
+          cn = cread(j + 1);  // the next step's C block (past the end: a stale window, unused)
         }
       }
       if ((nsteps & 3) == 0) {
