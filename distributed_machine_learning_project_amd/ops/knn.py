@@ -38,7 +38,9 @@ SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
 SCREEN_X2 = os.environ.get("DMLP_X2", "0") != "0"
 # slices of the host-rendered screen operands, each copied as soon as it is converted (1: measured
 # best on the bench shape — every extra slice costs ~20 us of copy-API time on the host)
-HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "1"))
+# host render + H2D of the screen operands in 2 pipelined slices: the first copy starts after half
+# the render (profiles/r2t_host_ops_chunks.txt: median 2.63 vs 2.74 and 3.03 vs 3.18 ms/step on two boxes)
+HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "2"))
 
 
 def eps_rel(A: int) -> float:
