@@ -184,6 +184,8 @@ class KnnCore {
   bool debug_, exact_, dynamic_;
   // KNN_FAST=0 disables the single-GPU host-operand pipeline (A/B against the device path)
   bool fast_ = !(getenv("KNN_FAST") && std::string(getenv("KNN_FAST")) == "0");
+  // host render + H2D of the screen operands in pipelined slices (the Python default too)
+  int host_slices_ = getenv("KNN_HOST_OPS_CHUNKS") ? std::max(1, std::atoi(getenv("KNN_HOST_OPS_CHUNKS"))) : 2;
   MPI_Win ctr_win_ = MPI_WIN_NULL;
   int64_t* ctr_base_ = nullptr;
   DevBuf<int64_t> res_;
@@ -503,7 +505,8 @@ class KnnCore {
     short* qhi = fq_hi_.get(Q_ * W);
     float* qn = fq_n_.get(Q_);
     const int rc = dmlp_host_ops_h2d(in->X.data(), N_, in->Qx.data(), Q_, A_, mu_h, KT, xhi_h,
-                                     xin_h, xnm_h, qhi_h, qn_h, xhi, xin, words, qhi, qn, 1, st);
+                                     xin_h, xnm_h, qhi_h, qn_h, xhi, xin, words, qhi, qn,
+                                     host_slices_, st);
     if (rc & 4) throw std::runtime_error("host operand copy failed");
     if (rc) { rt_.sync(); return false; }  // outside the screen's range: the device path decides
     HIPCHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), st));
