@@ -215,7 +215,8 @@ def _bench_native(a):
             times, out0 = [], None
             for r in range(a.warmup + steps):
                 met = os.path.join(td, f"{tag}_{r}.json")
-                env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy)
+                env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy,
+                           KNN_INGRESS=a.ingress)  # shm: per-GPU ingress from a shared window
                 cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [str(exe)]
                 if not dropin:
                     cmd += ["--input", path]

@@ -72,6 +72,24 @@ struct Output {  // rank 0 only
   std::string report;        // host-rendered report (serial / debug)
   HostBuf<char> text;        // GPU-rendered report bytes (page-locked D2H target)
   size_t text_len = 0;
+  const char* shared_text = nullptr;  // node-shared ingress: the report sits in the segment
+};
+
+// Node-shared ingress (KNN_INGRESS=shm, farm, P > 1 on one node): rank 0's parsed input copied
+// once, before the timed region, into an MPI-3 shared-memory window that every rank maps and
+// page-locks, plus an output region for the report (48 bytes per query bound).  Every rank then
+// copies its own query block and the dataset over its OWN PCIe link (no funnel through GPU 0)
+// and writes its report lines straight into the output region.
+struct SharedIn {
+  bool valid = false;
+  int64_t N = 0, Q = 0;
+  int A = 0;
+  const double* X = nullptr;
+  const int* labels = nullptr;
+  const double* Qx = nullptr;
+  const int* k = nullptr;
+  char* out = nullptr;
+  int64_t out_bytes = 0;
 };
 
 inline std::vector<char> read_all(const char* path) {
@@ -153,6 +171,8 @@ class KnnCore {
   hipStream_t wake_st_ = nullptr;
   HostBuf<char> wake_h_;
   bool wake_ = !(getenv("KNN_WAKE_D2H") && std::string(getenv("KNN_WAKE_D2H")) == "0");
+
+  void set_shared(const SharedIn& s) { sh_ = s; }
 
   void KNN(Input* in, Output* out) {
     wake_d2h();
@@ -393,7 +413,8 @@ class KnnCore {
       HIPCHK(hipMemcpyAsync(pg.data(), db, pg.size(), hipMemcpyDeviceToHost, rt_.stream));
       rt_.sync();
     }
-    if (rt_.world == 1 && fast_ && !exact_) {
+    const bool shm_ingress = getenv("KNN_INGRESS") && std::string(getenv("KNN_INGRESS")) == "shm";
+    if ((rt_.world == 1 || shm_ingress) && fast_ && !exact_) {
       // the single-GPU fast path once on a tiny input: its side stream, event, staging and
       // device buffers, the host pool's first job and the first copies on the side stream are
       // all paid here (measured ~16 ms of first-use cost otherwise)
@@ -410,8 +431,13 @@ class KnnCore {
       for (int64_t i = 0; i < w.N; ++i) w.labels[i] = (int)(i % 3);
       for (int64_t i = 0; i < w.Q; ++i) w.k[i] = 1 + (int)(i % 32);
       N_ = w.N; Q_ = w.Q; A_ = w.A; lo_ = 0; hi_ = 3; kmax_ = 32;
-      Output o;
-      (void)farm_fast(&w, &o);
+      if (rt_.world == 1) {
+        Output o;
+        (void)farm_fast(&w, &o);
+      } else {  // the per-rank pipeline of the node-shared farm (no collectives here)
+        FastOut fo;
+        (void)fast_core(w.X.data(), w.labels.data(), w.Qx.data(), w.k.data(), w.Q, fo);
+      }
       rt_.sync();
     }
     MPI_Barrier(MPI_COMM_WORLD);
@@ -482,13 +508,37 @@ class KnnCore {
     const int KT = std::max(1, (A_ + 31) / 32);
     if (dmlp_screen_x1_qw(KT) <= 0 || kmax_ > 32 || kmax_ > N_) return false;
     if (*std::min_element(in->k.begin(), in->k.end()) < 1) return false;
+    FastOut fo;
+    if (fast_core(in->X.data(), in->labels.data(), in->Qx.data(), in->k.data(), Q_, fo) != 0)
+      return false;
+    render(out, fo.cs, fo.lb, fo.dd, fo.ii);  // synchronizes the stream
+    for (int64_t q = 0; q < Q_; ++q)
+      if (fo.st_h[q]) return false;  // single-term overflow: redo the call on the general path
+    trace.mark("report");
+    return true;
+  }
+
+  // The pipeline of farm_fast for nq queries (Qx / k: this rank's block) against the whole
+  // dataset X; leaves the per-query status copy pending on the stream (fo.st_h, valid after the
+  // next sync).  Returns 0, or 1 when the data / queries are outside the screen's range (nothing
+  // left in flight).
+  struct FastOut {
+    double* dd = nullptr;
+    int* ii = nullptr;
+    int* lb = nullptr;
+    uint64_t* cs = nullptr;
+    std::vector<int> st_h;
+  };
+  int fast_core(const double* X, const int* labels, const double* Qx, const int* k, int64_t nq,
+                FastOut& fo) {
+    const int KT = std::max(1, (A_ + 31) / 32);
     hipStream_t st = rt_.stream;
     const int64_t nt = (N_ + 63) / 64, W = (int64_t)KT * 32;
     // page-locked staging for the rendered operands (host_ops_h2d copies from it)
-    const size_t b_xhi = nt * 64 * W * 2, b_xin = nt * 64 * 4, b_qhi = Q_ * W * 2, b_qn = Q_ * 4;
+    const size_t b_xhi = nt * 64 * W * 2, b_xin = nt * 64 * 4, b_qhi = nq * W * 2, b_qn = nq * 4;
     auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
     const size_t need = up(b_xhi) + up(b_xin) + 256 + up(b_qhi) + up(b_qn) + up(A_ * 8) +
-                        up(Q_ * 4);
+                        up(nq * 4);
     if (f_stage_.size() < need) f_stage_.resize(need);
     char* hp = f_stage_.data();
     uint16_t* xhi_h = (uint16_t*)hp; hp += up(b_xhi);
@@ -498,65 +548,121 @@ class KnnCore {
     float* qn_h = (float*)hp; hp += up(b_qn);
     double* mu_h = (double*)hp; hp += up(A_ * 8);
     int* id_h = (int*)hp;
-    dmlp_cpu_center(in->X.data(), N_, A_, mu_h);
+    dmlp_cpu_center(X, N_, A_, mu_h);
     short* xhi = fx_hi_.get(nt * 64 * W);
     float* xin = fx_in_.get(nt * 64);
     unsigned* words = f_words_.get(2);  // [0] xnmax bits, [1] bad (0: the host checked ranges)
-    short* qhi = fq_hi_.get(Q_ * W);
-    float* qn = fq_n_.get(Q_);
-    const int rc = dmlp_host_ops_h2d(in->X.data(), N_, in->Qx.data(), Q_, A_, mu_h, KT, xhi_h,
-                                     xin_h, xnm_h, qhi_h, qn_h, xhi, xin, words, qhi, qn,
-                                     host_slices_, st);
+    short* qhi = fq_hi_.get(nq * W);
+    float* qn = fq_n_.get(nq);
+    const int rc = dmlp_host_ops_h2d(X, N_, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h, qhi_h,
+                                     qn_h, xhi, xin, words, qhi, qn, host_slices_, st);
     if (rc & 4) throw std::runtime_error("host operand copy failed");
-    if (rc) { rt_.sync(); return false; }  // outside the screen's range: the device path decides
+    if (rc) { rt_.sync(); return 1; }  // outside the screen's range: the device path decides
     HIPCHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), st));
     trace.mark("h2d_operands");
-    int* kd = kd_.get(Q_);
-    HIPCHK(hipMemcpyAsync(kd, in->k.data(), Q_ * 4, hipMemcpyHostToDevice, st));
-    int* qi = f_qi_.get(Q_);
-    if (qi_len_ < Q_) {  // identity query index (grow-only; a larger get() also resets it)
-      for (int64_t q = 0; q < Q_; ++q) id_h[q] = (int)q;
-      HIPCHK(hipMemcpyAsync(qi, id_h, Q_ * 4, hipMemcpyHostToDevice, st));
-      qi_len_ = Q_;
+    int* kd = kd_.get(nq);
+    HIPCHK(hipMemcpyAsync(kd, k, nq * 4, hipMemcpyHostToDevice, st));
+    int* qi = f_qi_.get(nq);
+    if (qi_len_ < nq) {  // identity query index (grow-only; a larger get() also resets it)
+      for (int64_t q = 0; q < nq; ++q) id_h[q] = (int)q;
+      HIPCHK(hipMemcpyAsync(qi, id_h, nq * 4, hipMemcpyHostToDevice, st));
+      qi_len_ = nq;
     }
     const int kcls = kmax_;
     const int cap = dmlp_screen_x1_cap(kcls);
-    const int S = LocalKnn::slices_stream((int)Q_, dmlp_screen_x1_cols(KT, kcls), nt,
+    const int S = LocalKnn::slices_stream((int)nq, dmlp_screen_x1_cols(KT, kcls), nt,
                                           dmlp_screen_x1_waves_per_cu(kcls),
                                           dmlp_screen_x1_min_slices(nt));
-    int* ci = f_ci_.get((size_t)Q_ * S * cap);
-    int* cc = f_cc_.get((size_t)Q_ * S);
-    float* ch = f_ch_.get((size_t)Q_ * S * 2);
-    DMLPCHK(dmlp_screen_x1(KT, 1, A_, xhi, xin, nt, N_, qhi, qn, qi, kd, (int)Q_, kcls, words,
+    int* ci = f_ci_.get((size_t)nq * S * cap);
+    int* cc = f_cc_.get((size_t)nq * S);
+    float* ch = f_ch_.get((size_t)nq * S * 2);
+    DMLPCHK(dmlp_screen_x1(KT, 1, A_, xhi, xin, nt, N_, qhi, qn, qi, kd, (int)nq, kcls, words,
                            words + 1, S, ci, cc, ch, st));
     // fp64 rows + labels behind the screen, on the side stream — enqueued after everything the
     // screen needs, so no small copy of the main stream queues behind them on the copy engine
     double* Xd = X_.get(N_ * A_);
     int* Ld = lab_.get(N_);
-    double* Qd = Qx_.get(Q_ * A_);
-    HIPCHK(hipMemcpyAsync(Xd, in->X.data(), N_ * A_ * 8, hipMemcpyHostToDevice, side_));
-    HIPCHK(hipMemcpyAsync(Ld, in->labels.data(), N_ * 4, hipMemcpyHostToDevice, side_));
-    HIPCHK(hipMemcpyAsync(Qd, in->Qx.data(), Q_ * A_ * 8, hipMemcpyHostToDevice, side_));
+    double* Qd = Qx_.get(nq * A_);
+    HIPCHK(hipMemcpyAsync(Xd, X, N_ * A_ * 8, hipMemcpyHostToDevice, side_));
+    HIPCHK(hipMemcpyAsync(Ld, labels, N_ * 4, hipMemcpyHostToDevice, side_));
+    HIPCHK(hipMemcpyAsync(Qd, Qx, nq * A_ * 8, hipMemcpyHostToDevice, side_));
     HIPCHK(hipEventRecord(ev_rows_, side_));
     trace.mark("screen");
     HIPCHK(hipStreamWaitEvent(st, ev_rows_, 0));
-    double* dd = d_.get(Q_ * kmax_);
-    int* ii = ids_.get(Q_ * kmax_);
-    int* lb = labout_.get(Q_);
-    uint64_t* cs = cs_.get(Q_);
-    int* stat = f_st_.get(Q_);
+    fo.dd = d_.get(nq * kmax_);
+    fo.ii = ids_.get(nq * kmax_);
+    fo.lb = labout_.get(nq);
+    fo.cs = cs_.get(nq);
+    int* stat = f_st_.get(nq);
     // (the refine writes every row's padding and status itself: no fill passes)
-    DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, nullptr, kd,
-                               (int)Q_, dd, ii, kmax_, Ld, lo_, hi_, lb, cs, stat, nullptr, st));
+    DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, nullptr,
+                               kd, (int)nq, fo.dd, fo.ii, kmax_, Ld, lo_, hi_, fo.lb, fo.cs, stat,
+                               nullptr, st));
     trace.mark("refine");
-    std::vector<int> sh(Q_);
-    HIPCHK(hipMemcpyAsync(sh.data(), stat, Q_ * 4, hipMemcpyDeviceToHost, st));
-    render(out, cs, lb, dd, ii);  // synchronizes the stream
-    for (int64_t q = 0; q < Q_; ++q)
-      if (sh[q]) return false;  // single-term overflow: redo the call on the general path
+    fo.st_h.resize(nq);
+    HIPCHK(hipMemcpyAsync(fo.st_h.data(), stat, nq * 4, hipMemcpyDeviceToHost, st));
+    return 0;
+  }
+
+  // Farm over the node-shared segment, P > 1: every rank runs fast_core on its own query block
+  // straight from the segment (its own PCIe link), renders its report lines on its GPU and copies
+  // them into the segment's output region at its byte offset (one MPI_Allgather of the lengths).
+  // Every fallback decision is agreed by all ranks before anyone acts on it (MPI_Allreduce), so
+  // the general farm below runs on all of them or on none.
+  bool farm_fast_shared(Output* out) {
+    const int P = rt_.world, r = rt_.rank;
+    if (exact_ || debug_ || N_ == 0 || Q_ == 0 || sh_.N != N_ || sh_.Q != Q_ || sh_.A != A_)
+      return false;
+    std::vector<int64_t> cnt, off;
+    block_partition(Q_, P, cnt, off);
+    const int64_t a = off[r], nl = cnt[r];
+    const int KT = std::max(1, (A_ + 31) / 32);
+    int ok = dmlp_screen_x1_qw(KT) > 0 && kmax_ <= 32 && kmax_ <= N_ && nl <= (1 << 30);
+    if (ok && nl) ok = *std::min_element(sh_.k + a, sh_.k + a + nl) >= 1;
+    MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+    if (!ok) return false;
+    if (!side_) {
+      HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
+    }
+    FastOut fo;
+    int bad = nl ? fast_core(sh_.X, sh_.labels, sh_.Qx + a * A_, sh_.k + a, nl, fo) : 0;
+    int64_t len = 0;
+    char* txt = nullptr;
+    int64_t* off_d = nullptr;
+    if (!bad && nl) {
+      off_d = off_.get(dmlp_format_scratch((int)nl));
+      txt = txt_.get((size_t)dmlp_format_bound((int)nl));
+      DMLPCHK(dmlp_format_report(fo.cs, (int)nl, (int)a, off_d, txt, rt_.stream));
+      HIPCHK(hipMemcpyAsync(total_h_.data(), off_d + nl, 8, hipMemcpyDeviceToHost, rt_.stream));
+      rt_.sync();
+      len = total_h_.data()[0];
+      for (int64_t q = 0; q < nl; ++q) bad |= fo.st_h[q] != 0;  // single-term overflow
+    }
+    MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+    if (bad) return false;  // every rank redoes the call on the general farm
+    trace.mark("format");
+    std::vector<int64_t> lens(P);
+    MPI_Allgather(&len, 1, MPI_INT64_T, lens.data(), 1, MPI_INT64_T, MPI_COMM_WORLD);
+    int64_t at = 0;
+    for (int i = 0; i < r; ++i) at += lens[i];
+    int64_t total = 0;
+    for (int i = 0; i < P; ++i) total += lens[i];
+    if (total > sh_.out_bytes) throw std::runtime_error("shared output region too small");
+    if (len) {
+      HIPCHK(hipMemcpyAsync(sh_.out + at, txt, len, hipMemcpyDeviceToHost, rt_.stream));
+      rt_.sync();
+    }
+    MPI_Barrier(MPI_COMM_WORLD);  // every block is in the segment
+    if (r == 0) {
+      out->kstride = kmax_;
+      out->shared_text = sh_.out;
+      out->text_len = (size_t)total;
+    }
     trace.mark("report");
     return true;
   }
+  SharedIn sh_;
   int64_t qi_len_ = 0;
 
   // ---------------------------------------------------------------- farm (bench_4)
@@ -685,6 +791,7 @@ class KnnCore {
     const int P = rt_.world;
     if (ooc_rows_ > 0 && N_ > ooc_rows_) return farm_ooc(in, out);
     if (P == 1 && fast_ && farm_fast(in, out)) return;
+    if (P > 1 && sh_.valid && fast_ && farm_fast_shared(out)) return;
     std::vector<int64_t> cnt, off;
     block_partition(Q_, P, cnt, off);
     double* Xd = X_.get(N_ * A_);

@@ -79,7 +79,7 @@ def test_python_dynamic_farm_shared_counter(case, np_):
     assert _python(path, np_, "farm", env) == expect
 
 
-def _native(path, np_, strategy, extra=(), env_extra=None):
+def _native(path, np_, strategy, extra=(), env_extra=None, want_err=False):
     if not os.path.exists(ENGINE):
         pytest.skip("knn_engine not built")
     if not os.path.exists(MPIEXEC):
@@ -91,7 +91,7 @@ def _native(path, np_, strategy, extra=(), env_extra=None):
     r = subprocess.run(cmd, capture_output=True, env=env, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     assert b"p2p check OK" in r.stderr, r.stderr.decode()[-2000:]
-    return r.stdout
+    return (r.stdout, r.stderr) if want_err else r.stdout
 
 
 @pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "ring"])
@@ -170,3 +170,24 @@ def test_python_sharded_image_render(case_x1, np_):
     assert _python(path, np_, "farm", env) == expect
     assert _python(path, np_, "farm", dict(env, KNN_IMAGE_SHARD="0")) == expect
     assert _python(bad_path, np_, "farm", env) == bad_expect
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_native_shared_ingress_farm(case, case_x1, np_):
+    """knn_engine KNN_INGRESS=shm: the parsed input in an MPI-3 node-shared window, every rank
+    runs the host-operand fast path on its own query block over its own link and writes its
+    report lines into the window; out-of-range data in one shard, or k > 32, sends every rank
+    to the general farm together.  == oracle bytes in all cases."""
+    (path, expect), (bad_path, bad_expect) = case_x1
+    env = {"KNN_INGRESS": "shm", "KNN_TRACE": "1"}
+    out, err = _native(path, np_, "farm", env_extra=env, want_err=True)
+    assert out == expect
+    # the per-rank fast path ran on every rank (its phases), not the general farm's
+    for r in range(np_):
+        assert f"rank {r} h2d_operands".encode() in err, err.decode()[-2000:]
+    assert b"distribute" not in err
+    out, err = _native(bad_path, np_, "farm", env_extra=env, want_err=True)
+    assert out == bad_expect
+    assert b"distribute" in err  # the general farm, on every rank
+    gpath, gexpect = case
+    assert _native(gpath, np_, "farm", env_extra=env) == gexpect
