@@ -54,7 +54,17 @@ def _root_arrays(be, inp):
 
 def _meta(comm, inp, with_shared=False):
     """Sizes, label range, kmax (engine.cpp:27-35) [+ whether the input is a node-shared
-    segment that every rank has mapped]."""
+    segment that every rank has mapped].  With a node-shared segment (mapped by every rank by
+    construction: share_input is collective) each rank scans it itself, no broadcast."""
+    if getattr(inp, "shared", False):
+        from .. import _lib
+        N, A = inp.X.shape
+        Q = inp.Qx.shape[0]
+        lmin, lmax = _lib.i32_range(inp.labels)
+        lo, hi = (lmin, lmax + 1) if N else (0, 1)
+        kmax = max(1, _lib.i32_range(inp.k)[1]) if Q else 1
+        out = [N, Q, A, lo, hi, kmax, 1]
+        return out if with_shared else out[:6]
     if comm.is_root:
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
@@ -297,9 +307,15 @@ def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, r
     text = None
     if not debug:
         with tr.phase("report"):
-            text = _shared_egress(comm, be, inp, cs, a, report)
+            text = _shared_egress(comm, be, inp, cs, a, report, lb=lb)
     if comm.world == 1:
         return lb, cs, d if debug else None, i if debug else None, text
+    if not debug:
+        # every rank's (label, checksum) rows already sit in the segment (_shared_egress)
+        if not comm.is_root:
+            return None
+        res = torch.from_numpy(inp.res)  # copies: the segment is reused by the next call
+        return res[:, 0].to(torch.int32), res[:, 1].contiguous(), None, None, text
     with tr.phase("gather"):
         packed = torch.stack([lb.to(torch.int64), cs], dim=1)
         allp = comm.gather_rows(packed, counts, (2,), torch.int64)
@@ -312,10 +328,13 @@ def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, r
     return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii, text
 
 
-def _shared_egress(comm, be, inp, cs, qid_base, report=None):
+def _shared_egress(comm, be, inp, cs, qid_base, report=None, lb=None):
     """Every rank renders its block's report lines and copies them straight into the shared
     segment's output region at its byte offset; rank 0 gets a view of the whole report.
-    report: knn_gpu_pipelined's speculative rendering (used when still valid)."""
+    report: knn_gpu_pipelined's speculative rendering (used when still valid).  P > 1: the
+    lengths go through the segment's per-rank slots and two segment barriers order the writes
+    (no RCCL collective, no extra device sync); with lb given, the block's (label, checksum)
+    rows are copied into the segment's results region in the same pass."""
     torch = _torch()
     if be.on_gpu and report is not None and report.get("valid"):
         dev_text, n_h = report["text"]
@@ -330,16 +349,29 @@ def _shared_egress(comm, be, inp, cs, qid_base, report=None):
         from ..utils.io import format_report
         host = format_report(cs.numpy().view(np.uint64), qid_base)
         n = len(host)
-    lens = [v[0] for v in comm.allgather_ints([n])]
+    if comm.world > 1:
+        inp.slots[comm.rank] = n
+        inp.barrier(comm.world)  # every length is in its slot
+        lens = [int(v) for v in inp.slots[:comm.world]]
+    else:
+        lens = [n]
     off = sum(lens[:comm.rank])
+    nq = cs.shape[0]
     if n:
         dst = torch.from_numpy(inp.out[off:off + n])
         if be.on_gpu:
-            dst.copy_(dev_text[:n])  # D2H into the page-locked segment
-            torch.cuda.current_stream().synchronize()
+            dst.copy_(dev_text[:n], non_blocking=True)  # D2H into the page-locked segment
         else:
             dst.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
-    comm.barrier()
+    if lb is not None and comm.world > 1 and nq:
+        rows = torch.from_numpy(inp.res[qid_base:qid_base + nq])
+        rows.copy_(torch.stack([lb.to(torch.int64), cs], dim=1), non_blocking=True)
+    if be.on_gpu:
+        torch.cuda.current_stream().synchronize()
+    if comm.world > 1:
+        inp.barrier(comm.world)  # every block's text and rows are in the segment
+    else:
+        comm.barrier()
     return memoryview(inp.out)[:sum(lens)].toreadonly() if comm.is_root else None
 
 

@@ -14,9 +14,15 @@ Egress is symmetric: with the static farm each rank renders the report lines of 
 block on its GPU and copies them over its own PCIe link into the segment's output region at its
 byte offset, so rank 0 ends up holding the whole report in host memory without a funnel.
 
+Control plane: with every rank mapping the segment, the static farm's per-call bookkeeping
+between the ranks of a node (report lengths, the "every block is written" barrier, the per-query
+(label, checksum) rows) goes through it — atomics and plain stores on shared memory instead of
+RCCL collectives with a host sync each.
+
 Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — a summary for tools;
 the KNN strategies re-scan the labels and k inside every timed call), two int64 work counters at
-byte 64 (the dynamic farm's chunk claims, alternating per call), then labels i32[N], k i32[Q],
+byte 64 (the dynamic farm's chunk claims, alternating per call), a barrier counter at byte 96,
+per-rank int64 slots from byte 128 (report lengths), then labels i32[N], k i32[Q],
 X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), res i64[2*Q] (the dynamic farm's
 (label, checksum) per query), each section 4096-byte aligned.
 """
@@ -61,6 +67,9 @@ class SharedInput(KNNInput):
         self.out = np.frombuffer(mm, np.uint8, 48 * Q + 64, off["out"])
         self.res = np.frombuffer(mm, np.int64, 2 * Q, off["res"]).reshape(Q, 2)
         self.counters = np.frombuffer(mm, np.int64, 2, 64)
+        self.slots = np.frombuffer(mm, np.int64, (_ALIGN - 128) // 8, 128)
+        self._bar = np.frombuffer(mm, np.int64, 1, 96)
+        self._nbar = 0  # barriers this process has entered
         self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
         self._pinned = False
 
@@ -93,6 +102,28 @@ class SharedInput(KNNInput):
         every process that maps the segment (a fetch-and-add on shared memory, no server)."""
         from .. import _lib
         return int(_lib.lib().dmlp_atomic_fetch_add_i64(self.counters.ctypes.data + 8 * slot, 1))
+
+    def barrier(self, world: int, timeout_s: float = 600.0):
+        """Barrier of the `world` processes mapping the segment: one atomic add on a monotonic
+        counter, then a spin until every rank's add of this round has landed (the atomic is
+        sequentially consistent, so stores before it are visible to every rank after it)."""
+        import time
+        from .. import _lib
+        L = _lib.lib()
+        p = self._bar.ctypes.data
+        self._nbar += 1
+        target = self._nbar * world
+        L.dmlp_atomic_fetch_add_i64(p, 1)
+        t0 = None
+        spins = 0
+        while L.dmlp_atomic_fetch_add_i64(p, 0) < target:
+            spins += 1
+            if spins > 2000:
+                if t0 is None:
+                    t0 = time.monotonic()
+                elif time.monotonic() - t0 > timeout_s:
+                    raise TimeoutError("node-shared barrier: a rank did not arrive")
+                time.sleep(0)
 
     def reset_counter(self, slot: int):
         from .. import _lib
