@@ -132,3 +132,39 @@ def test_debug_output(workload):
     first = list(outs.values())[0].decode().splitlines()
     assert first[0].startswith("Label for Query 0 : ")
     assert first[1].startswith("Top-")
+
+
+def _segment_worker(path, rank, world, rounds, q):
+    from distributed_machine_learning_project_amd.utils.shm import SharedInput
+    s = SharedInput.attach(path)
+    seen = []
+    for r in range(rounds):
+        s.slots[rank] = 1000 * r + rank   # a value per rank and round
+        s.barrier(world)
+        seen.append([int(v) for v in s.slots[:world]])
+        s.barrier(world)                  # nobody overwrites a slot before everyone read it
+    q.put((rank, seen))
+
+
+def test_segment_barrier_and_slots(tmp_path):
+    """The node-shared segment's control plane (utils/shm.py): per-rank slots published before
+    a barrier are seen by every rank after it, round after round (the static farm's report
+    lengths); 4 processes, 25 rounds."""
+    import multiprocessing as mp
+    from distributed_machine_learning_project_amd.utils.io import generate
+    from distributed_machine_learning_project_amd.utils.shm import SharedInput
+    s = SharedInput.create(generate(64, 16, 4, 0.0, 1.0, 1, 4, 3, seed=1), directory=str(tmp_path))
+    world, rounds = 4, 25
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_segment_worker, args=(s.path, r, world, rounds, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    s.close()
+    for rank in range(world):
+        for r, row in enumerate(got[rank]):
+            assert row == [1000 * r + i for i in range(world)]
