@@ -217,16 +217,22 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     """Static farm over a node-shared input segment (utils/shm.py): every rank copies its own
     query block host->GPU over its own PCIe link — no funnel through GPU 0.  The replicated
     dataset (bench_4 @0xc199 broadcasts it) arrives by KNN_DATA_INGRESS:
-      allgather (default, P > 1): each rank H2Ds 1/P of the rows, one RCCL all-gather over xGMI
-                 completes the replica — PCIe bytes per GPU drop from N*A*8 to N*A*8/P and the
-                 host memory reads from P*N*A*8 to N*A*8;
-      h2d:       every rank copies the whole dataset from the segment;
+      allgather: each rank H2Ds 1/P of the rows, one RCCL all-gather over xGMI completes the
+                 replica — PCIe bytes per GPU drop from N*A*8 to N*A*8/P and the host memory
+                 reads from P*N*A*8 to N*A*8, but the all-gather's kernels wait for the screen;
+      h2d (default): every rank copies the whole dataset from the segment, behind the
+                 screen on the copy engines (the bf16 screen image: 1/P rendered per rank +
+                 one all-gather before the screen, KNN_IMAGE_SHARD);
       bcast:     rank 0 copies it, one RCCL broadcast."""
     import os
     torch = _torch()
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
-    mode = os.environ.get("KNN_DATA_INGRESS", "allgather") if comm.world > 1 else "h2d"
+    # P > 1 default: every GPU copies the fp64 rows over its own link (DMA engines, behind the
+    # screen); an RCCL all-gather of them would need CUs the screen holds (it fills every SIMD's
+    # register file), so it would run after the screen, on the critical path.  The bf16 screen
+    # image is still sharded + all-gathered (before the screen, when the GPU is idle).
+    mode = os.environ.get("KNN_DATA_INGRESS", "h2d") if comm.world > 1 else "h2d"
     max_rows = int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)
     if max_rows and N > max_rows:
         # out-of-core: the replica does not fit the device budget, stream it from the segment
@@ -283,8 +289,13 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
         # per-GPU H2D: the query chunks land while the earlier chunks already screen
         with tr.phase("h2d+compute"):
             kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
+            shard_img = (os.environ.get("KNN_IMAGE_SHARD", "1") == "1"
+                         and comm.on_gpu and comm.world > 1)
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax, report=rep, k_range=_lib_range(kl_h))
+                                       kstride=kmax, report=rep, k_range=_lib_range(kl_h),
+                                       image_shard=(comm.rank, comm.world, comm.allgather_into,
+                                                    comm.allreduce_max_)
+                                       if shard_img else None)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, rep)
     with tr.phase("h2d"):
         X = lab = None
