@@ -366,10 +366,13 @@ def test_merge_and_finalize(torch_cuda):
 
 
 @pytest.mark.parametrize("Lists,kin,kout", [(8, 16, 16), (8, 128, 128), (3, 40, 64), (64, 4, 8),
-                                             (2, 24, 32), (1, 8, 12), (12, 16, 16)])
+                                             (2, 24, 32), (1, 8, 12), (12, 16, 16),
+                                             (5, 13, 16), (2, 7, 9)])
 def test_merge_rank_shapes(torch_cuda, Lists, kin, kout):
-    """K4 merge at shard-merge shapes: disjoint ids, padded (+inf, -1) suffixes of random length,
-    per-query k in [0, kout] (bench_2 @0xbc70 custom op semantics via merge_cpu)."""
+    """K4 merge at shard-merge shapes (kin % 4 == 0 and L <= 8: the windowed register kernel;
+    other kin: the one-load-per-output register kernel; L > 8: the LDS merge path): disjoint
+    ids, padded (+inf, -1) suffixes of random length, per-query k in [0, kout] (bench_2 @0xbc70
+    custom op semantics via merge_cpu)."""
     torch = torch_cuda
     rng = np.random.default_rng(Lists * 1000 + kin)
     Q = 777

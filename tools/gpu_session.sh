@@ -73,6 +73,7 @@ for task in "$@"; do
     merge)
       step merge 300 rocprofv3 --kernel-trace --stats -d "$OUT/merge" -o run --output-format csv \
           -- python3 tools/merge_bench.py --p 8 --q 131072 --ks 16,128
+      DMLP_MERGE_WIN=0 step merge_seq 120 python3 tools/merge_bench.py --p 8 --q 131072 --ks 16,128
       find "$OUT/merge" -name '*kernel_stats.csv' -exec sh -c 'head -8 "$1" | cut -c1-160' _ {} \; ;;
     hostprof)
       step hostprof 300 python tools/host_profile.py --steps 100
