@@ -283,6 +283,22 @@ class KnnCore {
     if (r % 2 == 0) { snd(cur, n, to, st); rcv(nxt, n, from, st); }
     else { rcv(nxt, n, from, st); snd(cur, n, to, st); }
   }
+  // Equal-size all-gather of `bytes` per rank from `chunk` into `full` (rank order), on the engine
+  // stream: one ncclAllGather over xGMI, or host-staged MPI_Allgather in the test data plane.
+  void allgather_bytes(const void* chunk, void* full, int64_t bytes) {
+    sent_ += bytes * (rt_.world - 1);
+    if (!rt_.host_plane) {
+      NCCLCHK(ncclAllGather(chunk, full, (size_t)bytes, ncclUint8, rt_.nccl, rt_.stream));
+      return;
+    }
+    if (bytes > (int64_t)INT32_MAX / rt_.world) throw std::runtime_error("all-gather too large");
+    std::vector<char> h(bytes), all(bytes * rt_.world);
+    HIPCHK(hipMemcpyAsync(h.data(), chunk, bytes, hipMemcpyDeviceToHost, rt_.stream));
+    rt_.sync();
+    MPI_Allgather(h.data(), (int)bytes, MPI_BYTE, all.data(), (int)bytes, MPI_BYTE, MPI_COMM_WORLD);
+    HIPCHK(hipMemcpyAsync(full, all.data(), bytes * rt_.world, hipMemcpyHostToDevice, rt_.stream));
+    rt_.sync();  // `all` dies here
+  }
   template <typename T>
   void bcast(T* p, int64_t n) {
     const int64_t bytes = n * (int64_t)sizeof(T);
@@ -492,8 +508,8 @@ class KnnCore {
   // Returns false (nothing done) when the input is outside this path: k not in [1, 32] or
   // k > N, A > 64, data outside the screen's range; a query whose candidates overflow makes the
   // whole call fall back too (rare: data too tight for the single-term bound).
-  DevBuf<short> fx_hi_, fq_hi_;
-  DevBuf<float> fx_in_, fq_n_, f_ch_;
+  DevBuf<short> fx_hi_, fq_hi_, fx_hic_;
+  DevBuf<float> fx_in_, fq_n_, f_ch_, fx_inc_;
   DevBuf<unsigned> f_words_;
   DevBuf<double> f_mu_;
   DevBuf<int> f_ci_, f_cc_, f_qi_, f_st_;
@@ -529,11 +545,18 @@ class KnnCore {
     uint64_t* cs = nullptr;
     std::vector<int> st_h;
   };
+  // shard = true (node-shared farm, P > 1): this rank renders only its 1/P tile range of the
+  // dataset's screen image and one all-gather completes it; the data-range verdict and the max
+  // norm are agreed over MPI on the host first, so every rank takes the same branch.
   int fast_core(const double* X, const int* labels, const double* Qx, const int* k, int64_t nq,
-                FastOut& fo) {
+                FastOut& fo, bool shard = false) {
     const int KT = std::max(1, (A_ + 31) / 32);
     hipStream_t st = rt_.stream;
     const int64_t nt = (N_ + 63) / 64, W = (int64_t)KT * 32;
+    const int P = shard ? rt_.world : 1;
+    const int64_t tpr = (nt + P - 1) / P;  // tiles per rank (the last ranks' tails pad)
+    const int64_t t0 = shard ? std::min<int64_t>(rt_.rank * tpr, nt) : 0;
+    const int64_t t1 = shard ? std::min<int64_t>(t0 + tpr, nt) : nt;
     // page-locked staging for the rendered operands (host_ops_h2d copies from it)
     const size_t b_xhi = nt * 64 * W * 2, b_xin = nt * 64 * 4, b_qhi = nq * W * 2, b_qn = nq * 4;
     auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -549,15 +572,34 @@ class KnnCore {
     double* mu_h = (double*)hp; hp += up(A_ * 8);
     int* id_h = (int*)hp;
     dmlp_cpu_center(X, N_, A_, mu_h);
-    short* xhi = fx_hi_.get(nt * 64 * W);
-    float* xin = fx_in_.get(nt * 64);
+    short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
+    float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
+    short* xhi_c = shard ? fx_hic_.get(tpr * 64 * W) : xhi;
+    float* xin_c = shard ? fx_inc_.get(tpr * 64) : xin;
     unsigned* words = f_words_.get(2);  // [0] xnmax bits, [1] bad (0: the host checked ranges)
     short* qhi = fq_hi_.get(nq * W);
     float* qn = fq_n_.get(nq);
-    const int rc = dmlp_host_ops_h2d(X, N_, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h, qhi_h,
-                                     qn_h, xhi, xin, words, qhi, qn, host_slices_, st);
+    int rc = dmlp_host_ops_h2d_tiles(X, N_, t0, t1, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h,
+                                     qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn, host_slices_, st);
     if (rc & 4) throw std::runtime_error("host operand copy failed");
-    if (rc) { rt_.sync(); return 1; }  // outside the screen's range: the device path decides
+    if (shard) {
+      // every rank's verdict and max norm (host values) before any device collective
+      unsigned v[2] = {(unsigned)(rc & 3), *xnm_h};
+      MPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_UNSIGNED, MPI_MAX, MPI_COMM_WORLD);
+      if (v[0]) { rt_.sync(); return 1; }  // somewhere outside the screen's range
+      xnm_h[1] = v[1];  // (a second pinned word: the first one's copy may still be in flight)
+      HIPCHK(hipMemcpyAsync(words, xnm_h + 1, 4, hipMemcpyHostToDevice, st));
+      allgather_bytes(xhi_c, xhi, tpr * 64 * W * 2);
+      allgather_bytes(xin_c, xin, tpr * 64 * 4);
+    } else if (rc) {
+      rt_.sync();
+      return 1;  // outside the screen's range: the device path decides
+    }
+    if (nq == 0) {  // a rank without queries (Q < P) took part in the collectives only
+      fo.st_h.clear();
+      rt_.sync();
+      return 0;
+    }
     HIPCHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), st));
     trace.mark("h2d_operands");
     int* kd = kd_.get(nq);
@@ -626,7 +668,8 @@ class KnnCore {
       HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
     }
     FastOut fo;
-    int bad = nl ? fast_core(sh_.X, sh_.labels, sh_.Qx + a * A_, sh_.k + a, nl, fo) : 0;
+    // (every rank enters fast_core, even with no queries: the image all-gather is collective)
+    int bad = fast_core(sh_.X, sh_.labels, sh_.Qx + a * A_, sh_.k + a, nl, fo, image_shard_);
     int64_t len = 0;
     char* txt = nullptr;
     int64_t* off_d = nullptr;
@@ -663,6 +706,8 @@ class KnnCore {
     return true;
   }
   SharedIn sh_;
+  // KNN_IMAGE_SHARD=0: every rank renders the whole screen image (A/B)
+  bool image_shard_ = !(getenv("KNN_IMAGE_SHARD") && std::string(getenv("KNN_IMAGE_SHARD")) == "0");
   int64_t qi_len_ = 0;
 
   // ---------------------------------------------------------------- farm (bench_4)

@@ -191,3 +191,5 @@ def test_native_shared_ingress_farm(case, case_x1, np_):
     assert b"distribute" in err  # the general farm, on every rank
     gpath, gexpect = case
     assert _native(gpath, np_, "farm", env_extra=env) == gexpect
+    # every rank renders the whole screen image instead of its 1/np (A/B switch)
+    assert _native(path, np_, "farm", env_extra=dict(env, KNN_IMAGE_SHARD="0")) == expect
