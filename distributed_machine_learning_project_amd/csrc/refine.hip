@@ -897,12 +897,50 @@ __global__ void k_fmt_len(const uint64_t* __restrict__ cs, int nq, int qid_base,
   if (threadIdx.x == 1023) blocksum[blockIdx.x] = sh[1023];
 }
 
-__global__ void k_fmt_scan_blocks(int64_t* __restrict__ blocksum, int nb) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    int64_t acc = 0;
-    for (int b = 0; b < nb; ++b) { const int64_t v = blocksum[b]; blocksum[b] = acc; acc += v; }
-    blocksum[nb] = acc;
+// Exclusive scan of the block sums in place (+ the total at [nb]): one 1024-thread block,
+// 1024 sums per LDS pass with a running carry (a single-thread loop cost ~15 us at 128 blocks —
+// one dependent global round trip per block).
+__global__ void __launch_bounds__(1024) k_fmt_scan_blocks(int64_t* __restrict__ blocksum, int nb) {
+  __shared__ int64_t sh[1024];
+  int64_t carry = 0;
+  for (int c0 = 0; c0 < nb; c0 += 1024) {
+    const int b = c0 + (int)threadIdx.x;
+    const int64_t v = b < nb ? blocksum[b] : 0;
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+      const int64_t t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (b < nb) blocksum[b] = carry + sh[threadIdx.x] - v;  // exclusive
+    carry += sh[1023];
+    __syncthreads();  // sh is rewritten by the next pass
   }
+  if (threadIdx.x == 0) blocksum[nb] = carry;
+}
+
+// decimal digits of v written backwards so that the last one lands at txt[end - 1]: two 64-bit
+// divisions by 1e9 at most, then 32-bit digit extraction (no per-digit 64-bit division, no
+// dynamically indexed scratch buffer)
+__device__ __forceinline__ void put_dec(char* txt, int end, uint64_t v) {
+  int p = end;
+  while (v >= 1000000000ull) {
+    const uint64_t q = v / 1000000000ull;
+    uint32_t r = (uint32_t)(v - q * 1000000000ull);
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      txt[--p] = (char)('0' + r % 10u);
+      r /= 10u;
+    }
+    v = q;
+  }
+  uint32_t r = (uint32_t)v;
+  do {
+    txt[--p] = (char)('0' + r % 10u);
+    r /= 10u;
+  } while (r);
 }
 
 // Each block renders its 1024 lines into LDS, then stores the block's byte range with dword
@@ -924,16 +962,12 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
     int pos = (int)(endl - len);
     const char* pre = "Query ";
     for (int c = 0; c < 6; ++c) txt[pos++] = pre[c];
-    char tmp[24];
-    int n = 0;
-    uint64_t t = (uint64_t)qid;
-    do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
-    while (n) txt[pos++] = tmp[--n];
+    pos += ndig_u64((uint64_t)qid);
+    put_dec(txt, pos, (uint64_t)qid);
     const char* mid = " checksum: ";
     for (int c = 0; c < 11; ++c) txt[pos++] = mid[c];
-    t = v;
-    do { tmp[n++] = (char)('0' + t % 10); t /= 10; } while (t);
-    while (n) txt[pos++] = tmp[--n];
+    pos += ndig_u64(v);
+    put_dec(txt, pos, v);
     txt[pos++] = '\n';
   }
   __syncthreads();
@@ -1117,7 +1151,7 @@ extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int6
   int64_t* blocksum = line_off + nq + 1;
   hipLaunchKernelGGL(k_fmt_len, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off, blocksum);
   DMLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_fmt_scan_blocks, dim3(1), dim3(64), 0, st, blocksum, nb);
+  hipLaunchKernelGGL(k_fmt_scan_blocks, dim3(1), dim3(1024), 0, st, blocksum, nb);
   DMLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_fmt_write, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off,
                      blocksum, out);
