@@ -31,19 +31,22 @@ namespace {
 constexpr double kMaxAbs = 1.0e15;
 constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch of the data prep
 
-// pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN, default 40000)
+// pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN, default 100000:
+// ~2 ms, so workers are still awake when the next call's render starts instead of paying a
+// futex wake each step; the pool size leaves CPU quota for that, see pool_threads)
 int spin_budget() {
   static const int v = [] {
     const char* e = std::getenv("DMLP_POOL_SPIN");
-    return e ? std::max(0, std::atoi(e)) : 40000;
+    return e ? std::max(0, std::atoi(e)) : 100000;
   }();
   return v;
 }
 
 // Persistent workers: a per-call std::thread spawn (tens of microseconds each) would cost more
-// than the conversion itself.  After a job a worker spins ~100 us on the generation counter
-// before it sleeps on the condition variable, so back-to-back jobs (the chunked host-ops
-// pipeline dispatches one per PCIe slice) start in about a microsecond instead of a futex wake.
+// than the conversion itself.  After a job a worker spins (spin_budget) on the generation
+// counter before it sleeps on the condition variable, so back-to-back jobs (the chunked host-ops
+// pipeline dispatches one per PCIe slice, and the next call's follow within a step) start in
+// about a microsecond instead of a futex wake.
 class Pool {
  public:
   // The worker count is fixed before any worker starts: workers read it (size(),
@@ -146,12 +149,17 @@ int pool_threads() {
   int n = 0;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
   if (n <= 0) n = (int)std::thread::hardware_concurrency();
-  if (const int c = cgroup_cpus()) n = std::min(n, c);
   int local = 1;
   for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"})
     if (const char* e = std::getenv(v)) { local = std::max(1, std::atoi(e)); break; }
   // ranks pinned to disjoint CPU sets see only their own share; a shared mask is split
   if (local > 1 && n >= 2 * local) n /= local;
+  // the cgroup quota is shared by the node's ranks too; leave 2 CPUs of each rank's share to
+  // its main thread and the HIP runtime, so spinning workers never run the quota out
+  if (const int c = cgroup_cpus()) {
+    const int share = std::max(1, c / local);
+    n = std::min(n, share > 4 ? share - 2 : share);
+  }
   return std::max(1, std::min(n, kMaxPool));
 }
 
