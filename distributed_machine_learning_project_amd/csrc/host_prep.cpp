@@ -31,13 +31,18 @@ namespace {
 constexpr double kMaxAbs = 1.0e15;
 constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch of the data prep
 
-// pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN, default 100000:
-// ~2 ms, so workers are still awake when the next call's render starts instead of paying a
-// futex wake each step; the pool size leaves CPU quota for that, see pool_threads)
+// pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN; default 100000,
+// ~2 ms, so one rank's workers are still awake when its next call's render starts instead of
+// paying a futex wake each step — the pool size leaves CPU quota for that, see pool_threads;
+// 40000 with several ranks per node, whose pools share the cores)
 int spin_budget() {
   static const int v = [] {
     const char* e = std::getenv("DMLP_POOL_SPIN");
-    return e ? std::max(0, std::atoi(e)) : 100000;
+    if (e) return std::max(0, std::atoi(e));
+    // several ranks on the node (their pools share the cores): the shorter round-1 spin
+    for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"})
+      if (const char* l = std::getenv(v)) return std::atoi(l) > 1 ? 40000 : 100000;
+    return 100000;
   }();
   return v;
 }
