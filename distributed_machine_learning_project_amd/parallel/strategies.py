@@ -62,7 +62,9 @@ def _meta(comm, inp, with_shared=False):
         Q = inp.Qx.shape[0]
         lmin, lmax = _lib.i32_range(inp.labels)
         lo, hi = (lmin, lmax + 1) if N else (0, 1)
-        kmax = max(1, _lib.i32_range(inp.k)[1]) if Q else 1
+        kmin, kmx = _lib.i32_range(inp.k) if Q else (0, 0)
+        kmax = max(1, kmx) if Q else 1
+        inp.k_range_all = (kmin, kmx)  # this call's k bounds (the farm's world-1 dispatch)
         out = [N, Q, A, lo, hi, kmax, 1]
         return out if with_shared else out[:6]
     if comm.is_root:
@@ -292,7 +294,9 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             shard_img = (os.environ.get("KNN_IMAGE_SHARD", "1") == "1"
                          and comm.on_gpu and comm.world > 1)
             d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax, report=rep, k_range=_lib_range(kl_h),
+                                       kstride=kmax, report=rep,
+                                       k_range=(inp.k_range_all if comm.world == 1
+                                                else _lib_range(kl_h)),
                                        image_shard=(comm.rank, comm.world, comm.allgather_into,
                                                     comm.allreduce_max_)
                                        if shard_img else None)
