@@ -165,6 +165,7 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "warmup_steps_run": warm,
+            "numa_node": Comm._numa,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "weak",
