@@ -74,12 +74,17 @@ class SharedInput(KNNInput):
         self._pinned = False
 
     @staticmethod
-    def create(inp: KNNInput, directory: str = "/dev/shm") -> "SharedInput":
+    def create(inp: KNNInput, directory: str = "/dev/shm", query_nodes=None) -> "SharedInput":
+        """query_nodes: [(first query, end query, NUMA node), ...] — the query rows (and their
+        report bytes) of each block are placed on that node before they are written (the GPU
+        that reads them hangs off it); the dataset is interleaved over the nodes named."""
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
-        _, total = _layout(N, Q, A)
+        off, total = _layout(N, Q, A)
         path = os.path.join(directory, f"dmlp_input_{os.getpid()}_{uuid.uuid4().hex[:8]}")
         mm = np.memmap(path, np.uint8, "w+", shape=(total,))
+        if query_nodes:
+            _place(mm, off, N, Q, A, query_nodes)
         np.frombuffer(mm, np.int64, 4, 0)[:] = [_MAGIC, N, Q, A]
         s = SharedInput(mm, path, N, Q, A, owner=True)
         s.labels[:] = inp.labels
@@ -165,6 +170,50 @@ class SharedInput(KNNInput):
         self.unlink()
 
 
+def _mbind(addr: int, length: int, nodes, mode: int) -> bool:
+    """mbind(2) on [addr, addr + length) (page-aligned inward) — the policy of the shared tmpfs
+    object, so it decides where the pages land when rank 0 writes them.  False on any failure."""
+    import ctypes
+    page = os.sysconf("SC_PAGE_SIZE")
+    a0 = (addr + page - 1) // page * page
+    a1 = (addr + length) // page * page
+    if a1 <= a0 or not nodes or max(nodes) >= 64:
+        return False
+    mask = ctypes.c_ulong(sum(1 << n for n in set(nodes)))
+    libc = ctypes.CDLL(None, use_errno=True)
+    SYS_mbind = 237  # x86_64
+    rc = libc.syscall(SYS_mbind, ctypes.c_void_p(a0), ctypes.c_ulong(a1 - a0), ctypes.c_int(mode),
+                      ctypes.byref(mask), ctypes.c_ulong(65), ctypes.c_uint(0))
+    return rc == 0
+
+
+def _place(mm, off, N, Q, A, query_nodes):
+    """NUMA placement of a fresh segment (best effort: any failure leaves the default policy)."""
+    MPOL_BIND, MPOL_INTERLEAVE = 2, 3
+    base = mm.ctypes.data
+    nodes = sorted({n for _, _, n in query_nodes if n >= 0})
+    if not nodes:
+        return
+    if len(nodes) > 1:
+        _mbind(base + off["X"], 8 * N * A, nodes, MPOL_INTERLEAVE)
+    for a, b, n in query_nodes:
+        if n >= 0 and b > a:
+            _mbind(base + off["Qx"] + 8 * A * a, 8 * A * (b - a), [n], MPOL_BIND)
+            _mbind(base + off["out"] + 48 * a, 48 * (b - a), [n], MPOL_BIND)
+
+
+def gpu_numa_node(dev_index: int) -> int:
+    """NUMA node of GPU dev_index's PCIe root (sysfs), -1 if unknown."""
+    try:
+        import torch
+        p = torch.cuda.get_device_properties(dev_index)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            return int(f.read().strip())
+    except (OSError, ValueError, AttributeError, RuntimeError, ImportError):
+        return -1
+
+
 def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedInput:
     """Collective: rank 0 places `inp` in a node-shared segment, every rank maps it.  Single
     node only (all ranks must see the same /dev/shm)."""
@@ -172,7 +221,17 @@ def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedIn
     path = None
     s = None
     if comm.is_root:
-        s = SharedInput.create(inp)
+        qn = None
+        if comm.on_gpu and comm.world > 1 and os.environ.get("KNN_NUMA_BIND", "1") != "0":
+            # each rank's query block next to its GPU (ranks r -> device r mod devices, as
+            # Comm.init binds them; the static farm's balanced blocks)
+            import torch
+            from ..parallel.comm import block_partition
+            ndev = max(1, torch.cuda.device_count())
+            counts, displs = block_partition(inp.Qx.shape[0], comm.world)
+            qn = [(displs[r], displs[r] + counts[r], gpu_numa_node(r % ndev))
+                  for r in range(comm.world)]
+        s = SharedInput.create(inp, query_nodes=qn)
         path = s.path
     if comm.world > 1:
         obj = [path]
