@@ -7,7 +7,10 @@
 #include <mpi.h>
 #include <rccl/rccl.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <thread>
 #include <cmath>
@@ -136,6 +139,44 @@ struct Runtime {
   // and MPI (several ranks may then share one GPU — test mode)
   bool host_plane = getenv("KNN_DATA_PLANE") && std::string(getenv("KNN_DATA_PLANE")) == "host";
 
+  int numa = -1;  // NUMA node this rank is bound to (bind_numa), -1 if none
+  // Pin this rank to the CPUs of its GPU's NUMA node (within its affinity): first-touch then puts
+  // the page-locked arenas, the parsed input and the render pool's threads next to the GPU's
+  // PCIe root (the Python twin: parallel/comm.py Comm.bind_numa; profiles/r3m_numa.txt).
+  // KNN_NUMA_BIND=0 disables it.
+  static int bind_numa(int dev) {
+    if (getenv("KNN_NUMA_BIND") && std::string(getenv("KNN_NUMA_BIND")) == "0") return -1;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return -1;
+    for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+    int node = -1;
+    if (FILE* f = std::fopen((std::string("/sys/bus/pci/devices/") + bus + "/numa_node").c_str(), "r")) {
+      if (std::fscanf(f, "%d", &node) != 1) node = -1;
+      std::fclose(f);
+    }
+    if (node < 0) return -1;
+    FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
+    if (!f) return -1;
+    cpu_set_t want, have;
+    CPU_ZERO(&want);
+    int lo = 0, hi = 0;
+    char sep = 0;
+    while (std::fscanf(f, "%d", &lo) == 1) {
+      hi = lo;
+      sep = (char)std::fgetc(f);
+      if (sep == '-') {
+        if (std::fscanf(f, "%d", &hi) != 1) break;
+        sep = (char)std::fgetc(f);
+      }
+      for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c) CPU_SET(c, &want);
+      if (sep != ',') break;
+    }
+    std::fclose(f);
+    if (sched_getaffinity(0, sizeof(have), &have) != 0) return -1;
+    CPU_AND(&want, &want, &have);
+    if (CPU_COUNT(&want) == 0 || sched_setaffinity(0, sizeof(want), &want) != 0) return -1;
+    return node;
+  }
   void init(bool need_gpu = true) {
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
     MPI_Comm_size(MPI_COMM_WORLD, &world);
@@ -150,6 +191,7 @@ struct Runtime {
     if (ndev == 0) throw std::runtime_error("no HIP device");
     device = local % ndev;
     HIPCHK(hipSetDevice(device));
+    numa = bind_numa(device);  // before the arenas: their pages land next to the GPU
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     reserve_arenas();
     if (world > 1 && !host_plane) {
