@@ -168,3 +168,31 @@ def test_segment_barrier_and_slots(tmp_path):
     for rank in range(world):
         for r, row in enumerate(got[rank]):
             assert row == [1000 * r + i for i in range(world)]
+
+
+def test_segment_numa_placement(tmp_path, monkeypatch):
+    """NUMA placement of the node-shared segment (utils/shm.py _place/_mbind) is best effort and
+    never changes what is stored: a segment created with per-block query nodes holds the same
+    bytes as one created without, and an attach sees them.  Also: KNN_NUMA_BIND=0 turns the
+    per-rank binding off (parallel/comm.py Comm.bind_numa) and _mbind refuses empty / huge masks."""
+    from distributed_machine_learning_project_amd.parallel.comm import Comm
+    from distributed_machine_learning_project_amd.utils import shm
+    from distributed_machine_learning_project_amd.utils.io import generate
+    inp = generate(2048, 3000, 16, 0.0, 1.0, 1, 8, 5, seed=3)
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    plain = shm.SharedInput.create(inp, directory=str(tmp_path / "a"))
+    placed = shm.SharedInput.create(inp, directory=str(tmp_path / "b"),
+                                    query_nodes=[(0, 1500, 0), (1500, 3000, 0)])
+    again = shm.SharedInput.attach(placed.path)
+    for s in (placed, again):
+        assert s.N == plain.N and s.Q == plain.Q and s.A == plain.A
+        for name in ("X", "labels", "Qx", "k"):
+            assert np.array_equal(getattr(s, name), getattr(plain, name)), name
+    for s in (again, placed, plain):
+        s.close()
+    buf = np.zeros(1 << 16, np.uint8)
+    assert not shm._mbind(buf.ctypes.data, buf.nbytes, [], 2)
+    assert not shm._mbind(buf.ctypes.data, buf.nbytes, [64], 2)
+    monkeypatch.setenv("KNN_NUMA_BIND", "0")
+    assert Comm.bind_numa(0) == -1
