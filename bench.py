@@ -17,9 +17,18 @@ synthetic data with generate_input.py's distribution at the only shape BASELINE.
 number for: N=100000 points, A=32 attributes in [0,1000] (6 decimals), k=16, 10 labels, seed 42;
 Q = --q-per-gpu queries per GPU (default 2^17: whole rounds of 64-query waves on the 1024 SIMDs;
 weak scaling: per-GPU work is fixed).
-vs_baseline divides by 443.5 queries/s: BASELINE.md's best number at that shape (student
-engine.cpp, np=4: 1000 queries in 2255 ms; the CPU reference's cost per query does not depend on
-Q at fixed N, A, k).
+vs_baseline is null: BASELINE.md publishes no number for any bench_N.  The only number it quotes
+at this shape is the student engine.cpp on an 8-vCPU CPU sandbox (np=4: 1000 queries in 2255 ms);
+the ratio to that is reported under its own name, vs_student_engine_cpu_np4.
+
+Ranks: `python bench.py --gpus N` with N > 1 and no torchrun environment launches N ranks itself
+(torch.distributed.run as a child process, before this process makes any GPU call) and exits with
+their exit code; it refuses to run when fewer than N GPUs are visible, unless DMLP_DATA_PLANE=host
+(the one-GPU rehearsal: N ranks share the GPU over the host-staged gloo plane).  Under torchrun,
+--gpus must equal WORLD_SIZE.  Rank 0's JSON then carries the world the process group really had
+(rccl_world / data_plane), an RCCL all-reduce check and its bus bandwidth, and per rank: ms/step,
+NUMA node, phase times and PCIe / collective bytes from an untimed traced pass after the timed
+steps, plus a rank-by-rank comparison of the collective sequence (parallel/dist_api.py).
 """
 from __future__ import annotations
 
@@ -36,7 +45,36 @@ if ROOT not in sys.path:
 BASELINE_QPS = 1000.0 / 2.255  # engine.cpp np=4, N=1e5 Q=1e3 A=32 k=16 -> 2255 ms
 
 
+def _launch_ranks(a, argv):
+    """`python bench.py --gpus N` outside torchrun: start N ranks (one per GPU) and return their
+    exit code; None when this process is itself the (only) rank.  Nothing here initialises HIP
+    (torch.cuda.device_count() does not), so the children own the GPUs."""
+    if "WORLD_SIZE" in os.environ or a.gpus <= 1 or a.harness != "python":
+        return None
+    import subprocess
+    import torch
+    host_plane = os.environ.get("DMLP_DATA_PLANE", "") == "host"
+    ndev = torch.cuda.device_count()
+    if ndev < a.gpus and not host_plane:
+        print(f"[bench] --gpus {a.gpus} but only {ndev} GPU(s) visible; refusing to bench fewer "
+              f"ranks than asked (DMLP_DATA_PLANE=host rehearses {a.gpus} ranks on one GPU)",
+              file=sys.stderr, flush=True)
+        return 2
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     # >= 200 steps: the timed region is >= 0.5 s at the bench shape (a driver-side busy sampler
@@ -67,6 +105,9 @@ def main(argv=None):
                     help="compare a SHA-256 digest of the WHOLE rank-0 report (every query line) "
                          "with the CPU oracle's (C++ fp64 brute force, outside the timed region)")
     ap.add_argument("--no-busbw", action="store_true")
+    ap.add_argument("--diag-steps", type=int, default=3,
+                    help="untimed traced steps after the timed ones: per-rank phase times, PCIe "
+                         "and collective bytes, collective-sequence check (0: skip)")
     ap.add_argument("--harness", default="python", choices=["python", "native", "dropin"],
                     help="native: time the reference-contract binary (knn_engine: parse untimed, "
                          "'Time taken' = KNN + report + barrier, common.cpp:121-131) at this "
@@ -74,6 +115,9 @@ def main(argv=None):
     a = ap.parse_args(argv)
     if a.harness in ("native", "dropin"):
         return _bench_native(a)
+    rc = _launch_ranks(a, argv)
+    if rc is not None:
+        return rc
 
     import numpy as np
     import torch
@@ -82,10 +126,23 @@ def main(argv=None):
     from distributed_machine_learning_project_amd.parallel.engine import Engine
     from distributed_machine_learning_project_amd.utils.io import generate
 
+    host_plane = os.environ.get("DMLP_DATA_PLANE", "") == "host"
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world_env:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world_env}: refusing to label a "
+              f"{world_env}-rank run as {a.gpus} GPUs", file=sys.stderr, flush=True)
+        return 2
+    ndev = torch.cuda.device_count()
+    if world_env > 1 and ndev and ndev < world_env and not host_plane:
+        print(f"[bench] WORLD_SIZE={world_env} but only {ndev} GPU(s) visible (one rank per GPU; "
+              f"DMLP_DATA_PLANE=host rehearses several ranks on one GPU)", file=sys.stderr,
+              flush=True)
+        return 2
     comm = Comm.init("gpu" if torch.cuda.is_available() else "cpu")
     world = comm.world
-    if a.gpus != world and comm.is_root:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    if world != a.gpus:
+        print(f"[bench] process group has {world} ranks, --gpus {a.gpus}", file=sys.stderr)
+        return 2
     Q = a.q_per_gpu * world
     kmin = a.k if a.kmin is None else a.kmin
     kmax = max(kmin, a.k if a.kmax is None else a.kmax)
@@ -129,6 +186,7 @@ def main(argv=None):
     comm.sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_mine = elapsed
     # max over ranks
     el = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
     if world > 1:
@@ -136,8 +194,11 @@ def main(argv=None):
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms = elapsed / max(1, a.steps) * 1e3
+    my_ms = elapsed_mine / max(1, a.steps) * 1e3  # this rank's own clock
 
-    extra = {}
+    extra = _world_report(comm, host_plane, a)
+    if a.diag_steps > 0:
+        extra.update(_diagnostics(comm, eng, step, a.diag_steps, my_ms))
     if world > 1 and comm.backend == "nccl" and not a.no_busbw:
         extra["allreduce_busbw_GBps"] = round(_allreduce_busbw(comm), 1)
     if a.verify and comm.is_root:
@@ -169,7 +230,8 @@ def main(argv=None):
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_QPS, 1),
+            "vs_baseline": None,
+            "vs_student_engine_cpu_np4": round(value / BASELINE_QPS, 1),
             "dtype": "fp64",
             "screen": "none" if a.exact else "single-term bf16 MFMA screen (3-term escalation), "
                                              "exact fp64 re-rank (results bit-identical to the "
@@ -192,6 +254,77 @@ def main(argv=None):
     if a.ingress == "shm":
         inp.close()
     eng.close()
+    return 0
+
+
+def _world_report(comm, host_plane, a):
+    """What the process group really is: its size, the data plane, and (RCCL) one all-reduce
+    whose result proves every rank took part."""
+    import torch
+    out = {"rccl_world": None, "data_plane": "none (1 rank)" if comm.world == 1 else None}
+    if comm.world == 1:
+        return out
+    from distributed_machine_learning_project_amd.parallel import dist_api as dist
+    out["rccl_world"] = dist.get_world_size()
+    out["data_plane"] = ("RCCL over xGMI" if comm.backend == "nccl" else
+                         "host-staged gloo (DMLP_DATA_PLANE=host rehearsal)"
+                         if host_plane and comm.on_gpu else "gloo (CPU)")
+    t = torch.ones(1, dtype=torch.float32, device=comm.device)
+    dist.all_reduce(t)
+    out["allreduce_check"] = int(t.item())
+    if out["allreduce_check"] != comm.world:
+        raise RuntimeError(f"all-reduce of ones gave {out['allreduce_check']} on {comm.world} ranks")
+    return out
+
+
+def _diagnostics(comm, eng, step, n, my_ms):
+    """Untimed traced steps after the timed ones (the tracer syncs around every phase, so they
+    never run inside the timed region): per rank the mean phase times, the host<->device bytes
+    the pipeline issued and the collective bytes, gathered on rank 0 together with the
+    rank-by-rank comparison of the collective sequence."""
+    import torch
+    from distributed_machine_learning_project_amd.ops import knn as K
+    from distributed_machine_learning_project_amd.parallel import dist_api as dist
+    tr = eng.tracer
+    was = tr.enabled
+    tr.enabled, tr.records = True, []
+    K.io_bytes(reset=True)
+    if comm.world > 1:
+        dist.coll_log_start()
+    import contextlib
+    import io
+    with contextlib.redirect_stderr(io.StringIO()):  # the tracer's per-phase lines
+        for _ in range(n):
+            step()
+    comm.sync()
+    log = dist.coll_log_stop() if comm.world > 1 else []
+    tr.enabled = was
+    phases = {}
+    for name, v in tr.records:
+        phases[name] = phases.get(name, 0.0) + v / n
+    io_b = {k: v // n for k, v in K.io_bytes().items()}
+    coll_b = {}
+    for op, _, nb, _, _ in log:
+        coll_b[op] = coll_b.get(op, 0) + nb // n
+    mine = {"rank": comm.rank, "device": str(comm.device), "numa_node": type(comm)._numa,
+            "ms_per_step": round(my_ms, 4),
+            "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+            "pcie_bytes_per_step": io_b, "collective_bytes_per_step": coll_b}
+    rows = [mine]
+    check = None
+    if comm.world > 1:
+        rows = [None] * comm.world
+        torch.distributed.all_gather_object(rows, mine)
+        check = dist.check_collective_sequence(log)
+    if not comm.is_root:
+        return {}
+    out = {"per_rank": rows, "diag_steps": n}
+    if check is not None:
+        out["collective_check"] = check
+        if not check["ok"]:
+            print(f"[bench] collective sequences differ between ranks: {check['problems']}",
+                  file=sys.stderr, flush=True)
+    return out
 
 
 def _bench_native(a):
@@ -305,4 +438,4 @@ def _allreduce_busbw(comm, nbytes=256 << 20, iters=10):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

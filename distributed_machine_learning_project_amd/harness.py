@@ -53,11 +53,22 @@ def main(argv=None):
     rep = eng.report(out) if out is not None else b""
     comm.sync()
     comm.barrier()
+    t1 = time.perf_counter()
+    coll = None
+    if comm.world > 1 and os.environ.get("DMLP_COLL_CHECK", "0") not in ("", "0"):
+        # after the clock stopped: every rank's collective sequence compared on rank 0
+        from .parallel import dist_api
+        coll = dist_api.check_collective_sequence()
     if comm.is_root:
-        ms = int((time.perf_counter() - t0) * 1000)
+        ms = int((t1 - t0) * 1000)
         sys.stdout.buffer.write(rep)
         sys.stdout.flush()
         print(f"Time taken: {ms} ms", file=sys.stderr, flush=True)
+        if coll is not None:
+            print(f"[dmlp-coll] ok={coll['ok']} calls={coll['calls_per_rank']} "
+                  f"problems={coll['problems']}", file=sys.stderr, flush=True)
+            if not coll["ok"]:
+                return 3
     if a.ingress == "shm":
         inp.close()
     eng.close()

@@ -620,6 +620,17 @@ def _identity(n: int, dev):
     return t[:n]
 
 
+# host <-> device bytes issued by the pipelined path (bench.py's per-rank diagnostics)
+_IO = {"h2d": 0, "d2h": 0}
+
+
+def io_bytes(reset: bool = False):
+    out = dict(_IO)
+    if reset:
+        _IO["h2d"] = _IO["d2h"] = 0
+    return out
+
+
 _SIDE_STREAMS = {}
 _PIPE_DEBUG = os.environ.get("DMLP_PIPE_DEBUG") == "1"
 
@@ -722,6 +733,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
                                        _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
                                        HOST_OPS_CHUNKS, copy.cuda_stream)
         t_ops = time.perf_counter() - t_ops
+        _IO["h2d"] += (t1 - t0) * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
         if rc & 4:
             raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
         bad_d = None
@@ -748,6 +760,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             X, lab = gather(X, lab)  # RCCL all-gather behind the screen
         ev_x = torch.cuda.Event()
         ev_x.record(copy)
+    _IO["h2d"] += X.numel() * 8 + (lab.numel() * 4 if lab is not None else 0) + Q * A * 8
     ev = []
     with torch.cuda.stream(copy):
         Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
@@ -800,6 +813,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         if dst is not None and len(dst) >= L.dmlp_format_bound(Q):
             _lib.check(L.dmlp_d2h_async(dst.ctypes.data, _p(spec[0]), L.dmlp_format_bound(Q),
                                         _stream()), "d2h report")
+            _IO["d2h"] += L.dmlp_format_bound(Q)
             report["copied"] = True
         else:
             report["copied"] = False

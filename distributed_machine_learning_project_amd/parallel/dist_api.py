@@ -10,6 +10,9 @@ ring) runs unchanged on real HIP kernels.
 """
 from __future__ import annotations
 
+import hashlib
+import os
+
 import torch
 import torch.distributed as _d
 
@@ -26,6 +29,119 @@ destroy_process_group = _d.destroy_process_group
 broadcast_object_list = _d.broadcast_object_list
 
 
+# ---------------------------------------------------------------- collective-sequence log
+# The Python twin of knn_engine's KNN_P2P_CHECK (csrc/engine_core.h): every call below appends
+# (op, group members, bytes, dtype, peer) to a per-process list while logging is on
+# (DMLP_COLL_CHECK=1 or coll_log_start()).  check_collective_sequence() then compares the lists
+# of all ranks on rank 0: every collective must be entered by every member of its group with
+# the same bytes in the same order, and every send must meet a receive of the same size — a
+# rank-divergent sequence that would HANG at P = 8 fails here with the first mismatch instead.
+_LOG = None if os.environ.get("DMLP_COLL_CHECK", "0") in ("", "0") else []
+
+
+def coll_log_start():
+    global _LOG
+    _LOG = []
+
+
+def coll_log_stop():
+    global _LOG
+    out, _LOG = _LOG, None
+    return out or []
+
+
+def coll_log():
+    return list(_LOG or [])
+
+
+def _members(group):
+    if group is None or not _d.is_initialized():
+        return None  # the world
+    try:
+        return tuple(_d.get_process_group_ranks(group))
+    except Exception:  # noqa: BLE001 - older torch: no rank listing
+        return ("group", id(group))
+
+
+def _rec(op, t, group=None, peer=None, nbytes=None):
+    if _LOG is None:
+        return
+    nb = nbytes if nbytes is not None else (t.numel() * t.element_size() if t is not None else 0)
+    dt = str(t.dtype).replace("torch.", "") if t is not None else "-"
+    _LOG.append((op, _members(group), int(nb), dt, peer))
+
+
+def check_collective_sequence(log=None, group=None):
+    """Collective: gather every rank's log on rank 0 and compare.  Returns a summary dict on
+    rank 0 (``ok``, counts, bytes per rank and op, the first mismatch) and None elsewhere.
+    The gather itself is not logged."""
+    global _LOG
+    mine = coll_log() if log is None else list(log)
+    saved, _LOG = _LOG, None
+    try:
+        world = _d.get_world_size() if _d.is_initialized() else 1
+        rank = _d.get_rank() if _d.is_initialized() else 0
+        logs = [None] * world
+        if world > 1:
+            _d.all_gather_object(logs, mine, group=group)
+        else:
+            logs = [mine]
+    finally:
+        _LOG = saved
+    if rank != 0:
+        return None
+    return compare_logs(logs)
+
+
+def compare_logs(logs):
+    """Pure comparison of per-rank logs (index = rank)."""
+    world = len(logs)
+    problems = []
+    # collectives: per group, the members' sequences of (op, bytes, dtype) must be identical
+    seqs = {}
+    for r, lg in enumerate(logs):
+        for op, grp, nb, dt, peer in lg:
+            if op in ("send", "recv"):
+                continue
+            members = tuple(range(world)) if grp is None else grp
+            seqs.setdefault(members, {}).setdefault(r, []).append((op, nb, dt, peer))
+    for members, per in seqs.items():
+        ranks = [m for m in members if isinstance(m, int)]
+        ref_r = ranks[0] if ranks else min(per)
+        ref = per.get(ref_r, [])
+        for r in ranks:
+            got = per.get(r, [])
+            if got != ref:
+                n = next((i for i, (x, y) in enumerate(zip(ref, got)) if x != y),
+                         min(len(ref), len(got)))
+                problems.append({"group": list(members), "rank": r, "ref_rank": ref_r,
+                                 "index": n, "ref": list(ref[n]) if n < len(ref) else None,
+                                 "got": list(got[n]) if n < len(got) else None,
+                                 "ref_len": len(ref), "got_len": len(got)})
+                break
+    # point to point: for each ordered pair, the sizes sent must equal the sizes received
+    sent, recvd = {}, {}
+    for r, lg in enumerate(logs):
+        for op, grp, nb, dt, peer in lg:
+            if op == "send":
+                sent.setdefault((r, peer), []).append((nb, dt))
+            elif op == "recv":
+                recvd.setdefault((peer, r), []).append((nb, dt))
+    for pair in sorted(set(sent) | set(recvd), key=str):
+        if sent.get(pair, []) != recvd.get(pair, []):
+            problems.append({"p2p": list(pair), "sent": sent.get(pair, []),
+                             "received": recvd.get(pair, [])})
+    by_rank = []
+    for lg in logs:
+        b = {}
+        for op, _, nb, _, _ in lg:
+            b[op] = b.get(op, 0) + nb
+        by_rank.append(b)
+    digest = [hashlib.sha256(repr(lg).encode()).hexdigest()[:12] for lg in logs]
+    return {"ok": not problems, "calls_per_rank": [len(lg) for lg in logs],
+            "bytes_per_rank": by_rank, "digest_per_rank": digest, "problems": problems[:4]}
+
+
 def staged(t=None) -> bool:
     """True when `t` (a tensor or None) must travel through host memory."""
     if not _d.is_initialized() or _d.get_backend() != "gloo":
@@ -38,12 +154,14 @@ def _host(t):
 
 
 def barrier(group=None, device_ids=None):
+    _rec("barrier", None, group)
     if _d.get_backend(group) == "gloo":
         return _d.barrier(group=group)
     return _d.barrier(group=group, device_ids=device_ids)
 
 
 def broadcast(t, src, group=None):
+    _rec("broadcast", t, group, peer=src)
     if not staged(t):
         return _d.broadcast(t, src, group=group)
     h = _host(t)
@@ -52,6 +170,7 @@ def broadcast(t, src, group=None):
 
 
 def all_reduce(t, op=ReduceOp.SUM, group=None):
+    _rec("all_reduce", t, group)
     if not staged(t):
         return _d.all_reduce(t, op=op, group=group)
     h = _host(t)
@@ -60,6 +179,7 @@ def all_reduce(t, op=ReduceOp.SUM, group=None):
 
 
 def reduce(t, dst, op=ReduceOp.SUM, group=None):
+    _rec("reduce", t, group, peer=dst)
     if not staged(t):
         return _d.reduce(t, dst, op=op, group=group)
     h = _host(t)
@@ -69,6 +189,7 @@ def reduce(t, dst, op=ReduceOp.SUM, group=None):
 
 
 def gather(t, gather_list=None, dst=0, group=None):
+    _rec("gather", t, group, peer=dst)
     if not staged(t):
         return _d.gather(t, gather_list, dst=dst, group=group)
     h = _host(t)
@@ -80,6 +201,7 @@ def gather(t, gather_list=None, dst=0, group=None):
 
 
 def scatter(out, scatter_list=None, src=0, group=None):
+    _rec("scatter", out, group, peer=src)
     if not staged(out):
         return _d.scatter(out, scatter_list, src=src, group=group)
     h = torch.empty(out.shape, dtype=out.dtype)
@@ -89,6 +211,7 @@ def scatter(out, scatter_list=None, src=0, group=None):
 
 
 def all_gather_into_tensor(out, t, group=None):
+    _rec("all_gather", t, group)
     if not staged(t):
         return _d.all_gather_into_tensor(out, t, group=group)
     h = torch.empty(out.shape, dtype=out.dtype)
@@ -97,12 +220,14 @@ def all_gather_into_tensor(out, t, group=None):
 
 
 def send(t, dst, group=None):
+    _rec("send", t, None, peer=dst)
     if not staged(t):
         return _d.send(t, dst, group=group)
     _d.send(_host(t).contiguous(), dst, group=group)
 
 
 def recv(t, src=None, group=None):
+    _rec("recv", t, None, peer=src)
     if not staged(t):
         return _d.recv(t, src, group=group)
     h = torch.empty(t.shape, dtype=t.dtype)
@@ -125,6 +250,8 @@ class _StagedReq:
 
 
 def batch_isend_irecv(ops):
+    for op in ops:
+        _rec("send" if op.op is _d.isend else "recv", op.tensor, None, peer=op.peer)
     if not ops or not staged(ops[0].tensor):
         return _d.batch_isend_irecv(ops)
     reqs = []

@@ -181,14 +181,15 @@ def _farm_dynamic_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, call_id, chun
     chunks are claimed with an atomic fetch-and-add on a counter word in the shared mapping,
     each rank copies its claimed chunk straight from the segment to its GPU and writes the
     chunk's (label, checksum) rows back into the segment's results region; one barrier, and
-    rank 0 holds every result.  The two counters alternate by call: at the start of call c
-    rank 0 zeroes the one call c - 1 used (every rank finished with it — the call ended with a
-    barrier) while the ranks claim from the other."""
+    rank 0 holds every result.  The counter is chosen by a call generation kept in the segment
+    (SharedInput.begin_claims: rank 0 bumps it and zeroes that counter, a segment barrier
+    publishes it), so a second Engine on the same segment, or ranks whose call counts differ,
+    never claim from an exhausted counter.  Rank 0 finishes reading the results region before
+    it enters the next call's barrier, so no rank overwrites rows still being collected."""
     import os
     torch = _torch()
-    slot = call_id & 1
-    if comm.is_root:
-        inp.reset_counter(slot ^ 1)
+    slot = inp.begin_claims(comm.world, comm.is_root)
+    claimed = 0
     per_rank = int(os.environ.get("KNN_CHUNKS_PER_RANK", chunks_per_rank))
     nchunks = max(1, min(Q, comm.world * max(1, per_rank)))
     csz = (Q + nchunks - 1) // nchunks
@@ -207,11 +208,15 @@ def _farm_dynamic_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, call_id, chun
             d, i, lb, cs = be.knn(X, be.tensor(inp.Qx[a:b]), kc, labels=lab,
                                   label_range=(lo, hi), kstride=kmax)
             res[a:b].copy_(torch.stack([lb.to(torch.int64), cs], dim=1))  # D2H into the segment
+            claimed += b - a
+    inp.last_claimed = claimed  # queries this rank computed in this call (tests, diagnostics)
     comm.barrier()
     if not comm.is_root:
         return None
     with tr.phase("collect"):
         out = be.tensor(inp.res)
+        if be.on_gpu:  # the H2D reads the segment: done before the next call's barrier
+            torch.cuda.current_stream().synchronize()
     return out[:, 0].to(torch.int32), out[:, 1].contiguous(), None, None
 
 
@@ -376,6 +381,8 @@ def _shared_egress(comm, be, inp, cs, qid_base, report=None, lb=None):
         dst = torch.from_numpy(inp.out[off:off + n])
         if be.on_gpu:
             dst.copy_(dev_text[:n], non_blocking=True)  # D2H into the page-locked segment
+            from ..ops import knn as K
+            K._IO["d2h"] += n
         else:
             dst.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
     if lb is not None and comm.world > 1 and nq:

@@ -22,6 +22,7 @@ RCCL collectives with a host sync each.
 Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — a summary for tools;
 the KNN strategies re-scan the labels and k inside every timed call), two int64 work counters at
 byte 64 (the dynamic farm's chunk claims, alternating per call), a barrier counter at byte 96,
+a call generation at byte 80 (the dynamic farm: which counter a call claims from),
 per-rank int64 slots from byte 128 (report lengths), then labels i32[N], k i32[Q],
 X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), res i64[2*Q] (the dynamic farm's
 (label, checksum) per query), each section 4096-byte aligned.
@@ -67,6 +68,7 @@ class SharedInput(KNNInput):
         self.out = np.frombuffer(mm, np.uint8, 48 * Q + 64, off["out"])
         self.res = np.frombuffer(mm, np.int64, 2 * Q, off["res"]).reshape(Q, 2)
         self.counters = np.frombuffer(mm, np.int64, 2, 64)
+        self._gen = np.frombuffer(mm, np.int64, 1, 80)
         self.slots = np.frombuffer(mm, np.int64, (_ALIGN - 128) // 8, 128)
         self._bar = np.frombuffer(mm, np.int64, 1, 96)
         self._nbar = 0  # barriers this process has entered
@@ -134,6 +136,23 @@ class SharedInput(KNNInput):
         from .. import _lib
         _lib.lib().dmlp_atomic_store_i64(self.counters.ctypes.data + 8 * slot, 0)
 
+    def begin_claims(self, world: int, is_root: bool) -> int:
+        """Collective over the ranks mapping the segment: start a new round of claim() calls and
+        return the counter slot every rank claims from.  The call generation lives in the
+        segment (not in any one Engine), so a fresh Engine, or any caller whose call count does
+        not match the segment's history, still starts on a zeroed counter: rank 0 bumps the
+        generation and zeroes that generation's counter, then a segment barrier publishes both
+        (and keeps every rank out of the round until rank 0 is done with the previous one)."""
+        from .. import _lib
+        L = _lib.lib()
+        if is_root:
+            g = int(L.dmlp_atomic_fetch_add_i64(self._gen.ctypes.data, 0)) + 1
+            L.dmlp_atomic_store_i64(self.counters.ctypes.data + 8 * (g & 1), 0)
+            L.dmlp_atomic_store_i64(self._gen.ctypes.data, g)
+        if world > 1:
+            self.barrier(world)
+        return int(L.dmlp_atomic_fetch_add_i64(self._gen.ctypes.data, 0)) & 1
+
     @property
     def summary(self):
         """(label lo, label hi (exclusive), k min, k max) from the header."""
@@ -179,6 +198,9 @@ def _mbind(addr: int, length: int, nodes, mode: int) -> bool:
     a1 = (addr + length) // page * page
     if a1 <= a0 or not nodes or max(nodes) >= 64:
         return False
+    import platform
+    if platform.machine() != "x86_64":  # the syscall number below is x86_64's
+        return False
     mask = ctypes.c_ulong(sum(1 << n for n in set(nodes)))
     libc = ctypes.CDLL(None, use_errno=True)
     SYS_mbind = 237  # x86_64
@@ -188,8 +210,10 @@ def _mbind(addr: int, length: int, nodes, mode: int) -> bool:
 
 
 def _place(mm, off, N, Q, A, query_nodes):
-    """NUMA placement of a fresh segment (best effort: any failure leaves the default policy)."""
-    MPOL_BIND, MPOL_INTERLEAVE = 2, 3
+    """NUMA placement of a fresh segment (best effort: any failure leaves the default policy).
+    MPOL_PREFERRED, not MPOL_BIND: a node short of memory falls back to another node instead of
+    failing rank 0's tmpfs writes with SIGBUS."""
+    MPOL_PREFERRED, MPOL_INTERLEAVE = 1, 3
     base = mm.ctypes.data
     nodes = sorted({n for _, _, n in query_nodes if n >= 0})
     if not nodes:
@@ -198,8 +222,8 @@ def _place(mm, off, N, Q, A, query_nodes):
         _mbind(base + off["X"], 8 * N * A, nodes, MPOL_INTERLEAVE)
     for a, b, n in query_nodes:
         if n >= 0 and b > a:
-            _mbind(base + off["Qx"] + 8 * A * a, 8 * A * (b - a), [n], MPOL_BIND)
-            _mbind(base + off["out"] + 48 * a, 48 * (b - a), [n], MPOL_BIND)
+            _mbind(base + off["Qx"] + 8 * A * a, 8 * A * (b - a), [n], MPOL_PREFERRED)
+            _mbind(base + off["out"] + 48 * a, 48 * (b - a), [n], MPOL_PREFERRED)
 
 
 def gpu_numa_node(dev_index: int) -> int:

@@ -46,7 +46,10 @@ def case(tmp_path_factory):
 
 
 def _python(path, np_, strategy, env_extra=None):
-    env = dict(os.environ, PYTHONPATH=ROOT, DMLP_DATA_PLANE="host", OMP_NUM_THREADS="2")
+    # DMLP_COLL_CHECK: every rank logs its collective sequence (parallel/dist_api.py) and the
+    # harness compares them on rank 0 after the timed call (exit 3 on any divergence)
+    env = dict(os.environ, PYTHONPATH=ROOT, DMLP_DATA_PLANE="host", OMP_NUM_THREADS="2",
+               DMLP_COLL_CHECK="1")
     env.update(env_extra or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
            str(np_), "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m",
@@ -54,6 +57,7 @@ def _python(path, np_, strategy, env_extra=None):
            "--device", "gpu", "--input", path]
     r = subprocess.run(cmd, capture_output=True, env=env, timeout=180, cwd=ROOT)
     assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"[dmlp-coll] ok=True" in r.stderr, r.stderr.decode()[-2000:]
     return r.stdout
 
 
@@ -193,3 +197,24 @@ def test_native_shared_ingress_farm(case, case_x1, np_):
     assert _native(gpath, np_, "farm", env_extra=env) == gexpect
     # every rank renders the whole screen image instead of its 1/np (A/B switch)
     assert _native(path, np_, "farm", env_extra=dict(env, KNN_IMAGE_SHARD="0")) == expect
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_bench_self_launch_rehearsal(np_):
+    """bench.py --gpus N launches its own N ranks (no torchrun in front of it) and reports the
+    process group it really had; on one GPU the ranks share it over the host-staged plane.
+    The whole rank-0 report is checked against the fp64 oracle (--verify) and the ranks'
+    collective sequences are compared (root ingress: broadcast + scatter + gather)."""
+    import json
+    env = dict(os.environ, DMLP_DATA_PLANE="host", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(np_), "--steps", "3",
+           "--warmup", "1", "--min-warmup-s", "0", "--n-data", "20000", "--q-per-gpu", "2048",
+           "--verify", "--ingress", "root", "--no-busbw"]
+    r = subprocess.run(cmd, capture_output=True, env=env, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert res["n_gpus"] == np_ and res["rccl_world"] == np_
+    assert res["verify_ok"] and res["allreduce_check"] == np_
+    assert res["collective_check"]["ok"]
+    assert len(res["per_rank"]) == np_
+    assert all(c > 0 for c in res["collective_check"]["calls_per_rank"])
