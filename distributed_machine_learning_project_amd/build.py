@@ -135,21 +135,69 @@ def _engine_link_flags():
 
 
 def build_dropin(common_cpp: str, out: str | None = None, debug: bool = False,
-                 extra_flags=()) -> Path:
-    """Link the reference's own harness (its unmodified common.cpp, next to its common.h)
-    with include/engine.h + dropin_engine.cpp into a reference-compatible `engine` binary
-    (Makefile:10-15 equivalent; debug=True is the engine.debug target)."""
+                 extra_flags=(), inplace: bool = False) -> Path:
+    """Link the reference's own harness (its unmodified common.cpp and common.h) with
+    include/engine.h + dropin_engine.cpp into a reference-compatible `engine` binary
+    (Makefile:10-15 equivalent; debug=True is the engine.debug target).
+
+    common.cpp includes "engine.h" from its own directory (common.cpp:8), so it is compiled from
+    a private staging directory holding copies of common.cpp / common.h next to this package's
+    engine.h — never against a sibling engine.h in the reference tree.  (dropin_engine.cpp keeps
+    no state in the Engine object, so a binary built against the reference's engine.h works
+    too: inplace=True compiles common.cpp where it is, against whatever engine.h sits next to it,
+    exactly like the reference's Makefile with dropin_engine.cpp in place of engine.cpp.)"""
+    import tempfile
     build(engine=True)  # libdmlp + the MPI runtime links
     common_cpp = Path(common_cpp).resolve()
-    out = Path(out or (common_cpp.parent / ("engine.debug" if debug else "engine"))).resolve()
-    flags = ["-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
-             f"-I{PKG / 'include'}", f"-I{common_cpp.parent}", f"-I{CSRC}", f"-I{MPI_HOME}/include",
-             f"-I{ROCM}/include", *extra_flags]
-    if debug:
-        flags += ["-g", "-DDEBUG"]
-    _run(["g++", *flags, str(common_cpp), str(CSRC / "dropin_engine.cpp"), "-o", str(out),
-          *_engine_link_flags()])
+    # default output in this package's build directory (never written into the harness's tree)
+    BUILD.mkdir(exist_ok=True)
+    out = Path(out or (BUILD / ("engine.debug" if debug else "engine"))).resolve()
+    with tempfile.TemporaryDirectory(dir=BUILD, prefix="dropin_") as td:
+        stage = Path(td)
+        if inplace:
+            src, inc = common_cpp, common_cpp.parent
+        else:
+            src, inc = stage / "common.cpp", stage
+            shutil.copy2(common_cpp, src)
+            hdr = common_cpp.parent / "common.h"
+            if hdr.exists():
+                shutil.copy2(hdr, stage / "common.h")
+            shutil.copy2(PKG / "include" / "engine.h", stage / "engine.h")
+        flags = ["-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
+                 f"-I{inc}", f"-I{CSRC}", f"-I{common_cpp.parent}", f"-I{MPI_HOME}/include",
+                 f"-I{ROCM}/include", *extra_flags]
+        if debug:
+            flags += ["-g", "-DDEBUG"]
+        _run(["g++", *flags, str(src), str(CSRC / "dropin_engine.cpp"), "-o", str(out),
+              *_engine_link_flags()])
     return out
+
+
+REF_HARNESS = Path(os.environ.get("DMLP_REF_HARNESS", "/root/reference"))
+REF_STAGE = PKG / "_refharness"  # git-ignored, NOT gpurun-ignored (unlike _build/)
+
+
+def reference_harness() -> Path | None:
+    """The reference's common.cpp to build the drop-in against: the reference tree when this
+    machine has it, else the untracked copy build() staged in _refharness (it travels with
+    the working tree to GPU boxes, which have no reference tree; it is never committed)."""
+    for d in (REF_HARNESS, REF_STAGE):
+        if (d / "common.cpp").exists() and (d / "common.h").exists():
+            return d / "common.cpp"
+    return None
+
+
+def stage_reference_harness() -> Path | None:
+    """Copy the reference harness files (common.cpp, common.h, engine.h) into _refharness
+    (git-ignored) so drop-in tests and `bench.py --harness dropin` can build against the
+    reference's unmodified harness on a machine without the reference tree."""
+    if not (REF_HARNESS / "common.cpp").exists():
+        return None
+    REF_STAGE.mkdir(parents=True, exist_ok=True)
+    for f in ("common.cpp", "common.h", "engine.h"):
+        if (REF_HARNESS / f).exists():
+            shutil.copy2(REF_HARNESS / f, REF_STAGE / f)
+    return REF_STAGE / "common.cpp"
 
 
 def build(force: bool = False, engine: bool = True) -> Path:
@@ -158,6 +206,7 @@ def build(force: bool = False, engine: bool = True) -> Path:
     lib = build_lib(force)
     if engine:
         build_engine(force)
+    stage_reference_harness()
     return lib
 
 
@@ -169,11 +218,14 @@ def main(argv=None):
                     help="build a reference-compatible engine from the reference's common.cpp")
     ap.add_argument("--dropin-out", default=None)
     ap.add_argument("--dropin-debug", action="store_true", help="engine.debug (-DDEBUG)")
+    ap.add_argument("--dropin-inplace", action="store_true",
+                    help="compile common.cpp against the engine.h next to it (the reference's "
+                         "own header), as its Makefile would")
     a = ap.parse_args(argv)
     p = build(force=a.force, engine=not a.no_engine)
     print(f"built {p}")
     if a.dropin:
-        print(f"built {build_dropin(a.dropin, a.dropin_out, a.dropin_debug)}")
+        print(f"built {build_dropin(a.dropin, a.dropin_out, a.dropin_debug, inplace=a.dropin_inplace)}")
 
 
 if __name__ == "__main__":

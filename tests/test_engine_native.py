@@ -144,3 +144,65 @@ def test_dropin_engine_h_gpu(tmp_path, strategy):
     path, inp, res, lab, cs = _case(tmp_path, N=5000, Q=400, A=12, kmax=150)
     out = _run_dropin(_dropin(tmp_path), path, {"KNN_STRATEGY": strategy})
     assert out == dmlp.format_report(cs)
+
+
+# ---------------------------------------------------------------- the reference's own harness
+def _ref_dropin(tmp_path, debug=False, inplace=False):
+    """Build from the reference's unmodified common.cpp: staged next to this
+    package's engine.h, or in place against the reference's own engine.h (a copy of the tree,
+    so nothing is written into the reference).  The reference tree, or on a GPU box the
+    untracked copy build() staged in _refharness."""
+    ref_common = build.reference_harness()
+    if ref_common is None:
+        pytest.skip("reference common.cpp not present")
+    REF_COMMON = str(ref_common)
+    import shutil
+    src = REF_COMMON
+    if inplace:
+        tree = tmp_path / "reftree"
+        tree.mkdir(exist_ok=True)
+        for f in ("common.cpp", "common.h", "engine.h"):
+            shutil.copy2(os.path.join(os.path.dirname(REF_COMMON), f), tree / f)
+        src = str(tree / "common.cpp")
+    name = f"engine{'.debug' if debug else ''}{'.inplace' if inplace else ''}"
+    try:
+        return str(build.build_dropin(src, str(tmp_path / name), debug=debug, inplace=inplace))
+    except RuntimeError as e:
+        pytest.skip(f"drop-in build unavailable: {e}")
+
+
+def _debug_expect(inp, res, lab):
+    K = max(1, max(int(k) for k in inp.k))
+    d = np.full((inp.Q, K), np.inf)
+    i = np.full((inp.Q, K), -1, np.int32)
+    for q, (dq, iq) in enumerate(res):
+        d[q, :len(dq)] = dq
+        i[q, :len(iq)] = iq
+    return dmlp.format_debug(d, i, inp.k, lab)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("debug", [False, True])
+def test_reference_common_cpp_dropin_cpu(tmp_path, debug, inplace):
+    """The reference's own common.cpp + dropin_engine.cpp, built staged (this engine.h) and in
+    place (the reference's engine.h: the Engine object holds no state, the engine singleton
+    starts at MPI_Init), release and -DDEBUG, np 1 and 2: stdout == the fp64 oracle's bytes."""
+    path, inp, res, lab, cs = _case(tmp_path, N=700, Q=45, kmax=25)
+    exe = _ref_dropin(tmp_path, debug=debug, inplace=inplace)
+    expect = _debug_expect(inp, res, lab) if debug else dmlp.format_report(cs)
+    assert _run_dropin(exe, path, {"KNN_DEVICE": "cpu"}) == expect
+    if os.path.exists(MPIEXEC):
+        assert _run_dropin(exe, path, {"KNN_DEVICE": "cpu"}, np_=2) == expect
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reference_common_cpp_dropin_gpu(tmp_path, inplace):
+    """Same on the MI355X: release build (GPU-rendered report written to std::cout) and the
+    DEBUG listing (lists through the harness's reportResult); np 2 over the host-staged plane."""
+    path, inp, res, lab, cs = _case(tmp_path, N=5000, Q=400, A=12, kmax=150)
+    exe = _ref_dropin(tmp_path, inplace=inplace)
+    assert _run_dropin(exe, path, {}) == dmlp.format_report(cs)
+    assert _run_dropin(exe, path, {"KNN_DATA_PLANE": "host"}, np_=2) == dmlp.format_report(cs)
+    dbg = _ref_dropin(tmp_path, debug=True, inplace=inplace)
+    assert _run_dropin(dbg, path, {}) == _debug_expect(inp, res, lab)
