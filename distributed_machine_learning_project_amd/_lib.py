@@ -58,15 +58,6 @@ _SIGS = {
                              vp, vp, vp, vp]),
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
-    "dmlp_screen_x2_kmax": (i32, []),
-    "dmlp_screen_x2_qw": (i32, [i32]),
-    "dmlp_screen_x2_cap": (i32, [i32]),
-    "dmlp_screen_x2_waves_per_cu": (i32, [i32]),
-    "dmlp_set_x2_mode": (None, [i32]),
-    "dmlp_x2_debug_counters": (i32, [vp, i32]),
-    "dmlp_set_x2_pw": (None, [i32]),
-    "dmlp_screen_x2": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
-                             vp, vp, vp, vp]),
     "dmlp_set_x1_ct": (None, [i32]),
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,

@@ -31,7 +31,7 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unus
 
 # screen_x1: fmaxf over MFMA results without the IEEE-mode NaN quieting (v_max_f32 x, x, x per
 # operand); the kernel never produces or compares NaN
-PER_FILE = {"screen_x1.hip": ["-fno-honor-nans"], "screen_x2.hip": ["-fno-honor-nans"]}
+PER_FILE = {"screen_x1.hip": ["-fno-honor-nans"]}
 
 
 def _sources():

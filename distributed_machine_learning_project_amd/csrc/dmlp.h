@@ -111,22 +111,6 @@ int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit,
                    const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
                    void* stream);
 void dmlp_set_x1_mode(int mode);
-// 32x32x16 form of the single-term screen (screen_x2.hip): same arguments and output contract as
-// dmlp_screen_x1 (group entries for dmlp_refine_groups with cap = dmlp_screen_x2_cap), k <=
-// dmlp_screen_x2_kmax(), dmlp_screen_x2_qw(KT) queries per wave, one wave per SIMD.
-int dmlp_screen_x2_kmax(void);
-int dmlp_screen_x2_qw(int KT);
-int dmlp_screen_x2_cap(int kmax);
-int dmlp_screen_x2_waves_per_cu(int kmax);
-void dmlp_set_x2_mode(int mode);
-int dmlp_x2_debug_counters(unsigned long long* out, int reset);
-// 1 (default): per-wave streaming form; 0: 8-wave workgroups sharing an LDS ring (A/B)
-void dmlp_set_x2_pw(int on);
-int dmlp_screen_x2(int KT, int hl, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
-                   int64_t n_points, const void* qhi, const float* qn, const int* qidx,
-                   const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
-                   const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
-                   void* stream);
 
 void dmlp_set_x1_ct(int ct);
 int dmlp_x1_debug_counters(unsigned long long* out, int reset);

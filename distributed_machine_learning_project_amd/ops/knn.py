@@ -33,9 +33,6 @@ SCREEN_MAX_KT = 4       # A <= 128 on the screen path
 NUM_CUS = 256
 # "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
 SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
-# within the single-term class: DMLP_X2=1 selects the 32x32x16 kernel (screen_x2.hip) for k <= its
-# kmax (measured 1.49 ms vs x1's 1.37 ms on the bench shape — opt-in until it wins)
-SCREEN_X2 = os.environ.get("DMLP_X2", "0") != "0"
 # slices of the host-rendered screen operands, each copied as soon as it is converted (1: measured
 # best on the bench shape — every extra slice costs ~20 us of copy-API time on the host)
 # host render + H2D of the screen operands in 2 pipelined slices: the first copy starts after half
@@ -391,14 +388,7 @@ class _KnnCall:
             kcls = int(kk[idx].max())
             qidx = _h2d(idx.astype(np.int32), dev)
         cus = max(1, int(round(NUM_CUS * self.gpu_share)))
-        use_x2 = (impl == "x1" and SCREEN_X2 and kcls <= L.dmlp_screen_x2_kmax()
-                  and L.dmlp_screen_x2_qw(KT) > 0)
-        if use_x2:
-            cap = L.dmlp_screen_x2_cap(kcls)
-            S = _choose_slices_stream(nq, L.dmlp_screen_x2_qw(KT), ds.n_tiles,
-                                      L.dmlp_screen_x2_waves_per_cu(kcls),
-                                      int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
-        elif impl == "x1":
+        if impl == "x1":
             cap = L.dmlp_screen_x1_cap(kcls)
             S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), ds.n_tiles,
                                       L.dmlp_screen_x1_waves_per_cu(kcls),
@@ -416,12 +406,11 @@ class _KnnCall:
                _p(self.cs), _p(self.status), self._ovf.ptr(self._ovf_slot), s)
         if impl == "x1":
             cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
-            fn = L.dmlp_screen_x2 if use_x2 else L.dmlp_screen_x1
-            _lib.check(fn(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
+            _lib.check(L.dmlp_screen_x1(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
                           _p(self.qhi), _p(self.qn), _p(qidx), _p(self.kdev_eff),
                           nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                           _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
-                       "screen_x2" if use_x2 else "screen_x1")
+                       "screen_x1")
             if idx is None:
                 # every query goes through this refine: it writes each row's (+inf, -1) padding
                 # and each status itself, so no fill pass at all
@@ -842,8 +831,6 @@ def _apply_env_switches(L):
             L.dmlp_set_stream_groups(0)
         if os.environ.get("DMLP_X1_CT"):
             L.dmlp_set_x1_ct(int(os.environ["DMLP_X1_CT"]))
-        if os.environ.get("DMLP_X2_PW"):
-            L.dmlp_set_x2_pw(int(os.environ["DMLP_X2_PW"]))
         if os.environ.get("DMLP_STREAM_SUB"):
             L.dmlp_set_stream_sub(int(os.environ["DMLP_STREAM_SUB"]))
         _ENV_APPLIED[0] = True

@@ -186,18 +186,15 @@ def test_x1_screen_shapes(torch_cuda, A, kmax, monkeypatch):
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("x2", [True, False])
 @pytest.mark.parametrize("A,kmin,kmax,N,Q,lo,hi", [(8, 1, 16, 7777, 333, -100.0, 100.0),
                                                   (32, 16, 16, 20000, 700, 0.0, 1000.0),
                                                   (64, 1, 16, 9001, 260, -5.0, 5.0),
                                                   (32, 1, 1, 3000, 129, 0.0, 1000.0),
                                                   (20, 1, 12, 300000, 64, 0.0, 1000.0)])
-def test_single_term_screens(torch_cuda, x2, A, kmin, kmax, N, Q, lo, hi, monkeypatch):
-    """k <= 16 single-term class on both kernels: screen_x2.hip (32x32x16, 128 queries per
-    wave) and screen_x1.hip (16x16x32): KT 1/2, ragged query blocks and tiles, k = 1, and many
-    slices (few queries, N = 3e5 > one slice's 16-bit group range)."""
+def test_single_term_screens(torch_cuda, A, kmin, kmax, N, Q, lo, hi, monkeypatch):
+    """k <= 16 single-term class (screen_x1.hip, 16x16x32): KT 1/2, ragged query blocks and
+    tiles, k = 1, and many slices (few queries, N = 3e5 > one slice's 16-bit group range)."""
     monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
-    monkeypatch.setattr(K, "SCREEN_X2", x2)
     inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 6, seed=A + kmax + N)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0

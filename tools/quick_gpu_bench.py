@@ -39,7 +39,6 @@ def main():
             _lib.lib().dmlp_set_screen_mode(m)
             _lib.lib().dmlp_set_stream_mode(m)
             _lib.lib().dmlp_set_x1_mode(m)
-            _lib.lib().dmlp_set_x2_mode(m)
             ts = []
             for it in range(a.iters + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -69,13 +68,6 @@ def main():
                 calls = a.iters + 1
                 print("  per call: wave-steps %.4g  cand-path %.4g  appends %.4g  compactions %.4g"
                       % tuple(float(x) / calls for x in cnt[:4]))
-                c4 = np.zeros(8, np.uint64)
-                _lib.lib().dmlp_x2_debug_counters(c4.ctypes.data, 1)
-                if c4[5]:
-                    f = [float(x) / calls for x in c4[:6]]
-                    print("  x2 per call: tile branches %.4g  appends %.4g  compactions %.4g  "
-                          "compaction cycles %.1f%%  barrier cycles %.1f%% (of wave loop cycles)"
-                          % (f[0], f[1], f[2], 100 * f[3] / f[5], 100 * f[4] / f[5]))
                 c3 = np.zeros(8, np.uint64)
                 _lib.lib().dmlp_x1_debug_counters(c3.ctypes.data, 1)
                 if c3[0]:
@@ -84,7 +76,6 @@ def main():
         _lib.lib().dmlp_set_screen_mode(0)
         _lib.lib().dmlp_set_stream_mode(0)
         _lib.lib().dmlp_set_x1_mode(0)
-        _lib.lib().dmlp_set_x2_mode(0)
         return
     inp = dmlp.generate(a.n, a.q, a.a, 0.0, 1000.0, a.kmin, a.kmax, 10, seed=42)
     X = torch.from_numpy(inp.X).cuda()
