@@ -286,6 +286,15 @@ def _diagnostics(comm, eng, step, n, my_ms):
     from distributed_machine_learning_project_amd.ops import knn as K
     from distributed_machine_learning_project_amd.parallel import dist_api as dist
     tr = eng.tracer
+    # GPU-timestamped phase boundaries of the pipeline (hipEvents, no syncs) over n steps
+    tl = []
+    if comm.on_gpu:
+        K.set_pipe_events(True)
+        for _ in range(n + 1):
+            step()
+            tl.append(K.pipe_timeline())
+        K.set_pipe_events(False)
+        tl = tl[1:]  # the first has no previous call to measure the gap from
     was = tr.enabled
     tr.enabled, tr.records = True, []
     K.io_bytes(reset=True)
@@ -306,8 +315,13 @@ def _diagnostics(comm, eng, step, n, my_ms):
     coll_b = {}
     for op, _, nb, _, _ in log:
         coll_b[op] = coll_b.get(op, 0) + nb // n
+    timeline = {}
+    for row in tl:
+        for name, ms in row:
+            timeline[name] = timeline.get(name, 0.0) + ms / max(1, len(tl))
     mine = {"rank": comm.rank, "device": str(comm.device), "numa_node": type(comm)._numa,
             "ms_per_step": round(my_ms, 4),
+            "step_timeline_ms": {k: round(v, 4) for k, v in timeline.items()},
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},
             "pcie_bytes_per_step": io_b, "collective_bytes_per_step": coll_b}
     rows = [mine]
@@ -374,26 +388,39 @@ def _bench_native(a):
             path = os.path.join(td, f"{tag}.in")
             with open(path, "w") as f:
                 f.write(to_text(inp))
-            times, out0, harness_ms = [], None, []
+            times, out0, harness_ms, parts = [], None, [], {}
             for r in range(a.warmup + steps):
                 met = os.path.join(td, f"{tag}_{r}.json")
                 env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy,
                            KNN_INGRESS=a.ingress)  # shm: per-GPU ingress from a shared window
                 cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [str(exe)]
+                if dropin and P > 1:  # each rank opens the input (MPICH stdin forwarding: H5)
+                    import shlex
+                    cmd = cmd[:-1] + ["sh", "-c", f"exec {shlex.quote(str(exe))} < "
+                                                  f"{shlex.quote(path)}"]
                 if not dropin:
                     cmd += ["--input", path]
                     if a.schedule == "dynamic":
                         cmd += ["--schedule", "dynamic"]
-                with open(path, "rb") as fin:
-                    pr = subprocess.run(cmd, stdin=fin if dropin else None, capture_output=True,
-                                        env=env, timeout=600)
+                # stdout to a file, as run_bench.sh redirects it (run_bench.sh:82-84): a pipe would
+                # time this process's reader draining 6 MB of report, not the engine
+                outp, errp = os.path.join(td, "out.txt"), os.path.join(td, "err.txt")
+                with open(path, "rb") as fin, open(outp, "wb") as fo, open(errp, "wb") as fe:
+                    rc = subprocess.run(cmd, stdin=fin if dropin and P == 1 else None,
+                                        stdout=fo, stderr=fe, env=env, timeout=600).returncode
+                pr = subprocess.CompletedProcess(cmd, rc, open(outp, "rb").read(),
+                                                 open(errp, "rb").read())
                 if pr.returncode != 0:
                     raise RuntimeError(pr.stderr.decode()[-2000:])
                 if r >= a.warmup:
                     # KNN_METRICS: the engine's own microsecond clock (the harness prints whole
                     # milliseconds; the drop-in's covers Engine::KNN, pack and report included)
                     with open(met) as f:
-                        times.append(float(_json.load(f)["time_ms"]))
+                        mj = _json.load(f)
+                    times.append(float(mj["time_ms"]))
+                    for key in ("pack_ms", "knn_ms", "emit_ms"):
+                        if key in mj:
+                            parts.setdefault(key, []).append(float(mj[key]))
                     if dropin:
                         import re as _re
                         m = _re.search(rb"Time taken: (\d+) ms", pr.stderr)
@@ -403,6 +430,8 @@ def _bench_native(a):
                      "time_ms_min": round(min(times), 3), "runs": len(times)}
             if harness_ms:
                 entry["harness_time_taken_ms"] = harness_ms
+            for key, v in parts.items():
+                entry[key + "_median"] = round(statistics.median(v), 3)
             if tag == "q1000":
                 from distributed_machine_learning_project_amd.ops import knn as K
                 from distributed_machine_learning_project_amd.utils.io import format_report

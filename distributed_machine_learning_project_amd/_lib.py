@@ -54,6 +54,8 @@ _SIGS = {
     "dmlp_screen_x1_waves_per_cu": (i32, [i32]),
     "dmlp_screen_x1_min_slices": (i64, [i64]),
     "dmlp_screen_x1_bound": (None, [i32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "dmlp_screen_x1_bound2": (None, [i32, i32, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                     C.POINTER(C.c_float)]),
     "dmlp_screen_x1": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),

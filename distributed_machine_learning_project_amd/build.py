@@ -158,11 +158,11 @@ def build_dropin(common_cpp: str, out: str | None = None, debug: bool = False,
             src, inc = common_cpp, common_cpp.parent
         else:
             src, inc = stage / "common.cpp", stage
-            shutil.copy2(common_cpp, src)
+            shutil.copyfile(common_cpp, src)
             hdr = common_cpp.parent / "common.h"
             if hdr.exists():
-                shutil.copy2(hdr, stage / "common.h")
-            shutil.copy2(PKG / "include" / "engine.h", stage / "engine.h")
+                shutil.copyfile(hdr, stage / "common.h")
+            shutil.copyfile(PKG / "include" / "engine.h", stage / "engine.h")
         flags = ["-O3", "-std=c++17", "-ffp-contract=off", "-D__HIP_PLATFORM_AMD__",
                  f"-I{inc}", f"-I{CSRC}", f"-I{common_cpp.parent}", f"-I{MPI_HOME}/include",
                  f"-I{ROCM}/include", *extra_flags]
@@ -196,7 +196,9 @@ def stage_reference_harness() -> Path | None:
     REF_STAGE.mkdir(parents=True, exist_ok=True)
     for f in ("common.cpp", "common.h", "engine.h"):
         if (REF_HARNESS / f).exists():
-            shutil.copy2(REF_HARNESS / f, REF_STAGE / f)
+            if (REF_STAGE / f).exists():
+                (REF_STAGE / f).unlink()
+            shutil.copyfile(REF_HARNESS / f, REF_STAGE / f)
     return REF_STAGE / "common.cpp"
 
 

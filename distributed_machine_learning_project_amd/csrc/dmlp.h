@@ -34,7 +34,7 @@ int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int 
                       void* qlo, float* qn, unsigned* bad, void* stream);
 
 // host_prep.cpp: the screen's query operands rendered on the host (persistent thread pool) —
-// mu over the first min(N, 4096) rows like dmlp_center; qhi [Q][KT*32] bf16 bits, qn [Q] fp32.
+// mu over the first min(N, 4096) rows like dmlp_center; qhi [Q][KT*32] fp16 bits, qn [Q] fp32.
 // dmlp_cpu_prep_queries returns 1 if some |q - mu| is outside the screen's range.
 int dmlp_host_threads(void);
 void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu);
@@ -103,8 +103,13 @@ int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);
-// hl: fragment halves per (step, kt) in xfrag — 2 for prep.hip's hi/lo image, 1 for the hi-only
-// image of dmlp_cpu_prep_data (same for dmlp_refine_groups).
+// eps(q) = r1 |q'| max|x'| + r2 max|x'|^2 + r3 (|q'| + max|x'| + 2^-15) for image kind hl
+// (1: fp16 hi-only, 2: bf16 hi/lo)
+void dmlp_screen_x1_bound2(int A, int hl, float* r1, float* r2, float* r3);
+// hl: fragment halves per (step, kt) in xfrag — 2 for prep.hip's bf16 hi/lo image, 1 for the fp16
+// hi-only image of dmlp_cpu_prep_data (the query fragments qhi must be of the same element type:
+// fp16 from dmlp_cpu_prep_queries with hl = 1, bf16 from dmlp_prep_queries with hl = 2; same for
+// dmlp_refine_groups).
 int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
                    int64_t n_points, const void* qhi, const float* qn, const int* qidx,
                    const int* qk, int nq, int kmax, const unsigned* xnmax_bits,

@@ -142,6 +142,7 @@ class KnnCore {
   ~KnnCore() {
     if (ctr_win_ != MPI_WIN_NULL) MPI_Win_free(&ctr_win_);
     if (ev_rows_) (void)hipEventDestroy(ev_rows_);
+    if (ev_ops_) (void)hipEventDestroy(ev_ops_);
     if (wake_st_) (void)hipStreamDestroy(wake_st_);
     if (ring_ev_) (void)hipEventDestroy(ring_ev_);
     if (ring_done_) (void)hipEventDestroy(ring_done_);
@@ -434,8 +435,7 @@ class KnnCore {
       // the single-GPU fast path once on a tiny input: its side stream, event, staging and
       // device buffers, the host pool's first job and the first copies on the side stream are
       // all paid here (measured ~16 ms of first-use cost otherwise)
-      HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
+      make_side();
       Input w;
       w.N = 300; w.Q = 70; w.A = 8;
       w.labels.resize(w.N);
@@ -501,18 +501,18 @@ class KnnCore {
   // ---------------------------------------------------------------- fast single-GPU farm
   // The Python pipeline (ops/knn.py knn_gpu_pipelined) in native code, for one rank holding
   // everything: the host renders the single-term screen's operands (host_prep.cpp: the
-  // dataset's hi-only bf16 tile image + norms, the queries' bf16 fragments + norms — 15.7 MB
+  // dataset's fp16 hi-only tile image + norms, the queries' fp16 fragments + norms — 15.7 MB
   // instead of 59 MB of fp64 rows at the bench shape) and copies them on the main stream; the
   // fp64 rows, labels and queries cross PCIe on a second stream BEHIND the screen, and only the
   // exact re-rank waits for them; the report is rendered straight into the page-locked output.
-  // Returns false (nothing done) when the input is outside this path: k not in [1, 32] or
-  // k > N, A > 64, data outside the screen's range; a query whose candidates overflow makes the
-  // whole call fall back too (rare: data too tight for the single-term bound).
+  // Any k: LocalKnn::run serves 1 <= k <= 32 with the host operands, 32 < k <= 128 with the
+  // 3-term screen on a device image rendered from the landed rows, the rest exactly, and a query
+  // whose single-term candidates overflow escalates alone.  Returns false (nothing done) when
+  // the data or queries are outside the fp16 range (the device path then serves the call), or
+  // A > 64 (no x1 variant).
   DevBuf<short> fx_hi_, fq_hi_, fx_hic_;
-  DevBuf<float> fx_in_, fq_n_, f_ch_, fx_inc_;
+  DevBuf<float> fx_in_, fq_n_, fx_inc_;
   DevBuf<unsigned> f_words_;
-  DevBuf<double> f_mu_;
-  DevBuf<int> f_ci_, f_cc_, f_qi_, f_st_;
   HostBuf<char> f_stage_;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_rows_ = nullptr;
@@ -522,28 +522,23 @@ class KnnCore {
     // — is served too: render() then copies the lists and labels instead of the report text)
     if (rt_.world != 1 || exact_ || !in || N_ == 0 || Q_ == 0 || Q_ > (1 << 30)) return false;
     const int KT = std::max(1, (A_ + 31) / 32);
-    if (dmlp_screen_x1_qw(KT) <= 0 || kmax_ > 32 || kmax_ > N_) return false;
-    if (*std::min_element(in->k.begin(), in->k.end()) < 1) return false;
+    if (dmlp_screen_x1_qw(KT) <= 0) return false;
     FastOut fo;
     if (fast_core(in->X.data(), in->labels.data(), in->Qx.data(), in->k.data(), Q_, fo) != 0)
       return false;
     render(out, fo.cs, fo.lb, fo.dd, fo.ii);  // synchronizes the stream
-    for (int64_t q = 0; q < Q_; ++q)
-      if (fo.st_h[q]) return false;  // single-term overflow: redo the call on the general path
     trace.mark("report");
     return true;
   }
 
   // The pipeline of farm_fast for nq queries (Qx / k: this rank's block) against the whole
-  // dataset X; leaves the per-query status copy pending on the stream (fo.st_h, valid after the
-  // next sync).  Returns 0, or 1 when the data / queries are outside the screen's range (nothing
-  // left in flight).
+  // dataset X.  Returns 0 (results in fo, complete on the stream), or 1 when the data / queries
+  // are outside the fp16 screen's range (nothing left in flight).
   struct FastOut {
     double* dd = nullptr;
     int* ii = nullptr;
     int* lb = nullptr;
     uint64_t* cs = nullptr;
-    std::vector<int> st_h;
   };
   // shard = true (node-shared farm, P > 1): this rank renders only its 1/P tile range of the
   // dataset's screen image and one all-gather completes it; the data-range verdict and the max
@@ -560,8 +555,7 @@ class KnnCore {
     // page-locked staging for the rendered operands (host_ops_h2d copies from it)
     const size_t b_xhi = nt * 64 * W * 2, b_xin = nt * 64 * 4, b_qhi = nq * W * 2, b_qn = nq * 4;
     auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t need = up(b_xhi) + up(b_xin) + 256 + up(b_qhi) + up(b_qn) + up(A_ * 8) +
-                        up(nq * 4);
+    const size_t need = up(b_xhi) + up(b_xin) + 256 + up(b_qhi) + up(b_qn) + up(A_ * 8);
     if (f_stage_.size() < need) f_stage_.resize(need);
     char* hp = f_stage_.data();
     uint16_t* xhi_h = (uint16_t*)hp; hp += up(b_xhi);
@@ -569,16 +563,15 @@ class KnnCore {
     unsigned* xnm_h = (unsigned*)hp; hp += 256;
     uint16_t* qhi_h = (uint16_t*)hp; hp += up(b_qhi);
     float* qn_h = (float*)hp; hp += up(b_qn);
-    double* mu_h = (double*)hp; hp += up(A_ * 8);
-    int* id_h = (int*)hp;
+    double* mu_h = (double*)hp;
     dmlp_cpu_center(X, N_, A_, mu_h);
     short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
     float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
     short* xhi_c = shard ? fx_hic_.get(tpr * 64 * W) : xhi;
     float* xin_c = shard ? fx_inc_.get(tpr * 64) : xin;
     unsigned* words = f_words_.get(2);  // [0] xnmax bits, [1] bad (0: the host checked ranges)
-    short* qhi = fq_hi_.get(nq * W);
-    float* qn = fq_n_.get(nq);
+    short* qhi = fq_hi_.get(std::max<int64_t>(nq, 1) * W);
+    float* qn = fq_n_.get(std::max<int64_t>(nq, 1));
     int rc = dmlp_host_ops_h2d_tiles(X, N_, t0, t1, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h,
                                      qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn, host_slices_, st);
     if (rc & 4) throw std::runtime_error("host operand copy failed");
@@ -596,53 +589,34 @@ class KnnCore {
       return 1;  // outside the screen's range: the device path decides
     }
     if (nq == 0) {  // a rank without queries (Q < P) took part in the collectives only
-      fo.st_h.clear();
       rt_.sync();
       return 0;
     }
     HIPCHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), st));
     trace.mark("h2d_operands");
-    int* kd = kd_.get(nq);
-    HIPCHK(hipMemcpyAsync(kd, k, nq * 4, hipMemcpyHostToDevice, st));
-    int* qi = f_qi_.get(nq);
-    if (qi_len_ < nq) {  // identity query index (grow-only; a larger get() also resets it)
-      for (int64_t q = 0; q < nq; ++q) id_h[q] = (int)q;
-      HIPCHK(hipMemcpyAsync(qi, id_h, nq * 4, hipMemcpyHostToDevice, st));
-      qi_len_ = nq;
-    }
-    const int kcls = kmax_;
-    const int cap = dmlp_screen_x1_cap(kcls);
-    const int S = LocalKnn::slices_stream((int)nq, dmlp_screen_x1_cols(KT, kcls), nt,
-                                          dmlp_screen_x1_waves_per_cu(kcls),
-                                          dmlp_screen_x1_min_slices(nt));
-    int* ci = f_ci_.get((size_t)nq * S * cap);
-    int* cc = f_cc_.get((size_t)nq * S);
-    float* ch = f_ch_.get((size_t)nq * S * 2);
-    DMLPCHK(dmlp_screen_x1(KT, 1, A_, xhi, xin, nt, N_, qhi, qn, qi, kd, (int)nq, kcls, words,
-                           words + 1, S, ci, cc, ch, st));
-    // fp64 rows + labels behind the screen, on the side stream — enqueued after everything the
-    // screen needs, so no small copy of the main stream queues behind them on the copy engine
+    // fp64 rows + labels behind the screen, on the side stream — enqueued by LocalKnn::run right
+    // after the screen launch (everything the screen needs is queued by then), so no small copy
+    // of the main stream queues behind them on the copy engine
     double* Xd = X_.get(N_ * A_);
     int* Ld = lab_.get(N_);
     double* Qd = Qx_.get(nq * A_);
-    HIPCHK(hipMemcpyAsync(Xd, X, N_ * A_ * 8, hipMemcpyHostToDevice, side_));
-    HIPCHK(hipMemcpyAsync(Ld, labels, N_ * 4, hipMemcpyHostToDevice, side_));
-    HIPCHK(hipMemcpyAsync(Qd, Qx, nq * A_ * 8, hipMemcpyHostToDevice, side_));
-    HIPCHK(hipEventRecord(ev_rows_, side_));
-    trace.mark("screen");
-    HIPCHK(hipStreamWaitEvent(st, ev_rows_, 0));
+    auto issue_rows = [&]() {
+      // (no stream dependency: the previous call ended with a sync, nothing reads these yet)
+      HIPCHK(hipMemcpyAsync(Xd, X, N_ * A_ * 8, hipMemcpyHostToDevice, side_));
+      HIPCHK(hipMemcpyAsync(Ld, labels, N_ * 4, hipMemcpyHostToDevice, side_));
+      HIPCHK(hipMemcpyAsync(Qd, Qx, nq * A_ * 8, hipMemcpyHostToDevice, side_));
+      HIPCHK(hipEventRecord(ev_rows_, side_));
+      trace.mark("screen");
+    };
     fo.dd = d_.get(nq * kmax_);
     fo.ii = ids_.get(nq * kmax_);
     fo.lb = labout_.get(nq);
     fo.cs = cs_.get(nq);
-    int* stat = f_st_.get(nq);
-    // (the refine writes every row's padding and status itself: no fill passes)
-    DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, Xd, A_, Qd, xhi, xin, qhi, KT, 1, N_, nullptr,
-                               kd, (int)nq, fo.dd, fo.ii, kmax_, Ld, lo_, hi_, fo.lb, fo.cs, stat,
-                               nullptr, st));
-    trace.mark("refine");
-    fo.st_h.resize(nq);
-    HIPCHK(hipMemcpyAsync(fo.st_h.data(), stat, nq * 4, hipMemcpyDeviceToHost, st));
+    LocalKnn::HostX1 hx;
+    hx.xhi = xhi; hx.xin = xin; hx.words = words; hx.qhi = qhi; hx.qn = qn;
+    lk_.X = Xd; lk_.N = N_; lk_.A = A_; lk_.KT = KT;
+    lk_.run(Qd, nq, k, kmax_, fo.dd, fo.ii, Ld, lo_, hi_, fo.lb, fo.cs, &hx, ev_rows_, issue_rows);
+    trace.mark("knn");
     return 0;
   }
 
@@ -659,14 +633,10 @@ class KnnCore {
     block_partition(Q_, P, cnt, off);
     const int64_t a = off[r], nl = cnt[r];
     const int KT = std::max(1, (A_ + 31) / 32);
-    int ok = dmlp_screen_x1_qw(KT) > 0 && kmax_ <= 32 && kmax_ <= N_ && nl <= (1 << 30);
-    if (ok && nl) ok = *std::min_element(sh_.k + a, sh_.k + a + nl) >= 1;
+    int ok = dmlp_screen_x1_qw(KT) > 0 && nl <= (1 << 30);
     MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
     if (!ok) return false;
-    if (!side_) {
-      HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
-    }
+    if (!side_) make_side();
     FastOut fo;
     // (every rank enters fast_core, even with no queries: the image all-gather is collective)
     int bad = fast_core(sh_.X, sh_.labels, sh_.Qx + a * A_, sh_.k + a, nl, fo, image_shard_);
@@ -680,7 +650,6 @@ class KnnCore {
       HIPCHK(hipMemcpyAsync(total_h_.data(), off_d + nl, 8, hipMemcpyDeviceToHost, rt_.stream));
       rt_.sync();
       len = total_h_.data()[0];
-      for (int64_t q = 0; q < nl; ++q) bad |= fo.st_h[q] != 0;  // single-term overflow
     }
     MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
     if (bad) return false;  // every rank redoes the call on the general farm
@@ -704,6 +673,12 @@ class KnnCore {
     }
     trace.mark("report");
     return true;
+  }
+  hipEvent_t ev_ops_ = nullptr;
+  void make_side() {
+    HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_ops_, hipEventDisableTiming));
   }
   SharedIn sh_;
   // KNN_IMAGE_SHARD=0: every rank renders the whole screen image (A/B)

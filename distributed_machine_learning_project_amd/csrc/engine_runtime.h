@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -366,45 +367,119 @@ struct LocalKnn {
     return S;
   }
 
+  // The host-rendered single-term operands (host_prep.cpp, fp16, hl = 1), already on the device
+  // (or in flight on the stream): the x1 class screens with them, so neither the dataset image
+  // nor the query fragments are rendered on the device unless a query needs the 3-term screens.
+  struct HostX1 {
+    const void* xhi = nullptr;
+    const float* xin = nullptr;
+    unsigned* words = nullptr;  // [0] xnmax bits, [1] bad (0)
+    const void* qhi = nullptr;
+    const float* qn = nullptr;
+  };
+  DevBuf<int> ident_, ovf_;
+  int64_t ident_len_ = 0;
+  std::vector<int> ident_h_;
+  int* identity(int64_t n) {  // device 0, 1, ..., n-1 (grow-only)
+    int* p = ident_.get(std::max<int64_t>(n, 1));
+    if (ident_len_ < n) {
+      ident_h_.resize(n);
+      for (int64_t i = 0; i < n; ++i) ident_h_[i] = (int)i;
+      HIPCHK(hipMemcpyAsync(p, ident_h_.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+      ident_len_ = n;
+    }
+    return p;
+  }
+
   // Exact top-k (+ vote/checksum when labels != nullptr) of queries Qx [Q][A] (device).
-  // k_host drives dispatch; out_* are [Q][kstride]; lab/cs may be null.
+  // k_host drives dispatch; out_* are [Q][kstride]; lab/cs may be null.  Per-query classes:
+  // 1 <= k <= 32 the single-term x1 screen (host operands hx when given, else the device image
+  // prepare() rendered), 32 < k <= 128 the 3-term LDS screen, the rest the exact path; a query
+  // whose x1 candidates overflow escalates alone (3-term screen, then exact).  With hx the
+  // fp64 rows X / Qx may still be in flight: everything that reads them waits for `rows`, and
+  // the device image (for 3-term work) is rendered on first need (prepare() was not called).
   void run(const double* Qx, int64_t Q, const int* k_host, int kstride, double* out_d,
-           int* out_i, const int* labels, int lab_lo, int lab_hi, int* lab, uint64_t* cs) {
+           int* out_i, const int* labels, int lab_lo, int lab_hi, int* lab, uint64_t* cs,
+           const HostX1* hx = nullptr, hipEvent_t rows = nullptr,
+           const std::function<void()>& issue_rows = nullptr) {
     if (Q == 0) return;
+    // issue_rows() enqueues the fp64 row copies (recording `rows`): right after the first
+    // screen launch, so that this call's small copies never queue behind them on the copy
+    // engine, or before the first wait on them if no screen runs
+    bool rows_issued = !issue_rows;
+    auto launch_rows = [&]() {
+      if (!rows_issued) { issue_rows(); rows_issued = true; }
+    };
     std::vector<int> kk(Q), a, b, f, rest;
+    bool all_a = true;
     for (int64_t q = 0; q < Q; ++q) kk[q] = (int)std::min<int64_t>(k_host[q], N);
     const bool screen = KT <= 4 && N > 0;
+    const bool x1_ok = dmlp_screen_x1_qw(KT) > 0;
     for (int64_t q = 0; q < Q; ++q) {
-      if (kk[q] < 1) { rest.push_back((int)q); continue; }
-      if (screen && kk[q] <= 32) a.push_back((int)q);
-      else if (screen && kk[q] <= 128) b.push_back((int)q);
-      else f.push_back((int)q);
+      if (kk[q] < 1) { rest.push_back((int)q); all_a = false; continue; }
+      if (screen && kk[q] <= 32 && (x1_ok || !hx)) a.push_back((int)q);
+      else if (screen && kk[q] <= 128) { b.push_back((int)q); all_a = false; }
+      else { f.push_back((int)q); all_a = false; }
       if (k_host[q] > N) rest.push_back((int)q);
     }
+    bool rows_waited = rows == nullptr;
+    auto wait_rows = [&]() {
+      launch_rows();
+      if (!rows_waited) { HIPCHK(hipStreamWaitEvent(st, rows, 0)); rows_waited = true; }
+    };
+    bool dev_ready = hx == nullptr;  // device image (prepare) + device query fragments
+    bool qprep = false;
+    auto need_dev = [&]() {
+      if (!dev_ready) {
+        wait_rows();
+        prepare(X, N, A);
+        dev_ready = true;
+      }
+      if (!qprep) {
+        DMLPCHK(dmlp_prep_queries(Qx, Q, A, mu.p, KT, qhi.get(Q * KT * 32), qlo.get(Q * KT * 32),
+                                  qn.get(Q), words.p + 1, st));
+        qprep = true;
+      }
+    };
     int* kd = kdev.get(Q);
     HIPCHK(hipMemcpyAsync(kd, kk.data(), Q * sizeof(int), hipMemcpyHostToDevice, st));
-    // padding (+inf, -1) for k > N, like bench_2's {1e18, -1} sentinel
-    HIPCHK(hipMemsetAsync(out_i, 0xff, (size_t)Q * kstride * sizeof(int), st));
-    DMLPCHK(dmlp_fill_f64(out_d, (int64_t)Q * kstride, INFINITY, st));
     int* stat = status.get(Q);
-    HIPCHK(hipMemsetAsync(stat, 0, Q * sizeof(int), st));
     const bool fin = labels != nullptr;
+    // (the x1 refine writes every row's padding and status itself; the other paths need fills)
+    bool filled = false;
+    auto fill = [&]() {
+      if (filled) return;
+      // padding (+inf, -1) for k > N, like bench_2's {1e18, -1} sentinel
+      HIPCHK(hipMemsetAsync(out_i, 0xff, (size_t)Q * kstride * sizeof(int), st));
+      DMLPCHK(dmlp_fill_f64(out_d, (int64_t)Q * kstride, INFINITY, st));
+      HIPCHK(hipMemsetAsync(stat, 0, Q * sizeof(int), st));
+      filled = true;
+    };
+    int* ovf = ovf_.get(1);
+    HIPCHK(hipMemsetAsync(ovf, 0, sizeof(int), st));
+    // once, before any kernel writes results: every refine writes its queries' padding and
+    // status itself, so the fill is only needed for rows no refine covers (exact path, k < 1)
+    if (!all_a || !hx) fill();
     if (!a.empty() || !b.empty()) {
-      DMLPCHK(dmlp_prep_queries(Qx, Q, A, mu.p, KT, qhi.get(Q * KT * 32), qlo.get(Q * KT * 32),
-                                qn.get(Q), words.p + 1, st));
       const float er = eps_rel(A);
       const int64_t nt = (N + 63) / 64;
       const int qw = dmlp_screen_stream_qw(KT);
-      // default: single-term bf16 screen (screen_x1.hip); KNN_SCREEN=stream: 3-term streaming
+      // default: single-term screen (screen_x1.hip); KNN_SCREEN=stream: 3-term streaming
       const char* impl = std::getenv("KNN_SCREEN");
-      const bool x1 = dmlp_screen_x1_qw(KT) > 0 && !(impl && std::string(impl) == "stream");
+      const bool use_x1 = x1_ok && !(impl && std::string(impl) == "stream" && !hx);
       // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 128)
-      auto pass = [&](const std::vector<int>& idx, int impl, DevBuf<int>& qbuf) {
-        const int nq = (int)idx.size();
-        int* qi = qbuf.get(nq);
-        HIPCHK(hipMemcpyAsync(qi, idx.data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
+      auto pass = [&](const std::vector<int>* idx, int impl, DevBuf<int>& qbuf) {
+        const int nq = idx ? (int)idx->size() : (int)Q;
+        int* qi;
+        if (idx) {
+          qi = qbuf.get(nq);
+          HIPCHK(hipMemcpyAsync(qi, idx->data(), nq * sizeof(int), hipMemcpyHostToDevice, st));
+        } else {
+          qi = identity(Q);
+        }
         int kcls = 1;
-        for (int q : idx) kcls = std::max(kcls, kk[q]);
+        if (idx) for (int q : *idx) kcls = std::max(kcls, kk[q]);
+        else for (int64_t q = 0; q < Q; ++q) kcls = std::max(kcls, kk[q]);
         const int cap = impl == 0 ? dmlp_screen_x1_cap(kcls)
                         : impl == 1 ? dmlp_screen_stream_cap(kcls) : (kcls <= 32 ? 128 : 256);
         const int S = impl == 0 ? slices_stream(nq, dmlp_screen_x1_cols(KT, kcls), nt,
@@ -416,13 +491,22 @@ struct LocalKnn {
         int* cc = cand_cnt.get((size_t)nq * S);
         if (impl == 0) {
           float* ch = cand_h.get((size_t)nq * S * 2);
-          DMLPCHK(dmlp_screen_x1(KT, 2, A, xfrag.p, xinit.p, nt, N, qhi.p, qn.p, qi, kd, nq, kcls,
-                                 words.p, words.p + 1, S, ci, cc, ch, st));
-          DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xfrag.p, xinit.p, qhi.p, KT, 2, N,
-                                     qi, kd, nq, out_d, out_i, kstride, fin ? labels : nullptr,
-                                     lab_lo, lab_hi, lab, cs, stat, nullptr, st));
+          const void* xf = hx ? hx->xhi : (const void*)xfrag.p;
+          const float* xi = hx ? hx->xin : xinit.p;
+          unsigned* wd = hx ? hx->words : words.p;
+          const void* qh = hx ? hx->qhi : (const void*)qhi.p;
+          const float* qnn = hx ? hx->qn : qn.p;
+          const int hl = hx ? 1 : 2;
+          DMLPCHK(dmlp_screen_x1(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1, S,
+                                 ci, cc, ch, st));
+          wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
+          DMLPCHK(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xf, xi, qh, KT, hl, N,
+                                     idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
+                                     fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, ovf,
+                                     st));
           return;
         }
+        need_dev();
         if (impl == 1)
           DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq, kcls,
                                      words.p, words.p + 1, er, S, ci, cc, st));
@@ -430,30 +514,46 @@ struct LocalKnn {
           DMLPCHK(dmlp_screen(KT, cap, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq,
                               words.p, words.p + 1, er, S, ci, cc, st));
         DMLPCHK(dmlp_refine(cap, ci, cc, S, X, A, Qx, qi, kd, nq, out_d, out_i, kstride,
-                            fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, nullptr, st));
+                            fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, ovf, st));
       };
-      const int first_a = x1 ? 0 : (qw > 0 ? 1 : 2);
-      if (!a.empty()) pass(a, first_a, qidx_a);
-      if (!b.empty()) pass(b, 2, qidx_b);
-      // one host sync: which screened queries overflowed
-      std::vector<int> sh(Q);
-      HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+      if (!hx) need_dev();  // the device operands of every screen
+      const int first_a = use_x1 ? 0 : (qw > 0 ? 1 : 2);
+      if (!a.empty()) pass(all_a ? nullptr : &a, first_a, qidx_a);
+      if (!b.empty()) pass(&b, 2, qidx_b);
+      // one host sync: the overflow count (4 bytes); the per-query status only when some
+      // screened query overflowed
+      int novf = 0;
+      HIPCHK(hipMemcpyAsync(&novf, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
       wait();
-      if (first_a == 0) {
-        // single-term overflow (data too tight for its bound): escalate to the 3-term screen
+      if (novf) {
+        std::vector<int> sh(Q);
+        HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+        wait();
         std::vector<int> esc;
-        for (int q : a)
-          if (sh[q]) esc.push_back(q);
+        if (first_a == 0)
+          for (int q : a)
+            if (sh[q]) esc.push_back(q);
         if (!esc.empty()) {
-          pass(esc, qw > 0 ? 1 : 2, qidx_e);
-          HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+          // single-term overflow (data too tight for its bound): those queries alone go to the
+          // 3-term screen
+          HIPCHK(hipMemsetAsync(ovf, 0, sizeof(int), st));
+          for (int q : esc) HIPCHK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
+          pass(&esc, qw > 0 ? 1 : 2, qidx_e);
+          HIPCHK(hipMemcpyAsync(&novf, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
           wait();
+          if (novf) {
+            HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+            wait();
+          } else {
+            std::fill(sh.begin(), sh.end(), 0);
+          }
         }
+        for (int64_t q = 0; q < Q; ++q)
+          if (sh[q]) f.push_back((int)q);
       }
-      for (int64_t q = 0; q < Q; ++q)
-        if (sh[q]) f.push_back((int)q);
     }
     if (!f.empty()) {
+      wait_rows();
       std::sort(f.begin(), f.end());
       // k <= dmlp_exact_topk_kmax_for(N) (64, or 256 for large N): fused streaming exact kernel
       // (exact.hip); k <= 2048: radix select over exact rows; larger k: rows + segmented sort
@@ -476,12 +576,12 @@ struct LocalKnn {
         const std::vector<int>& v = pass == 0 ? small : big;
         if (v.empty()) continue;
         HIPCHK(hipMemcpyAsync(qi + base, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice, st));
-        const int rows = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)v.size(),
-                                                                     (1ll << 27) / std::max<int64_t>(1, N)));
-        const int64_t wsb = pass == 0 ? dmlp_fallback_select_bytes(rows, N) : dmlp_fallback_bytes(rows, N);
+        const int rows_ = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)v.size(),
+                                                                      (1ll << 27) / std::max<int64_t>(1, N)));
+        const int64_t wsb = pass == 0 ? dmlp_fallback_select_bytes(rows_, N) : dmlp_fallback_bytes(rows_, N);
         char* ws = fb_ws.get(wsb);
-        for (size_t c0 = 0; c0 < v.size(); c0 += rows) {
-          const int nb = (int)std::min<size_t>(rows, v.size() - c0);
+        for (size_t c0 = 0; c0 < v.size(); c0 += rows_) {
+          const int nb = (int)std::min<size_t>(rows_, v.size() - c0);
           if (pass == 0)
             DMLPCHK(dmlp_fallback_select(X, N, A, Qx, qi + base + c0, kd, nb, ws, wsb, out_d, out_i,
                                          kstride, st));
@@ -494,6 +594,7 @@ struct LocalKnn {
       rest.insert(rest.end(), f.begin(), f.end());
     }
     if (fin && !rest.empty()) {
+      wait_rows();
       std::sort(rest.begin(), rest.end());
       rest.erase(std::unique(rest.begin(), rest.end()), rest.end());
       // the vote/checksum of k > N queries covers the padding, so use the unclamped k

@@ -6,8 +6,11 @@
 // these operands have landed, with the fp64 queries copied behind the screen.  mu is the mean of
 // the first min(N, 4096) rows, exactly the rows k_center (prep.hip) uses.
 //
-// The bits match prep.hip: c = q - mu in fp64; hi = bf16_rn(fp32_rn(c)); |c| >= 1e15 or NaN
-// flags the input as outside the screen's range (the caller then takes the device path).
+// The host render is the fp16 single-term image (hl = 1 for dmlp_screen_x1 / dmlp_refine_groups):
+// c = q - mu in fp64; hi = fp16_rn(fp32_rn(c)) — 11 significant bits where bf16 has 8, so the
+// single-term error bound is 4x tighter and fewer groups reach the re-rank; |c| >= 65504 (the
+// fp16 range) or NaN flags the input as outside the screen's range (the caller then takes the
+// device path, whose bf16 hi/lo image covers any finite data below 1e15).
 #include "dmlp.h"
 
 #include <algorithm>
@@ -28,7 +31,7 @@
 
 namespace {
 
-constexpr double kMaxAbs = 1.0e15;
+constexpr double kMaxAbs = 65504.0;  // the largest finite fp16
 constexpr int kMaxPool = 16;  // pool size cap; also sizes the per-part scratch of the data prep
 
 // pause iterations a worker spins after a job before it sleeps (DMLP_POOL_SPIN; default 100000,
@@ -173,11 +176,22 @@ Pool& pool() {
   return p;
 }
 
-inline uint16_t bf16_rn(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs only)
-  return (uint16_t)(u >> 16);
+// fp32 -> fp16, round to nearest even, subnormals included (|f| < 65504 by the range check;
+// the same bits as F16C's vcvtps2ph with _MM_FROUND_TO_NEAREST_INT).
+inline uint16_t f16_rn(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // >= 65520: inf (flagged anyway)
+  if (ax < 0x38800000u) {                                    // < 2^-14: fp16 subnormal or zero
+    float af;
+    std::memcpy(&af, &ax, 4);
+    // af * 2^24 is exact; nearbyint rounds half to even in the default rounding mode
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(af * 16777216.0f));
+  }
+  uint32_t r = ax - 0x38000000u;        // rebias the exponent 127 -> 15
+  r += 0xfffu + ((r >> 13) & 1u);       // round the 13 dropped mantissa bits to nearest even
+  return (uint16_t)(sign | (r >> 13));  // a carry into the exponent is the correct rounding
 }
 
 }  // namespace
@@ -213,7 +227,7 @@ int prep_range_scalar(const double* Qx, int64_t q0, int64_t q1, int A, const dou
       double c = r[a] - mu[a];
       if (!(std::fabs(c) < kMaxAbs)) { ok = 0; c = 0.0; }
       s4[a & 3] += c * c;
-      h[a] = bf16_rn((float)c);
+      h[a] = f16_rn((float)c);
     }
     for (int a = A; a < W; ++a) h[a] = 0;
     qn[q] = (float)((s4[0] + s4[2]) + (s4[1] + s4[3]));
@@ -222,12 +236,11 @@ int prep_range_scalar(const double* Qx, int64_t q0, int64_t q1, int A, const dou
 }
 
 // A multiple of 8: 4 doubles per vector, partial sums s4[a & 3] exactly as the scalar row.
-__attribute__((target("avx2"))) int prep_range_avx2(const double* Qx, int64_t q0, int64_t q1,
-                                                     int A, const double* mu, int W,
-                                                     uint16_t* qhi, float* qn) {
+__attribute__((target("avx2,f16c"))) int prep_range_avx2(const double* Qx, int64_t q0, int64_t q1,
+                                                          int A, const double* mu, int W,
+                                                          uint16_t* qhi, float* qn) {
   const __m256d lim = _mm256_set1_pd(kMaxAbs);
   const __m256d sgn = _mm256_set1_pd(-0.0);
-  const __m256i rnd = _mm256_set1_epi32(0x7fff), one = _mm256_set1_epi32(1);
   __m256d okv = _mm256_castsi256_pd(_mm256_set1_epi64x(-1));
   for (int64_t q = q0; q < q1; ++q) {
     const double* r = Qx + q * A;
@@ -244,13 +257,8 @@ __attribute__((target("avx2"))) int prep_range_avx2(const double* Qx, int64_t q0
       acc = _mm256_add_pd(acc, _mm256_mul_pd(c0, c0));
       acc = _mm256_add_pd(acc, _mm256_mul_pd(c1, c1));
       const __m256 f = _mm256_set_m128(_mm256_cvtpd_ps(c1), _mm256_cvtpd_ps(c0));
-      __m256i u = _mm256_castps_si256(f);
-      u = _mm256_add_epi32(u, _mm256_add_epi32(rnd, _mm256_and_si256(_mm256_srli_epi32(u, 16), one)));
-      u = _mm256_srli_epi32(u, 16);
-      // 8 x u32 -> 8 x u16 (values < 2^16): pack within lanes, then gather the two halves
-      const __m256i p = _mm256_packus_epi32(u, u);
-      const __m256i o = _mm256_permute4x64_epi64(p, 0x08);
-      _mm_storeu_si128((__m128i*)(h + a), _mm256_castsi256_si128(o));
+      _mm_storeu_si128((__m128i*)(h + a),
+                       _mm256_cvtps_ph(f, _MM_FROUND_TO_NEAREST_INT | _MM_FROUND_NO_EXC));
     }
     for (int a = A; a < W; ++a) h[a] = 0;
     alignas(32) double s4[4];
@@ -262,14 +270,14 @@ __attribute__((target("avx2"))) int prep_range_avx2(const double* Qx, int64_t q0
 
 int prep_range_any(const double* Qx, int64_t q0, int64_t q1, int A, const double* mu, int W,
                    uint16_t* qhi, float* qn) {
-  static const bool avx2 = __builtin_cpu_supports("avx2");
+  static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("f16c");
   if (avx2 && A % 8 == 0) return prep_range_avx2(Qx, q0, q1, A, mu, W, qhi, qn);
   return prep_range_scalar(Qx, q0, q1, A, mu, W, qhi, qn);
 }
 
 }  // namespace
 
-// qhi: [Q][KT*32] bf16 bits (zero padded), qn: [Q] fp32 |q - mu|^2.  Returns 1 if some
+// qhi: [Q][KT*32] fp16 bits (zero padded), qn: [Q] fp32 |q - mu|^2.  Returns 1 if some
 // |q - mu| is outside the screen's range (outputs then not usable), else 0.
 extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
                                      uint16_t* qhi, float* qn) {
@@ -286,12 +294,12 @@ extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const d
 
 namespace {
 
-// One point's contribution to the hi-only tile image: 8 attributes (one 16-byte fragment chunk)
+// One point's contribution to the fp16 hi-only tile image: 8 attributes (one 16-byte fragment chunk)
 // per (kt, kg), |c|^2 in fp64.  The chunk of point p = t*64 + rt*16 + r, attributes kt*32 + kg*8
 // .. +7, sits at uint4 index ((t*4 + rt)*KT + kt)*64 + kg*16 + r (prep.hip's layout, lo dropped).
 int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, const double* mu,
                     int KT, uint16_t* xhi, float* xinit, float* nmax) {
-  static const bool avx2 = __builtin_cpu_supports("avx2");
+  static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("f16c");
   const int W = KT * 32;
   int ok = 1;
   float mx = 0.0f;

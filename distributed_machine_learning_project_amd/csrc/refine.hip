@@ -107,7 +107,8 @@ __device__ __forceinline__ void finalize_wave(const int* ids, int k, const int* 
 // (ordered 16-bit group-max key << 16 | slice-relative group index) and cand_h holds each
 // slice's final threshold and the query's screen error bound eps.  The k-th largest key over all slices gives h = a_k' - 2 eps (a lower
 // bound on a_k - eps, exactly the screen's own rule, but global); a member survives iff its
-// single-term score  s = -|x'|^2/2 + <hi(q'), hi(x')>  (recomputed from the screen's bf16 image;
+// single-term score  s = -|x'|^2/2 + <hi(q'), hi(x')>  (recomputed from the screen's image: bf16
+// for hl = 2, fp16 for hl = 1;
 // any summation order obeys the same error bound) is >= h.  Only survivors get exact distances.
 struct GroupIn {
   const float* cand_h;    // [nq * S][2]: slice threshold, query eps
@@ -124,8 +125,8 @@ struct GroupIn {
 // variant sizes its LDS for k <= 32 (the screen's limit) and labels in [lo, lo + 256) (wider
 // label ranges take wave_vote's counting fallback), so more waves stay resident to hide the
 // gathers that dominate this kernel.
-template <int E, int GROUPS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 : 1))) void k_refine(
+template <int E, int GROUPS, bool F16 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1 ? 8 : GROUPS ? 4 : 1))) void k_refine(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int S, int cap,
     const double* __restrict__ X, int A, const double* __restrict__ Qx,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
@@ -281,6 +282,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
           const int pl = id & 63;
           const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * gin.hl * 64) + (pl & 15);
           float sc = gin.xinit[id];
+          // F16: the host's fp16 image + fp16 query fragments (hl = 1); else bf16 (a template
+          // parameter: both decodes in one body pushed this 64-VGPR kernel into scratch spills)
 #pragma unroll
           for (int kt = 0; kt < KT; ++kt) {
             const u32x4* fk = fr + (int64_t)(((pl >> 4) * KT + kt) * gin.hl) * 64;
@@ -290,8 +293,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS ? 8 
 #pragma unroll
               for (int q2 = 0; q2 < 4; ++q2) {
                 const unsigned qw = qraw[kt * 4 + kq][q2];
-                sc += __uint_as_float(qw << 16) * __uint_as_float(w[q2] << 16);
-                sc += __uint_as_float(qw & 0xffff0000u) * __uint_as_float(w[q2] & 0xffff0000u);
+                if constexpr (F16) {  // products exact in fp32 either way: any order obeys the bound
+                  sc += (float)__builtin_bit_cast(_Float16, (unsigned short)(qw & 0xffffu)) *
+                        (float)__builtin_bit_cast(_Float16, (unsigned short)(w[q2] & 0xffffu));
+                  sc += (float)__builtin_bit_cast(_Float16, (unsigned short)(qw >> 16)) *
+                        (float)__builtin_bit_cast(_Float16, (unsigned short)(w[q2] >> 16));
+                } else {
+                  sc += __uint_as_float(qw << 16) * __uint_as_float(w[q2] << 16);
+                  sc += __uint_as_float(qw & 0xffff0000u) * __uint_as_float(w[q2] & 0xffff0000u);
+                }
               }
             }
           }
@@ -1023,12 +1033,17 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
   const int64_t n_tiles = (n_points + 63) / 64;
   const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
                     (int)((n_tiles + S - 1) / S)};
-#define DMLP_REFINE_G(KTV)                                                                     \
-  hipLaunchKernelGGL((k_refine<2, KTV>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
+#define DMLP_REFINE_G(KTV, F16)                                                                \
+  hipLaunchKernelGGL((k_refine<2, KTV, F16>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
                      labels, label_lo, label_hi, out_label, out_cs, status, ovf_count, gin)
-  if (KT == 1) DMLP_REFINE_G(1);
-  else DMLP_REFINE_G(2);
+  if (KT == 1) {
+    if (hl == 1) DMLP_REFINE_G(1, true);
+    else DMLP_REFINE_G(1, false);
+  } else {
+    if (hl == 1) DMLP_REFINE_G(2, true);
+    else DMLP_REFINE_G(2, false);
+  }
 #undef DMLP_REFINE_G
   DMLP_LAUNCH_CHECK();
   return 0;

@@ -17,6 +17,11 @@
 //    one-column-at-a-time ballot radix cost ~2.5k cycles per column; here a batch costs about as
 //    much for all 64 columns, and every column's threshold rises at each batch.
 //
+// Element type: hl = 2 (prep.hip's device image) is bf16 hi/lo and runs v_mfma_f32_16x16x32_bf16;
+// hl = 1 (host_prep.cpp's hi-only image and query fragments) is fp16 and runs
+// v_mfma_f32_16x16x32_f16 at the same rate — 3 more significant bits per operand, a 4x tighter
+// bound r1 (plus r3, the absolute error of fp16 subnormals), so fewer groups reach the re-rank.
+//
 // Layout (mfma_f32_16x16x32_bf16): lane (c = lane & 15, kg = lane >> 4) of column tile ct holds
 // query column ct*16 + c and rows kg*4 .. kg*4+3 of the 16-point step.  The A operand (data
 // fragments, hi half of prep.hip's hi/lo image) streams from L2 into a D-deep register ring; the
@@ -54,6 +59,17 @@ struct X1Cfg {
 };
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// one 16x16x32 MFMA on 8 two-byte elements per lane: fp16 (F16) or bf16 bits
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // fp32 bits -> order-preserving u32 (only the top 16 bits are meaningful for a truncated key)
@@ -64,12 +80,12 @@ __device__ __forceinline__ unsigned unord32(unsigned o) {
   return o ^ ((o >> 31) ? 0x80000000u : 0xffffffffu);
 }
 
-template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE>
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE, bool F16>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32) ? 1 : 2))) void k_screen_x1(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
-    const unsigned* __restrict__ bad, float r1, float r2, int S, int tiles_per_slice,
+    const unsigned* __restrict__ bad, float r1, float r2, float r3, int S, int tiles_per_slice,
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
     float* __restrict__ cand_h) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
@@ -133,7 +149,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       const int col = ct * 16 + c;
       lh[col] = h[ct];
       lk[col] = valid ? qk[q] : 0;
-      leps[col] = valid ? r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax : 0.0f;
+      leps[col] = valid ? r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax +
+                              r3 * (sqrtf(qn[q]) + sqrtf(xnmax)) + r3 * 0x1p-15f
+                        : 0.0f;
       lflag[col] = 0;
     }
   }
@@ -293,10 +311,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
 #define DMLP_MFMA(R, AB)                                                                        \
   do {                                                                                          \
     _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
-      acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][0], bh[ct][0],                 \
-                                                            (MODE & 4) ? f32x4{0, 0, 0, 0} : Xi[R], 0, 0, 0); \
+      acc[AB][ct] = mfma16<F16>(A[R][0], bh[ct][0], (MODE & 4) ? f32x4{0, 0, 0, 0} : Xi[R]);      \
       _Pragma("unroll") for (int kt = 1; kt < KT; ++kt)                                         \
-        acc[AB][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[R][kt], bh[ct][kt], acc[AB][ct], 0, 0, 0); \
+        acc[AB][ct] = mfma16<F16>(A[R][kt], bh[ct][kt], acc[AB][ct]);                           \
     }                                                                                           \
   } while (0)
 #define DMLP_EPILOGUE(AB, J)                                                                    \
@@ -412,10 +429,10 @@ int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
 int g_x1_ct = 4;
 int x1_ct(int kmax) { return x1_sub(kmax) == 16 ? g_x1_ct : 4; }
 
-template <int KT, int SUB, int DEPTH, int CHECK, int CTV>
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, bool F16>
 int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
-              const unsigned* xnmax, const unsigned* bad, float r1, float r2, int S,
+              const unsigned* xnmax, const unsigned* bad, float r1, float r2, float r3, int S,
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
@@ -423,9 +440,9 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
   const int64_t grid = (int64_t)n_qblocks * S;
   if (grid <= 0) return 0;
 #define DMLP_X1_LAUNCH(M)                                                                      \
-  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
+  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M, F16>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
-                     (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, S, tps,          \
+                     (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h)
   switch (g_x1_mode) {
     case 1: DMLP_X1_LAUNCH(1); break;
@@ -449,11 +466,24 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
 //     |a - a_exact| <= r1 |q'| max|x'| + r2 max|x'|^2,
 //     r1 = 2u + u^2 + (A+2) 2^-24 (1+u)^2,   r2 = (A+2) 2^-24 / 2 + 2^-24,
 //   both taken x1.25 for the fp32 evaluation of the bound itself.
-extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
-  const double u = std::ldexp(1.0, -9) * (1.0 + std::ldexp(1.0, -15));
+//
+// fp16 operands (hl = 1): hi() = fp16(fp32(c)) has |c - hi(c)| <= u|c| + 2^-25 with
+// u = 2^-11 (1 + 2^-12) (the 2^-25 is half an fp16 subnormal step: |c| < 2^-14), and
+// fp16 x fp16 products are exact in fp32 as well, so the bound gains
+//     r3 (sum_a |q_a| + |x_a|) <= r3 (|q'| + max|x'|),  r3 = 2^-25 (1 + u) sqrt(A),
+// (x1.25 like the others) and the kernel adds r3 2^-15 >= A 2^-50 for the subnormal products.
+extern "C" void dmlp_screen_x1_bound2(int A, int hl, float* r1, float* r2, float* r3) {
+  const bool f16 = hl == 1;
+  const double u = f16 ? std::ldexp(1.0, -11) * (1.0 + std::ldexp(1.0, -12))
+                       : std::ldexp(1.0, -9) * (1.0 + std::ldexp(1.0, -15));
   const double e24 = std::ldexp(1.0, -24);
   *r1 = (float)(1.25 * (2.0 * u + u * u + (A + 2) * e24 * (1.0 + u) * (1.0 + u)));
   *r2 = (float)(1.25 * ((A + 2) * e24 * 0.5 + e24));
+  *r3 = f16 ? (float)(1.25 * std::ldexp(1.0, -25) * (1.0 + u) * std::sqrt((double)A)) : 0.0f;
+}
+extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
+  float r3;
+  dmlp_screen_x1_bound2(A, 2, r1, r2, &r3);
 }
 extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
 extern "C" int dmlp_screen_x1_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
@@ -494,18 +524,27 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
   if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
   if (kmax > 32 || KT < 1 || KT > 2 || A > KT * 32) return -3;
   if (hl != 1 && hl != 2) return -1;
-  float r1, r2;
-  dmlp_screen_x1_bound(A, &r1, &r2);
+  float r1, r2, r3;
+  dmlp_screen_x1_bound2(A, hl, &r1, &r2, &r3);
   hipStream_t st = (hipStream_t)stream;
 #define DMLP_X1_ARGS hl, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
-                     r2, S, cand_ids, cand_cnt, cand_h, st
+                     r2, r3, S, cand_ids, cand_cnt, cand_h, st
   const int sub = x1_sub(kmax);
   const int ct = x1_ct(kmax);
-  if (KT == 1) {
-    if (sub == 32) return launch_x1<1, 32, 4, 2, 4>(DMLP_X1_ARGS);
-    return ct == 8 ? launch_x1<1, 16, 4, 2, 8>(DMLP_X1_ARGS) : launch_x1<1, 16, 4, 2, 4>(DMLP_X1_ARGS);
-  }
-  if (sub == 32) return launch_x1<2, 32, 4, 2, 4>(DMLP_X1_ARGS);
-  return ct == 8 ? launch_x1<2, 16, 4, 2, 8>(DMLP_X1_ARGS) : launch_x1<2, 16, 4, 2, 4>(DMLP_X1_ARGS);
+  // hl = 1: the host's fp16 image + fp16 query fragments; hl = 2: prep.hip's bf16 hi/lo image
+#define DMLP_X1_PICK(F16)                                                                      \
+  do {                                                                                         \
+    if (KT == 1) {                                                                             \
+      if (sub == 32) return launch_x1<1, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                      \
+      return ct == 8 ? launch_x1<1, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                            \
+                     : launch_x1<1, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                           \
+    }                                                                                          \
+    if (sub == 32) return launch_x1<2, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                        \
+    return ct == 8 ? launch_x1<2, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                              \
+                   : launch_x1<2, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                             \
+  } while (0)
+  if (hl == 1) DMLP_X1_PICK(true);
+  DMLP_X1_PICK(false);
+#undef DMLP_X1_PICK
 #undef DMLP_X1_ARGS
 }

@@ -343,10 +343,8 @@ class _KnnCall:
         x1_ok = SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(KT) > 0
         self.stream_ok = SCREEN_IMPL != "lds" and L.dmlp_screen_stream_qw(KT) > 0
         self.first_a = "x1" if x1_ok else ("stream" if self.stream_ok else "lds")
-        if self.prepped is not None and self.all_a and self.first_a == "x1":
-            self.qhi, self.qn = self.prepped  # x1 reads neither qlo nor the fp64 rows
-            self.qlo = None
-        else:
+        self.qhi = self.qlo = self.qn = None  # device (bf16) query operands, rendered on need
+        if not (self.prepped is not None and ds.hl == 1 and self.first_a == "x1"):
             self._prep_on_device()
         self.kdev_eff = self.k_dev if kk is self.k_host else _h2d(kk.astype(np.int32), dev)
         if self.all_a or len(self.cls_a):
@@ -375,7 +373,7 @@ class _KnnCall:
     def _screen_pass(self, idx, impl):
         torch = _torch()
         if impl != "x1" and self.qlo is None:
-            self._prep_on_device()  # escalation after a host-prepared x1 pass
+            self._prep_on_device()  # 3-term class / escalation after a host-prepared x1 pass
         L = _lib.lib()
         ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
         N = ds.N
@@ -406,11 +404,23 @@ class _KnnCall:
                _p(self.cs), _p(self.status), self._ovf.ptr(self._ovf_slot), s)
         if impl == "x1":
             cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
+            # the host's fp16 image (hl = 1) pairs with the host's fp16 query fragments, prep.hip's
+            # bf16 image (hl = 2) with the device's bf16 ones
+            if ds.hl == 1:
+                if self.prepped is None:
+                    raise RuntimeError("x1 on the host fp16 image needs the host query operands")
+                x1_qhi, x1_qn = self.prepped
+            else:
+                if self.qhi is None:
+                    self._prep_on_device()
+                x1_qhi, x1_qn = self.qhi, self.qn
+            _mark("screen_start")
             _lib.check(L.dmlp_screen_x1(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
-                          _p(self.qhi), _p(self.qn), _p(qidx), _p(self.kdev_eff),
+                          _p(x1_qhi), _p(x1_qn), _p(qidx), _p(self.kdev_eff),
                           nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
                           _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
                        "screen_x1")
+            _mark("screen_done")
             if idx is None:
                 # every query goes through this refine: it writes each row's (+inf, -1) padding
                 # and each status itself, so no fill pass at all
@@ -419,9 +429,10 @@ class _KnnCall:
             self._wait_qx()
             _lib.check(L.dmlp_refine_groups(
                 cap, _p(cand_ids), _p(cand_cnt), _p(cand_h), S, _p(ds.X), A, _p(self.Qx),
-                _p(ds.xfrag), _p(ds.xinit), _p(self.qhi), KT, ds.hl, N,
+                _p(ds.xfrag), _p(ds.xinit), _p(x1_qhi), KT, ds.hl, N,
                 _p(qidx) if idx is not None else None, _p(self.kdev_eff), nq,
                 _p(self.out_d), _p(self.out_i), self.ks, *fin), "refine_groups")
+            _mark("refine_done")
             self._keep = (qidx, cand_ids, cand_cnt, cand_h)
             return
         if ds.hl != 2:
@@ -623,6 +634,50 @@ def io_bytes(reset: bool = False):
 _SIDE_STREAMS = {}
 _PIPE_DEBUG = os.environ.get("DMLP_PIPE_DEBUG") == "1"
 
+# DMLP_PIPE_EVENTS=1: GPU timestamps (hipEvents) at the phase boundaries of knn_gpu_pipelined,
+# read after the call's sync — a step timeline without a profiler (no host syncs added).
+# pipe_timeline() returns the last call's [(phase, ms since the call entered)].
+_EVENTS = os.environ.get("DMLP_PIPE_EVENTS") == "1"
+_MARKS = []
+_LAST_TIMELINE = []
+_PREV_END = [None]  # the previous call's last mark: the gap between calls
+
+
+def set_pipe_events(on: bool):
+    global _EVENTS
+    _EVENTS = bool(on)
+    _PREV_END[0] = None
+
+
+def _mark(name, stream=None):
+    if not _EVENTS:
+        return
+    torch = _torch()
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(stream if stream is not None else torch.cuda.current_stream())
+    _MARKS.append((name, e))
+
+
+def _close_marks():
+    global _LAST_TIMELINE
+    if not _EVENTS or not _MARKS:
+        return
+    _MARKS[-1][1].synchronize()
+    t0 = _MARKS[0][1]
+    out = []
+    if _PREV_END[0] is not None:
+        out.append(("prev_call_done", round(-_PREV_END[0].elapsed_time(t0), 4)))
+    for name, e in _MARKS:
+        e.synchronize()
+        out.append((name, round(t0.elapsed_time(e), 4)))
+    _LAST_TIMELINE = out
+    _PREV_END[0] = _MARKS[-1][1]
+    _MARKS.clear()
+
+
+def pipe_timeline():
+    return list(_LAST_TIMELINE)
+
 
 def _side_stream(name):
     torch = _torch()
@@ -672,6 +727,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     t_enter = time.perf_counter()
     _ARENA.reset()
     copy.wait_stream(main)  # buffers recycled from the previous call
+    _MARKS.clear()
+    _mark("enter", copy)
     Q = len(Q_host)
     A = X_host.shape[1]
     KT = max(1, (A + 31) // 32)
@@ -683,9 +740,10 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     Qh = np.ascontiguousarray(Q_host, np.float64)
     if Q and k_range is None:
         k_range = (int(k_host.min()), int(k_host.max()))
+    # the host renders the single-term (x1) operands whenever x1 serves this A; queries with k
+    # outside [1, 32] (3-term class, exact path) and escalations get device operands on need
     host_ops = (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
-                and L.dmlp_screen_x1_qw(KT) > 0 and k_range[0] >= 1
-                and k_range[1] <= min(SCREEN_KMAX_A, N))
+                and L.dmlp_screen_x1_qw(KT) > 0)
     dsops = prepped = mu_d = None
     if host_ops:
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
@@ -739,6 +797,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             dsops, prepped = (xhi, xin, xnm, bad_d), (qhi, qn)
         else:
             mu_d = None  # outside the screen's range: the device path decides
+    _mark("operands_landed", copy)
     with torch.cuda.stream(copy):
         ev_p = torch.cuda.Event()
         ev_p.record(copy)
@@ -759,6 +818,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             e = torch.cuda.Event()
             e.record(copy)
             ev.append(e)
+    _mark("rows_landed", copy)
     for t in (X, Qd) + ((lab,) if lab is not None else ()) + (prepped or ()) + (dsops or ()):
         if t is not None:
             t.record_stream(main)
@@ -796,18 +856,22 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)
         calls.append(call.launch())
     spec = None
+    _mark("knn_queued")
     if report is not None and fin and Q > 0:
         spec = format_report_dev_async(oc, report.get("qid_base", 0))
+        _mark("format_done")
         dst = report.get("dst")
         if dst is not None and len(dst) >= L.dmlp_format_bound(Q):
             _lib.check(L.dmlp_d2h_async(dst.ctypes.data, _p(spec[0]), L.dmlp_format_bound(Q),
                                         _stream()), "d2h report")
             _IO["d2h"] += L.dmlp_format_bound(Q)
             report["copied"] = True
+            _mark("report_d2h_done")
         else:
             report["copied"] = False
     t_launched = time.perf_counter()
     n_fb = sum(call.finish().n_fallback for call in calls)
+    _close_marks()
     if report is not None:
         report["valid"] = spec is not None and not any(c.cs_modified for c in calls)
         report["text"] = spec

@@ -7,6 +7,7 @@
 //   * every job gives identical bytes when repeated back to back (the spin path) and after the
 //     workers went to sleep (the condvar path);
 //   * the queries' operands match a serial scalar recomputation of the documented rounding.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -27,11 +28,22 @@ static int fails = 0;
     }                                                                     \
   } while (0)
 
-static uint16_t bf16_rn_ref(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// fp32 -> fp16 bits, round to nearest even, by arithmetic (independent of host_prep.cpp's
+// bit manipulation and of F16C): the fp16 grid spacing at |f| is 2^(e - 10) for normal values
+// (2^-24 below 2^-14), rounding is done on the exact double quotient with nearbyint (ties to even).
+static uint16_t f16_rn_ref(float f) {
+  const double a = std::fabs((double)f);
+  const uint16_t sign = std::signbit(f) ? 0x8000 : 0;
+  if (a == 0.0) return sign;
+  int e;
+  std::frexp(a, &e);  // a = m 2^e, m in [0.5, 1)
+  const int ex = std::max(e - 1, -14);            // unbiased exponent of the fp16 binade
+  const double step = std::ldexp(1.0, ex - 10);   // spacing of the fp16 grid there
+  double m = std::nearbyint(a / step);            // exact quotient, rounded half to even
+  int bex = ex;
+  if (m >= 2048.0) { m /= 2.0; ++bex; }           // rounded up into the next binade
+  if (m < 1024.0) return (uint16_t)(sign | (uint16_t)m);  // subnormal (bex == -14)
+  return (uint16_t)(sign | (uint16_t)((bex + 15) << 10) | (uint16_t)(m - 1024.0));
 }
 
 struct Ops {
@@ -103,10 +115,10 @@ int main() {
     EXPECT(same(one, again));
     EXPECT(same(one, slept));
     // queries: serial recomputation of the documented rounding (c = q - mu in fp64,
-    // hi = bf16_rn(fp32(c)), |c|^2 accumulated in fp64 and rounded to fp32 once)
+    // hi = fp16_rn(fp32(c)), |c|^2 accumulated in fp64 and rounded to fp32 once)
     for (int64_t q = 0; q < Q; ++q) {
       for (int a = 0; a < KT * 32; ++a) {
-        const uint16_t want = a < A ? bf16_rn_ref((float)(Qx[q * A + a] - mu[a])) : 0;
+        const uint16_t want = a < A ? f16_rn_ref((float)(Qx[q * A + a] - mu[a])) : 0;
         if (one.qhi[q * KT * 32 + a] != want) { EXPECT(one.qhi[q * KT * 32 + a] == want); break; }
       }
       EXPECT(std::isfinite(one.qn[q]) && one.qn[q] >= 0.0f);

@@ -110,11 +110,18 @@ def _dropin(tmp_path, debug=False):
 
 
 def _run_dropin(exe, path, env, np_=1):
-    cmd = ([MPIEXEC, "-n", str(np_)] if np_ > 1 else []) + [exe]
     e = dict(os.environ)
     e.update(env)
-    with open(path, "rb") as f:
-        r = subprocess.run(cmd, stdin=f, capture_output=True, timeout=180, env=e)
+    if np_ > 1:
+        # every rank opens the file as its stdin (only rank 0 reads it, common.cpp:93): MPICH's
+        # stdin forwarding to rank 0 can die with SIGPIPE on larger inputs
+        import shlex
+        cmd = [MPIEXEC, "-n", str(np_), "sh", "-c",
+               f"exec {shlex.quote(exe)} < {shlex.quote(str(path))}"]
+        r = subprocess.run(cmd, stdin=subprocess.DEVNULL, capture_output=True, timeout=180, env=e)
+    else:
+        with open(path, "rb") as f:
+            r = subprocess.run([exe], stdin=f, capture_output=True, timeout=180, env=e)
     assert r.returncode == 0, r.stderr.decode()
     assert b"Time taken: " in r.stderr
     return r.stdout
@@ -162,7 +169,8 @@ def _ref_dropin(tmp_path, debug=False, inplace=False):
         tree = tmp_path / "reftree"
         tree.mkdir(exist_ok=True)
         for f in ("common.cpp", "common.h", "engine.h"):
-            shutil.copy2(os.path.join(os.path.dirname(REF_COMMON), f), tree / f)
+            if not (tree / f).exists():  # (copyfile: the sources may be read-only)
+                shutil.copyfile(os.path.join(os.path.dirname(REF_COMMON), f), tree / f)
         src = str(tree / "common.cpp")
     name = f"engine{'.debug' if debug else ''}{'.inplace' if inplace else ''}"
     try:
@@ -206,3 +214,31 @@ def test_reference_common_cpp_dropin_gpu(tmp_path, inplace):
     assert _run_dropin(exe, path, {"KNN_DATA_PLANE": "host"}, np_=2) == dmlp.format_report(cs)
     dbg = _ref_dropin(tmp_path, debug=True, inplace=inplace)
     assert _run_dropin(dbg, path, {}) == _debug_expect(inp, res, lab)
+
+
+@pytest.mark.gpu
+def test_fast_path_serves_any_k_and_escalates_per_query(tmp_path):
+    """knn_engine's single-GPU host-operand pipeline no longer gives up on the
+    whole call — k in [1, 64] (the x1 class plus the 3-term class on a device image rendered from
+    the landed rows) and one query among 600 duplicate points (its single-term candidates
+    overflow: that query alone escalates to the 3-term screen / exact path) stay on the fast
+    path (its KNN_TRACE phases), and print the oracle's bytes."""
+    rng = np.random.default_rng(17)
+    N, Q, A = 6000, 300, 16
+    X = np.round(rng.uniform(0, 1000, (N, A)), 6)
+    X[:600] = X[0]                      # 600 identical points: ties far beyond any buffer
+    Qx = np.round(rng.uniform(0, 1000, (Q, A)), 6)
+    Qx[7] = X[0]
+    k = rng.integers(1, 65, Q).astype(np.int32)
+    k[7] = 12
+    labels = rng.integers(0, 5, N).astype(np.int32)
+    inp = dmlp.KNNInput(labels, X, k, Qx)
+    path = tmp_path / "tight.in"
+    path.write_text(dmlp.to_text(inp))
+    inp = dmlp.parse_input(path.read_text())
+    _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    out, err = _run(["--strategy", "farm"], path, env={"KNN_TRACE": "1"})
+    assert out == dmlp.format_report(cs)
+    phases = [l.split()[3] for l in err.splitlines() if l.startswith("[dmlp-trace]")]
+    assert "h2d_operands" in phases and "knn" in phases, phases  # the fast path, not "compute"
+    assert "distribute" not in phases

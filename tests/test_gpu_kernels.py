@@ -234,7 +234,7 @@ def test_pipelined_chunks_match(torch_cuda, chunks, kmin):
 
 @pytest.mark.parametrize("case", ["escalate", "slices", "ragged"])
 def test_pipelined_host_image_paths(torch_cuda, case, monkeypatch):
-    """The host's hi-only dataset image (hl = 1) through the x1 screen and group refine:
+    """The host's fp16 hi-only dataset image (hl = 1) through the x1 screen and group refine:
     tight 1-D data escalates to the 3-term screen (device hi/lo image rendered on demand from
     the fp64 rows), few queries split the data into many slices, and A = 40 / N % 64 != 0
     exercises KT = 2 and a ragged last tile."""
@@ -263,8 +263,9 @@ def test_pipelined_host_image_paths(torch_cuda, case, monkeypatch):
 
 
 def test_host_data_image_matches_device(torch_cuda):
-    """dmlp_cpu_prep_data's hi-only image == the hi halves of prep.hip's hi/lo image; xinit and
-    the max norm agree to fp32 rounding of differently ordered fp64 sums."""
+    """dmlp_cpu_prep_data's fp16 hi-only image is the fp16 rounding of the same centred values
+    prep.hip renders (in prep.hip's tile layout); xinit and the max norm agree with the device
+    prep to fp32 rounding of differently ordered fp64 sums."""
     torch = torch_cuda
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
@@ -278,10 +279,13 @@ def test_host_data_image_matches_device(torch_cuda):
     nm_h = np.zeros(1, np.uint32)
     assert L.dmlp_cpu_prep_data(inp.X.ctypes.data, N, A, mu.ctypes.data, KT, img.ctypes.data,
                                 xin_h.ctypes.data, nm_h.ctypes.data) == 0
+    c = np.zeros((n_tiles * 64, KT * 32))
+    c[:N, :A] = inp.X - mu
+    ref = c.astype(np.float32).astype(np.float16).view(np.uint16)
+    ref = ref.reshape(n_tiles, 4, 16, KT, 4, 8).transpose(0, 1, 3, 4, 2, 5).reshape(-1)
+    np.testing.assert_array_equal(img, ref)
     ds = K.prepare_dataset(torch.from_numpy(inp.X).cuda(), mu=torch.from_numpy(mu).cuda())
     torch.cuda.synchronize()
-    dev = ds.xfrag.cpu().numpy().view(np.uint16).reshape(n_tiles, 4, KT, 2, 64 * 8)
-    np.testing.assert_array_equal(dev[:, :, :, 0].reshape(-1), img)
     np.testing.assert_allclose(ds.xinit.cpu().numpy()[:N], xin_h[:N], rtol=1e-6)
     assert np.isneginf(ds.xinit.cpu().numpy()[N:]).all()
     np.testing.assert_allclose(ds.xnmax_bits.cpu().numpy().view(np.float32),
@@ -289,8 +293,9 @@ def test_host_data_image_matches_device(torch_cuda):
 
 
 def test_host_prep_matches_device_prep(torch_cuda):
-    """dmlp_cpu_prep_queries renders the same bf16 fragments as the device prep (qn within
-    fp64 summation order, rounded to fp32)."""
+    """dmlp_cpu_prep_queries renders the fp16 rounding of the centred queries whose bf16 split
+    the device prep renders (hi + lo of the device = the fp32 value to 16 bits), and the same
+    qn (within fp64 summation order, rounded to fp32)."""
     torch = torch_cuda
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
@@ -302,6 +307,8 @@ def test_host_prep_matches_device_prep(torch_cuda):
     qn_h = np.zeros(Q, np.float32)
     assert L.dmlp_cpu_prep_queries(inp.Qx.ctypes.data, Q, A, mu.ctypes.data, KT, hh.ctypes.data,
                                    qn_h.ctypes.data) == 0
+    c = inp.Qx - mu
+    np.testing.assert_array_equal(hh[:, :A], c.astype(np.float32).astype(np.float16).view(np.uint16))
     Qx = torch.from_numpy(inp.Qx).cuda()
     mu_d = torch.from_numpy(mu).cuda()
     qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device="cuda")
@@ -312,7 +319,10 @@ def test_host_prep_matches_device_prep(torch_cuda):
     _lib.check(L.dmlp_prep_queries(Qx.data_ptr(), Q, A, mu_d.data_ptr(), KT, qhi.data_ptr(),
                                    qlo.data_ptr(), qn.data_ptr(), bad.data_ptr(), s), "prep")
     torch.cuda.synchronize()
-    np.testing.assert_array_equal(qhi.cpu().numpy().view(np.uint16).reshape(Q, -1), hh)
+    hi = qhi.cpu().numpy().view(np.uint16).reshape(Q, -1)[:, :A].astype(np.uint32) << 16
+    lo = qlo.cpu().numpy().view(np.uint16).reshape(Q, -1)[:, :A].astype(np.uint32) << 16
+    dev = hi.view(np.float32).astype(np.float64) + lo.view(np.float32).astype(np.float64)
+    np.testing.assert_allclose(dev, c.astype(np.float32), rtol=2 ** -15, atol=1e-30)
     np.testing.assert_allclose(qn.cpu().numpy(), qn_h, rtol=1e-6)
 
 
@@ -398,3 +408,30 @@ def test_format_report_gpu(torch_cuda):
     cs[:3] = [0, 1, 2**64 - 1]
     g = K.format_report_gpu(torch.from_numpy(cs.view(np.int64)).cuda(), qid_base=7)
     assert g == dmlp.format_report(cs, qid_base=7)
+
+
+def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
+    """knn_gpu_pipelined keeps the host's fp16 x1 operands for the k <= 32 queries when other
+    queries need the 3-term class (k in (32, 128]) or the exact path (k > 128), and when one
+    query's candidates overflow (600 duplicate points): per-query dispatch, bit-exact."""
+    torch = torch_cuda
+    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    rng = np.random.default_rng(23)
+    N, Q, A = 8000, 500, 32
+    X = np.round(rng.uniform(0, 1000, (N, A)), 6)
+    X[:600] = X[0]
+    Qx = np.round(rng.uniform(0, 1000, (Q, A)), 6)
+    Qx[3] = X[0]
+    k = rng.integers(1, 160, Q).astype(np.int32)
+    k[3] = 10
+    labels = rng.integers(0, 7, N).astype(np.int32)
+    Xp = torch.from_numpy(X).pin_memory().numpy()
+    Qp = torch.from_numpy(Qx).pin_memory().numpy()
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, labels, (0, 7), Qp, k)
+    torch.cuda.synchronize()
+    d_ref, i_ref = K.knn_cpu(X, Qx, k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, k, labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)

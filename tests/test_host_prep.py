@@ -1,15 +1,16 @@
 """Host-side screen operands (csrc/host_prep.cpp) against a NumPy rendering of the same bits:
-c = q - mu in fp64, hi = bf16_rn(fp32_rn(c)), |c|^2 in fp64 rounded to fp32, out-of-range
-rows flagged.  Both the AVX2 path (A % 8 == 0) and the portable path (other A) run."""
+c = q - mu in fp64, hi = fp16_rn(fp32_rn(c)) (subnormals included), |c|^2 in fp64 rounded to
+fp32, rows outside the fp16 range flagged.  Both the AVX2/F16C path (A % 8 == 0) and the
+portable path (other A) run."""
 import numpy as np
 import pytest
 
 from distributed_machine_learning_project_amd import _lib
 
 
-def _bf16_ref(c):
-    u = c.astype(np.float32).view(np.uint32).astype(np.uint64)
-    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+def _f16_ref(c):
+    # numpy's float32 -> float16 cast rounds to nearest even, subnormals included
+    return c.astype(np.float32).astype(np.float16).view(np.uint16)
 
 
 @pytest.mark.parametrize("A", [32, 40, 7, 64])
@@ -28,19 +29,44 @@ def test_cpu_prep_queries_bits(A):
                                  qn.ctypes.data)
     assert rc == 0
     c = Qx - mu
-    np.testing.assert_array_equal(hh[:, :A], _bf16_ref(c))
+    np.testing.assert_array_equal(hh[:, :A], _f16_ref(c))
     assert (hh[:, A:] == 0).all()
     np.testing.assert_allclose(qn, (c * c).sum(1), rtol=1e-6)
+
+
+@pytest.mark.parametrize("A", [32, 7])
+def test_cpu_prep_fp16_rounding_edges(A):
+    """Ties, subnormals, the largest finite fp16 range and signed zeros, both code paths."""
+    L = _lib.lib()
+    rng = np.random.default_rng(1)
+    vals = np.concatenate([
+        rng.uniform(-65000, 65000, 4000),
+        rng.uniform(-1e-4, 1e-4, 4000),                       # fp16 subnormals
+        (np.arange(-2000, 2000) + 0.5) * 2.0 ** -10,          # ties at the mantissa LSB
+        np.ldexp(rng.integers(1, 2 ** 12, 2000).astype(np.float64), -24),  # subnormal ties
+        [0.0, -0.0, 65503.0, -65503.0, 2.0 ** -14, 2.0 ** -25, 3 * 2.0 ** -26]])
+    Q = len(vals) // A
+    Qx = vals[:Q * A].reshape(Q, A).copy()
+    KT = (A + 31) // 32
+    mu = np.zeros(A)
+    hh = np.zeros((Q, KT * 32), np.uint16)
+    qn = np.zeros(Q, np.float32)
+    assert L.dmlp_cpu_prep_queries(Qx.ctypes.data, Q, A, mu.ctypes.data, KT, hh.ctypes.data,
+                                   qn.ctypes.data) == 0
+    np.testing.assert_array_equal(hh[:, :A], _f16_ref(Qx))
 
 
 def test_cpu_prep_queries_flags_range():
     L = _lib.lib()
     A = 32
     Qx = np.ones((5000, A))
-    Qx[1234, 5] = 1e16
+    Qx[1234, 5] = 70000.0  # beyond the fp16 range
     mu = np.zeros(A)
     hh = np.zeros((5000, 32), np.uint16)
     qn = np.zeros(5000, np.float32)
+    assert L.dmlp_cpu_prep_queries(Qx.ctypes.data, 5000, A, mu.ctypes.data, 1, hh.ctypes.data,
+                                   qn.ctypes.data) == 1
+    Qx[1234, 5] = 1e16
     assert L.dmlp_cpu_prep_queries(Qx.ctypes.data, 5000, A, mu.ctypes.data, 1, hh.ctypes.data,
                                    qn.ctypes.data) == 1
     Qx[1234, 5] = np.nan
@@ -49,13 +75,13 @@ def test_cpu_prep_queries_flags_range():
 
 
 def _hi_image_ref(X, mu, KT):
-    """prep.hip's tile image with the lo halves dropped: uint16 [n_tiles][4][KT][64 lanes][8],
+    """prep.hip's tile layout, hi halves only, as fp16: uint16 [n_tiles][4][KT][64 lanes][8],
     lane = r + 16 * kg holds attributes kt*32 + kg*8 .. +7 of point t*64 + rt*16 + r."""
     N, A = X.shape
     n_tiles = (N + 63) // 64
     c = np.zeros((n_tiles * 64, KT * 32))
     c[:N, :A] = X - mu
-    h = _bf16_ref(c)  # zero rows / columns render as 0
+    h = _f16_ref(c)  # zero rows / columns render as 0
     img = h.reshape(n_tiles, 4, 16, KT, 4, 8)          # t, rt, r, kt, kg, j
     return img.transpose(0, 1, 3, 4, 2, 5).reshape(-1)  # t, rt, kt, kg, r, j
 

@@ -15,6 +15,8 @@
 #   sweep      bench sweep over N / A / k (profiles/ sweep table)
 #   exact      bench.py --exact (fp64-only path)
 #   harness    bench.py --harness native (knn_engine through the reference contract)
+#   dropin     bench.py --harness dropin (engine.h drop-in linked with the reference's common.cpp)
+#   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
 set -u
@@ -46,11 +48,11 @@ for task in "$@"; do
       step exact 300 python bench.py --exact --steps 5 --warmup 1 ;;
     prof)
       step prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-          -- python3 bench.py --steps 10 --warmup 2 --no-busbw
+          -- python3 bench.py --steps 10 --warmup 2 --no-busbw --diag-steps 0
       find "$OUT/prof" -name '*kernel_stats.csv' -exec sh -c 'head -12 "$1" | cut -c1-200' _ {} \; ;;
     timeline)
       step timeline 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/tl" -o run \
-          --output-format csv -- python3 bench.py --steps 4 --warmup 2 --no-busbw
+          --output-format csv -- python3 bench.py --steps 4 --warmup 2 --no-busbw --diag-steps 0
       python3 tools/timeline.py "$OUT/tl" 7 > "$OUT/timeline.txt"; tail -40 "$OUT/timeline.txt" ;;
     pmc)
       n=0
@@ -70,6 +72,14 @@ for task in "$@"; do
       step sweep 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep.jsonl" --timeout 170 ;;
     harness)
       step harness 600 python bench.py --harness native ;;
+    dropin)
+      step dropin 600 python bench.py --harness dropin --steps 5 --warmup 1 ;;
+    split)
+      for q in 131072 65536 32768; do
+        step split_$q 240 rocprofv3 --kernel-trace --stats -d "$OUT/split_$q" -o run --output-format csv \
+            -- python3 tools/quick_gpu_bench.py --q $q --iters 6 --check 200
+        find "$OUT/split_$q" -name '*kernel_stats.csv' -exec sh -c 'head -6 "$1" | cut -c1-150' _ {} \;
+      done ;;
     merge)
       step merge 300 rocprofv3 --kernel-trace --stats -d "$OUT/merge" -o run --output-format csv \
           -- python3 tools/merge_bench.py --p 8 --q 131072 --ks 16,128
