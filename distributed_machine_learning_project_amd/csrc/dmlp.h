@@ -56,6 +56,15 @@ int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, i
                       const double* mu, int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d, void* xnm_d,
                       void* qhi_d, void* qn_d, int chunks, void* stream);
+// Query parts of a pipelined call: render + copy part p, then queue its single-term screen
+// (fp16 host image) on part_streams[p] behind the copy (prep.hip).  0, | 2 out of range, | 4 error.
+int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const double* mu, int KT,
+                           uint16_t* qhi_h, float* qn_h, void* qhi_d, void* qn_d, int parts,
+                           void* copy, void* const* part_streams, const void* xfrag,
+                           const float* xinit, int64_t n_tiles, int64_t n_points, const int* qidx,
+                           const int* const* kdev, int kmax, const unsigned* xnmax_bits,
+                           const unsigned* bad, int S, int* const* cand_ids, int* const* cand_cnt,
+                           float* const* cand_h);
 // Same, the dataset part restricted to tiles [t0, t1) (device image pointers at tile t0's slot;
 // *xnm = +inf when the range is outside the screen's range): the per-rank shard of a sharded render.
 int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1, const double* Qx,

@@ -161,7 +161,9 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
   const bool root = s->rt.rank == 0;
   dmlp_rt::Input in;
   dmlp_rt::Output out;
+  s->core->trace.begin();
   if (root) pack(dataset, queries, p.num_attrs, in);
+  s->core->trace.mark("pack");
   const auto t1 = std::chrono::steady_clock::now();
   s->core->KNN(root ? &in : nullptr, root ? &out : nullptr);
   const auto t2 = std::chrono::steady_clock::now();
@@ -184,6 +186,8 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
       write_report(out.report.data(), out.report.size(), queries);
     }
   }
+  s->core->trace.mark("emit");
+  (void)s->core->trace.finish();  // KNN_TRACE=1: per-phase lines on stderr (after the work)
   // KNN_METRICS=path: this call's time with microsecond resolution (the harness prints whole ms)
   if (root) {
     if (const char* m = getenv("KNN_METRICS")) {

@@ -7,6 +7,7 @@
 #include <mpi.h>
 #include <rccl/rccl.h>
 
+#include <dirent.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -144,9 +145,10 @@ struct Runtime {
   // Pin this rank to the CPUs of its GPU's NUMA node (within its affinity): first-touch then puts
   // the page-locked arenas, the parsed input and the render pool's threads next to the GPU's
   // PCIe root (the Python twin: parallel/comm.py Comm.bind_numa; profiles/r3m_numa.txt).
-  // KNN_NUMA_BIND=0 disables it.
-  static int bind_numa(int dev) {
-    if (getenv("KNN_NUMA_BIND") && std::string(getenv("KNN_NUMA_BIND")) == "0") return -1;
+  // Every thread of the process is re-pinned (the HIP runtime's and MPI's, started before the
+  // bind, too), and DMLP_NODE_RANKS tells the render pool how many of the node's `local_world`
+  // ranks (local rank r drives GPU r % ndev) share the mask.  KNN_NUMA_BIND=0 disables it.
+  static int numa_node(int dev) {
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return -1;
     for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
@@ -155,6 +157,11 @@ struct Runtime {
       if (std::fscanf(f, "%d", &node) != 1) node = -1;
       std::fclose(f);
     }
+    return node;
+  }
+  static int bind_numa(int dev, int local_world = 1, int ndev = 1) {
+    if (getenv("KNN_NUMA_BIND") && std::string(getenv("KNN_NUMA_BIND")) == "0") return -1;
+    const int node = numa_node(dev);
     if (node < 0) return -1;
     FILE* f = std::fopen(("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist").c_str(), "r");
     if (!f) return -1;
@@ -176,6 +183,14 @@ struct Runtime {
     if (sched_getaffinity(0, sizeof(have), &have) != 0) return -1;
     CPU_AND(&want, &want, &have);
     if (CPU_COUNT(&want) == 0 || sched_setaffinity(0, sizeof(want), &want) != 0) return -1;
+    if (DIR* d = opendir("/proc/self/task")) {
+      while (dirent* e = readdir(d))
+        if (e->d_name[0] != '.') (void)sched_setaffinity(std::atoi(e->d_name), sizeof(want), &want);
+      closedir(d);
+    }
+    int share = 0;
+    for (int r = 0; r < std::max(1, local_world); ++r) share += numa_node(r % std::max(1, ndev)) == node;
+    setenv("DMLP_NODE_RANKS", std::to_string(std::max(1, share)).c_str(), 1);
     return node;
   }
   void init(bool need_gpu = true) {
@@ -184,6 +199,8 @@ struct Runtime {
     MPI_Comm shm;
     MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &shm);
     MPI_Comm_rank(shm, &local);
+    int local_world = 1;
+    MPI_Comm_size(shm, &local_world);
     MPI_Comm_free(&shm);
     if (!need_gpu) return;  // serial KD-tree strategy (bench.debug): host only
     gpu = true;
@@ -192,7 +209,7 @@ struct Runtime {
     if (ndev == 0) throw std::runtime_error("no HIP device");
     device = local % ndev;
     HIPCHK(hipSetDevice(device));
-    numa = bind_numa(device);  // before the arenas: their pages land next to the GPU
+    numa = bind_numa(device, local_world, ndev);  // before the arenas: pages land next to the GPU
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     reserve_arenas();
     if (world > 1 && !host_plane) {

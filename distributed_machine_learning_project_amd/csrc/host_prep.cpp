@@ -133,7 +133,7 @@ class Pool {
 
 // CPUs this process may run on (the affinity mask, not the machine: a GPU box grants each job a
 // share of a 256-thread host), divided among the ranks of the node that share that mask
-// (LOCAL_WORLD_SIZE, set by torchrun / the MPI launchers), at most 16 — the conversions are bound
+// (DMLP_NODE_RANKS / LOCAL_WORLD_SIZE, set by the NUMA binding / torchrun / the MPI launchers), at most 16 — the conversions are bound
 // by memory, not cores.  DMLP_HOST_THREADS overrides (clamped to [1, 16]).
 // CPUs' worth of time the cgroup grants (cgroup v2 cpu.max "quota period"; 0 = unlimited or
 // unknown).  A container can see a 256-CPU affinity mask with a 16-CPU quota: sizing the pool by
@@ -160,8 +160,12 @@ int pool_threads() {
   int local = 1;
   for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"})
     if (const char* e = std::getenv(v)) { local = std::max(1, std::atoi(e)); break; }
-  // ranks pinned to disjoint CPU sets see only their own share; a shared mask is split
-  if (local > 1 && n >= 2 * local) n /= local;
+  // ranks pinned to disjoint CPU sets see only their own share; a shared mask is split among the
+  // ranks that share it: those bound to this NUMA node (DMLP_NODE_RANKS, set by the NUMA binding:
+  // parallel/comm.py, engine_runtime.h), else every local rank
+  int sharing = local;
+  if (const char* e = std::getenv("DMLP_NODE_RANKS")) sharing = std::max(1, std::atoi(e));
+  if (sharing > 1 && n >= 2 * sharing) n /= sharing;
   // the cgroup quota is shared by the node's ranks too; leave 2 CPUs of each rank's share to
   // its main thread and the HIP runtime, so spinning workers never run the quota out
   if (const int c = cgroup_cpus()) {

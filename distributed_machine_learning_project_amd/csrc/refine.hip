@@ -1069,7 +1069,9 @@ extern "C" int dmlp_merge(const double* in_d, const int* in_i, int L, int64_t li
   if (L <= 8) {  // one lane per query, heads in registers (writes every slot of [0, kout))
     const dim3 g((nq + 255) / 256), b(256);
     hipStream_t st = (hipStream_t)stream;
-    const bool win = kin % 4 == 0 && ((uintptr_t)in_d & 15) == 0 && ((uintptr_t)in_i & 15) == 0 &&
+    // 16-byte window loads: every list start (l * list_stride + q * kin) must be 4-aligned too
+    const bool win = kin % 4 == 0 && list_stride % 4 == 0 && ((uintptr_t)in_d & 15) == 0 &&
+                     ((uintptr_t)in_i & 15) == 0 &&
                      !(getenv("DMLP_MERGE_WIN") && getenv("DMLP_MERGE_WIN")[0] == '0');
     if (win) {
 #define DMLP_MERGE_WIN(LV)                                                                     \

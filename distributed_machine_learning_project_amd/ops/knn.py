@@ -38,6 +38,10 @@ SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
 # host render + H2D of the screen operands in 2 pipelined slices: the first copy starts after half
 # the render (profiles/r2t_host_ops_chunks.txt: median 2.63 vs 2.74 and 3.03 vs 3.18 ms/step on two boxes)
 HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "2"))
+# query parts of the host-operand pipeline (knn_gpu_pipelined): each part's screen starts as soon
+# as its operands land, on its own stream, while the host renders the next part (1: one screen
+# after the whole query image)
+HOST_OPS_PARTS = int(os.environ.get("DMLP_HOST_OPS_PARTS", "4"))
 
 
 def eps_rel(A: int) -> float:
@@ -281,6 +285,7 @@ class _KnnCall:
         self.exact = exact
         self.gpu_share = gpu_share
         self.prepped = prepped
+        self.pre_screen = None  # (cand_ids, cand_cnt, cand_h, S): x1 screen queued elsewhere
         self.qx_event = qx_event
         self.want_fin = finalize and ds.labels is not None
         # k > N: pad with (+inf,-1) like bench_2
@@ -370,6 +375,22 @@ class _KnnCall:
                                        _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
                    "prep_queries")
 
+    def x1_buffers(self):
+        """Candidate buffers + slice count of this call's all-queries x1 pass, for a screen that
+        dmlp_host_ops_x1_parts queues natively; launch() then only adds the refine."""
+        torch = _torch()
+        L = _lib.lib()
+        KT, kcls, nq = self.ds.KT, self.kmax, self.Q
+        cap = L.dmlp_screen_x1_cap(kcls)
+        cus = max(1, int(round(NUM_CUS * self.gpu_share)))
+        S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), self.ds.n_tiles,
+                                  L.dmlp_screen_x1_waves_per_cu(kcls),
+                                  int(L.dmlp_screen_x1_min_slices(self.ds.n_tiles)), cus)
+        self.pre_screen = (torch.empty(nq * S * cap, dtype=torch.int32, device=self.dev),
+                           torch.empty(nq * S, dtype=torch.int32, device=self.dev),
+                           torch.empty(nq * S * 2, dtype=torch.float32, device=self.dev), S)
+        return self.pre_screen
+
     def _screen_pass(self, idx, impl):
         torch = _torch()
         if impl != "x1" and self.qlo is None:
@@ -386,7 +407,12 @@ class _KnnCall:
             kcls = int(kk[idx].max())
             qidx = _h2d(idx.astype(np.int32), dev)
         cus = max(1, int(round(NUM_CUS * self.gpu_share)))
-        if impl == "x1":
+        pre = self.pre_screen if impl == "x1" and idx is None else None
+        self.pre_screen = None
+        if pre is not None:
+            cap = L.dmlp_screen_x1_cap(kcls)
+            cand_ids, cand_cnt, cand_h, S = pre
+        elif impl == "x1":
             cap = L.dmlp_screen_x1_cap(kcls)
             S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), ds.n_tiles,
                                       L.dmlp_screen_x1_waves_per_cu(kcls),
@@ -398,12 +424,14 @@ class _KnnCall:
         else:
             cap = 128 if kcls <= SCREEN_KMAX_A else 256
             S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
-        cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
-        cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
+        if pre is None:
+            cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
+            cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
         fin = (_p(ds.labels) if self.want_fin else None, ds.label_lo, ds.label_hi, _p(self.lab),
                _p(self.cs), _p(self.status), self._ovf.ptr(self._ovf_slot), s)
         if impl == "x1":
-            cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
+            if pre is None:
+                cand_h = torch.empty(nq * S * 2, dtype=torch.float32, device=dev)
             # the host's fp16 image (hl = 1) pairs with the host's fp16 query fragments, prep.hip's
             # bf16 image (hl = 2) with the device's bf16 ones
             if ds.hl == 1:
@@ -414,12 +442,13 @@ class _KnnCall:
                 if self.qhi is None:
                     self._prep_on_device()
                 x1_qhi, x1_qn = self.qhi, self.qn
-            _mark("screen_start")
-            _lib.check(L.dmlp_screen_x1(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
-                          _p(x1_qhi), _p(x1_qn), _p(qidx), _p(self.kdev_eff),
-                          nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
-                          _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
-                       "screen_x1")
+            if pre is None:
+                _mark("screen_start")
+                _lib.check(L.dmlp_screen_x1(KT, ds.hl, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles, N,
+                              _p(x1_qhi), _p(x1_qn), _p(qidx), _p(self.kdev_eff),
+                              nq, kcls, _p(ds.xnmax_bits), _p(ds.bad), S,
+                              _p(cand_ids), _p(cand_cnt), _p(cand_h), s),
+                           "screen_x1")
             _mark("screen_done")
             if idx is None:
                 # every query goes through this refine: it writes each row's (+inf, -1) padding
@@ -691,7 +720,7 @@ def _side_stream(name):
 def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=None,
                       chunks: int = 1, finalize: bool = True, exact: bool = False, gather=None,
                       mu_rows=None, X_full_host=None, report=None, k_range=None,
-                      image_shard=None):
+                      image_shard=None, _host_ops=True):
     """Host arrays in (page-locked for real overlap), device results out, with the fp64 rows
     copied behind the screen ("H2D overlapped with compute").
 
@@ -742,8 +771,12 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
         k_range = (int(k_host.min()), int(k_host.max()))
     # the host renders the single-term (x1) operands whenever x1 serves this A; queries with k
     # outside [1, 32] (3-term class, exact path) and escalations get device operands on need
-    host_ops = (chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
+    host_ops = (_host_ops and chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
                 and L.dmlp_screen_x1_qw(KT) > 0)
+    # query parts (HOST_OPS_PARTS): a single local replica, every k on the x1 class
+    parts = (HOST_OPS_PARTS if host_ops and HOST_OPS_PARTS > 1 and gather is None
+             and (image_shard is None or image_shard[1] <= 1) and k_range[0] >= 1
+             and k_range[1] <= min(SCREEN_KMAX_A, N) and Q >= HOST_OPS_PARTS * 8192 else 1)
     dsops = prepped = mu_d = None
     if host_ops:
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
@@ -775,10 +808,26 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             qn = torch.empty(Q, dtype=torch.float32, device=dev)
         # host conversion of each slice overlaps the PCIe copy of the previous one
         t_ops = t_ops0 = time.perf_counter()
-        rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data, Q, A,
+        rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data,
+                                       Q if parts == 1 else 0, A,
                                        mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
                                        _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
                                        HOST_OPS_CHUNKS, copy.cuda_stream)
+        if parts > 1 and rc == 0:
+            _mark("data_landed", copy)
+            r = _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride,
+                                 finalize, k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn,
+                                 copy, main)
+            if r is None:  # a query outside the screen's range: the device path decides
+                return knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host,
+                                         kstride, chunks, finalize, exact, gather, mu_rows,
+                                         X_full_host, report, k_range, image_shard,
+                                         _host_ops=False)
+            ds, od, oi, ol, oc, calls = r
+            t_ops = time.perf_counter() - t_ops
+            _IO["h2d"] += n_tiles * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
+            return _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter,
+                                   t_ops0, t_ops, True)
         t_ops = time.perf_counter() - t_ops
         _IO["h2d"] += (t1 - t0) * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
         if rc & 4:
@@ -855,6 +904,103 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             main.wait_event(ev[c])
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, exact, ks, out=out)
         calls.append(call.launch())
+    return _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter,
+                           t_ops0 if host_ops else t_enter, t_ops if host_ops else 0.0,
+                           prepped is not None)
+
+
+def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride, finalize,
+                     k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn, copy, main):
+    """knn_gpu_pipelined's query-part front (the dataset image is queued on `copy`): part p's
+    calls are set up on their own stream, dmlp_host_ops_x1_parts renders each part and queues its
+    screen behind its copy, then the fp64 rows follow on `copy` and every part's refine waits for
+    them.  None when a query is outside the screen's range (the part streams are drained)."""
+    import ctypes
+    torch = _torch()
+    L = _lib.lib()
+    dev = qhi.device
+    Q, A = Qh.shape
+    N = len(X_host)
+    W = KT * 32
+    with torch.cuda.stream(copy):
+        X = torch.empty((N, A), dtype=torch.float64, device=dev)
+        lab = (torch.empty(N, dtype=torch.int32, device=dev) if labels_host is not None else None)
+        Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    if lab is not None and finalize:
+        lo, hi = label_range
+        lab_ds = lab
+    else:
+        lo, hi, lab_ds = 0, 1, None
+    ds = DeviceDataset(X, lab_ds, lo, hi, KT, mu_d, xhi, xin, xnm, bad, True, hl=1)
+    fin = finalize and ds.labels is not None
+    ks = max(1, k_range[1]) if kstride is None else kstride
+    od = torch.empty((Q, ks), dtype=torch.float64, device=dev)
+    oi = torch.empty((Q, ks), dtype=torch.int32, device=dev)
+    ol = torch.empty(Q, dtype=torch.int32, device=dev) if fin else None
+    oc = torch.empty(Q, dtype=torch.int64, device=dev) if fin else None
+    pss = [_side_stream(f"part{p}") for p in range(parts)]
+    bounds = [Q * p // parts for p in range(parts + 1)]
+    shared = [t for t in (X, lab, Qd, bad, xhi, xin, xnm, qhi, qn, mu_d, od, oi, ol, oc)
+              if t is not None]
+    # (created on main before the part streams wait for it)
+    qidx = _identity(max(bounds[p + 1] - bounds[p] for p in range(parts)), dev)
+    calls, bufs = [], []
+    for p, ps in enumerate(pss):
+        a, b = bounds[p], bounds[p + 1]
+        ps.wait_stream(main)
+        ps.wait_stream(copy)
+        for t in shared:
+            t.record_stream(ps)
+        with torch.cuda.stream(ps):
+            out = (od[a:b], oi[a:b], ol[a:b] if fin else None, oc[a:b] if fin else None)
+            call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, False, ks,
+                            gpu_share=1.0 / parts, out=out, prepped=(qhi[a * W:b * W], qn[a:b]),
+                            k_range=k_range)
+            bufs.append(call.x1_buffers())
+        calls.append(call)
+    S = bufs[0][3]
+    if any(bf[3] != S for bf in bufs):
+        raise RuntimeError("query parts disagree on the slice count")
+    arr = lambda xs: (ctypes.c_void_p * parts)(*xs)
+    _mark("parts_start", copy)
+    rc = L.dmlp_host_ops_x1_parts(
+        Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT, hb[3].data_ptr(), hb[4].data_ptr(), _p(qhi),
+        _p(qn), parts, copy.cuda_stream, arr([ps.cuda_stream for ps in pss]), _p(xhi), _p(xin),
+        ds.n_tiles, N, _p(qidx), arr([c.k_dev.data_ptr() for c in calls]), k_range[1], _p(xnm),
+        _p(bad), S, arr([bf[0].data_ptr() for bf in bufs]), arr([bf[1].data_ptr() for bf in bufs]),
+        arr([bf[2].data_ptr() for bf in bufs]))
+    if rc & 4:
+        raise RuntimeError("dmlp_host_ops_x1_parts: copy or launch failed")
+    if rc:
+        for ps in pss:
+            ps.synchronize()
+        copy.synchronize()
+        return None
+    _mark("operands_landed", copy)
+    with torch.cuda.stream(copy):
+        X.copy_(torch.from_numpy(np.ascontiguousarray(X_host)), non_blocking=True)
+        if lab is not None:
+            lab.copy_(torch.from_numpy(np.ascontiguousarray(labels_host, np.int32)),
+                      non_blocking=True)
+        Qd.copy_(torch.from_numpy(Qh), non_blocking=True)
+        ev_rows = torch.cuda.Event()
+        ev_rows.record(copy)
+    _mark("rows_landed", copy)
+    _IO["h2d"] += X.numel() * 8 + (lab.numel() * 4 if lab is not None else 0) + Q * A * 8
+    for call, ps in zip(calls, pss):
+        call.qx_event = ev_rows
+        with torch.cuda.stream(ps):
+            call.launch()
+        main.wait_stream(ps)
+    return ds, od, oi, ol, oc, calls
+
+
+def _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter, t_ops0, t_ops,
+                    host_ops):
+    """Report render + D2H behind the re-rank, then each call's finish (the one host sync)."""
+    L = _lib.lib()
+    fin = finalize and ds.labels is not None
     spec = None
     _mark("knn_queued")
     if report is not None and fin and Q > 0:
@@ -879,9 +1025,9 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     if _PIPE_DEBUG:
         import sys
         print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms (before host ops "
-              f"{1e3 * (t_ops0 - t_enter) if host_ops else 0:.3f} ms), finish "
+              f"{1e3 * (t_ops0 - t_enter):.3f} ms), finish "
               f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host ops "
-              f"{prepped is not None} ({1e3 * t_ops if host_ops else 0:.3f} ms)", file=sys.stderr)
+              f"{host_ops} ({1e3 * t_ops:.3f} ms), calls {len(calls)}", file=sys.stderr)
     return ds, od, oi, ol, oc, n_fb
 
 

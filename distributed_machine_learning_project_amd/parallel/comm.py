@@ -81,22 +81,34 @@ class Comm:
     _numa = -1  # NUMA node this process was bound to (bind_numa), -1 if none
 
     @staticmethod
-    def bind_numa(dev_index: int) -> int:
-        """Pin this process to the CPUs of its GPU's NUMA node (within its current affinity),
-        before any large host allocation: first-touch then places the input, the page-locked
-        staging and the render pool's threads next to the GPU's PCIe root, so the host render
-        and the H2D copies never cross the socket link (unpinned, ~1 run in 3 measured ~20 %
-        slower: profiles/r3m_numa.txt).  KNN_NUMA_BIND=0 disables it.  Returns the node or -1."""
-        if os.environ.get("KNN_NUMA_BIND", "1") == "0":
-            return -1
+    def _numa_node(dev_index: int) -> int:
+        """NUMA node of a GPU's PCIe function (sysfs), -1 if unknown."""
         torch = _torch()
         try:
             p = torch.cuda.get_device_properties(dev_index)
             bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
             with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
-                node = int(f.read().strip())
-            if node < 0:
-                return -1
+                return int(f.read().strip())
+        except (OSError, ValueError, AttributeError, RuntimeError):
+            return -1
+
+    @staticmethod
+    def bind_numa(dev_index: int, local_world: int = 1) -> int:
+        """Pin this process to the CPUs of its GPU's NUMA node (within its current affinity),
+        before any large host allocation: first-touch then places the input, the page-locked
+        staging and the render pool's threads next to the GPU's PCIe root, so the host render
+        and the H2D copies never cross the socket link (unpinned, ~1 run in 3 measured ~20 %
+        slower: profiles/r3m_numa.txt).  Every thread of the process is re-pinned (the HIP
+        runtime's and torch's, started before this call, too), and DMLP_NODE_RANKS tells the
+        render pool how many of the node's local ranks (local rank r drives GPU r % ndev) share
+        this mask.  KNN_NUMA_BIND=0 disables it.  Returns the node or -1."""
+        if os.environ.get("KNN_NUMA_BIND", "1") == "0":
+            return -1
+        torch = _torch()
+        node = Comm._numa_node(dev_index)
+        if node < 0:
+            return -1
+        try:
             with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
                 cpus = set()
                 for part in f.read().strip().split(","):
@@ -106,9 +118,19 @@ class Comm:
             if not mine:
                 return -1
             os.sched_setaffinity(0, mine)
-            return node
-        except (OSError, ValueError, AttributeError, RuntimeError):
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    os.sched_setaffinity(int(tid), mine)
+                except OSError:
+                    pass  # a thread that just exited
+        except (OSError, ValueError):
             return -1
+        ndev = max(1, torch.cuda.device_count())
+        nodes = {}
+        share = sum(1 for r in range(max(1, local_world))
+                    if nodes.setdefault(r % ndev, Comm._numa_node(r % ndev)) == node)
+        os.environ["DMLP_NODE_RANKS"] = str(max(1, share))
+        return node
 
     @staticmethod
     def init(device: str = "auto", timeout_s: int = 600) -> "Comm":
@@ -124,7 +146,7 @@ class Comm:
             ndev = torch.cuda.device_count()
             torch.cuda.set_device(local_rank % max(1, ndev))
             dev = torch.device("cuda", torch.cuda.current_device())
-            Comm._numa = Comm.bind_numa(dev.index)
+            Comm._numa = Comm.bind_numa(dev.index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         else:
             dev = torch.device("cpu")
         # DMLP_DATA_PLANE=host: gloo over host-staged copies of the device tensors (dist_api.py)

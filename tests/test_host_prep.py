@@ -118,3 +118,29 @@ def test_cpu_prep_data_flags_range():
     nmax = np.zeros(1, np.uint32)
     assert L.dmlp_cpu_prep_data(X.ctypes.data, 3000, 32, mu.ctypes.data, 1, img.ctypes.data,
                                 xinit.ctypes.data, nmax.ctypes.data) == 1
+
+
+def test_pool_splits_mask_among_node_ranks():
+    """The render pool divides its CPU mask among the local ranks bound to the same NUMA node
+    (DMLP_NODE_RANKS, set by the NUMA binding), not among every rank of the machine."""
+    import os
+    import subprocess
+    import sys
+
+    def threads(**env):
+        e = {k: v for k, v in os.environ.items()
+             if k not in ("LOCAL_WORLD_SIZE", "DMLP_NODE_RANKS", "DMLP_HOST_THREADS")}
+        e.update(env)
+        r = subprocess.run([sys.executable, "-c", "from distributed_machine_learning_project_amd "
+                            "import _lib; print(_lib.lib().dmlp_host_threads())"],
+                           capture_output=True, text=True, env=e, check=True)
+        return int(r.stdout.strip())
+
+    alone = threads()
+    if alone < 8:
+        pytest.skip("needs >= 8 CPUs in the affinity mask")
+    all_local = threads(LOCAL_WORLD_SIZE="4")
+    node_pair = threads(LOCAL_WORLD_SIZE="4", DMLP_NODE_RANKS="2")
+    node_one = threads(LOCAL_WORLD_SIZE="4", DMLP_NODE_RANKS="1")
+    assert all_local <= node_pair <= node_one
+    assert node_one > all_local

@@ -16,6 +16,7 @@
 #   exact      bench.py --exact (fp64-only path)
 #   harness    bench.py --harness native (knn_engine through the reference contract)
 #   dropin     bench.py --harness dropin (engine.h drop-in linked with the reference's common.cpp)
+#   parts      bench.py with 4 / 2 / 1 query parts of the host-operand pipeline (+ --verify at 4)
 #   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
@@ -73,7 +74,21 @@ for task in "$@"; do
     harness)
       step harness 600 python bench.py --harness native ;;
     dropin)
-      step dropin 600 python bench.py --harness dropin --steps 5 --warmup 1 ;;
+      step dropin 600 python bench.py --harness dropin --steps 5 --warmup 1
+      python -m distributed_machine_learning_project_amd.build --dropin \
+          distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
+      python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
+          --max 1000 --minK 16 --maxK 16 --num_labels 10 --output /tmp/dropin_bench.in > /dev/null
+      for i in 1 2 3; do
+        KNN_TRACE=1 timeout -k 10 120 /tmp/eng_dropin < /tmp/dropin_bench.in > /tmp/dropin.out \
+            2> "$OUT/dropin_trace_$i.txt" || exit 1
+      done
+      cat "$OUT/dropin_trace_3.txt" ;;
+    parts)
+      DMLP_HOST_OPS_PARTS=4 step parts_verify 300 python bench.py --steps 5 --warmup 1 --verify
+      for P in 4 2 1; do
+        DMLP_HOST_OPS_PARTS=$P step parts_$P 300 python bench.py --steps 100 --warmup 10
+      done ;;
     split)
       for q in 131072 65536 32768; do
         step split_$q 240 rocprofv3 --kernel-trace --stats -d "$OUT/split_$q" -o run --output-format csv \
