@@ -54,6 +54,7 @@ _SIGS = {
     "dmlp_screen_x1_cols": (i32, [i32, i32]),
     "dmlp_screen_x1_cap": (i32, [i32]),
     "dmlp_screen_x1_waves_per_cu": (i32, [i32]),
+    "dmlp_screen_x1_waves_per_cu_kt": (i32, [i32, i32]),
     "dmlp_screen_x1_min_slices": (i64, [i64]),
     "dmlp_screen_x1_bound": (None, [i32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "dmlp_screen_x1_bound2": (None, [i32, i32, C.POINTER(C.c_float), C.POINTER(C.c_float),

@@ -100,7 +100,7 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
                        const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
                        const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
                        void* stream);
-// Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT <= 2: 64 queries
+// Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT in {1,2,4,8}: 64 queries
 // per workgroup; A and the real point count are needed for the error bound and to drop padding
 // rows; S >= dmlp_screen_x1_min_slices.  Output per (query, slice): up to dmlp_screen_x1_cap(kmax)
 // 4-row group entries (ordered 16-bit key << 16 | slice-relative group index; count -1 =
@@ -110,6 +110,7 @@ int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cols(int KT, int kmax);
 int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
+int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax);  // A > 64: one wave per SIMD
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);
 // eps(q) = r1 |q'| max|x'| + r2 max|x'|^2 + r3 (|q'| + max|x'| + 2^-15) for image kind hl
@@ -145,7 +146,7 @@ int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S, const 
                 int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
                 int* out_label, uint64_t* out_cs, int* status, int* ovf_count, void* stream);
 // Same for the single-term screen's group output: members of each group whose single-term score
-// (recomputed from xfrag / xinit / qhi, KT <= 2) reaches the (query, slice) threshold cand_h get
+// (recomputed from xfrag / xinit / qhi, KT in {1,2,4,8}) reaches the (query, slice) threshold cand_h get
 // exact distances.  status = 1 also when the survivors exceed 256 (pathological ties).
 // qidx may be null: query p is row p (the all-queries pass).
 int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,

@@ -337,7 +337,7 @@ struct LocalKnn {
   DevBuf<unsigned> words;  // [0] xnmax bits, [1] bad
   DevBuf<short> qhi, qlo;
   DevBuf<float> qn, cand_h;
-  DevBuf<int> qidx_a, qidx_b, qidx_e, qidx_f, kdev, cand_ids, cand_cnt, status;
+  DevBuf<int> qidx_a, qidx_b, qidx_c, qidx_e, qidx_f, kdev, cand_ids, cand_cnt, status;
   DevBuf<char> fb_ws;
   int KT = 1;
   int64_t N = 0;
@@ -353,7 +353,7 @@ struct LocalKnn {
     N = N_;
     A = A_;
     KT = std::max(1, (A + 31) / 32);
-    if (KT > 4 || N == 0) return;
+    if (KT > 8 || N == 0) return;
     const int64_t nt = (N + 63) / 64;
     HIPCHK(hipMemsetAsync(words.get(2), 0, 2 * sizeof(unsigned), st));
     DMLPCHK(dmlp_center(Xd, N, A, mu.get(A), st));
@@ -411,7 +411,7 @@ struct LocalKnn {
   // Exact top-k (+ vote/checksum when labels != nullptr) of queries Qx [Q][A] (device).
   // k_host drives dispatch; out_* are [Q][kstride]; lab/cs may be null.  Per-query classes:
   // 1 <= k <= 32 the single-term x1 screen (host operands hx when given, else the device image
-  // prepare() rendered), 32 < k <= 128 the 3-term LDS screen, the rest the exact path; a query
+  // prepare() rendered), 32 < k <= 256 the 3-term LDS screen (cap 256 / 512), the rest the exact path; a query
   // whose x1 candidates overflow escalates alone (3-term screen, then exact).  With hx the
   // fp64 rows X / Qx may still be in flight: everything that reads them waits for `rows`, and
   // the device image (for 3-term work) is rendered on first need (prepare() was not called).
@@ -427,15 +427,19 @@ struct LocalKnn {
     auto launch_rows = [&]() {
       if (!rows_issued) { issue_rows(); rows_issued = true; }
     };
-    std::vector<int> kk(Q), a, b, f, rest;
+    std::vector<int> kk(Q), a, b, c, f, rest;
     bool all_a = true;
     for (int64_t q = 0; q < Q; ++q) kk[q] = (int)std::min<int64_t>(k_host[q], N);
-    const bool screen = KT <= 4 && N > 0;
+    // A <= 128: every screen; A <= 256: the single-term screen alone (k <= 32), the 3-term
+    // kernels' classes and escalations take the exact path
+    const bool lds_ok = KT <= 4;
     const bool x1_ok = dmlp_screen_x1_qw(KT) > 0;
+    const bool screen = (lds_ok || x1_ok) && N > 0;
     for (int64_t q = 0; q < Q; ++q) {
       if (kk[q] < 1) { rest.push_back((int)q); all_a = false; continue; }
       if (screen && kk[q] <= 32 && (x1_ok || !hx)) a.push_back((int)q);
-      else if (screen && kk[q] <= 128) { b.push_back((int)q); all_a = false; }
+      else if (screen && lds_ok && kk[q] <= 128) { b.push_back((int)q); all_a = false; }
+      else if (screen && lds_ok && kk[q] <= 256) { c.push_back((int)q); all_a = false; }
       else { f.push_back((int)q); all_a = false; }
       if (k_host[q] > N) rest.push_back((int)q);
     }
@@ -477,13 +481,13 @@ struct LocalKnn {
     // once, before any kernel writes results: every refine writes its queries' padding and
     // status itself, so the fill is only needed for rows no refine covers (exact path, k < 1)
     if (!all_a || !hx) fill();
-    if (!a.empty() || !b.empty()) {
+    if (!a.empty() || !b.empty() || !c.empty()) {
       const float er = eps_rel(A);
       const int64_t nt = (N + 63) / 64;
       const int qw = dmlp_screen_stream_qw(KT);
       // default: single-term screen (screen_x1.hip); KNN_SCREEN=stream: 3-term streaming
       const char* impl = std::getenv("KNN_SCREEN");
-      const bool use_x1 = x1_ok && !(impl && std::string(impl) == "stream" && !hx);
+      const bool use_x1 = x1_ok && (!lds_ok || !(impl && std::string(impl) == "stream" && !hx));
       // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 128)
       auto pass = [&](const std::vector<int>* idx, int impl, DevBuf<int>& qbuf) {
         const int nq = idx ? (int)idx->size() : (int)Q;
@@ -498,9 +502,10 @@ struct LocalKnn {
         if (idx) for (int q : *idx) kcls = std::max(kcls, kk[q]);
         else for (int64_t q = 0; q < Q; ++q) kcls = std::max(kcls, kk[q]);
         const int cap = impl == 0 ? dmlp_screen_x1_cap(kcls)
-                        : impl == 1 ? dmlp_screen_stream_cap(kcls) : (kcls <= 32 ? 128 : 256);
+                        : impl == 1 ? dmlp_screen_stream_cap(kcls)
+                                    : (kcls <= 32 ? 128 : kcls <= 128 ? 256 : 512);
         const int S = impl == 0 ? slices_stream(nq, dmlp_screen_x1_cols(KT, kcls), nt,
-                                                dmlp_screen_x1_waves_per_cu(kcls),
+                                                dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                                 dmlp_screen_x1_min_slices(nt))
                       : impl == 1 ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))
                                   : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
@@ -537,6 +542,7 @@ struct LocalKnn {
       const int first_a = use_x1 ? 0 : (qw > 0 ? 1 : 2);
       if (!a.empty()) pass(all_a ? nullptr : &a, first_a, qidx_a);
       if (!b.empty()) pass(&b, 2, qidx_b);
+      if (!c.empty()) pass(&c, 2, qidx_c);
       // one host sync: the overflow count (4 bytes); the per-query status only when some
       // screened query overflowed
       int novf = 0;
@@ -550,7 +556,7 @@ struct LocalKnn {
         if (first_a == 0)
           for (int q : a)
             if (sh[q]) esc.push_back(q);
-        if (!esc.empty()) {
+        if (!esc.empty() && (qw > 0 || lds_ok)) {
           // single-term overflow (data too tight for its bound): those queries alone go to the
           // 3-term screen
           HIPCHK(hipMemsetAsync(ovf, 0, sizeof(int), st));

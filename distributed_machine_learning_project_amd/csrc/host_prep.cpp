@@ -285,6 +285,7 @@ int prep_range_any(const double* Qx, int64_t q0, int64_t q1, int A, const double
 // |q - mu| is outside the screen's range (outputs then not usable), else 0.
 extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
                                      uint16_t* qhi, float* qn) {
+  if (KT < 1 || KT > 8 || A > KT * 32) return 1;
   const int W = KT * 32;
   std::atomic<int> ok{1};
   std::function<void(int, int)> job = [&](int part, int parts) {
@@ -307,7 +308,7 @@ int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, c
   const int W = KT * 32;
   int ok = 1;
   float mx = 0.0f;
-  alignas(32) uint16_t h[128];
+  alignas(32) uint16_t h[256];  // W <= 256 (KT <= 8; dmlp_cpu_prep_data_tiles checks)
   alignas(32) float qn1[1];
   for (int64_t p = p0; p < p1; ++p) {
     float ssf;
@@ -346,6 +347,7 @@ int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, c
 extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu,
                                         int KT, int64_t t0, int64_t t1, uint16_t* xhi,
                                         float* xinit, float* nmax) {
+  if (KT < 1 || KT > 8 || A > KT * 32) return 1;
   std::atomic<int> ok{1};
   float mx[kMaxPool] = {0.0f};  // one slot per pool part (pool().size() <= kMaxPool)
   std::function<void(int, int)> job = [&](int part, int parts) {

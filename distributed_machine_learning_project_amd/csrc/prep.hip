@@ -97,7 +97,7 @@ __global__ void k_prep_frag(const double* __restrict__ X, int64_t N, int A,
 // Fragments + norms in one pass: one thread per (point, 8-attribute group) as in k_prep_frag;
 // the G = 4*KT threads of a point are adjacent lanes, so |x - mu|^2 is a G-lane xor-shuffle
 // reduction and every thread keeps its 8 centred values in registers (the row is read once).
-// G must be a power of two (KT = 1, 2, 4); the wave folds its max norm before the one atomic.
+// G must be a power of two (KT = 1, 2, 4, 8); the wave folds its max norm before the one atomic.
 template <int G>
 __global__ __launch_bounds__(256) void k_prep_frag_norm(const double* __restrict__ X, int64_t N,
                                                        int A, const double* __restrict__ mu,
@@ -263,7 +263,7 @@ extern "C" int dmlp_prep_data(const double* X, int64_t N, int A, const double* m
   if (KT < 1 || A > KT * 32) return -1;
   const int64_t n_tiles = (N + 63) / 64;
   const int64_t total = n_tiles * 64 * KT * 4;
-  if (total > 0 && (KT == 1 || KT == 2 || KT == 4)) {
+  if (total > 0 && (KT == 1 || KT == 2 || KT == 4 || KT == 8)) {
     const dim3 grid((unsigned)((total + 255) / 256));
     hipStream_t st = (hipStream_t)stream;
     if (KT == 1)
@@ -272,8 +272,11 @@ extern "C" int dmlp_prep_data(const double* X, int64_t N, int A, const double* m
     else if (KT == 2)
       hipLaunchKernelGGL(k_prep_frag_norm<8>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
                          (uint4*)xfrag, xinit, xnmax_bits, bad);
-    else
+    else if (KT == 4)
       hipLaunchKernelGGL(k_prep_frag_norm<16>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
+                         (uint4*)xfrag, xinit, xnmax_bits, bad);
+    else
+      hipLaunchKernelGGL(k_prep_frag_norm<32>, grid, dim3(256), 0, st, X, N, A, mu, n_tiles,
                          (uint4*)xfrag, xinit, xnmax_bits, bad);
     DMLP_LAUNCH_CHECK();
   } else if (total > 0) {
@@ -294,7 +297,7 @@ extern "C" int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const doubl
   if (KT < 1 || A > KT * 32) return -1;
   if (Q <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (KT == 1 || KT == 2 || KT == 4) {
+  if (KT == 1 || KT == 2 || KT == 4 || KT == 8) {
     const int64_t total = Q * KT * 4;
     const dim3 grid((unsigned)((total + 255) / 256));
     if (KT == 1)
@@ -303,8 +306,11 @@ extern "C" int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const doubl
     else if (KT == 2)
       hipLaunchKernelGGL(k_prep_queries_g<8>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
                          (uint4*)qlo, qn, bad);
-    else
+    else if (KT == 4)
       hipLaunchKernelGGL(k_prep_queries_g<16>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
+                         (uint4*)qlo, qn, bad);
+    else
+      hipLaunchKernelGGL(k_prep_queries_g<32>, grid, dim3(256), 0, st, Qx, Q, A, mu, (uint4*)qhi,
                          (uint4*)qlo, qn, bad);
     DMLP_LAUNCH_CHECK();
     return 0;

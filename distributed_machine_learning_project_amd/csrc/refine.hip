@@ -121,7 +121,7 @@ struct GroupIn {
   int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
 };
 
-// GROUPS = KT of the single-term screen (1 or 2) for group-mode input, 0 otherwise.  The group
+// GROUPS = KT of the single-term screen (1, 2, 4 or 8) for group-mode input, 0 otherwise.  The group
 // variant sizes its LDS for k <= 32 (the screen's limit) and labels in [lo, lo + 256) (wider
 // label ranges take wave_vote's counting fallback), so more waves stay resident to hide the
 // gathers that dominate this kernel.
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
   __shared__ double s_rd[4][KMAX];
   __shared__ int s_ri[4][KMAX];
   __shared__ int s_pre[4][SMAX + 1];
-  __shared__ int s_hist[4][HCAP];
+  __shared__ __attribute__((aligned(16))) int s_hist[4][HCAP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int p = blockIdx.x * 4 + wave;
   if (p >= nq) return;
@@ -153,7 +153,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
   // group mode: everything that depends only on (p, q) is requested here, in one batch, instead
   // of one dependent latency after another (this kernel is bound by its chain of gathers)
   constexpr int KTG = GROUPS ? GROUPS : 1;
-  u32x4 qraw[KTG * 4];
+  // A > 64 (KT = 4, 8): hi(q') is read from LDS at each use (staged below) — 64 / 128 registers
+  // held through the member loop would spill
+  constexpr bool QLDS = GROUPS >= 4;
+  u32x4 qraw[QLDS ? 1 : KTG * 4];
   float g_eps = 0.0f, g_h1 = 0.0f;
   unsigned ebuf = 0;  // S == 1: entry `lane` of the query's single slice
   if (GROUPS) {
@@ -251,7 +254,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
     constexpr int KT = GROUPS ? GROUPS : 1;  // (dead code for GROUPS == 0)
     // hi(q') stays packed (two bf16 per dword, 16 VGPRs per KT): unpacked at each use — a
     // 32-float copy would push this 64-register kernel into scratch spills
-    if (KT != 1) {
+    u32x4* const qs = (u32x4*)s_hist[wave];  // (the histogram is dead once hq is known)
+    if constexpr (QLDS) {
+      static_assert(KT * 4 * 16 <= HCAP * 4, "query fragments must fit the histogram scratch");
+      for (int f = lane; f < KT * 4; f += 64)
+        qs[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
+      dmlp::wave_sync();
+    } else if (KT != 1) {
 #pragma unroll
       for (int f = 0; f < KT * 4; ++f)
         qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
@@ -290,9 +299,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
 #pragma unroll
             for (int kq = 0; kq < 4; ++kq) {
               const u32x4 w = fk[16 * kq];
+              const u32x4 qv = QLDS ? qs[kt * 4 + kq] : qraw[QLDS ? 0 : kt * 4 + kq];
 #pragma unroll
               for (int q2 = 0; q2 < 4; ++q2) {
-                const unsigned qw = qraw[kt * 4 + kq][q2];
+                const unsigned qw = qv[q2];
                 if constexpr (F16) {  // products exact in fp32 either way: any order obeys the bound
                   sc += (float)__builtin_bit_cast(_Float16, (unsigned short)(qw & 0xffffu)) *
                         (float)__builtin_bit_cast(_Float16, (unsigned short)(w[q2] & 0xffffu));
@@ -1010,12 +1020,18 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   if (S < 1 || S > 256) return -1;
   const dim3 grid((nq + 3) / 4), block(256);
   hipStream_t st = (hipStream_t)stream;
-  // cap is only the id stride per (query, slice).  P = 256 slots cover k + 64 for every screened
-  // k (<= 128); a larger P would cut the resident waves that hide the row-gather latency
+  // cap is only the id stride per (query, slice).  P = 256 slots cover k + 64 for every k of the
+  // cap <= 256 screens (<= 128); a larger P would cut the resident waves that hide the
+  // row-gather latency, so only the cap-512 screen (128 < k <= 256) takes P = 512
   if (cap < 1) return -2;
-  hipLaunchKernelGGL((k_refine<4, 0>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
-                     Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
-                     out_label, out_cs, status, ovf_count, GroupIn{});
+  if (cap > 256)
+    hipLaunchKernelGGL((k_refine<8, 0>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
+                       Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
+                       out_label, out_cs, status, ovf_count, GroupIn{});
+  else
+    hipLaunchKernelGGL((k_refine<4, 0>), grid, block, 0, st, cand_ids, cand_cnt, S, cap, X, A,
+                       Qx, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo, label_hi,
+                       out_label, out_cs, status, ovf_count, GroupIn{});
   DMLP_LAUNCH_CHECK();
   return 0;
 }
@@ -1028,7 +1044,8 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
                                   const int* labels, int label_lo, int label_hi, int* out_label,
                                   uint64_t* out_cs, int* status, int* ovf_count, void* stream) {
   if (nq <= 0) return 0;
-  if (S < 1 || S > 256 || cap < 1 || KT < 1 || KT > 2 || n_points > 0x7fffffff) return -1;
+  if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
+  if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return -1;
   if (hl != 1 && hl != 2) return -1;
   const int64_t n_tiles = (n_points + 63) / 64;
   const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
@@ -1040,9 +1057,15 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
   if (KT == 1) {
     if (hl == 1) DMLP_REFINE_G(1, true);
     else DMLP_REFINE_G(1, false);
-  } else {
+  } else if (KT == 2) {
     if (hl == 1) DMLP_REFINE_G(2, true);
     else DMLP_REFINE_G(2, false);
+  } else if (KT == 4) {
+    if (hl == 1) DMLP_REFINE_G(4, true);
+    else DMLP_REFINE_G(4, false);
+  } else {
+    if (hl == 1) DMLP_REFINE_G(8, true);
+    else DMLP_REFINE_G(8, false);
   }
 #undef DMLP_REFINE_G
   DMLP_LAUNCH_CHECK();

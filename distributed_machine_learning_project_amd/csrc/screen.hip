@@ -356,12 +356,15 @@ int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const 
 
 }  // namespace
 
-// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*KT + 256) + WAVES*16*CAP*8 <= 160 KiB.
+// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*KT + 256) + WAVES*16*CAP*8 <= 160 KiB.  CAP = 512 serves
+// 128 < k <= 256 (a column compacts to >= k entries and refills 448 - k before the next batch).
 #define DMLP_SCREEN_CONFIGS(X)                                                                \
   X(1, 128, 8) X(2, 128, 4) X(3, 128, 4) X(4, 128, 4) X(1, 256, 4) X(2, 256, 2) X(3, 256, 2) \
-  X(4, 256, 2)
+  X(4, 256, 2) X(1, 512, 2) X(2, 512, 1) X(3, 512, 1) X(4, 512, 1)
 
-extern "C" int dmlp_screen_kmax(int cap) { return cap == 128 ? 32 : (cap == 256 ? 128 : 0); }
+extern "C" int dmlp_screen_kmax(int cap) {
+  return cap == 128 ? 32 : (cap == 256 ? 128 : (cap == 512 ? 256 : 0));
+}
 
 extern "C" int dmlp_screen_lds_bytes(int KT, int cap) {
 #define DMLP_LDS_CASE(kt, cp, w) \

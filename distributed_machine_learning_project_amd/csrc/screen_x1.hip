@@ -81,7 +81,7 @@ __device__ __forceinline__ unsigned unord32(unsigned o) {
 }
 
 template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE, bool F16>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32) ? 1 : 2))) void k_screen_x1(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32 || KT >= 4) ? 1 : 2))) void k_screen_x1(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
@@ -444,13 +444,18 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h)
-  switch (g_x1_mode) {
-    case 1: DMLP_X1_LAUNCH(1); break;
-    case 2: DMLP_X1_LAUNCH(2); break;
-    case 4: DMLP_X1_LAUNCH(4); break;
-    case 6: DMLP_X1_LAUNCH(6); break;
-    case 8: DMLP_X1_LAUNCH(8); break;
-    default: DMLP_X1_LAUNCH(0); break;
+  // ablation modes only for the A <= 64 variants (each mode is a full kernel instantiation)
+  if constexpr (KT <= 2) {
+    switch (g_x1_mode) {
+      case 1: DMLP_X1_LAUNCH(1); break;
+      case 2: DMLP_X1_LAUNCH(2); break;
+      case 4: DMLP_X1_LAUNCH(4); break;
+      case 6: DMLP_X1_LAUNCH(6); break;
+      case 8: DMLP_X1_LAUNCH(8); break;
+      default: DMLP_X1_LAUNCH(0); break;
+    }
+  } else {
+    DMLP_X1_LAUNCH(0);
   }
 #undef DMLP_X1_LAUNCH
   DMLP_LAUNCH_CHECK();
@@ -486,10 +491,11 @@ extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
   dmlp_screen_x1_bound2(A, 2, r1, r2, &r3);
 }
 extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
-extern "C" int dmlp_screen_x1_qw(int KT) { return (KT == 1 || KT == 2) ? 64 : 0; }
+static bool x1_kt_ok(int KT) { return KT == 1 || KT == 2 || KT == 4 || KT == 8; }
+extern "C" int dmlp_screen_x1_qw(int KT) { return x1_kt_ok(KT) ? 64 : 0; }
 // queries per wave (= workgroup) of the variant that serves kmax
 extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
-  return (KT == 1 || KT == 2) ? 16 * x1_ct(kmax) : 0;
+  return x1_kt_ok(KT) ? 16 * (KT >= 4 ? 4 : x1_ct(kmax)) : 0;
 }
 // group ids per (query, slice) (refine expands each to its 4 members)
 extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
@@ -497,6 +503,11 @@ extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {
   return x1_sub(kmax) == 16 ? (x1_ct(kmax) == 8 ? 4 : 8) : 4;
+}
+// the same for an image of KT fragments per step: A > 64 (KT = 4, 8) runs one wave per SIMD (the
+// query and ring fragments take the registers of two)
+extern "C" int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax) {
+  return KT >= 4 ? 4 : dmlp_screen_x1_waves_per_cu(kmax);
 }
 // a slice must stay below 2^16 4-row groups (16-bit group index in an entry)
 extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles + 4095) / 4096; }
@@ -522,7 +533,7 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 || n_points > n_tiles * 64) return -1;
   if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
-  if (kmax > 32 || KT < 1 || KT > 2 || A > KT * 32) return -3;
+  if (kmax > 32 || !x1_kt_ok(KT) || A > KT * 32) return -3;
   if (hl != 1 && hl != 2) return -1;
   float r1, r2, r3;
   dmlp_screen_x1_bound2(A, hl, &r1, &r2, &r3);
@@ -539,9 +550,17 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
       return ct == 8 ? launch_x1<1, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                            \
                      : launch_x1<1, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                           \
     }                                                                                          \
-    if (sub == 32) return launch_x1<2, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                        \
-    return ct == 8 ? launch_x1<2, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                              \
-                   : launch_x1<2, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                             \
+    if (KT == 2) {                                                                             \
+      if (sub == 32) return launch_x1<2, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                      \
+      return ct == 8 ? launch_x1<2, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                            \
+                     : launch_x1<2, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                           \
+    }                                                                                          \
+    if (KT == 4) {                                                                             \
+      if (sub == 32) return launch_x1<4, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                      \
+      return launch_x1<4, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                                     \
+    }                                                                                          \
+    if (sub == 32) return launch_x1<8, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                        \
+    return launch_x1<8, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                                       \
   } while (0)
   if (hl == 1) DMLP_X1_PICK(true);
   DMLP_X1_PICK(false);

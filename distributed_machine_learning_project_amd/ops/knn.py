@@ -29,7 +29,9 @@ from .. import _lib
 
 SCREEN_KMAX_A = 32      # cap 128 class
 SCREEN_KMAX_B = 128     # cap 256 class
-SCREEN_MAX_KT = 4       # A <= 128 on the screen path
+SCREEN_KMAX_C = 256     # cap 512 class
+SCREEN_MAX_KT = 8       # A <= 256 on the screen path (the single-term screen; the 3-term
+LDS_MAX_KT = 4          # kernels serve A <= 128: beyond, their classes take the exact path)
 NUM_CUS = 256
 # "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
 SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
@@ -320,22 +322,29 @@ class _KnnCall:
         L = _lib.lib()
         _apply_env_switches(L)
         ds, kk, Q, A = self.ds, self.kk, self.Q, self.A
-        self.use_screen = ds.screen_ok and not self.exact and Q > 0
+        # A > 128: only the single-term screen serves the dataset (its classes: k <= 32)
+        self.lds_ok = ds.KT <= LDS_MAX_KT
+        self.use_screen = (ds.screen_ok and not self.exact and Q > 0 and
+                           (self.lds_ok or (SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(ds.KT) > 0)))
         empty = np.empty(0, np.int64)
         # common case (every k in [1, 32], k <= N): one class, identity query index, no per-query
         # host scans — this host path runs while the GPU waits for its first kernel
         self.all_a = self.use_screen and self.kmin >= 1 and self.kmax <= min(SCREEN_KMAX_A, ds.N)
         if self.all_a:
-            self.cls_a, self.cls_b = None, empty
+            self.cls_a, self.cls_b, self.cls_c = None, empty, empty
         else:
             self.cls_a = (np.nonzero((kk >= 1) & (kk <= SCREEN_KMAX_A))[0] if self.use_screen
                           else empty)
             self.cls_b = (np.nonzero((kk > SCREEN_KMAX_A) & (kk <= SCREEN_KMAX_B))[0]
-                          if self.use_screen else empty)
+                          if self.use_screen and self.lds_ok else empty)
+            self.cls_c = (np.nonzero((kk > SCREEN_KMAX_B) & (kk <= SCREEN_KMAX_C))[0]
+                          if self.use_screen and self.lds_ok else empty)
             self.on_screen = np.zeros(Q, bool)
             self.on_screen[self.cls_a] = True
             self.on_screen[self.cls_b] = True
-        self.screened = self.use_screen and (self.all_a or len(self.cls_a) or len(self.cls_b))
+            self.on_screen[self.cls_c] = True
+        self.screened = self.use_screen and (self.all_a or len(self.cls_a) or len(self.cls_b)
+                                             or len(self.cls_c))
         self.stream = _torch().cuda.current_stream()
         if not self.screened:
             return self
@@ -356,6 +365,8 @@ class _KnnCall:
             self._screen_pass(self.cls_a, self.first_a)
         if len(self.cls_b):
             self._screen_pass(self.cls_b, "lds")
+        if len(self.cls_c):
+            self._screen_pass(self.cls_c, "lds")
         return self
 
     def _wait_qx(self):
@@ -384,7 +395,7 @@ class _KnnCall:
         cap = L.dmlp_screen_x1_cap(kcls)
         cus = max(1, int(round(NUM_CUS * self.gpu_share)))
         S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), self.ds.n_tiles,
-                                  L.dmlp_screen_x1_waves_per_cu(kcls),
+                                  L.dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                   int(L.dmlp_screen_x1_min_slices(self.ds.n_tiles)), cus)
         self.pre_screen = (torch.empty(nq * S * cap, dtype=torch.int32, device=self.dev),
                            torch.empty(nq * S, dtype=torch.int32, device=self.dev),
@@ -415,14 +426,14 @@ class _KnnCall:
         elif impl == "x1":
             cap = L.dmlp_screen_x1_cap(kcls)
             S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), ds.n_tiles,
-                                      L.dmlp_screen_x1_waves_per_cu(kcls),
+                                      L.dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                       int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
         elif impl == "stream":
             cap = L.dmlp_screen_stream_cap(kcls)
             S = _choose_slices_stream(nq, L.dmlp_screen_stream_qw(KT), ds.n_tiles,
                                       L.dmlp_screen_stream_waves_per_cu(kcls), 1, cus)
         else:
-            cap = 128 if kcls <= SCREEN_KMAX_A else 256
+            cap = (128 if kcls <= SCREEN_KMAX_A else 256 if kcls <= SCREEN_KMAX_B else 512)
             S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
         if pre is None:
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
@@ -509,7 +520,7 @@ class _KnnCall:
             # the refine kernels count overflowed queries into this call's counter slot: one
             # 4-byte read (and the call's one host sync) instead of a reduce over the status
             n_ovf = self._ovf.read(self._ovf_slot, self.stream)
-            if n_ovf and self.first_a == "x1":
+            if n_ovf and self.first_a == "x1" and (self.stream_ok or self.lds_ok):
                 st = self.status.cpu().numpy()
                 esc = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
                 n_esc = len(esc)

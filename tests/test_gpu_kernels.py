@@ -435,3 +435,51 @@ def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
     np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
     np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
+@pytest.mark.parametrize("A,kmax", [(65, 16), (100, 32), (128, 16), (129, 16), (200, 30),
+                                    (256, 16)])
+def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
+    """Single-term screen for A > 64 (KT = 4 and 8, one wave per SIMD) with the group refine
+    staging hi(q') in LDS; A > 128 has no 3-term kernel, so the x1 class is its only screen."""
+    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    inp = dmlp.generate(6000, 300, A, 0.0, 1000.0, 1, kmax, 6, seed=A + kmax)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 0
+    assert_same(r, refs)
+
+
+@pytest.mark.parametrize("A", [32, 64, 100, 128])
+def test_screen_k_up_to_256(torch_cuda, A):
+    """128 < k <= 256 on the cap-512 LDS screen (3-term) and the P = 512 refine, mixed with the
+    cap-256 class in one call."""
+    inp = dmlp.generate(20000, 300, A, 0.0, 1000.0, 100, 256, 8, seed=A)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 0
+    assert_same(r, refs)
+
+
+@pytest.mark.parametrize("case", ["parts", "out_of_range", "wide"])
+def test_pipelined_query_parts(torch_cuda, case, monkeypatch):
+    """The query-part front (HOST_OPS_PARTS): each part's screen is queued natively behind its
+    own operand copy on its own stream.  out_of_range puts one query of the last part outside
+    the fp16 range, so the parts already screened are drained and the call reruns on the
+    device path; wide runs KT = 8."""
+    torch = torch_cuda
+    monkeypatch.setattr(K, "HOST_OPS_PARTS", 4)
+    A = 256 if case == "wide" else 32
+    inp = dmlp.generate(8000 if case == "wide" else 20000, 32768, A, 0.0, 1000.0, 1, 32, 10,
+                        seed=31)
+    if case == "out_of_range":
+        inp.Qx[-5, 3] = 1.0e6
+    Xp = torch.from_numpy(inp.X).pin_memory().numpy()
+    Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k)
+    torch.cuda.synchronize()
+    assert ds.hl == (2 if case == "out_of_range" else 1)
+    d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)

@@ -6,6 +6,7 @@
 #
 # tasks:
 #   tests      pytest -m gpu (the round-end GPU tier)
+#   ktests     the GPU tests selected by KTESTS (a pytest -k expression)
 #   bench      python bench.py (defaults: 1 GPU, headline config)
 #   verify     python bench.py --verify (every report line vs the exact CPU path)
 #   prof       rocprofv3 --kernel-trace --stats over a short bench run (kernel split)
@@ -41,6 +42,9 @@ for task in "$@"; do
     tests)
       step tests 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
           --timeout-method thread ;;
+    ktests)  # a subset of the GPU tier: KTESTS='<pytest -k expression>'
+      step ktests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+          --timeout-method thread -k "${KTESTS:?KTESTS}" ;;
     bench)
       step bench 300 python bench.py ;;
     verify)
