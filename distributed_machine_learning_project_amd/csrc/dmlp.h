@@ -45,6 +45,10 @@ int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, 
 int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
                        uint16_t* xhi, float* xinit, unsigned* xnmax_bits);
 // Async device->host copy on `stream` (dst: page-locked or host-registered memory).
+// Lossless 6-decimal transfer: int32 m with x == fl(m / 1e6) bit for bit (0 = every value
+// passed, 1 = ship fp64), and the device reconstruction of the fp64 rows.
+int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst);
+int dmlp_rows_from_i32(const int* src, int64_t n, double* dst, void* stream);
 int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream);
 int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu, int KT,
                              int64_t t0, int64_t t1, uint16_t* xhi, float* xinit, float* nmax);
@@ -100,6 +104,13 @@ int dmlp_screen_stream(int KT, const void* xfrag, const float* xinit, int64_t n_
                        const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
                        const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
                        void* stream);
+// 32-attribute fragments per row of the screen images for A attributes: A <= 256 rounds up to
+// 1, 2, 4 or 8 (the single-term screen's variants; the zero padding costs MFMA work only), wider
+// rows take ceil(A / 32) (exact path only).
+static inline int dmlp_screen_kt(int A) {
+  const int kt = A > 32 ? (A + 31) / 32 : 1;
+  return kt > 8 ? kt : (kt <= 1 ? 1 : kt <= 2 ? 2 : kt <= 4 ? 4 : 8);
+}
 // Single-term bf16 screen (screen_x1.hip) for k <= dmlp_screen_x1_kmax() and KT in {1,2,4,8}: 64 queries
 // per workgroup; A and the real point count are needed for the error bound and to drop padding
 // rows; S >= dmlp_screen_x1_min_slices.  Output per (query, slice): up to dmlp_screen_x1_cap(kmax)

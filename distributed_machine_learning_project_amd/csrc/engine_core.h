@@ -521,7 +521,7 @@ class KnnCore {
     // (debug_ = lists mode — the engine.h drop-in hands every list to the harness's reportResult
     // — is served too: render() then copies the lists and labels instead of the report text)
     if (rt_.world != 1 || exact_ || !in || N_ == 0 || Q_ == 0 || Q_ > (1 << 30)) return false;
-    const int KT = std::max(1, (A_ + 31) / 32);
+    const int KT = dmlp_screen_kt(A_);
     if (dmlp_screen_x1_qw(KT) <= 0) return false;
     FastOut fo;
     if (fast_core(in->X.data(), in->labels.data(), in->Qx.data(), in->k.data(), Q_, fo) != 0)
@@ -545,7 +545,7 @@ class KnnCore {
   // norm are agreed over MPI on the host first, so every rank takes the same branch.
   int fast_core(const double* X, const int* labels, const double* Qx, const int* k, int64_t nq,
                 FastOut& fo, bool shard = false) {
-    const int KT = std::max(1, (A_ + 31) / 32);
+    const int KT = dmlp_screen_kt(A_);
     hipStream_t st = rt_.stream;
     const int64_t nt = (N_ + 63) / 64, W = (int64_t)KT * 32;
     const int P = shard ? rt_.world : 1;
@@ -632,7 +632,7 @@ class KnnCore {
     std::vector<int64_t> cnt, off;
     block_partition(Q_, P, cnt, off);
     const int64_t a = off[r], nl = cnt[r];
-    const int KT = std::max(1, (A_ + 31) / 32);
+    const int KT = dmlp_screen_kt(A_);
     int ok = dmlp_screen_x1_qw(KT) > 0 && nl <= (1 << 30);
     MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
     if (!ok) return false;

@@ -352,7 +352,7 @@ struct LocalKnn {
     X = Xd;
     N = N_;
     A = A_;
-    KT = std::max(1, (A + 31) / 32);
+    KT = dmlp_screen_kt(A);
     if (KT > 8 || N == 0) return;
     const int64_t nt = (N + 63) / 64;
     HIPCHK(hipMemsetAsync(words.get(2), 0, 2 * sizeof(unsigned), st));

@@ -338,6 +338,62 @@ int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, c
 
 }  // namespace
 
+namespace {
+
+// Lossless 6-decimal ingest: x == fl(m / 1e6) for an int32 m (text inputs written with "%.6f",
+// like generate_input.py's, parse to exactly these doubles).  Bitwise check, so -0.0 and any
+// value with more digits fail and the caller ships fp64 instead.
+int rows_i32_scalar(const double* src, int64_t a, int64_t b, int32_t* dst) {
+  int ok = 1;
+  for (int64_t i = a; i < b; ++i) {
+    const double m = std::nearbyint(src[i] * 1.0e6);
+    if (!(std::fabs(m) <= 2147483647.0)) { ok = 0; dst[i] = 0; continue; }
+    dst[i] = (int32_t)m;
+    const double back = (double)dst[i] / 1.0e6;  // from the int, as the device does (-0.0 fails)
+    if (std::memcmp(&back, src + i, 8) != 0) ok = 0;
+  }
+  return ok;
+}
+
+__attribute__((target("avx2"))) int rows_i32_avx2(const double* src, int64_t a, int64_t b,
+                                                  int32_t* dst) {
+  const __m256d sc = _mm256_set1_pd(1.0e6);
+  const __m256d lim = _mm256_set1_pd(2147483647.0);
+  const __m256d sgn = _mm256_set1_pd(-0.0);
+  __m256i okv = _mm256_set1_epi64x(-1);
+  int64_t i = a;
+  for (; i + 4 <= b; i += 4) {
+    const __m256d x = _mm256_loadu_pd(src + i);
+    const __m256d m = _mm256_round_pd(_mm256_mul_pd(x, sc), _MM_FROUND_TO_NEAREST_INT | _MM_FROUND_NO_EXC);
+    const __m256d inr = _mm256_cmp_pd(_mm256_andnot_pd(sgn, m), lim, _CMP_LE_OQ);
+    const __m256d mm = _mm256_and_pd(m, inr);  // out of range (or NaN): 0, flagged below
+    const __m128i mi = _mm256_cvtpd_epi32(mm);
+    const __m256d back = _mm256_div_pd(_mm256_cvtepi32_pd(mi), sc);
+    const __m256i same = _mm256_cmpeq_epi64(_mm256_castpd_si256(back), _mm256_castpd_si256(x));
+    okv = _mm256_and_si256(okv, _mm256_and_si256(same, _mm256_castpd_si256(inr)));
+    _mm_storeu_si128((__m128i*)(dst + i), mi);
+  }
+  int ok = _mm256_movemask_pd(_mm256_castsi256_pd(okv)) == 0xf;
+  return rows_i32_scalar(src, i, b, dst) && ok;
+}
+
+}  // namespace
+
+// src[0 .. n) -> dst as int32 m with src[i] == fl(m / 1e6) bit for bit; returns 0 when every value
+// passed (dst then reconstructs src exactly: prep.hip dmlp_rows_from_i32), 1 otherwise.
+extern "C" int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  std::atomic<int> ok{1};
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    const int64_t a = n * part / parts, b = n * (part + 1) / parts;
+    const int r = avx2 ? rows_i32_avx2(src, a, b, dst) : rows_i32_scalar(src, a, b, dst);
+    if (!r) ok.store(0, std::memory_order_relaxed);
+  };
+  if (n < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+  return ok.load() ? 0 : 1;
+}
+
 // Dataset screen operands on the host for tiles [t0, t1) of the image: xhi = prep.hip's tile
 // image with the lo halves dropped ([n_tiles][4][KT][64] x 16 B, what the single-term screen and
 // the group refine read), xinit[n_tiles*64] = -|x - mu|^2 / 2 (fp32; -inf for padding rows),

@@ -458,6 +458,31 @@ extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, i
                                  qhi_h, qn_h, xhi_d, xin_d, xnm_d, qhi_d, qn_d, chunks, stream);
 }
 
+__global__ __launch_bounds__(256) void k_rows_from_i32(const int* __restrict__ src, int64_t n,
+                                                      double* __restrict__ dst) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    const int4 m = *(const int4*)(src + i);
+    // IEEE division (correctly rounded, as the host's check): the exact input doubles
+    *(double2*)(dst + i) = double2{(double)m.x / 1.0e6, (double)m.y / 1.0e6};
+    *(double2*)(dst + i + 2) = double2{(double)m.z / 1.0e6, (double)m.w / 1.0e6};
+  } else {
+    for (int64_t j = i; j < n; ++j) dst[j] = (double)src[j] / 1.0e6;
+  }
+}
+
+// fp64 rows from their lossless int32 form (host_prep.cpp dmlp_cpu_rows_i32): dst[i] = m / 1e6.
+// src and dst 16-byte aligned.
+extern "C" int dmlp_rows_from_i32(const int* src, int64_t n, double* dst, void* stream) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return -1;
+  const int64_t blocks = (n + 1023) / 1024;
+  hipLaunchKernelGGL(k_rows_from_i32, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     src, n, dst);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream) {
   if (bytes <= 0) return 0;
   const hipError_t e = hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost,

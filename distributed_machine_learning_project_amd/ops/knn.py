@@ -44,6 +44,16 @@ HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "2"))
 # as its operands land, on its own stream, while the host renders the next part (1: one screen
 # after the whole query image)
 HOST_OPS_PARTS = int(os.environ.get("DMLP_HOST_OPS_PARTS", "4"))
+# fp64 rows of the host-operand pipeline cross PCIe as lossless int32 when every value is a
+# 6-decimal number (knn._issue_rows)
+ROWS_I32 = os.environ.get("DMLP_ROWS_I32", "1") != "0"
+
+
+def screen_kt(A: int) -> int:
+    """32-attribute fragments per row of the screen images (dmlp.h dmlp_screen_kt): A <= 256
+    rounds up to 1, 2, 4 or 8, the single-term screen's variants."""
+    kt = max(1, (A + 31) // 32)
+    return kt if kt > 8 else 1 << (kt - 1).bit_length()
 
 
 def eps_rel(A: int) -> float:
@@ -174,7 +184,7 @@ def prepare_dataset(X, labels=None, label_range=None, mu=None) -> DeviceDataset:
     X = X.contiguous()
     assert X.is_cuda and X.dtype == torch.float64 and X.dim() == 2
     N, A = X.shape
-    KT = max(1, (A + 31) // 32)
+    KT = screen_kt(A)
     screen_ok = KT <= SCREEN_MAX_KT and N > 0
     dev = X.device
     mu_given = mu is not None
@@ -771,7 +781,7 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     _mark("enter", copy)
     Q = len(Q_host)
     A = X_host.shape[1]
-    KT = max(1, (A + 31) // 32)
+    KT = screen_kt(A)
     k_host = np.ascontiguousarray(k_host, np.int32)
     chunks = max(1, min(chunks, Q // 2048 if Q >= 4096 else 1))
     bounds = [Q * c // chunks for c in range(chunks + 1)]
@@ -990,21 +1000,45 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         return None
     _mark("operands_landed", copy)
     with torch.cuda.stream(copy):
-        X.copy_(torch.from_numpy(np.ascontiguousarray(X_host)), non_blocking=True)
         if lab is not None:
             lab.copy_(torch.from_numpy(np.ascontiguousarray(labels_host, np.int32)),
                       non_blocking=True)
-        Qd.copy_(torch.from_numpy(Qh), non_blocking=True)
+        _issue_rows(((np.ascontiguousarray(X_host, np.float64), X), (Qh, Qd)), copy)
         ev_rows = torch.cuda.Event()
         ev_rows.record(copy)
     _mark("rows_landed", copy)
-    _IO["h2d"] += X.numel() * 8 + (lab.numel() * 4 if lab is not None else 0) + Q * A * 8
+    _IO["h2d"] += lab.numel() * 4 if lab is not None else 0
     for call, ps in zip(calls, pss):
         call.qx_event = ev_rows
         with torch.cuda.stream(ps):
             call.launch()
         main.wait_stream(ps)
     return ds, od, oi, ol, oc, calls
+
+
+def _issue_rows(pairs, copy):
+    """Queue the H2D of fp64 host rows into device tensors on `copy`, each (host, device) pair
+    as lossless int32 when every value is a 6-decimal number (x == fl(m / 1e6), checked bit for
+    bit on the host: half the PCIe bytes, the device divides back — prep.hip
+    dmlp_rows_from_i32), else as fp64.  The host packs pair i + 1 while pair i crosses PCIe.
+    DMLP_ROWS_I32=0 always ships fp64."""
+    torch = _torch()
+    L = _lib.lib()
+    for host, dev_t in pairs:
+        n = host.size
+        if n == 0:
+            continue
+        if ROWS_I32:
+            hb = _ARENA.alloc(n * 4)
+            if L.dmlp_cpu_rows_i32(host.ctypes.data, n, hb.data_ptr()) == 0:
+                db = torch.empty(n, dtype=torch.int32, device=dev_t.device)
+                db.copy_(hb.view(torch.int32), non_blocking=True)
+                _lib.check(L.dmlp_rows_from_i32(_p(db), n, _p(dev_t), copy.cuda_stream),
+                           "rows_from_i32")
+                _IO["h2d"] += n * 4
+                continue
+        dev_t.copy_(torch.from_numpy(host).view(dev_t.shape), non_blocking=True)
+        _IO["h2d"] += n * 8
 
 
 def _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter, t_ops0, t_ops,

@@ -459,12 +459,13 @@ def test_screen_k_up_to_256(torch_cuda, A):
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("case", ["parts", "out_of_range", "wide"])
+@pytest.mark.parametrize("case", ["parts", "out_of_range", "wide", "fp64_rows"])
 def test_pipelined_query_parts(torch_cuda, case, monkeypatch):
     """The query-part front (HOST_OPS_PARTS): each part's screen is queued natively behind its
     own operand copy on its own stream.  out_of_range puts one query of the last part outside
     the fp16 range, so the parts already screened are drained and the call reruns on the
-    device path; wide runs KT = 8."""
+    device path; wide runs KT = 8; fp64_rows has dataset values with more than 6 decimals, so
+    its rows cross as fp64 while the queries' cross as lossless int32."""
     torch = torch_cuda
     monkeypatch.setattr(K, "HOST_OPS_PARTS", 4)
     A = 256 if case == "wide" else 32
@@ -472,6 +473,8 @@ def test_pipelined_query_parts(torch_cuda, case, monkeypatch):
                         seed=31)
     if case == "out_of_range":
         inp.Qx[-5, 3] = 1.0e6
+    if case == "fp64_rows":
+        inp.X[7, 5] += 1e-9
     Xp = torch.from_numpy(inp.X).pin_memory().numpy()
     Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
     ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k)

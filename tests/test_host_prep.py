@@ -144,3 +144,24 @@ def test_pool_splits_mask_among_node_ranks():
     node_one = threads(LOCAL_WORLD_SIZE="4", DMLP_NODE_RANKS="1")
     assert all_local <= node_pair <= node_one
     assert node_one > all_local
+
+
+def test_rows_i32_lossless_check():
+    """6-decimal inputs (generate_input.py's "%.6f") travel as int32 m with x == fl(m / 1e6) bit
+    for bit; anything else (more digits, -0.0, |x| >= 2^31 / 1e6, NaN) is refused."""
+    from distributed_machine_learning_project_amd import _lib
+    import distributed_machine_learning_project_amd as dmlp
+    L = _lib.lib()
+    inp = dmlp.generate(5000, 10, 32, -1000.0, 1000.0, 1, 4, 3, seed=9)
+    x = np.ascontiguousarray(inp.X.reshape(-1))
+    m = np.empty(len(x), np.int32)
+    assert L.dmlp_cpu_rows_i32(x.ctypes.data, len(x), m.ctypes.data) == 0
+    back = m.astype(np.float64) / 1.0e6
+    assert np.array_equal(back.view(np.uint64), x.view(np.uint64))
+    for bad in (0.1234567, -0.0, 2147.483648, float("nan"), 1e300):
+        y = x[:1001].copy()  # odd length: the scalar tail too
+        y[np.random.default_rng(1).integers(0, 1001)] = bad
+        assert L.dmlp_cpu_rows_i32(y.ctypes.data, len(y), m.ctypes.data) == 1, bad
+        y[-1] = bad
+        y[:-1] = x[:1000]
+        assert L.dmlp_cpu_rows_i32(y.ctypes.data, len(y), m.ctypes.data) == 1, bad

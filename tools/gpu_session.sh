@@ -12,6 +12,7 @@
 #   prof       rocprofv3 --kernel-trace --stats over a short bench run (kernel split)
 #   timeline   rocprofv3 kernel + memory-copy trace of the last steps (tools/timeline.py)
 #   pmc        one --pmc pass per counter group over the screen + refine (tools/pmc_summary.py)
+#   exactprof  the fused exact kernel (bench.py --exact): kernel split + one PMC pass
 #   engine     native knn_engine: every strategy vs the CPU oracle bytes (tools/engine_check.sh)
 #   sweep      bench sweep over N / A / k (profiles/ sweep table)
 #   exact      bench.py --exact (fp64-only path)
@@ -70,6 +71,15 @@ for task in "$@"; do
         step pmc$n 120 rocprofv3 --kernel-trace --pmc $C -d "$OUT/pmc$n" -o run --output-format csv \
             -- python3 tools/quick_gpu_bench.py --q 131072 --iters 2 --check 0
       done
+      python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
+    exactprof)  # the fused exact kernel: kernel split + one counter pass
+      step exact_stats 300 rocprofv3 --kernel-trace --stats -d "$OUT/exact_stats" -o run \
+          --output-format csv -- python3 bench.py --exact --steps 3 --warmup 1 --no-busbw --diag-steps 0
+      find "$OUT/exact_stats" -name '*kernel_stats.csv' -exec sh -c 'head -6 "$1" | cut -c1-160' _ {} \;
+      step exact_pmc 180 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY \
+          SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU \
+          -d "$OUT/pmc_exact" -o run --output-format csv \
+          -- python3 bench.py --exact --steps 1 --warmup 1 --no-busbw --diag-steps 0
       python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
     engine)
       step engine 400 bash tools/engine_check.sh "$OUT/engine" ;;
