@@ -516,6 +516,16 @@ class KnnCore {
   HostBuf<char> f_stage_;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_rows_ = nullptr;
+  // lossless int32 row transfer (KNN_ROWS_I32=0: always fp64): page-locked + device staging
+  const bool rows_i32_ = !(getenv("KNN_ROWS_I32") && std::string(getenv("KNN_ROWS_I32")) == "0");
+  struct PinnedInts {
+    HostBuf<int> b;
+    int* get(int64_t n) {
+      if ((int64_t)b.size() < n) b.resize((size_t)n);
+      return b.data();
+    }
+  } f_i32_;
+  DevBuf<int> f_i32d_;
 
   bool farm_fast(Input* in, Output* out) {
     // (debug_ = lists mode — the engine.h drop-in hands every list to the harness's reportResult
@@ -602,9 +612,22 @@ class KnnCore {
     double* Qd = Qx_.get(nq * A_);
     auto issue_rows = [&]() {
       // (no stream dependency: the previous call ended with a sync, nothing reads these yet)
-      HIPCHK(hipMemcpyAsync(Xd, X, N_ * A_ * 8, hipMemcpyHostToDevice, side_));
       HIPCHK(hipMemcpyAsync(Ld, labels, N_ * 4, hipMemcpyHostToDevice, side_));
-      HIPCHK(hipMemcpyAsync(Qd, Qx, nq * A_ * 8, hipMemcpyHostToDevice, side_));
+      // the host packs the rows while the screen runs: lossless int32 when every value is a
+      // 6-decimal number (half the PCIe bytes; the device divides back), else fp64
+      const int64_t nx = N_ * A_, nqa = nq * A_;
+      int* hx32 = rows_i32_ ? f_i32_.get(nx + nqa + 4) : nullptr;
+      int* dx32 = rows_i32_ ? f_i32d_.get(nx + nqa + 4) : nullptr;
+      auto rows = [&](const double* src, int64_t n, double* dst, int64_t at) {
+        if (rows_i32_ && dmlp_cpu_rows_i32(src, n, hx32 + at) == 0) {
+          HIPCHK(hipMemcpyAsync(dx32 + at, hx32 + at, n * 4, hipMemcpyHostToDevice, side_));
+          DMLPCHK(dmlp_rows_from_i32(dx32 + at, n, dst, side_));
+        } else {
+          HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, side_));
+        }
+      };
+      rows(X, nx, Xd, 0);
+      rows(Qx, nqa, Qd, (nx + 3) & ~int64_t(3));  // (16-byte aligned for the decode kernel)
       HIPCHK(hipEventRecord(ev_rows_, side_));
       trace.mark("screen");
     };

@@ -796,8 +796,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
                 and L.dmlp_screen_x1_qw(KT) > 0)
     # query parts (HOST_OPS_PARTS): a single local replica, every k on the x1 class
     parts = (HOST_OPS_PARTS if host_ops and HOST_OPS_PARTS > 1 and gather is None
-             and (image_shard is None or image_shard[1] <= 1) and k_range[0] >= 1
-             and k_range[1] <= min(SCREEN_KMAX_A, N) and Q >= HOST_OPS_PARTS * 8192 else 1)
+             and k_range[0] >= 1 and k_range[1] <= min(SCREEN_KMAX_A, N)
+             and Q >= HOST_OPS_PARTS * 8192 else 1)
     dsops = prepped = mu_d = None
     if host_ops:
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
@@ -834,19 +834,36 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
                                        mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
                                        _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
                                        HOST_OPS_CHUNKS, copy.cuda_stream)
-        if parts > 1 and rc == 0:
-            _mark("data_landed", copy)
-            r = _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride,
-                                 finalize, k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn,
-                                 copy, main)
-            if r is None:  # a query outside the screen's range: the device path decides
+        if parts > 1:
+            bad_d = None
+            if sh is not None:
+                # the image collectives, on every rank whatever its own verdict (the same
+                # sequence as the one-part path below)
+                with torch.cuda.stream(copy):
+                    sh[2](xhi.view(torch.int32), xhi_c.view(torch.int32))
+                    sh[2](xin, xin_c)
+                    sh[3](xnm)
+                    bad_d = (xnm >= 0x7f800000).to(torch.int32)
+                rc &= ~1  # the data verdict is the reduced one, on the device
+            if rc & 4:
+                raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
+            r = None
+            if rc == 0:
+                _mark("data_landed", copy)
+                r = _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host,
+                                     kstride, finalize, k_range, KT, mu_h, mu_d, hb, xhi, xin,
+                                     xnm, qhi, qn, copy, main, bad_d)
+            if r is None:
+                # data or a query outside the screen's range: the device path decides (no
+                # collective on it; the pinned staging is reused only once its copies are done)
+                copy.synchronize()
                 return knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host,
                                          kstride, chunks, finalize, exact, gather, mu_rows,
                                          X_full_host, report, k_range, image_shard,
                                          _host_ops=False)
             ds, od, oi, ol, oc, calls = r
             t_ops = time.perf_counter() - t_ops
-            _IO["h2d"] += n_tiles * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
+            _IO["h2d"] += (t1 - t0) * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
             return _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter,
                                    t_ops0, t_ops, True)
         t_ops = time.perf_counter() - t_ops
@@ -931,7 +948,8 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
 
 
 def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride, finalize,
-                     k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn, copy, main):
+                     k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn, copy, main,
+                     bad=None):
     """knn_gpu_pipelined's query-part front (the dataset image is queued on `copy`): part p's
     calls are set up on their own stream, dmlp_host_ops_x1_parts renders each part and queues its
     screen behind its copy, then the fp64 rows follow on `copy` and every part's refine waits for
@@ -947,7 +965,8 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         X = torch.empty((N, A), dtype=torch.float64, device=dev)
         lab = (torch.empty(N, dtype=torch.int32, device=dev) if labels_host is not None else None)
         Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
-        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        if bad is None:  # (sharded image: the reduced verdict)
+            bad = torch.zeros(1, dtype=torch.int32, device=dev)
     if lab is not None and finalize:
         lo, hi = label_range
         lab_ds = lab
