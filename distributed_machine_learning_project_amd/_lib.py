@@ -30,6 +30,11 @@ _SIGS = {
     "dmlp_cpu_prep_data_tiles": (i32, [vp, i64, i32, vp, i32, i64, i64, vp, vp, vp]),
     "dmlp_host_ops_h2d": (i32, [vp, i64, vp, i64, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                 vp, i32, vp]),
+    "dmlp_cpu_center_rows": (None, [vp, i64, i32, vp]),
+    "dmlp_cpu_prep_queries_rows": (i32, [vp, i64, i32, vp, i32, vp, vp]),
+    "dmlp_cpu_prep_data_tiles_rows": (i32, [vp, i64, i32, vp, i32, i64, i64, vp, vp, vp]),
+    "dmlp_cpu_rows_i32_rows": (i32, [vp, i64, i32, vp]),
+    "dmlp_cpu_gather_rows": (None, [vp, i64, i32, vp]),
     "dmlp_cpu_rows_i32": (i32, [vp, i64, vp]),
     "dmlp_rows_from_i32": (i32, [vp, i64, vp, vp]),
     "dmlp_host_ops_x1_parts": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp,

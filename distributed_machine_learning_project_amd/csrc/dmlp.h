@@ -45,6 +45,22 @@ int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, 
 int dmlp_cpu_prep_data(const double* X, int64_t N, int A, const double* mu, int KT,
                        uint16_t* xhi, float* xinit, unsigned* xnmax_bits);
 // Async device->host copy on `stream` (dst: page-locked or host-registered memory).
+// Row-pointer-table variants of the host render (the engine.h drop-in reads the harness's
+// per-point attribute vectors in place): centre, screen operands + H2D, lossless int32 pack,
+// fp64 pack.
+void dmlp_cpu_center_rows(const double* const* rows, int64_t N, int A, double* mu);
+int dmlp_cpu_prep_queries_rows(const double* const* rows, int64_t Q, int A, const double* mu,
+                               int KT, uint16_t* qhi, float* qn);
+int dmlp_cpu_prep_data_tiles_rows(const double* const* rows, int64_t N, int A, const double* mu,
+                                  int KT, int64_t t0, int64_t t1, uint16_t* xhi, float* xinit,
+                                  float* nmax);
+int dmlp_host_ops_h2d_tiles_rows(const double* const* Xr, int64_t N, int64_t t0, int64_t t1,
+                                 const double* const* Qr, int64_t Q, int A, const double* mu,
+                                 int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
+                                 uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d,
+                                 void* xnm_d, void* qhi_d, void* qn_d, int chunks, void* stream);
+int dmlp_cpu_rows_i32_rows(const double* const* rows, int64_t nrows, int A, int32_t* dst);
+void dmlp_cpu_gather_rows(const double* const* rows, int64_t nrows, int A, double* dst);
 // Lossless 6-decimal transfer: int32 m with x == fl(m / 1e6) bit for bit (0 = every value
 // passed, 1 = ship fp64), and the device reconstruction of the fp64 rows.
 int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst);

@@ -175,6 +175,28 @@ class KnnCore {
 
   void set_shared(const SharedIn& s) { sh_ = s; }
 
+  // The single-GPU fast path straight from tables of row pointers (the engine.h drop-in: the
+  // harness's per-point attribute vectors; `in` carries N, Q, A, labels and k, no rows).  Returns
+  // false, with nothing done, whenever that path does not apply (more ranks, another strategy,
+  // data outside the fp16 screen's range, ...): the caller then packs the rows and calls KNN.
+  bool KNN_rows(Input* in, const double* const* Xr, const double* const* Qr, Output* out) {
+    if (rt_.world != 1 || strategy_ != "farm" || dynamic_ || !fast_ || exact_ || !in) return false;
+    if (in->N == 0 || in->Q == 0 || in->Q > (1 << 30)) return false;
+    if (dmlp_screen_x1_qw(dmlp_screen_kt(in->A)) <= 0) return false;
+    wake_d2h();
+    N_ = in->N; Q_ = in->Q; A_ = in->A;
+    lo_ = *std::min_element(in->labels.begin(), in->labels.end());
+    hi_ = *std::max_element(in->labels.begin(), in->labels.end()) + 1;
+    kmax_ = std::max(1, *std::max_element(in->k.begin(), in->k.end()));
+    if (!side_) make_side();
+    FastOut fo;
+    if (fast_core(nullptr, in->labels.data(), nullptr, in->k.data(), Q_, fo, false, Xr, Qr) != 0)
+      return false;
+    render(out, fo.cs, fo.lb, fo.dd, fo.ii);  // synchronizes the stream
+    trace.mark("report");
+    return true;
+  }
+
   void KNN(Input* in, Output* out) {
     wake_d2h();
     // sizes (engine.cpp:27-35): N, Q, A, label range, kmax
@@ -518,13 +540,16 @@ class KnnCore {
   hipEvent_t ev_rows_ = nullptr;
   // lossless int32 row transfer (KNN_ROWS_I32=0: always fp64): page-locked + device staging
   const bool rows_i32_ = !(getenv("KNN_ROWS_I32") && std::string(getenv("KNN_ROWS_I32")) == "0");
-  struct PinnedInts {
-    HostBuf<int> b;
-    int* get(int64_t n) {
+  template <typename T>
+  struct Pinned {
+    HostBuf<T> b;
+    T* get(int64_t n) {
       if ((int64_t)b.size() < n) b.resize((size_t)n);
       return b.data();
     }
-  } f_i32_;
+  };
+  Pinned<int> f_i32_;
+  Pinned<double> f_f64_;  // fp64 rows gathered from a row table (inputs that are not 6-decimal)
   DevBuf<int> f_i32d_;
 
   bool farm_fast(Input* in, Output* out) {
@@ -553,8 +578,12 @@ class KnnCore {
   // shard = true (node-shared farm, P > 1): this rank renders only its 1/P tile range of the
   // dataset's screen image and one all-gather completes it; the data-range verdict and the max
   // norm are agreed over MPI on the host first, so every rank takes the same branch.
+  // Xr / Qr (non-null): the rows come from tables of row pointers instead of X / Qx (the engine.h
+  // drop-in: the harness's per-point vectors, read in place — the render, the int32 pack and, if
+  // needed, an fp64 gather read them; nothing packs the AoS input first).
   int fast_core(const double* X, const int* labels, const double* Qx, const int* k, int64_t nq,
-                FastOut& fo, bool shard = false) {
+                FastOut& fo, bool shard = false, const double* const* Xr = nullptr,
+                const double* const* Qr = nullptr) {
     const int KT = dmlp_screen_kt(A_);
     hipStream_t st = rt_.stream;
     const int64_t nt = (N_ + 63) / 64, W = (int64_t)KT * 32;
@@ -574,7 +603,8 @@ class KnnCore {
     uint16_t* qhi_h = (uint16_t*)hp; hp += up(b_qhi);
     float* qn_h = (float*)hp; hp += up(b_qn);
     double* mu_h = (double*)hp;
-    dmlp_cpu_center(X, N_, A_, mu_h);
+    if (Xr) dmlp_cpu_center_rows(Xr, N_, A_, mu_h);
+    else dmlp_cpu_center(X, N_, A_, mu_h);
     short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
     float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
     short* xhi_c = shard ? fx_hic_.get(tpr * 64 * W) : xhi;
@@ -582,8 +612,12 @@ class KnnCore {
     unsigned* words = f_words_.get(2);  // [0] xnmax bits, [1] bad (0: the host checked ranges)
     short* qhi = fq_hi_.get(std::max<int64_t>(nq, 1) * W);
     float* qn = fq_n_.get(std::max<int64_t>(nq, 1));
-    int rc = dmlp_host_ops_h2d_tiles(X, N_, t0, t1, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h,
-                                     qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn, host_slices_, st);
+    int rc = Xr ? dmlp_host_ops_h2d_tiles_rows(Xr, N_, t0, t1, Qr, nq, A_, mu_h, KT, xhi_h, xin_h,
+                                              xnm_h, qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn,
+                                              host_slices_, st)
+                : dmlp_host_ops_h2d_tiles(X, N_, t0, t1, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h,
+                                          qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn, host_slices_,
+                                          st);
     if (rc & 4) throw std::runtime_error("host operand copy failed");
     if (shard) {
       // every rank's verdict and max norm (host values) before any device collective
@@ -616,18 +650,27 @@ class KnnCore {
       // the host packs the rows while the screen runs: lossless int32 when every value is a
       // 6-decimal number (half the PCIe bytes; the device divides back), else fp64
       const int64_t nx = N_ * A_, nqa = nq * A_;
-      int* hx32 = rows_i32_ ? f_i32_.get(nx + nqa + 4) : nullptr;
-      int* dx32 = rows_i32_ ? f_i32d_.get(nx + nqa + 4) : nullptr;
-      auto rows = [&](const double* src, int64_t n, double* dst, int64_t at) {
-        if (rows_i32_ && dmlp_cpu_rows_i32(src, n, hx32 + at) == 0) {
+      const int64_t qat = (nx + 3) & ~int64_t(3);  // (16-byte aligned for the decode kernel)
+      int* hx32 = rows_i32_ ? f_i32_.get(qat + nqa) : nullptr;
+      int* dx32 = rows_i32_ ? f_i32d_.get(qat + nqa) : nullptr;
+      auto rows = [&](const double* src, const double* const* tab, int64_t nr, double* dst,
+                      int64_t at) {
+        const int64_t n = nr * A_;
+        if (rows_i32_ && (tab ? dmlp_cpu_rows_i32_rows(tab, nr, A_, hx32 + at)
+                              : dmlp_cpu_rows_i32(src, n, hx32 + at)) == 0) {
           HIPCHK(hipMemcpyAsync(dx32 + at, hx32 + at, n * 4, hipMemcpyHostToDevice, side_));
           DMLPCHK(dmlp_rows_from_i32(dx32 + at, n, dst, side_));
-        } else {
-          HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, side_));
+          return;
         }
+        if (tab) {  // not 6-decimal: pack the fp64 rows from the table first
+          double* h = f_f64_.get(qat + nqa) + at;
+          dmlp_cpu_gather_rows(tab, nr, A_, h);
+          src = h;
+        }
+        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, side_));
       };
-      rows(X, nx, Xd, 0);
-      rows(Qx, nqa, Qd, (nx + 3) & ~int64_t(3));  // (16-byte aligned for the decode kernel)
+      rows(X, Xr, N_, Xd, 0);
+      rows(Qx, Qr, nq, Qd, qat);
       HIPCHK(hipEventRecord(ev_rows_, side_));
       trace.mark("screen");
     };

@@ -202,7 +202,22 @@ inline uint16_t f16_rn(float f) {
 
 extern "C" int dmlp_host_threads(void) { return pool().size(); }
 
-extern "C" void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu) {
+namespace {
+
+// Row sources: a row-major block, or a table of row pointers (the engine.h drop-in reads the
+// harness's per-point attribute vectors in place — no packing pass over the AoS input).
+struct FlatRows {
+  const double* X;
+  int A;
+  const double* operator()(int64_t i) const { return X + i * A; }
+};
+struct TableRows {
+  const double* const* R;
+  const double* operator()(int64_t i) const { return R[i]; }
+};
+
+template <class Src>
+void center(Src src, int64_t N, int A, double* mu) {
   const int64_t n = std::min<int64_t>(N, 4096);
   // column sums in a local block: accumulating in place would reload / store mu[a] on every
   // row (the compiler cannot rule out mu aliasing X)
@@ -210,21 +225,31 @@ extern "C" void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu) {
     const int w = std::min(64, A - a0);
     double acc[64] = {0.0};
     for (int64_t i = 0; i < n; ++i) {
-      const double* r = X + i * A + a0;
+      const double* r = src(i) + a0;
       for (int a = 0; a < w; ++a) acc[a] += r[a];
     }
     for (int a = 0; a < w; ++a) mu[a0 + a] = n ? acc[a] / (double)n : 0.0;
   }
 }
 
+}  // namespace
+
+extern "C" void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu) {
+  center(FlatRows{X, A}, N, A, mu);
+}
+extern "C" void dmlp_cpu_center_rows(const double* const* rows, int64_t N, int A, double* mu) {
+  center(TableRows{rows}, N, A, mu);
+}
+
 namespace {
 
 // Portable row: the reference for the AVX2 path's bits (four fixed partial sums for |c|^2).
-int prep_range_scalar(const double* Qx, int64_t q0, int64_t q1, int A, const double* mu, int W,
+template <class Src>
+int prep_range_scalar(Src src, int64_t q0, int64_t q1, int A, const double* mu, int W,
                       uint16_t* qhi, float* qn) {
   int ok = 1;
   for (int64_t q = q0; q < q1; ++q) {
-    const double* r = Qx + q * A;
+    const double* r = src(q);
     uint16_t* h = qhi + q * W;
     double s4[4] = {0.0, 0.0, 0.0, 0.0};
     for (int a = 0; a < A; ++a) {
@@ -240,14 +265,15 @@ int prep_range_scalar(const double* Qx, int64_t q0, int64_t q1, int A, const dou
 }
 
 // A multiple of 8: 4 doubles per vector, partial sums s4[a & 3] exactly as the scalar row.
-__attribute__((target("avx2,f16c"))) int prep_range_avx2(const double* Qx, int64_t q0, int64_t q1,
+template <class Src>
+__attribute__((target("avx2,f16c"))) int prep_range_avx2(Src src, int64_t q0, int64_t q1,
                                                           int A, const double* mu, int W,
                                                           uint16_t* qhi, float* qn) {
   const __m256d lim = _mm256_set1_pd(kMaxAbs);
   const __m256d sgn = _mm256_set1_pd(-0.0);
   __m256d okv = _mm256_castsi256_pd(_mm256_set1_epi64x(-1));
   for (int64_t q = q0; q < q1; ++q) {
-    const double* r = Qx + q * A;
+    const double* r = src(q);
     uint16_t* h = qhi + q * W;
     __m256d acc = _mm256_setzero_pd();
     for (int a = 0; a < A; a += 8) {
@@ -272,11 +298,26 @@ __attribute__((target("avx2,f16c"))) int prep_range_avx2(const double* Qx, int64
   return _mm256_movemask_pd(okv) == 0xf;
 }
 
-int prep_range_any(const double* Qx, int64_t q0, int64_t q1, int A, const double* mu, int W,
+template <class Src>
+int prep_range_any(Src src, int64_t q0, int64_t q1, int A, const double* mu, int W,
                    uint16_t* qhi, float* qn) {
   static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("f16c");
-  if (avx2 && A % 8 == 0) return prep_range_avx2(Qx, q0, q1, A, mu, W, qhi, qn);
-  return prep_range_scalar(Qx, q0, q1, A, mu, W, qhi, qn);
+  if (avx2 && A % 8 == 0) return prep_range_avx2(src, q0, q1, A, mu, W, qhi, qn);
+  return prep_range_scalar(src, q0, q1, A, mu, W, qhi, qn);
+}
+
+template <class Src>
+int prep_queries(Src src, int64_t Q, int A, const double* mu, int KT, uint16_t* qhi, float* qn) {
+  if (KT < 1 || KT > 8 || A > KT * 32) return 1;
+  const int W = KT * 32;
+  std::atomic<int> ok{1};
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    const int64_t q0 = Q * part / parts, q1 = Q * (part + 1) / parts;
+    if (!prep_range_any(src, q0, q1, A, mu, W, qhi, qn)) ok.store(0, std::memory_order_relaxed);
+  };
+  if (Q * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+  return ok.load() ? 0 : 1;
 }
 
 }  // namespace
@@ -285,16 +326,12 @@ int prep_range_any(const double* Qx, int64_t q0, int64_t q1, int A, const double
 // |q - mu| is outside the screen's range (outputs then not usable), else 0.
 extern "C" int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
                                      uint16_t* qhi, float* qn) {
-  if (KT < 1 || KT > 8 || A > KT * 32) return 1;
-  const int W = KT * 32;
-  std::atomic<int> ok{1};
-  std::function<void(int, int)> job = [&](int part, int parts) {
-    const int64_t q0 = Q * part / parts, q1 = Q * (part + 1) / parts;
-    if (!prep_range_any(Qx, q0, q1, A, mu, W, qhi, qn)) ok.store(0, std::memory_order_relaxed);
-  };
-  if (Q * (int64_t)A < (int64_t)1 << 14) job(0, 1);
-  else pool().run(job);
-  return ok.load() ? 0 : 1;
+  return prep_queries(FlatRows{Qx, A}, Q, A, mu, KT, qhi, qn);
+}
+// The same from a table of row pointers (qhi / qn indexed like the table).
+extern "C" int dmlp_cpu_prep_queries_rows(const double* const* rows, int64_t Q, int A,
+                                          const double* mu, int KT, uint16_t* qhi, float* qn) {
+  return prep_queries(TableRows{rows}, Q, A, mu, KT, qhi, qn);
 }
 
 namespace {
@@ -302,7 +339,8 @@ namespace {
 // One point's contribution to the fp16 hi-only tile image: 8 attributes (one 16-byte fragment chunk)
 // per (kt, kg), |c|^2 in fp64.  The chunk of point p = t*64 + rt*16 + r, attributes kt*32 + kg*8
 // .. +7, sits at uint4 index ((t*4 + rt)*KT + kt)*64 + kg*16 + r (prep.hip's layout, lo dropped).
-int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, const double* mu,
+template <class Src>
+int prep_data_range(Src X, int64_t N, int64_t p0, int64_t p1, int A, const double* mu,
                     int KT, uint16_t* xhi, float* xinit, float* nmax) {
   static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("f16c");
   const int W = KT * 32;
@@ -313,10 +351,11 @@ int prep_data_range(const double* X, int64_t N, int64_t p0, int64_t p1, int A, c
   for (int64_t p = p0; p < p1; ++p) {
     float ssf;
     if (p < N) {
+      const FlatRows row{X(p), A};
       if (avx2 && A % 8 == 0) {
-        if (!prep_range_avx2(X + p * A, 0, 1, A, mu, W, h, qn1)) ok = 0;
+        if (!prep_range_avx2(row, 0, 1, A, mu, W, h, qn1)) ok = 0;
       } else {
-        if (!prep_range_scalar(X + p * A, 0, 1, A, mu, W, h, qn1)) ok = 0;
+        if (!prep_range_scalar(row, 0, 1, A, mu, W, h, qn1)) ok = 0;
       }
       ssf = qn1[0];
       xinit[p] = -0.5f * ssf;
@@ -379,6 +418,35 @@ __attribute__((target("avx2"))) int rows_i32_avx2(const double* src, int64_t a, 
 
 }  // namespace
 
+// The same over rows [0, nrows) of a pointer table (A values each, dst row-major).
+extern "C" int dmlp_cpu_rows_i32_rows(const double* const* rows, int64_t nrows, int A,
+                                      int32_t* dst) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  std::atomic<int> ok{1};
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    const int64_t a = nrows * part / parts, b = nrows * (part + 1) / parts;
+    int good = 1;
+    for (int64_t r = a; r < b; ++r)
+      good &= avx2 ? rows_i32_avx2(rows[r], 0, A, dst + r * A)
+                   : rows_i32_scalar(rows[r], 0, A, dst + r * A);
+    if (!good) ok.store(0, std::memory_order_relaxed);
+  };
+  if (nrows * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+  return ok.load() ? 0 : 1;
+}
+
+// Pack the rows of a pointer table row-major into dst (fp64, the pool's threads).
+extern "C" void dmlp_cpu_gather_rows(const double* const* rows, int64_t nrows, int A,
+                                     double* dst) {
+  std::function<void(int, int)> job = [&](int part, int parts) {
+    const int64_t a = nrows * part / parts, b = nrows * (part + 1) / parts;
+    for (int64_t r = a; r < b; ++r) std::memcpy(dst + r * A, rows[r], sizeof(double) * A);
+  };
+  if (nrows * (int64_t)A < (int64_t)1 << 14) job(0, 1);
+  else pool().run(job);
+}
+
 // src[0 .. n) -> dst as int32 m with src[i] == fl(m / 1e6) bit for bit; returns 0 when every value
 // passed (dst then reconstructs src exactly: prep.hip dmlp_rows_from_i32), 1 otherwise.
 extern "C" int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst) {
@@ -400,9 +468,10 @@ extern "C" int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst) {
 // *nmax = the rounded-up max |x - mu|^2 over these tiles (fp32).  The buffers are the whole
 // image's (tile offsets are applied here).  Returns 1 if some |x - mu| is outside the screen's
 // range.
-extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu,
-                                        int KT, int64_t t0, int64_t t1, uint16_t* xhi,
-                                        float* xinit, float* nmax) {
+namespace {
+template <class Src>
+int prep_data_tiles(Src X, int64_t N, int A, const double* mu, int KT, int64_t t0, int64_t t1,
+                    uint16_t* xhi, float* xinit, float* nmax) {
   if (KT < 1 || KT > 8 || A > KT * 32) return 1;
   std::atomic<int> ok{1};
   float mx[kMaxPool] = {0.0f};  // one slot per pool part (pool().size() <= kMaxPool)
@@ -417,6 +486,18 @@ extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const
   for (float v : mx) m = std::max(m, v);
   *nmax = m;
   return ok.load() ? 0 : 1;
+}
+}  // namespace
+
+extern "C" int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu,
+                                        int KT, int64_t t0, int64_t t1, uint16_t* xhi,
+                                        float* xinit, float* nmax) {
+  return prep_data_tiles(FlatRows{X, A}, N, A, mu, KT, t0, t1, xhi, xinit, nmax);
+}
+extern "C" int dmlp_cpu_prep_data_tiles_rows(const double* const* rows, int64_t N, int A,
+                                             const double* mu, int KT, int64_t t0, int64_t t1,
+                                             uint16_t* xhi, float* xinit, float* nmax) {
+  return prep_data_tiles(TableRows{rows}, N, A, mu, KT, t0, t1, xhi, xinit, nmax);
 }
 
 // The whole image; *xnmax_bits = the max as fp32 bits.

@@ -344,12 +344,13 @@ extern "C" int dmlp_host_unregister(void* p) {
 // xhi_d / xin_d point at the slot of tile t0 (a per-rank shard buffer that a collective then
 // completes).  *xnm_d gets this range's max norm; if the range holds data outside the screen's
 // range (return bit 1) it gets +inf instead, so a max-reduce over ranks tells every rank.
-extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1,
-                                       const double* Qx, int64_t Q, int A, const double* mu,
-                                       int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
-                                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d,
-                                       void* xnm_d, void* qhi_d, void* qn_d, int chunks,
-                                       void* stream) {
+// (rows: X / Qx row-major, or — Xr / Qr non-null — tables of row pointers)
+static int host_ops_h2d_tiles(const double* X, const double* const* Xr, int64_t N, int64_t t0,
+                              int64_t t1, const double* Qx, const double* const* Qr, int64_t Q,
+                              int A, const double* mu, int KT, uint16_t* xhi_h, float* xin_h,
+                              unsigned* xnm_h, uint16_t* qhi_h, float* qn_h, void* xhi_d,
+                              void* xin_d, void* xnm_d, void* qhi_d, void* qn_d, int chunks,
+                              void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t n_tiles = (N + 63) / 64;
   t0 = t0 < 0 ? 0 : (t0 > n_tiles ? n_tiles : t0);
@@ -375,7 +376,9 @@ extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, i
     const int64_t a = t0 + (t1 - t0) * c / chunks, b = t0 + (t1 - t0) * (c + 1) / chunks;
     if (b <= a) continue;
     float mc = 0.0f;
-    if (dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, a, b, xhi_h, xin_h, &mc)) rc |= 1;
+    if (Xr ? dmlp_cpu_prep_data_tiles_rows(Xr, N, A, mu, KT, a, b, xhi_h, xin_h, &mc)
+           : dmlp_cpu_prep_data_tiles(X, N, A, mu, KT, a, b, xhi_h, xin_h, &mc))
+      rc |= 1;
     m = mc > m ? mc : m;
     mark();
     h2d((char*)xhi_d + (a - t0) * 64 * W * 2, xhi_h + a * 64 * W, (b - a) * 64 * W * 2);
@@ -387,7 +390,9 @@ extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, i
   for (int c = 0; c < chunks; ++c) {
     const int64_t q0 = Q * c / chunks, q1 = Q * (c + 1) / chunks;
     if (q1 <= q0) continue;
-    if (dmlp_cpu_prep_queries(Qx + q0 * A, q1 - q0, A, mu, KT, qhi_h + q0 * W, qn_h + q0)) rc |= 2;
+    if (Qr ? dmlp_cpu_prep_queries_rows(Qr + q0, q1 - q0, A, mu, KT, qhi_h + q0 * W, qn_h + q0)
+           : dmlp_cpu_prep_queries(Qx + q0 * A, q1 - q0, A, mu, KT, qhi_h + q0 * W, qn_h + q0))
+      rc |= 2;
     mark();
     h2d((char*)qhi_d + q0 * W * 2, qhi_h + q0 * W, (q1 - q0) * W * 2);
     h2d((float*)qn_d + q0, qn_h + q0, (q1 - q0) * 4);
@@ -400,6 +405,25 @@ extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, i
     fprintf(stderr, "\n");
   }
   return rc;
+}
+
+extern "C" int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1,
+                                       const double* Qx, int64_t Q, int A, const double* mu,
+                                       int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
+                                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d,
+                                       void* xnm_d, void* qhi_d, void* qn_d, int chunks,
+                                       void* stream) {
+  return host_ops_h2d_tiles(X, nullptr, N, t0, t1, Qx, nullptr, Q, A, mu, KT, xhi_h, xin_h, xnm_h,
+                            qhi_h, qn_h, xhi_d, xin_d, xnm_d, qhi_d, qn_d, chunks, stream);
+}
+extern "C" int dmlp_host_ops_h2d_tiles_rows(const double* const* Xr, int64_t N, int64_t t0,
+                                            int64_t t1, const double* const* Qr, int64_t Q, int A,
+                                            const double* mu, int KT, uint16_t* xhi_h,
+                                            float* xin_h, unsigned* xnm_h, uint16_t* qhi_h,
+                                            float* qn_h, void* xhi_d, void* xin_d, void* xnm_d,
+                                            void* qhi_d, void* qn_d, int chunks, void* stream) {
+  return host_ops_h2d_tiles(nullptr, Xr, N, t0, t1, nullptr, Qr, Q, A, mu, KT, xhi_h, xin_h,
+                            xnm_h, qhi_h, qn_h, xhi_d, xin_d, xnm_d, qhi_d, qn_d, chunks, stream);
 }
 
 // Query parts of one pipelined local call: part p (rows [Q p / P, Q (p + 1) / P)) is rendered on
