@@ -605,6 +605,7 @@ class KnnCore {
     double* mu_h = (double*)hp;
     if (Xr) dmlp_cpu_center_rows(Xr, N_, A_, mu_h);
     else dmlp_cpu_center(X, N_, A_, mu_h);
+    trace.mark("center");
     short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
     float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
     short* xhi_c = shard ? fx_hic_.get(tpr * 64 * W) : xhi;
@@ -669,10 +670,12 @@ class KnnCore {
         }
         HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, side_));
       };
+      trace.mark("screen_queued");
       rows(X, Xr, N_, Xd, 0);
+      trace.mark("rows_x");
       rows(Qx, Qr, nq, Qd, qat);
       HIPCHK(hipEventRecord(ev_rows_, side_));
-      trace.mark("screen");
+      trace.mark("rows_q");
     };
     fo.dd = d_.get(nq * kmax_);
     fo.ii = ids_.get(nq * kmax_);

@@ -41,9 +41,10 @@ SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
 # the render (profiles/r2t_host_ops_chunks.txt: median 2.63 vs 2.74 and 3.03 vs 3.18 ms/step on two boxes)
 HOST_OPS_CHUNKS = int(os.environ.get("DMLP_HOST_OPS_CHUNKS", "2"))
 # query parts of the host-operand pipeline (knn_gpu_pipelined): each part's screen starts as soon
-# as its operands land, on its own stream, while the host renders the next part (1: one screen
-# after the whole query image)
-HOST_OPS_PARTS = int(os.environ.get("DMLP_HOST_OPS_PARTS", "4"))
+# as its operands land, on its own stream, while the host renders the next part.  1 (one screen
+# after the whole query image) is the default: 2 / 4 parts measured 2.76 / 4.29 ms against 2.58
+# (profiles/r4j_query_parts_ab.txt) — concurrent part screens cost more than the front they hide
+HOST_OPS_PARTS = int(os.environ.get("DMLP_HOST_OPS_PARTS", "1"))
 # fp64 rows of the host-operand pipeline cross PCIe as lossless int32 when every value is a
 # 6-decimal number (knn._issue_rows)
 ROWS_I32 = os.environ.get("DMLP_ROWS_I32", "1") != "0"
@@ -794,10 +795,12 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     # outside [1, 32] (3-term class, exact path) and escalations get device operands on need
     host_ops = (_host_ops and chunks == 1 and not exact and SCREEN_IMPL == "x1" and Q > 0 and N > 0
                 and L.dmlp_screen_x1_qw(KT) > 0)
-    # query parts (HOST_OPS_PARTS): a single local replica, every k on the x1 class
-    parts = (HOST_OPS_PARTS if host_ops and HOST_OPS_PARTS > 1 and gather is None
-             and k_range[0] >= 1 and k_range[1] <= min(SCREEN_KMAX_A, N)
-             and Q >= HOST_OPS_PARTS * 8192 else 1)
+    # every k on the x1 class and one local replica: the screen(s) are queued natively right
+    # behind the query operands and before the host packs the fp64 rows (_pipelined_parts),
+    # in HOST_OPS_PARTS query parts
+    split = (host_ops and gather is None and k_range[0] >= 1
+             and k_range[1] <= min(SCREEN_KMAX_A, N))
+    parts = max(1, HOST_OPS_PARTS) if split and Q >= HOST_OPS_PARTS * 8192 else 1
     dsops = prepped = mu_d = None
     if host_ops:
         src = np.ascontiguousarray((Xf if mu_rows is None else mu_rows)[:4096], np.float64)
@@ -827,32 +830,30 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             xnm = torch.empty(1, dtype=torch.int32, device=dev)
             qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
             qn = torch.empty(Q, dtype=torch.float32, device=dev)
-        # host conversion of each slice overlaps the PCIe copy of the previous one
         t_ops = t_ops0 = time.perf_counter()
-        rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data,
-                                       Q if parts == 1 else 0, A,
-                                       mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
-                                       _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
-                                       HOST_OPS_CHUNKS, copy.cuda_stream)
-        if parts > 1:
-            bad_d = None
-            if sh is not None:
-                # the image collectives, on every rank whatever its own verdict (the same
-                # sequence as the one-part path below)
-                with torch.cuda.stream(copy):
-                    sh[2](xhi.view(torch.int32), xhi_c.view(torch.int32))
-                    sh[2](xin, xin_c)
-                    sh[3](xnm)
-                    bad_d = (xnm >= 0x7f800000).to(torch.int32)
-                rc &= ~1  # the data verdict is the reduced one, on the device
-            if rc & 4:
-                raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
-            r = None
-            if rc == 0:
-                _mark("data_landed", copy)
-                r = _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host,
-                                     kstride, finalize, k_range, KT, mu_h, mu_d, hb, xhi, xin,
-                                     xnm, qhi, qn, copy, main, bad_d)
+        if split:
+            def render_data(bad):
+                """The dataset image (+ the sharded image's collectives) on `copy`."""
+                rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data, 0, A,
+                                               mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
+                                               _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
+                                               HOST_OPS_CHUNKS, copy.cuda_stream)
+                if sh is not None:
+                    # the image collectives, on every rank whatever its own verdict (the same
+                    # sequence as the path below)
+                    with torch.cuda.stream(copy):
+                        sh[2](xhi.view(torch.int32), xhi_c.view(torch.int32))
+                        sh[2](xin, xin_c)
+                        sh[3](xnm)
+                        bad.copy_((xnm >= 0x7f800000).to(torch.int32))
+                    rc &= ~1  # the data verdict is the reduced one, on the device
+                if rc & 4:
+                    raise RuntimeError("dmlp_host_ops_h2d: hipMemcpyAsync failed")
+                return rc
+
+            r = _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride,
+                                 finalize, k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn,
+                                 copy, main, render_data)
             if r is None:
                 # data or a query outside the screen's range: the device path decides (no
                 # collective on it; the pinned staging is reused only once its copies are done)
@@ -866,6 +867,11 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             _IO["h2d"] += (t1 - t0) * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
             return _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter,
                                    t_ops0, t_ops, True)
+        # host conversion of each slice overlaps the PCIe copy of the previous one
+        rc = L.dmlp_host_ops_h2d_tiles(Xc.ctypes.data, N, t0, t1, Qh.ctypes.data, Q, A,
+                                       mu_h.ctypes.data, KT, *[b.data_ptr() for b in hb],
+                                       _p(xhi_c), _p(xin_c), _p(xnm), _p(qhi), _p(qn),
+                                       HOST_OPS_CHUNKS, copy.cuda_stream)
         t_ops = time.perf_counter() - t_ops
         _IO["h2d"] += (t1 - t0) * 64 * (KT * 64 + 4) + 4 + Q * (KT * 64 + 4)
         if rc & 4:
@@ -949,11 +955,14 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
 
 def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride, finalize,
                      k_range, KT, mu_h, mu_d, hb, xhi, xin, xnm, qhi, qn, copy, main,
-                     bad=None):
-    """knn_gpu_pipelined's query-part front (the dataset image is queued on `copy`): part p's
-    calls are set up on their own stream, dmlp_host_ops_x1_parts renders each part and queues its
-    screen behind its copy, then the fp64 rows follow on `copy` and every part's refine waits for
-    them.  None when a query is outside the screen's range (the part streams are drained)."""
+                     render_data):
+    """knn_gpu_pipelined's front when every k is on the single-term class: the calls of the
+    query parts are set up first (their own streams), then render_data(bad) queues the dataset
+    image on `copy`, dmlp_host_ops_x1_parts renders each query part and queues its screen behind
+    its copy, and only then does the host pack the fp64 rows (lossless int32 when it can) — the
+    screens run meanwhile; every part's refine waits for the rows.  None when the data or a query
+    is outside the screen's range (the streams are drained).  One part is the default: 2 and 4
+    parts measured slower (profiles/r4j_query_parts_ab.txt)."""
     import ctypes
     torch = _torch()
     L = _lib.lib()
@@ -965,8 +974,7 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         X = torch.empty((N, A), dtype=torch.float64, device=dev)
         lab = (torch.empty(N, dtype=torch.int32, device=dev) if labels_host is not None else None)
         Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
-        if bad is None:  # (sharded image: the reduced verdict)
-            bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)  # (sharded: the reduced verdict)
     if lab is not None and finalize:
         lo, hi = label_range
         lab_ds = lab
@@ -1003,7 +1011,11 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
     if any(bf[3] != S for bf in bufs):
         raise RuntimeError("query parts disagree on the slice count")
     arr = lambda xs: (ctypes.c_void_p * parts)(*xs)
-    _mark("parts_start", copy)
+    if render_data(bad):
+        for ps in pss:
+            ps.synchronize()
+        return None
+    _mark("data_landed", copy)
     rc = L.dmlp_host_ops_x1_parts(
         Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT, hb[3].data_ptr(), hb[4].data_ptr(), _p(qhi),
         _p(qn), parts, copy.cuda_stream, arr([ps.cuda_stream for ps in pss]), _p(xhi), _p(xin),

@@ -97,7 +97,14 @@ for task in "$@"; do
         KNN_TRACE=1 timeout -k 10 120 /tmp/eng_dropin < /tmp/dropin_bench.in > /tmp/dropin.out \
             2> "$OUT/dropin_trace_$i.txt" || exit 1
       done
-      cat "$OUT/dropin_trace_3.txt" ;;
+      KNN_ROWS_I32=0 KNN_TRACE=1 timeout -k 10 120 /tmp/eng_dropin < /tmp/dropin_bench.in \
+          > /tmp/dropin.out 2> "$OUT/dropin_trace_fp64rows.txt" || exit 1
+      for i in 1 2; do  # the same input through knn_engine (row-major arrays, its own parser)
+        KNN_TRACE=1 timeout -k 10 120 distributed_machine_learning_project_amd/knn_engine \
+            --input /tmp/dropin_bench.in > /tmp/native.out 2> "$OUT/native_trace_$i.txt" || exit 1
+      done
+      cmp /tmp/dropin.out /tmp/native.out && echo "dropin == native report bytes"
+      tail -n 12 "$OUT/dropin_trace_3.txt" "$OUT/dropin_trace_fp64rows.txt" "$OUT/native_trace_2.txt" ;;
     parts)
       DMLP_HOST_OPS_PARTS=4 step parts_verify 300 python bench.py --steps 5 --warmup 1 --verify
       for P in 4 2 1; do
