@@ -538,7 +538,8 @@ class _KnnCall:
                 if n_esc:
                     self.cs_modified = True
                     self._screen_pass(esc, "stream" if self.stream_ok else "lds")
-                    n_ovf = self._ovf.read(self._ovf_slot, self.stream)
+                    # (the escalation ran on this stream, which may not be the launch stream)
+                    n_ovf = self._ovf.read(self._ovf_slot, torch.cuda.current_stream())
         fb = (np.empty(0, np.int64) if self.all_a
               else np.nonzero(~self.on_screen & (kk >= 1))[0])
         if n_ovf:
