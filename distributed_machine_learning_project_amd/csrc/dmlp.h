@@ -84,7 +84,7 @@ int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const double* mu,
                            const float* xinit, int64_t n_tiles, int64_t n_points, const int* qidx,
                            const int* const* kdev, int kmax, const unsigned* xnmax_bits,
                            const unsigned* bad, int S, int* const* cand_ids, int* const* cand_cnt,
-                           float* const* cand_h);
+                           float* const* cand_h, int chunks);
 // Same, the dataset part restricted to tiles [t0, t1) (device image pointers at tile t0's slot;
 // *xnm = +inf when the range is outside the screen's range): the per-rank shard of a sharded render.
 int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1, const double* Qx,

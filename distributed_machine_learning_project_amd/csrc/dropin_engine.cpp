@@ -19,6 +19,7 @@
 //     prints the DEBUG listing itself (common.cpp:72-78).
 #include <mpi.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <fstream>
@@ -126,18 +127,31 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
   in.k.resize(in.Q);
   xr.resize(in.N);
   qr.resize(in.Q);
-  for (int64_t i = 0; i < in.N; ++i) {
-    const DataPoint& d = dataset[i];
-    if ((int)d.attrs.size() != A) throw std::runtime_error("data point with wrong attribute count");
-    in.labels[i] = d.label;
-    xr[i] = d.attrs.data();
-  }
-  for (int64_t i = 0; i < in.Q; ++i) {
-    const Query& q = queries[i];
-    if ((int)q.attrs.size() != A) throw std::runtime_error("query with wrong attribute count");
-    in.k[i] = q.k;
-    qr[i] = q.attrs.data();
-  }
+  // a few threads (each row's header is a separate cache line of the harness's vectors)
+  const int64_t rows = in.N + in.Q;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(8, rows / 16384 + 1));
+  std::atomic<bool> bad{false};
+  auto work = [&](int t) {
+    const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
+    for (int64_t r = a; r < b; ++r) {
+      if (r < in.N) {
+        const DataPoint& d = dataset[r];
+        if ((int)d.attrs.size() != A) bad = true;
+        in.labels[r] = d.label;
+        xr[r] = d.attrs.data();
+      } else {
+        const Query& q = queries[r - in.N];
+        if ((int)q.attrs.size() != A) bad = true;
+        in.k[r - in.N] = q.k;
+        qr[r - in.N] = q.attrs.data();
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  if (bad) throw std::runtime_error("data point or query with wrong attribute count");
 }
 
 // The GPU report uses the query's index as its id; the harness numbers queries by index too

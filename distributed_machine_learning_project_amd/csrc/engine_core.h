@@ -15,6 +15,11 @@
 
 namespace dmlp_rt {
 
+// Page-locked host buffers (arena-backed) once a GPU runtime is up; every HostBuf<T> shares it.
+inline bool& host_bufs_pinned() {
+  static bool v = false;
+  return v;
+}
 
 // Host array that is page-locked when a GPU is in use (H2D/D2H then run as DMA at full PCIe
 // rate instead of through the runtime's pageable staging buffers).
@@ -23,7 +28,9 @@ struct HostBuf {
   T* p = nullptr;
   size_t n = 0;
   bool pinned = false;
-  static bool& use_pinned() { static bool v = false; return v; }
+  // one switch for every element type (a per-T static left the drop-in's byte / int staging
+  // pageable: synchronous staged copies)
+  static bool& use_pinned() { return host_bufs_pinned(); }
   HostBuf() = default;
   HostBuf(const HostBuf&) = delete;
   HostBuf& operator=(const HostBuf&) = delete;

@@ -93,8 +93,7 @@ int main(int argc, char** argv) {
   try {
     rt.init(strategy != "serial");
     // rank 0 parses straight into page-locked arrays (part of ingest, untimed)
-    HostBuf<double>::use_pinned() = rt.gpu;
-    HostBuf<char>::use_pinned() = rt.gpu;
+    HostBuf<double>::use_pinned() = rt.gpu;  // (every HostBuf<T>)
     Input in;
     if (rt.rank == 0) {
       in = parse(read_all(input));

@@ -394,15 +394,33 @@ struct LocalKnn {
     const void* qhi = nullptr;
     const float* qn = nullptr;
   };
+  // grow-only page-locked ints (arena-backed while the arena has room)
+  struct PinnedInts {
+    int* p = nullptr;
+    size_t n = 0;
+    int* get(int64_t m) {
+      if ((size_t)m > n) {
+        if (p && !host_arena().owns(p)) (void)hipHostFree(p);
+        const size_t want = std::max<size_t>((size_t)m, 1024);
+        p = (int*)host_arena().take(want * sizeof(int));
+        if (!p && hipHostMalloc((void**)&p, want * sizeof(int), hipHostMallocDefault) != hipSuccess)
+          throw std::runtime_error("page-locked allocation failed");
+        n = want;
+      }
+      return p;
+    }
+    ~PinnedInts() {
+      if (p && !host_arena().owns(p)) (void)hipHostFree(p);
+    }
+  } kk_h_, ident_h_;
   DevBuf<int> ident_, ovf_;
   int64_t ident_len_ = 0;
-  std::vector<int> ident_h_;
   int* identity(int64_t n) {  // device 0, 1, ..., n-1 (grow-only)
     int* p = ident_.get(std::max<int64_t>(n, 1));
     if (ident_len_ < n) {
-      ident_h_.resize(n);
-      for (int64_t i = 0; i < n; ++i) ident_h_[i] = (int)i;
-      HIPCHK(hipMemcpyAsync(p, ident_h_.data(), n * sizeof(int), hipMemcpyHostToDevice, st));
+      int* h = ident_h_.get(n);
+      for (int64_t i = 0; i < n; ++i) h[i] = (int)i;
+      HIPCHK(hipMemcpyAsync(p, h, n * sizeof(int), hipMemcpyHostToDevice, st));
       ident_len_ = n;
     }
     return p;
@@ -427,15 +445,21 @@ struct LocalKnn {
     auto launch_rows = [&]() {
       if (!rows_issued) { issue_rows(); rows_issued = true; }
     };
-    std::vector<int> kk(Q), a, b, c, f, rest;
-    bool all_a = true;
-    for (int64_t q = 0; q < Q; ++q) kk[q] = (int)std::min<int64_t>(k_host[q], N);
+    std::vector<int> a, b, c, f, rest;
+    // page-locked k (a pageable source would make the copy wait for the stream)
+    int* kk = kk_h_.get(Q);
     // A <= 128: every screen; A <= 256: the single-term screen alone (k <= 32), the 3-term
     // kernels' classes and escalations take the exact path
     const bool lds_ok = KT <= 4;
     const bool x1_ok = dmlp_screen_x1_qw(KT) > 0;
     const bool screen = (lds_ok || x1_ok) && N > 0;
+    // the common case (every k in [1, 32], k <= N, on the x1 class) needs no per-class lists
+    bool all_a = screen && (x1_ok || !hx);
     for (int64_t q = 0; q < Q; ++q) {
+      kk[q] = (int)std::min<int64_t>(k_host[q], N);
+      all_a = all_a && k_host[q] >= 1 && k_host[q] <= 32 && k_host[q] <= N;
+    }
+    for (int64_t q = 0; q < Q && !all_a; ++q) {
       if (kk[q] < 1) { rest.push_back((int)q); all_a = false; continue; }
       if (screen && kk[q] <= 32 && (x1_ok || !hx)) a.push_back((int)q);
       else if (screen && lds_ok && kk[q] <= 128) { b.push_back((int)q); all_a = false; }
@@ -463,7 +487,7 @@ struct LocalKnn {
       }
     };
     int* kd = kdev.get(Q);
-    HIPCHK(hipMemcpyAsync(kd, kk.data(), Q * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(kd, kk, Q * sizeof(int), hipMemcpyHostToDevice, st));
     int* stat = status.get(Q);
     const bool fin = labels != nullptr;
     // (the x1 refine writes every row's padding and status itself; the other paths need fills)
@@ -481,7 +505,7 @@ struct LocalKnn {
     // once, before any kernel writes results: every refine writes its queries' padding and
     // status itself, so the fill is only needed for rows no refine covers (exact path, k < 1)
     if (!all_a || !hx) fill();
-    if (!a.empty() || !b.empty() || !c.empty()) {
+    if (all_a || !a.empty() || !b.empty() || !c.empty()) {
       const float er = eps_rel(A);
       const int64_t nt = (N + 63) / 64;
       const int qw = dmlp_screen_stream_qw(KT);
@@ -540,7 +564,7 @@ struct LocalKnn {
       };
       if (!hx) need_dev();  // the device operands of every screen
       const int first_a = use_x1 ? 0 : (qw > 0 ? 1 : 2);
-      if (!a.empty()) pass(all_a ? nullptr : &a, first_a, qidx_a);
+      if (all_a || !a.empty()) pass(all_a ? nullptr : &a, first_a, qidx_a);
       if (!b.empty()) pass(&b, 2, qidx_b);
       if (!c.empty()) pass(&c, 2, qidx_c);
       // one host sync: the overflow count (4 bytes); the per-query status only when some
@@ -553,9 +577,13 @@ struct LocalKnn {
         HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
         wait();
         std::vector<int> esc;
-        if (first_a == 0)
+        if (first_a == 0 && all_a) {
+          for (int64_t q = 0; q < Q; ++q)
+            if (sh[q]) esc.push_back((int)q);
+        } else if (first_a == 0) {
           for (int q : a)
             if (sh[q]) esc.push_back(q);
+        }
         if (!esc.empty() && (qw > 0 || lds_ok)) {
           // single-term overflow (data too tight for its bound): those queries alone go to the
           // 3-term screen

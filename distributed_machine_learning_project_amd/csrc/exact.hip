@@ -17,14 +17,16 @@
 #include "dmlp.h"
 #include "dmlp_device.h"
 #include <math.h>
+#include <stdlib.h>
 
 namespace {
 
 // QB queries per workgroup (RI = QB / 16 rows per thread), PJ points per thread per tile
 // (tile = 16 PJ points), CB candidate slots per query, AC attributes per LDS chunk.
-template <int QB_, int PJ_, int CB_, int AC_>
+template <int QB_, int PJ_, int CB_, int AC_, int WPE_ = 2>
 struct Ex {
   static constexpr int QB = QB_, PJ = PJ_, PT = 16 * PJ_, CB = CB_, AC = AC_;
+  static constexpr int WPE = WPE_;    // waves per SIMD the kernel is compiled for
   static constexpr int AS = AC + 2;   // LDS row stride in doubles: 16-byte aligned rows (b128)
   static constexpr int RI = QB / 16;  // rows (queries) per thread
   static constexpr int EPL = (CB + 63) / 64;  // buffer entries per lane in a compaction
@@ -34,6 +36,10 @@ struct Ex {
   static constexpr int LDS = STG + BUF;
 };
 using ExK16 = Ex<64, 8, 48, 16>;    // k <= 16: 2 workgroups per CU
+// A/B (DMLP_EXACT_VARIANT=1): a 4x4 micro-tile and 32-slot buffers — 43 KiB of LDS and <= 168
+// VGPRs, so 3 workgroups (3 waves per SIMD) hide the LDS / barrier latency the 2-wave 4x8 tile
+// waits on (profiles/r4j: 33 % of wave cycles waiting), at 1.5x the LDS reads per fp64 op
+using ExK16w3 = Ex<64, 4, 32, 16, 3>;
 using ExK32 = Ex<64, 8, 64, 16>;
 using ExK64 = Ex<64, 8, 128, 16>;
 using ExK256 = Ex<16, 16, 384, 8>;  // k <= 256: 16 queries per workgroup, 384-slot buffers
@@ -102,7 +108,7 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
 }
 
 template <class C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_exact_topk(const double* __restrict__ X, int64_t N, int A,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C::WPE))) void k_exact_topk(const double* __restrict__ X, int64_t N, int A,
                                                     const double* __restrict__ Qx,
                                                     const int* __restrict__ qidx,
                                                     const int* __restrict__ qk, int nb,
@@ -268,6 +274,10 @@ extern "C" int dmlp_exact_topk(const double* X, int64_t N, int A, const double* 
   if (nb <= 0 || N <= 0) return 0;
   if (N > 0x7fffffff || A < 1 || kmax > 256) return -1;
   hipStream_t st = (hipStream_t)stream;
+  const char* ev = getenv("DMLP_EXACT_VARIANT");
+  const int variant = ev ? atoi(ev) : 0;
+  if (kmax <= 16 && variant == 1)
+    return launch_exact<ExK16w3>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 16) return launch_exact<ExK16>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 32) return launch_exact<ExK32>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 64) return launch_exact<ExK64>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);

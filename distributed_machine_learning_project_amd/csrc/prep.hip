@@ -443,7 +443,7 @@ extern "C" int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const 
                                       const int* qidx, const int* const* kdev, int kmax,
                                       const unsigned* xnmax_bits, const unsigned* bad, int S,
                                       int* const* cand_ids, int* const* cand_cnt,
-                                      float* const* cand_h) {
+                                      float* const* cand_h, int chunks) {
   static std::vector<hipEvent_t> evs;  // one per part, re-recorded every call
   while ((int)evs.size() < parts) {
     hipEvent_t e;
@@ -452,17 +452,23 @@ extern "C" int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const 
   }
   hipStream_t cs = (hipStream_t)copy;
   const int64_t W = (int64_t)KT * 32;
+  chunks = chunks < 1 ? 1 : chunks;
   for (int p = 0; p < parts; ++p) {
     const int64_t q0 = Q * p / parts, q1 = Q * (p + 1) / parts;
     if (q1 <= q0) continue;
-    if (dmlp_cpu_prep_queries(Qx + q0 * A, q1 - q0, A, mu, KT, qhi_h + q0 * W, qn_h + q0))
-      return 2;
+    // the part in `chunks` slices: each slice's copy overlaps the render of the next
+    for (int c = 0; c < chunks; ++c) {
+      const int64_t a = q0 + (q1 - q0) * c / chunks, b = q0 + (q1 - q0) * (c + 1) / chunks;
+      if (b <= a) continue;
+      if (dmlp_cpu_prep_queries(Qx + a * A, b - a, A, mu, KT, qhi_h + a * W, qn_h + a)) return 2;
+      if (hipMemcpyAsync((char*)qhi_d + a * W * 2, qhi_h + a * W, (size_t)((b - a) * W * 2),
+                         hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipMemcpyAsync((float*)qn_d + a, qn_h + a, (size_t)((b - a) * 4),
+                         hipMemcpyHostToDevice, cs) != hipSuccess)
+        return 4;
+    }
     hipStream_t ps = (hipStream_t)part_streams[p];
-    if (hipMemcpyAsync((char*)qhi_d + q0 * W * 2, qhi_h + q0 * W, (size_t)((q1 - q0) * W * 2),
-                       hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipMemcpyAsync((float*)qn_d + q0, qn_h + q0, (size_t)((q1 - q0) * 4),
-                       hipMemcpyHostToDevice, cs) != hipSuccess ||
-        hipEventRecord(evs[p], cs) != hipSuccess || hipStreamWaitEvent(ps, evs[p], 0) != hipSuccess)
+    if (hipEventRecord(evs[p], cs) != hipSuccess || hipStreamWaitEvent(ps, evs[p], 0) != hipSuccess)
       return 4;
     if (dmlp_screen_x1(KT, 1, A, xfrag, xinit, n_tiles, n_points, (const char*)qhi_d + q0 * W * 2,
                        (const float*)qn_d + q0, qidx, kdev[p], (int)(q1 - q0), kmax, xnmax_bits,

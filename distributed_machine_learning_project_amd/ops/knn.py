@@ -1022,7 +1022,7 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         _p(qn), parts, copy.cuda_stream, arr([ps.cuda_stream for ps in pss]), _p(xhi), _p(xin),
         ds.n_tiles, N, _p(qidx), arr([c.k_dev.data_ptr() for c in calls]), k_range[1], _p(xnm),
         _p(bad), S, arr([bf[0].data_ptr() for bf in bufs]), arr([bf[1].data_ptr() for bf in bufs]),
-        arr([bf[2].data_ptr() for bf in bufs]))
+        arr([bf[2].data_ptr() for bf in bufs]), HOST_OPS_CHUNKS)
     if rc & 4:
         raise RuntimeError("dmlp_host_ops_x1_parts: copy or launch failed")
     if rc:

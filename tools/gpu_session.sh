@@ -13,6 +13,7 @@
 #   timeline   rocprofv3 kernel + memory-copy trace of the last steps (tools/timeline.py)
 #   pmc        one --pmc pass per counter group over the screen + refine (tools/pmc_summary.py)
 #   exactprof  the fused exact kernel (bench.py --exact): kernel split + one PMC pass
+#   exactab    fused exact kernel variants A/B (bench.py --exact, DMLP_EXACT_VARIANT 0 / 1)
 #   engine     native knn_engine: every strategy vs the CPU oracle bytes (tools/engine_check.sh)
 #   sweep      bench sweep over N / A / k (profiles/ sweep table)
 #   exact      bench.py --exact (fp64-only path)
@@ -81,6 +82,12 @@ for task in "$@"; do
           -d "$OUT/pmc_exact" -o run --output-format csv \
           -- python3 bench.py --exact --steps 1 --warmup 1 --no-busbw --diag-steps 0
       python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
+    exactab)  # fused exact kernel variants (DMLP_EXACT_VARIANT), --verify on the A/B arm
+      for V in 0 1 0 1; do
+        DMLP_EXACT_VARIANT=$V step exact_v$V 300 python bench.py --exact --steps 3 --warmup 1 --no-busbw
+      done
+      DMLP_EXACT_VARIANT=1 step exact_v1_verify 300 python bench.py --exact --steps 2 --warmup 1 \
+          --no-busbw --verify ;;
     engine)
       step engine 400 bash tools/engine_check.sh "$OUT/engine" ;;
     sweep)
