@@ -37,6 +37,8 @@ int dmlp_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int 
 // mu over the first min(N, 4096) rows like dmlp_center; qhi [Q][KT*32] fp16 bits, qn [Q] fp32.
 // dmlp_cpu_prep_queries returns 1 if some |q - mu| is outside the screen's range.
 int dmlp_host_threads(void);
+// fn(ctx, part, parts) on the render pool's workers and the caller (host_prep.cpp)
+void dmlp_host_pool_run(void (*fn)(void*, int, int), void* ctx);
 void dmlp_cpu_center(const double* X, int64_t N, int A, double* mu);
 int dmlp_cpu_prep_queries(const double* Qx, int64_t Q, int A, const double* mu, int KT,
                           uint16_t* qhi, float* qn);

@@ -127,11 +127,10 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
   in.k.resize(in.Q);
   xr.resize(in.N);
   qr.resize(in.Q);
-  // a few threads (each row's header is a separate cache line of the harness's vectors)
+  // on the render pool (warm workers, no thread start per call)
   const int64_t rows = in.N + in.Q;
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(8, rows / 16384 + 1));
   std::atomic<bool> bad{false};
-  auto work = [&](int t) {
+  auto work = [&](int t, int nt) {
     const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
     for (int64_t r = a; r < b; ++r) {
       if (r < in.N) {
@@ -147,10 +146,8 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
       }
     }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
+  using Work = decltype(work);
+  dmlp_host_pool_run([](void* c, int t, int nt) { (*(Work*)c)(t, nt); }, &work);
   if (bad) throw std::runtime_error("data point or query with wrong attribute count");
 }
 

@@ -36,10 +36,9 @@ struct Ex {
   static constexpr int LDS = STG + BUF;
 };
 using ExK16 = Ex<64, 8, 48, 16>;    // k <= 16: 2 workgroups per CU
-// A/B (DMLP_EXACT_VARIANT=1): a 4x4 micro-tile and 32-slot buffers — 43 KiB of LDS and <= 168
-// VGPRs, so 3 workgroups (3 waves per SIMD) hide the LDS / barrier latency the 2-wave 4x8 tile
-// waits on (profiles/r4j: 33 % of wave cycles waiting), at 1.5x the LDS reads per fp64 op
-using ExK16w3 = Ex<64, 4, 32, 16, 3>;
+// (measured and dropped: a 4x4 micro-tile with 32-slot buffers at 3 waves per SIMD — 73.5 ms
+// against 54.1 ms, profiles/r4l_exact_variants.txt: the extra LDS reads per fp64 op cost more
+// than the occupancy hides)
 using ExK32 = Ex<64, 8, 64, 16>;
 using ExK64 = Ex<64, 8, 128, 16>;
 using ExK256 = Ex<16, 16, 384, 8>;  // k <= 256: 16 queries per workgroup, 384-slot buffers
@@ -274,10 +273,6 @@ extern "C" int dmlp_exact_topk(const double* X, int64_t N, int A, const double* 
   if (nb <= 0 || N <= 0) return 0;
   if (N > 0x7fffffff || A < 1 || kmax > 256) return -1;
   hipStream_t st = (hipStream_t)stream;
-  const char* ev = getenv("DMLP_EXACT_VARIANT");
-  const int variant = ev ? atoi(ev) : 0;
-  if (kmax <= 16 && variant == 1)
-    return launch_exact<ExK16w3>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 16) return launch_exact<ExK16>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 32) return launch_exact<ExK32>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
   if (kmax <= 64) return launch_exact<ExK64>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);

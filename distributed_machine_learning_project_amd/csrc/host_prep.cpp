@@ -202,6 +202,14 @@ inline uint16_t f16_rn(float f) {
 
 extern "C" int dmlp_host_threads(void) { return pool().size(); }
 
+// fn(ctx, part, parts) on every worker of the render pool and the caller (parts = the pool's
+// size); returns when all parts are done.  For host passes of other modules (the drop-in's
+// index of the harness's vectors) that should not pay a thread start each.
+extern "C" void dmlp_host_pool_run(void (*fn)(void*, int, int), void* ctx) {
+  std::function<void(int, int)> job = [&](int part, int parts) { fn(ctx, part, parts); };
+  pool().run(job);
+}
+
 namespace {
 
 // Row sources: a row-major block, or a table of row pointers (the engine.h drop-in reads the

@@ -145,14 +145,12 @@ def test_exact_mode(torch_cuda):
     (700, 33, 3, 200, 256, 0, 2),          # heavy exact ties (3 attrs in {0, 1, 2}); k near N/3
     (300, 20, 16, 250, 256, 0, 1000),      # k close to N
 ])
-@pytest.mark.parametrize("variant", ["0", "1"])
-def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, variant, monkeypatch):
+def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, monkeypatch):
     """exact.hip (the --exact path and the fallback for k <= 256) == the CPU path, bit for bit:
-    every variant (DMLP_EXACT_VARIANT=1: the 3-wave 4x4 tile for k <= 16), ties broken by larger
-    id, per-query k mixed within a workgroup.  Forced for every k (DMLP_EXACT_FUSED=2): at these
-    small N the dispatch would pick rows + select for k > 64."""
+    every variant, ties broken by larger id, per-query k mixed within a workgroup.  Forced for
+    every k (DMLP_EXACT_FUSED=2): at these small N the dispatch would pick rows + select for
+    k > 64."""
     monkeypatch.setenv("DMLP_EXACT_FUSED", "2")
-    monkeypatch.setenv("DMLP_EXACT_VARIANT", variant)
     inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 5, seed=N + A)
     r, refs = run_both(torch_cuda, inp, exact=True)
     assert_same(r, refs)

@@ -13,9 +13,9 @@
 #   timeline   rocprofv3 kernel + memory-copy trace of the last steps (tools/timeline.py)
 #   pmc        one --pmc pass per counter group over the screen + refine (tools/pmc_summary.py)
 #   exactprof  the fused exact kernel (bench.py --exact): kernel split + one PMC pass
-#   exactab    fused exact kernel variants A/B (bench.py --exact, DMLP_EXACT_VARIANT 0 / 1)
 #   engine     native knn_engine: every strategy vs the CPU oracle bytes (tools/engine_check.sh)
 #   sweep      bench sweep over N / A / k (profiles/ sweep table)
+#   sweepa     the sweep at N 1e5 / 1e6 with A 32 / 128 / 256
 #   exact      bench.py --exact (fp64-only path)
 #   harness    bench.py --harness native (knn_engine through the reference contract)
 #   dropin     bench.py --harness dropin (engine.h drop-in linked with the reference's common.cpp)
@@ -82,16 +82,13 @@ for task in "$@"; do
           -d "$OUT/pmc_exact" -o run --output-format csv \
           -- python3 bench.py --exact --steps 1 --warmup 1 --no-busbw --diag-steps 0
       python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
-    exactab)  # fused exact kernel variants (DMLP_EXACT_VARIANT), --verify on the A/B arm
-      for V in 0 1 0 1; do
-        DMLP_EXACT_VARIANT=$V step exact_v$V 300 python bench.py --exact --steps 3 --warmup 1 --no-busbw
-      done
-      DMLP_EXACT_VARIANT=1 step exact_v1_verify 300 python bench.py --exact --steps 2 --warmup 1 \
-          --no-busbw --verify ;;
     engine)
       step engine 400 bash tools/engine_check.sh "$OUT/engine" ;;
     sweep)
       step sweep 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep.jsonl" --timeout 170 ;;
+    sweepa)  # N 1e5 / 1e6 x A 32 / 128 / 256 x k 16 / 1-64 / 200
+      step sweepa 1100 python3 -u tools/bench_sweep.py --out "$OUT/sweep.jsonl" --timeout 150 \
+          --ns 100000,1000000 --attrs 32,128,256 ;;
     harness)
       step harness 600 python bench.py --harness native ;;
     dropin)
