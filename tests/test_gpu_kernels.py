@@ -77,7 +77,8 @@ def test_select_and_sort_fallback_paths(torch_cuda):
     k = np.concatenate([rng.integers(129, 2049, 40), rng.integers(2049, 6001, 20)]).astype(np.int32)
     inp = dmlp.KNNInput(labels, np.ascontiguousarray(X), k, Qx)
     r, refs = run_both(torch_cuda, inp)
-    assert r.n_fallback == 60
+    # k in (128, 256] is screened (cap-512 LDS screen); every larger k takes the exact path
+    assert r.n_fallback == int((k > K.SCREEN_KMAX_C).sum())
     assert_same(r, refs)
 
 
