@@ -196,9 +196,11 @@ def stage_reference_harness() -> Path | None:
     REF_STAGE.mkdir(parents=True, exist_ok=True)
     for f in ("common.cpp", "common.h", "engine.h"):
         if (REF_HARNESS / f).exists():
-            if (REF_STAGE / f).exists():
-                (REF_STAGE / f).unlink()
-            shutil.copyfile(REF_HARNESS / f, REF_STAGE / f)
+            # copy + atomic rename: concurrent builders (pytest -n workers) never see a
+            # half-written or missing file
+            tmp = REF_STAGE / f"{f}.{os.getpid()}.tmp"
+            shutil.copyfile(REF_HARNESS / f, tmp)
+            os.replace(tmp, REF_STAGE / f)
     return REF_STAGE / "common.cpp"
 
 
