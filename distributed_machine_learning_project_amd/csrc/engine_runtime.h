@@ -448,9 +448,9 @@ struct LocalKnn {
     std::vector<int> a, b, c, f, rest;
     // page-locked k (a pageable source would make the copy wait for the stream)
     int* kk = kk_h_.get(Q);
-    // A <= 128: every screen; A <= 256: the single-term screen alone (k <= 32), the 3-term
-    // kernels' classes and escalations take the exact path
-    const bool lds_ok = KT <= 4;
+    // A <= 256 (KT <= 8): every class on a screen (the LDS 3-term screen streams KT = 8 tiles
+    // as two 32 KiB stages); wider rows take the exact path
+    const bool lds_ok = KT <= 8;
     const bool x1_ok = dmlp_screen_x1_qw(KT) > 0;
     const bool screen = (lds_ok || x1_ok) && N > 0;
     // the common case (every k in [1, 32], k <= N, on the x1 class) needs no per-class lists

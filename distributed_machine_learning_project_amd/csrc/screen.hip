@@ -16,7 +16,9 @@
 // Geometry (gfx950): one workgroup = WAVES waves, each wave owns 16 queries (one MFMA column
 // tile) for the whole stream; query bf16 fragments live in VGPRs.  The data slice streams
 // through a 2-deep LDS ring of 64-point tiles (lane-linear 1 KiB fragments laid out by
-// prep.hip).  Staging goes through registers (global_load_dwordx4 issued one step ahead,
+// prep.hip); a tile wider than KT = 4 (A in (128, 256]) streams as NST = KT / 4 stages of four
+// 32-attribute fragments each (32 KiB + the norm row), the accumulators carried across a tile's
+// stages and the epilogue run after its last one, so the ring stays 2 x 32 KiB.  Staging goes through registers (global_load_dwordx4 issued one step ahead,
 // ds_write_b128 after the barrier): no LDS-DMA is ever in flight, so hipcc never has to drain
 // vmcnt in front of the candidate-buffer LDS traffic.  Candidate buffers ({score, id} x CAP per
 // query) live in LDS; append offsets come from in-register per-column counts and a 4-lane
@@ -45,13 +47,17 @@ __device__ unsigned long long g_screen_dbg[8];
 
 template <int KT, int WAVES, int CAP>
 struct ScreenCfg {
-  static constexpr int FRAGS = 4 * KT * 2;  // 1 KiB fragments per tile
+  static constexpr int KTS = KT > 4 ? 4 : KT;  // 32-attribute fragments per LDS stage
+  static constexpr int NST = KT / KTS;         // stages per 64-point tile
+  static constexpr int TILE_FRAGS = 4 * KT * 2;  // 1 KiB fragments per tile of the image
+  static constexpr int FRAGS = 4 * KTS * 2;    // 1 KiB fragments per stage
   static constexpr int TILE_BYTES = FRAGS * 1024 + 256;
   static constexpr int G = FRAGS / WAVES;   // staged 16-B vectors per lane per tile
   static constexpr int D = G <= 2 ? 4 : (G <= 4 ? 3 : 2);  // register-ring depth (tiles)
   static constexpr int SUB = CAP / 4;      // per-lane sub-buffer entries
   static constexpr int LDS = 2 * TILE_BYTES + WAVES * 64 * (SUB + 1) * 8;
   static_assert(FRAGS % WAVES == 0, "fragments must split evenly over waves");
+  static_assert(KT % KTS == 0 && D % NST == 0, "a tile's stages must map to fixed ring slots");
   static_assert(LDS <= 163840, "LDS budget");
   static_assert(CAP % 64 == 0, "CAP multiple of 64");
 };
@@ -66,6 +72,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
     int* __restrict__ cand_cnt) {
   using C = ScreenCfg<KT, WAVES, CAP>;
   constexpr int E = CAP / 64;
+  constexpr int KTS = C::KTS, NST = C::NST;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const tiles = smem;
   i32x2* const bufs = (i32x2*)(smem + 2 * C::TILE_BYTES);
@@ -92,6 +99,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   int t1 = t0 + tiles_per_slice;
   if (t1 > n_tiles) t1 = n_tiles;
   const int nt = t1 > t0 ? t1 - t0 : 0;
+  const int nst = nt * NST;  // LDS stages of the slice
 
   // ---- this lane's query (column)
   const int pbase = (qb * WAVES + wave) * 16;
@@ -115,21 +123,26 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   int cnt = 0;  // entries in this lane's own sub-buffer (negative: column overflowed)
   i32x2* const wbuf = bufs + wave * 64 * (SUB + 1);
 
-  // ---- D-deep register ring for the tile stream: tile j lives in register set j % D, so D-1
-  // tiles are in flight while one is consumed (the stream is latency-bound otherwise).
+  // ---- D-deep register ring for the stage stream: stage j lives in register set j % D, so D-1
+  // stages are in flight while one is consumed (the stream is latency-bound otherwise).
   // Macros, not lambdas, and native vector types: HIP's uint4 (a union struct) and captured
   // arrays both defeat SROA and end up in scratch.
   constexpr int D = C::D;
   u32x4 stg[D][C::G];
   float stx[D];
-  // Loads are issued unconditionally (tile index clamped, every wave fetches the 256-B xinit
-  // row) so the vmcnt bookkeeping is path-independent and hipcc emits counted waits.
+  // Loads are issued unconditionally (stage index clamped, every wave fetches the 256-B xinit
+  // row) so the vmcnt bookkeeping is path-independent and hipcc emits counted waits.  Stage
+  // fragment f = (rt * KTS + ktl) * 2 + hilo is image fragment (rt * KT + h * KTS + ktl) * 2 + hilo
+  // of its tile (h: the stage within the tile; the identity when NST = 1).
 #define DMLP_LOAD_TILE(I, R)                                                      \
   do {                                                                            \
-    const int t_ = t0 + ((I) < nt ? (I) : nt - 1);                                \
-    const u32x4* src_ = xfrag + (int64_t)t_ * (C::FRAGS * 64);                    \
-    _Pragma("unroll") for (int g = 0; g < C::G; ++g) stg[R][g] =                  \
-        src_[(wave + g * WAVES) * 64 + lane];                                     \
+    const int i_ = (I) < nst ? (I) : nst - 1;                                     \
+    const int t_ = t0 + i_ / NST, h_ = i_ % NST;                                  \
+    const u32x4* src_ = xfrag + (int64_t)t_ * (C::TILE_FRAGS * 64);               \
+    _Pragma("unroll") for (int g = 0; g < C::G; ++g) {                            \
+      const int f_ = wave + g * WAVES, rt_ = f_ / (2 * KTS);                      \
+      stg[R][g] = src_[((rt_ * KT + h_ * KTS) * 2 + f_ - rt_ * 2 * KTS) * 64 + lane]; \
+    }                                                                             \
     stx[R] = xinit[(int64_t)t_ * 64 + lane];                                      \
   } while (0)
 #define DMLP_STORE_TILE(I, R)                                                     \
@@ -210,18 +223,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   };
 
   // ---- prologue
-  if (nt > 0) {
+  f32x4 acc[4];  // carried across the stages of a tile
+  if (nst > 0) {
     DMLP_LOAD_TILE(0, 0);
     DMLP_STORE_TILE(0, 0);
 #pragma unroll
     for (int r = 1; r < D; ++r) DMLP_LOAD_TILE(r, r);
   }
 
-  for (int i0 = 0; i0 < nt; i0 += D) {
+  for (int i0 = 0; i0 < nst; i0 += D) {
 #pragma unroll
   for (int r = 0; r < D; ++r) {
     const int i = i0 + r;
-    if (i >= nt) break;
+    if (i >= nst) break;
+    const int hs = r % NST;  // stage within the tile (i0 is a multiple of D, D of NST)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -231,30 +246,31 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
     if (!(mode & 4)) DMLP_LOAD_TILE(i + D, r);
 
     const char* tb = tiles + (i & 1) * C::TILE_BYTES;
-    f32x4 acc[4];
-    bf16x8 ah[4][KT], al[4][KT];
+    bf16x8 ah[4][KTS], al[4][KTS];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) {
-      acc[rt] = *(const f32x4*)(tb + C::FRAGS * 1024 + rt * 64 + kg * 16);
+      if (hs == 0) acc[rt] = *(const f32x4*)(tb + C::FRAGS * 1024 + rt * 64 + kg * 16);
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        ah[rt][kt] = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 0) * 1024 + lane * 16);
-        al[rt][kt] = *(const bf16x8*)(tb + ((rt * KT + kt) * 2 + 1) * 1024 + lane * 16);
+      for (int kt = 0; kt < KTS; ++kt) {
+        ah[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * 2 + 0) * 1024 + lane * 16);
+        al[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * 2 + 1) * 1024 + lane * 16);
       }
     }
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
+    for (int kt = 0; kt < KTS; ++kt) {
       if (mode & 2) break;  // ablation: no matrix work
+      const bf16x8 qh = bh[hs * KTS + kt], ql = bl[hs * KTS + kt];
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], bh[kt], acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], qh, acc[rt], 0, 0, 0);
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], bl[kt], acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], ql, acc[rt], 0, 0, 0);
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt][kt], bh[kt], acc[rt], 0, 0, 0);
+        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt][kt], qh, acc[rt], 0, 0, 0);
     }
+    if (hs == NST - 1) {  // a whole tile accumulated: the epilogue
     float mr[4];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt)
@@ -274,7 +290,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
       }
       // candidate path: append this lane's passing (score, id) pairs to its own sub-buffer
       i32x2* mys = sub_ptr(c, kg);
-      const int idbase = (t0 + i) * 64 + kg * 4;
+      const int idbase = (t0 + i / NST) * 64 + kg * 4;
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt) {
         if (__ballot(mr[rt] >= h)) {
@@ -295,8 +311,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
         compact(cc);
       }
     }
-    if (!(mode & 4)) DMLP_STORE_TILE(i + 1, (r + 1) % D);  // past the end: idle buffer
     if (mode & 1) asm volatile("" ::"v"(mx));  // keep the epilogue alive in ablations
+    }  // epilogue
+    if (!(mode & 4)) DMLP_STORE_TILE(i + 1, (r + 1) % D);  // past the end: idle buffer
   }
   }
 #undef DMLP_LOAD_TILE
@@ -356,11 +373,13 @@ int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const 
 
 }  // namespace
 
-// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*KT + 256) + WAVES*16*CAP*8 <= 160 KiB.  CAP = 512 serves
+// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*min(KT, 4) + 256) + WAVES*16*CAP*8 <= 160 KiB (KT = 8:
+// two 32 KiB stages per tile).  CAP = 512 serves
 // 128 < k <= 256 (a column compacts to >= k entries and refills 448 - k before the next batch).
 #define DMLP_SCREEN_CONFIGS(X)                                                                \
   X(1, 128, 8) X(2, 128, 4) X(3, 128, 4) X(4, 128, 4) X(1, 256, 4) X(2, 256, 2) X(3, 256, 2) \
-  X(4, 256, 2) X(1, 512, 2) X(2, 512, 1) X(3, 512, 1) X(4, 512, 1)
+  X(4, 256, 2) X(1, 512, 2) X(2, 512, 1) X(3, 512, 1) X(4, 512, 1) X(8, 128, 4) X(8, 256, 2) \
+  X(8, 512, 1)
 
 extern "C" int dmlp_screen_kmax(int cap) {
   return cap == 128 ? 32 : (cap == 256 ? 128 : (cap == 512 ? 256 : 0));

@@ -30,8 +30,8 @@ from .. import _lib
 SCREEN_KMAX_A = 32      # cap 128 class
 SCREEN_KMAX_B = 128     # cap 256 class
 SCREEN_KMAX_C = 256     # cap 512 class
-SCREEN_MAX_KT = 8       # A <= 256 on the screen path (the single-term screen; the 3-term
-LDS_MAX_KT = 4          # kernels serve A <= 128: beyond, their classes take the exact path)
+SCREEN_MAX_KT = 8       # A <= 256 on the screen path: the single-term screen and the LDS 3-term
+LDS_MAX_KT = 8          # screen (KT = 8 tiles stream through LDS as two 32 KiB stages)
 NUM_CUS = 256
 # "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
 SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
@@ -333,7 +333,7 @@ class _KnnCall:
         L = _lib.lib()
         _apply_env_switches(L)
         ds, kk, Q, A = self.ds, self.kk, self.Q, self.A
-        # A > 128: only the single-term screen serves the dataset (its classes: k <= 32)
+        # A <= 256 (KT <= 8): every class on a screen; wider rows take the exact path
         self.lds_ok = ds.KT <= LDS_MAX_KT
         self.use_screen = (ds.screen_ok and not self.exact and Q > 0 and
                            (self.lds_ok or (SCREEN_IMPL == "x1" and L.dmlp_screen_x1_qw(ds.KT) > 0)))

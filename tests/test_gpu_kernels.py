@@ -442,7 +442,7 @@ def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
                                     (256, 16)])
 def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
     """Single-term screen for A > 64 (KT = 4 and 8, one wave per SIMD) with the group refine
-    staging hi(q') in LDS; A > 128 has no 3-term kernel, so the x1 class is its only screen."""
+    staging hi(q') in LDS."""
     monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
     inp = dmlp.generate(6000, 300, A, 0.0, 1000.0, 1, kmax, 6, seed=A + kmax)
     r, refs = run_both(torch_cuda, inp)
@@ -450,11 +450,21 @@ def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("A", [32, 64, 100, 128])
+@pytest.mark.parametrize("A", [32, 64, 100, 128, 200, 256])
 def test_screen_k_up_to_256(torch_cuda, A):
     """128 < k <= 256 on the cap-512 LDS screen (3-term) and the P = 512 refine, mixed with the
-    cap-256 class in one call."""
+    cap-256 class in one call; A in (128, 256] streams each tile as two LDS stages."""
     inp = dmlp.generate(20000, 300, A, 0.0, 1000.0, 100, 256, 8, seed=A)
+    r, refs = run_both(torch_cuda, inp)
+    assert r.n_fallback == 0
+    assert_same(r, refs)
+
+
+@pytest.mark.parametrize("A", [160, 256])
+def test_wide_rows_every_class(torch_cuda, A):
+    """A in (128, 256] with k over all three screen classes (x1 for k <= 32, cap-256 and
+    cap-512 LDS screens above): nothing takes the exact path."""
+    inp = dmlp.generate(12000, 400, A, 0.0, 1000.0, 1, 200, 7, seed=A + 1)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
     assert_same(r, refs)
