@@ -74,6 +74,10 @@ _SIGS = {
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
                           vp, vp]),
+    "dmlp_screen_hl": (i32, [i32, i32, i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp,
+                             f32, i32, vp, vp, vp]),
+    "dmlp_screen_waves_hl": (i32, [i32, i32, i32]),
+    "dmlp_screen_lds_bytes_hl": (i32, [i32, i32, i32]),
     "dmlp_refine": (i32, [i32, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_exact_rows": (i32, [vp, i64, i32, vp, vp, i32, vp, i64, vp]),
     "dmlp_fallback_bytes": (i64, [i32, i64]),

@@ -108,6 +108,15 @@ int dmlp_screen(int KT, int cap, const void* xfrag, const float* xinit, int64_t 
                 int* cand_ids, int* cand_cnt, void* stream);
 int dmlp_screen_lds_bytes(int KT, int cap);
 int dmlp_screen_waves(int KT, int cap);
+// hl = 2: the call above; hl = 1: the single-term form on the host's fp16 image and fp16 query
+// fragments (dmlp_host_ops_h2d's operands; qlo / eps_rel unused, A selects the bound).
+int dmlp_screen_hl(int KT, int cap, int hl, int A, const void* xfrag, const float* xinit,
+                   int64_t n_tiles, const void* qhi, const void* qlo, const float* qn,
+                   const int* qidx, const int* qk, int nq, const unsigned* xnmax_bits,
+                   const unsigned* bad, float eps_rel, int S, int* cand_ids, int* cand_cnt,
+                   void* stream);
+int dmlp_screen_lds_bytes_hl(int KT, int cap, int hl);
+int dmlp_screen_waves_hl(int KT, int cap, int hl);
 
 // Barrier-free streaming screen (screen_stream.hip) for k <= dmlp_screen_stream_kmax() and
 // KT <= 2: dmlp_screen_stream_qw(KT) queries per workgroup (0 = unsupported KT); kmax = the

@@ -35,6 +35,10 @@ namespace {
 struct DropinState {
   dmlp_rt::Runtime rt;
   std::unique_ptr<dmlp_rt::KnnCore> core;
+  // the row index's tables, kept across calls: fresh vectors every call cost ~1 ms of page
+  // faults and zero-fills at the bench shape (profiles/r4l_dropin_trace.txt "index")
+  std::vector<int> labels, k;
+  std::vector<const double*> xr, qr;
 };
 
 DropinState*& state() {
@@ -203,13 +207,15 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
   s->core->trace.begin();
   bool done = false;
   auto t1 = t0;
-  if (root && s->rt.world == 1) {
+  const bool own_tables = root && s->rt.world == 1;
+  if (own_tables) {
     // one rank: the fast path reads the harness's vectors in place (no pack pass)
-    std::vector<const double*> xr, qr;
-    index_rows(dataset, queries, p.num_attrs, in, xr, qr);
+    std::swap(in.labels, s->labels);
+    std::swap(in.k, s->k);
+    index_rows(dataset, queries, p.num_attrs, in, s->xr, s->qr);
     s->core->trace.mark("index");
     t1 = std::chrono::steady_clock::now();
-    done = s->core->KNN_rows(&in, xr.data(), qr.data(), &out);
+    done = s->core->KNN_rows(&in, s->xr.data(), s->qr.data(), &out);
   }
   if (!done) {
     if (root) pack(dataset, queries, p.num_attrs, in);
@@ -238,6 +244,10 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     }
   }
   s->core->trace.mark("emit");
+  if (own_tables) {  // back to the state for the next call (allocated, already faulted in)
+    std::swap(in.labels, s->labels);
+    std::swap(in.k, s->k);
+  }
   (void)s->core->trace.finish();  // KNN_TRACE=1: per-phase lines on stderr (after the work)
   // KNN_METRICS=path: this call's time with microsecond resolution (the harness prints whole ms)
   if (root) {

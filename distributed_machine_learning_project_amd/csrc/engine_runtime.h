@@ -337,7 +337,7 @@ struct LocalKnn {
   DevBuf<unsigned> words;  // [0] xnmax bits, [1] bad
   DevBuf<short> qhi, qlo;
   DevBuf<float> qn, cand_h;
-  DevBuf<int> qidx_a, qidx_b, qidx_c, qidx_e, qidx_f, kdev, cand_ids, cand_cnt, status;
+  DevBuf<int> qidx_a, qidx_b, qidx_c, qidx_e, qidx_e2, qidx_f, kdev, cand_ids, cand_cnt, status;
   DevBuf<char> fb_ws;
   int KT = 1;
   int64_t N = 0;
@@ -512,7 +512,8 @@ struct LocalKnn {
       // default: single-term screen (screen_x1.hip); KNN_SCREEN=stream: 3-term streaming
       const char* impl = std::getenv("KNN_SCREEN");
       const bool use_x1 = x1_ok && (!lds_ok || !(impl && std::string(impl) == "stream" && !hx));
-      // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 128)
+      // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 256),
+      // 3 LDS-shared single-term on the host operands hx (k <= 256: no device image)
       auto pass = [&](const std::vector<int>* idx, int impl, DevBuf<int>& qbuf) {
         const int nq = idx ? (int)idx->size() : (int)Q;
         int* qi;
@@ -532,7 +533,7 @@ struct LocalKnn {
                                                 dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                                 dmlp_screen_x1_min_slices(nt))
                       : impl == 1 ? slices_stream(nq, qw, nt, dmlp_screen_stream_waves_per_cu(kcls))
-                                  : slices_lds(nq, dmlp_screen_waves(KT, cap), nt);
+                                  : slices_lds(nq, dmlp_screen_waves_hl(KT, cap, impl == 3 ? 1 : 2), nt);
         int* ci = cand_ids.get((size_t)nq * S * cap);
         int* cc = cand_cnt.get((size_t)nq * S);
         if (impl == 0) {
@@ -552,6 +553,14 @@ struct LocalKnn {
                                      st));
           return;
         }
+        if (impl == 3) {
+          DMLPCHK(dmlp_screen_hl(KT, cap, 1, A, hx->xhi, hx->xin, nt, hx->qhi, nullptr, hx->qn, qi,
+                                 kd, nq, hx->words, hx->words + 1, 0.0f, S, ci, cc, st));
+          wait_rows();
+          DMLPCHK(dmlp_refine(cap, ci, cc, S, X, A, Qx, qi, kd, nq, out_d, out_i, kstride,
+                              fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, ovf, st));
+          return;
+        }
         need_dev();
         if (impl == 1)
           DMLPCHK(dmlp_screen_stream(KT, xfrag.p, xinit.p, nt, qhi.p, qlo.p, qn.p, qi, kd, nq, kcls,
@@ -565,8 +574,13 @@ struct LocalKnn {
       if (!hx) need_dev();  // the device operands of every screen
       const int first_a = use_x1 ? 0 : (qw > 0 ? 1 : 2);
       if (all_a || !a.empty()) pass(all_a ? nullptr : &a, first_a, qidx_a);
-      if (!b.empty()) pass(&b, 2, qidx_b);
-      if (!c.empty()) pass(&c, 2, qidx_c);
+      // k > 32 on the single-term LDS screen when the host operands are here (KNN_LDS_SINGLE=0:
+      // always 3-term); its overflows escalate to the 3-term LDS screen below
+      const char* ls = std::getenv("KNN_LDS_SINGLE");
+      const int bc_impl = (hx && !(ls && std::string(ls) == "0") &&
+                           dmlp_screen_waves_hl(KT, 128, 1) > 0) ? 3 : 2;
+      if (!b.empty()) pass(&b, bc_impl, qidx_b);
+      if (!c.empty()) pass(&c, bc_impl, qidx_c);
       // one host sync: the overflow count (4 bytes); the per-query status only when some
       // screened query overflowed
       int novf = 0;
@@ -576,7 +590,7 @@ struct LocalKnn {
         std::vector<int> sh(Q);
         HIPCHK(hipMemcpyAsync(sh.data(), stat, Q * sizeof(int), hipMemcpyDeviceToHost, st));
         wait();
-        std::vector<int> esc;
+        std::vector<int> esc, esc_bc;
         if (first_a == 0 && all_a) {
           for (int64_t q = 0; q < Q; ++q)
             if (sh[q]) esc.push_back((int)q);
@@ -584,12 +598,21 @@ struct LocalKnn {
           for (int q : a)
             if (sh[q]) esc.push_back(q);
         }
-        if (!esc.empty() && (qw > 0 || lds_ok)) {
+        if (bc_impl == 3) {
+          for (int q : b)
+            if (sh[q]) esc_bc.push_back(q);
+          for (int q : c)
+            if (sh[q]) esc_bc.push_back(q);
+        }
+        if (!(qw > 0 || lds_ok)) esc.clear();
+        if (!esc.empty() || !esc_bc.empty()) {
           // single-term overflow (data too tight for its bound): those queries alone go to the
           // 3-term screen
           HIPCHK(hipMemsetAsync(ovf, 0, sizeof(int), st));
           for (int q : esc) HIPCHK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
-          pass(&esc, qw > 0 ? 1 : 2, qidx_e);
+          for (int q : esc_bc) HIPCHK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
+          if (!esc.empty()) pass(&esc, qw > 0 ? 1 : 2, qidx_e);
+          if (!esc_bc.empty()) pass(&esc_bc, 2, qidx_e2);
           HIPCHK(hipMemcpyAsync(&novf, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
           wait();
           if (novf) {

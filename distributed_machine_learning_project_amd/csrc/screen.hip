@@ -26,11 +26,19 @@
 // alone (bitonic sort of the scores across the wave).
 // Block -> (query block, data slice) is XCD-aware when S % 8 == 0: every XCD streams only its
 // own S/8 slices, so each slice is fetched into exactly one XCD's L2.
+//
+// HL = 1: the single-term form on the host's fp16 image and fp16 query fragments (the operands
+// screen_x1.hip reads, already on the device when the host rendered them): one
+// v_mfma_f32_16x16x32_f16 per fragment instead of three bf16 products, half the LDS staging, and
+// the single-term error bound (dmlp_screen_x1_bound2, ~2^-10 relative instead of ~2^-16: a few
+// percent more candidates at k in (32, 256]).  Per-point (score, id) entries as for HL = 2.
 #include "dmlp.h"
 #include "dmlp_device.h"
 #include <float.h>
 
 namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // Ablation switch for profiling only (bit 0: no candidate path, bit 1: no MFMA, bit 2: no tile
 // streaming).  Results are wrong unless it is 0; set through dmlp_set_screen_mode.
@@ -45,15 +53,16 @@ __device__ unsigned long long g_screen_dbg[8];
     }                                                       \
   } while (0)
 
-template <int KT, int WAVES, int CAP>
+template <int KT, int WAVES, int CAP, int HL = 2>
 struct ScreenCfg {
   static constexpr int KTS = KT > 4 ? 4 : KT;  // 32-attribute fragments per LDS stage
   static constexpr int NST = KT / KTS;         // stages per 64-point tile
-  static constexpr int TILE_FRAGS = 4 * KT * 2;  // 1 KiB fragments per tile of the image
-  static constexpr int FRAGS = 4 * KTS * 2;    // 1 KiB fragments per stage
+  static constexpr int TILE_FRAGS = 4 * KT * HL;  // 1 KiB fragments per tile of the image
+  static constexpr int FRAGS = 4 * KTS * HL;   // 1 KiB fragments per stage
   static constexpr int TILE_BYTES = FRAGS * 1024 + 256;
   static constexpr int G = FRAGS / WAVES;   // staged 16-B vectors per lane per tile
-  static constexpr int D = G <= 2 ? 4 : (G <= 4 ? 3 : 2);  // register-ring depth (tiles)
+  static constexpr int D0 = G <= 2 ? 4 : (G <= 4 ? 3 : 2);
+  static constexpr int D = (D0 + NST - 1) / NST * NST;  // register-ring depth (stages)
   static constexpr int SUB = CAP / 4;      // per-lane sub-buffer entries
   static constexpr int LDS = 2 * TILE_BYTES + WAVES * 64 * (SUB + 1) * 8;
   static_assert(FRAGS % WAVES == 0, "fragments must split evenly over waves");
@@ -62,15 +71,15 @@ struct ScreenCfg {
   static_assert(CAP % 64 == 0, "CAP multiple of 64");
 };
 
-template <int KT, int WAVES, int CAP>
+template <int KT, int WAVES, int CAP, int HL>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
     const u32x4* __restrict__ xfrag, const float* __restrict__ xinit, int n_tiles,
     const bf16x8* __restrict__ qhi, const bf16x8* __restrict__ qlo, const float* __restrict__ qn,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq,
     const unsigned* __restrict__ xnmax_bits, const unsigned* __restrict__ bad, float eps_rel,
-    int S, int tiles_per_slice, int n_qblocks, int mode, int* __restrict__ cand_ids,
-    int* __restrict__ cand_cnt) {
-  using C = ScreenCfg<KT, WAVES, CAP>;
+    float r1, float r2, float r3, int S, int tiles_per_slice, int n_qblocks, int mode,
+    int* __restrict__ cand_ids, int* __restrict__ cand_cnt) {
+  using C = ScreenCfg<KT, WAVES, CAP, HL>;
   constexpr int E = CAP / 64;
   constexpr int KTS = C::KTS, NST = C::NST;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -111,13 +120,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   }
   const float xnmax = __uint_as_float(*xnmax_bits);
   const int q = valid ? qidx[p] : 0;
-  bf16x8 bh[KT], bl[KT];
+  bf16x8 bh[KT], bl[HL == 2 ? KT : 1];
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     bh[kt] = qhi[(q * KT + kt) * 4 + kg];
-    bl[kt] = qlo[(q * KT + kt) * 4 + kg];
+    if constexpr (HL == 2) bl[kt] = qlo[(q * KT + kt) * 4 + kg];
   }
-  const float eps = eps_rel * (qn[q] + xnmax);
+  // |a - a_exact| <= eps: the 3-term bound (HL = 2), or screen_x1.hip's single-term fp16 bound
+  const float eps = HL == 2 ? eps_rel * (qn[q] + xnmax)
+                            : r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax +
+                                  r3 * (sqrtf(qn[q]) + sqrtf(xnmax)) + r3 * 0x1p-15f;
   const int kq = valid ? qk[q] : 0;
   float h = valid ? -FLT_MAX : INFINITY;
   int cnt = 0;  // entries in this lane's own sub-buffer (negative: column overflowed)
@@ -132,16 +144,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
   float stx[D];
   // Loads are issued unconditionally (stage index clamped, every wave fetches the 256-B xinit
   // row) so the vmcnt bookkeeping is path-independent and hipcc emits counted waits.  Stage
-  // fragment f = (rt * KTS + ktl) * 2 + hilo is image fragment (rt * KT + h * KTS + ktl) * 2 + hilo
-  // of its tile (h: the stage within the tile; the identity when NST = 1).
+  // fragment f = (rt * KTS + ktl) * HL + hilo is image fragment (rt * KT + h * KTS + ktl) * HL +
+  // hilo of its tile (h: the stage within the tile; the identity when NST = 1).
 #define DMLP_LOAD_TILE(I, R)                                                      \
   do {                                                                            \
     const int i_ = (I) < nst ? (I) : nst - 1;                                     \
     const int t_ = t0 + i_ / NST, h_ = i_ % NST;                                  \
     const u32x4* src_ = xfrag + (int64_t)t_ * (C::TILE_FRAGS * 64);               \
     _Pragma("unroll") for (int g = 0; g < C::G; ++g) {                            \
-      const int f_ = wave + g * WAVES, rt_ = f_ / (2 * KTS);                      \
-      stg[R][g] = src_[((rt_ * KT + h_ * KTS) * 2 + f_ - rt_ * 2 * KTS) * 64 + lane]; \
+      const int f_ = wave + g * WAVES, rt_ = f_ / (HL * KTS);                     \
+      stg[R][g] = src_[((rt_ * KT + h_ * KTS) * HL + f_ - rt_ * HL * KTS) * 64 + lane]; \
     }                                                                             \
     stx[R] = xinit[(int64_t)t_ * 64 + lane];                                      \
   } while (0)
@@ -246,29 +258,39 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
     if (!(mode & 4)) DMLP_LOAD_TILE(i + D, r);
 
     const char* tb = tiles + (i & 1) * C::TILE_BYTES;
-    bf16x8 ah[4][KTS], al[4][KTS];
+    bf16x8 ah[4][KTS], al[4][HL == 2 ? KTS : 1];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt) {
       if (hs == 0) acc[rt] = *(const f32x4*)(tb + C::FRAGS * 1024 + rt * 64 + kg * 16);
 #pragma unroll
       for (int kt = 0; kt < KTS; ++kt) {
-        ah[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * 2 + 0) * 1024 + lane * 16);
-        al[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * 2 + 1) * 1024 + lane * 16);
+        ah[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * HL + 0) * 1024 + lane * 16);
+        if constexpr (HL == 2)
+          al[rt][kt] = *(const bf16x8*)(tb + ((rt * KTS + kt) * 2 + 1) * 1024 + lane * 16);
       }
     }
 #pragma unroll
     for (int kt = 0; kt < KTS; ++kt) {
       if (mode & 2) break;  // ablation: no matrix work
-      const bf16x8 qh = bh[hs * KTS + kt], ql = bl[hs * KTS + kt];
+      const bf16x8 qh = bh[hs * KTS + kt];
+      if constexpr (HL == 1) {  // single term: hi(q') * hi(x'), fp16 operands
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], qh, acc[rt], 0, 0, 0);
+        for (int rt = 0; rt < 4; ++rt)
+          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ah[rt][kt]),
+                                                           __builtin_bit_cast(f16x8, qh), acc[rt],
+                                                           0, 0, 0);
+      } else {
+        const bf16x8 ql = bl[hs * KTS + kt];
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], ql, acc[rt], 0, 0, 0);
+        for (int rt = 0; rt < 4; ++rt)
+          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], qh, acc[rt], 0, 0, 0);
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
-        acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt][kt], qh, acc[rt], 0, 0, 0);
+        for (int rt = 0; rt < 4; ++rt)
+          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[rt][kt], ql, acc[rt], 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt)
+          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[rt][kt], qh, acc[rt], 0, 0, 0);
+      }
     }
     if (hs == NST - 1) {  // a whole tile accumulated: the epilogue
     float mr[4];
@@ -345,13 +367,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_screen(
 #undef DMLP_GATHER
 }
 
-template <int KT, int WAVES, int CAP>
+template <int KT, int WAVES, int CAP, int HL>
 int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const void* qhi,
                   const void* qlo, const float* qn, const int* qidx, const int* qk, int nq,
-                  const unsigned* xnmax, const unsigned* bad, float eps_rel, int S,
-                  int* cand_ids, int* cand_cnt, hipStream_t stream) {
-  using C = ScreenCfg<KT, WAVES, CAP>;
-  auto kern = k_screen<KT, WAVES, CAP>;
+                  const unsigned* xnmax, const unsigned* bad, float eps_rel, float r1, float r2,
+                  float r3, int S, int* cand_ids, int* cand_cnt, hipStream_t stream) {
+  using C = ScreenCfg<KT, WAVES, CAP, HL>;
+  auto kern = k_screen<KT, WAVES, CAP, HL>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -365,7 +387,7 @@ int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const 
   if (grid <= 0) return 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(WAVES * 64), C::LDS, stream,
                      (const u32x4*)xfrag, xinit, (int)n_tiles, (const bf16x8*)qhi,
-                     (const bf16x8*)qlo, qn, qidx, qk, nq, xnmax, bad, eps_rel, S, tps,
+                     (const bf16x8*)qlo, qn, qidx, qk, nq, xnmax, bad, eps_rel, r1, r2, r3, S, tps,
                      n_qblocks, g_screen_mode, cand_ids, cand_cnt);
   DMLP_LAUNCH_CHECK();
   return 0;
@@ -373,48 +395,76 @@ int launch_screen(const void* xfrag, const float* xinit, int64_t n_tiles, const 
 
 }  // namespace
 
-// (KT, CAP) -> WAVES: LDS = 2*(8 KiB*min(KT, 4) + 256) + WAVES*16*CAP*8 <= 160 KiB (KT = 8:
-// two 32 KiB stages per tile).  CAP = 512 serves
-// 128 < k <= 256 (a column compacts to >= k entries and refills 448 - k before the next batch).
+// (KT, CAP) -> WAVES, 3-term (HL = 2): LDS = 2*(8 KiB*min(KT, 4) + 256) + WAVES*16*CAP*8 <= 160 KiB
+// (KT = 8: two 32 KiB stages per tile).  CAP = 512 serves 128 < k <= 256 (a column compacts to
+// >= k entries and refills 448 - k before the next batch).
 #define DMLP_SCREEN_CONFIGS(X)                                                                \
-  X(1, 128, 8) X(2, 128, 4) X(3, 128, 4) X(4, 128, 4) X(1, 256, 4) X(2, 256, 2) X(3, 256, 2) \
-  X(4, 256, 2) X(1, 512, 2) X(2, 512, 1) X(3, 512, 1) X(4, 512, 1) X(8, 128, 4) X(8, 256, 2) \
-  X(8, 512, 1)
+  X(1, 128, 8, 2) X(2, 128, 4, 2) X(3, 128, 4, 2) X(4, 128, 4, 2) X(1, 256, 4, 2)              \
+  X(2, 256, 2, 2) X(3, 256, 2, 2) X(4, 256, 2, 2) X(1, 512, 2, 2) X(2, 512, 1, 2)              \
+  X(3, 512, 1, 2) X(4, 512, 1, 2) X(8, 128, 4, 2) X(8, 256, 2, 2) X(8, 512, 1, 2)              \
+  DMLP_SCREEN_CONFIGS_1(X)
+// single-term fp16 (HL = 1, host image): half the staging, WAVES <= fragments per stage
+#define DMLP_SCREEN_CONFIGS_1(X)                                                              \
+  X(1, 128, 4, 1) X(2, 128, 8, 1) X(4, 128, 4, 1) X(8, 128, 4, 1) X(1, 256, 4, 1)              \
+  X(2, 256, 4, 1) X(4, 256, 2, 1) X(8, 256, 2, 1) X(1, 512, 2, 1) X(2, 512, 2, 1)              \
+  X(4, 512, 1, 1) X(8, 512, 1, 1)
 
 extern "C" int dmlp_screen_kmax(int cap) {
   return cap == 128 ? 32 : (cap == 256 ? 128 : (cap == 512 ? 256 : 0));
 }
 
-extern "C" int dmlp_screen_lds_bytes(int KT, int cap) {
-#define DMLP_LDS_CASE(kt, cp, w) \
-  if (KT == kt && cap == cp) return ScreenCfg<kt, w, cp>::LDS;
+extern "C" int dmlp_screen_lds_bytes_hl(int KT, int cap, int hl) {
+#define DMLP_LDS_CASE(kt, cp, w, h) \
+  if (KT == kt && cap == cp && hl == h) return ScreenCfg<kt, w, cp, h>::LDS;
   DMLP_SCREEN_CONFIGS(DMLP_LDS_CASE)
 #undef DMLP_LDS_CASE
   return -1;
 }
+extern "C" int dmlp_screen_lds_bytes(int KT, int cap) { return dmlp_screen_lds_bytes_hl(KT, cap, 2); }
 
-extern "C" int dmlp_screen_waves(int KT, int cap) {
-#define DMLP_W_CASE(kt, cp, w) \
-  if (KT == kt && cap == cp) return w;
+// waves per workgroup of the (KT, cap, hl) variant (-1: none)
+extern "C" int dmlp_screen_waves_hl(int KT, int cap, int hl) {
+#define DMLP_W_CASE(kt, cp, w, h) \
+  if (KT == kt && cap == cp && hl == h) return w;
   DMLP_SCREEN_CONFIGS(DMLP_W_CASE)
 #undef DMLP_W_CASE
   return -1;
+}
+extern "C" int dmlp_screen_waves(int KT, int cap) { return dmlp_screen_waves_hl(KT, cap, 2); }
+
+// hl = 2: the 3-term screen on prep.hip's bf16 hi/lo image and device query fragments (qlo used,
+// eps_rel the 3-term bound); hl = 1: the single-term screen on the host's fp16 image and fp16
+// query fragments (qlo and eps_rel unused; A selects the single-term bound).
+extern "C" int dmlp_screen_hl(int KT, int cap, int hl, int A, const void* xfrag,
+                              const float* xinit, int64_t n_tiles, const void* qhi,
+                              const void* qlo, const float* qn, const int* qidx, const int* qk,
+                              int nq, const unsigned* xnmax_bits, const unsigned* bad,
+                              float eps_rel, int S, int* cand_ids, int* cand_cnt, void* stream) {
+  if (nq <= 0) return 0;
+  if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
+  if (hl != 1 && hl != 2) return -1;
+  float r1 = 0.0f, r2 = 0.0f, r3 = 0.0f;
+  if (hl == 1) {
+    if (A < 1 || A > KT * 32) return -1;
+    dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
+  }
+  hipStream_t st = (hipStream_t)stream;
+#define DMLP_SCREEN_CASE(kt, cp, w, h)                                                          \
+  if (KT == kt && cap == cp && hl == h)                                                         \
+    return launch_screen<kt, w, cp, h>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq,       \
+                                       xnmax_bits, bad, eps_rel, r1, r2, r3, S, cand_ids,       \
+                                       cand_cnt, st);
+  DMLP_SCREEN_CONFIGS(DMLP_SCREEN_CASE)
+#undef DMLP_SCREEN_CASE
+  return -2;
 }
 
 extern "C" int dmlp_screen(int KT, int cap, const void* xfrag, const float* xinit, int64_t n_tiles,
                            const void* qhi, const void* qlo, const float* qn, const int* qidx,
                            const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
                            float eps_rel, int S, int* cand_ids, int* cand_cnt, void* stream) {
-  if (nq <= 0) return 0;
-  if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64) return -1;
-  hipStream_t st = (hipStream_t)stream;
-#define DMLP_SCREEN_CASE(kt, cp, w)                                                         \
-  if (KT == kt && cap == cp)                                                                \
-    return launch_screen<kt, w, cp>(xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq,      \
-                                    xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, st);
-  DMLP_SCREEN_CONFIGS(DMLP_SCREEN_CASE)
-#undef DMLP_SCREEN_CASE
-  return -2;
+  return dmlp_screen_hl(KT, cap, 2, KT * 32, xfrag, xinit, n_tiles, qhi, qlo, qn, qidx, qk, nq,
+                        xnmax_bits, bad, eps_rel, S, cand_ids, cand_cnt, stream);
 }
 
 extern "C" void dmlp_set_screen_mode(int mode) { g_screen_mode = mode; }

@@ -48,6 +48,10 @@ HOST_OPS_PARTS = int(os.environ.get("DMLP_HOST_OPS_PARTS", "1"))
 # fp64 rows of the host-operand pipeline cross PCIe as lossless int32 when every value is a
 # 6-decimal number (knn._issue_rows)
 ROWS_I32 = os.environ.get("DMLP_ROWS_I32", "1") != "0"
+# k in (32, 256] (the cap-256 / cap-512 classes) on the single-term LDS screen over the host's
+# fp16 operands when the host rendered them (no device hi/lo image, a third of the MFMA work);
+# its overflows escalate to the 3-term LDS screen.  DMLP_LDS_SINGLE=0: always 3-term (A/B)
+LDS_SINGLE = os.environ.get("DMLP_LDS_SINGLE", "1") != "0"
 
 
 def screen_kt(A: int) -> int:
@@ -374,10 +378,14 @@ class _KnnCall:
         self.kdev_eff = self.k_dev if kk is self.k_host else _h2d(kk.astype(np.int32), dev)
         if self.all_a or len(self.cls_a):
             self._screen_pass(self.cls_a, self.first_a)
+        # k > 32: the single-term LDS screen on the host operands when they are here
+        self.single_bc = (LDS_SINGLE and ds.hl == 1 and self.prepped is not None
+                          and L.dmlp_screen_waves_hl(KT, 128, 1) > 0)
+        lds_impl = "lds1" if self.single_bc else "lds"
         if len(self.cls_b):
-            self._screen_pass(self.cls_b, "lds")
+            self._screen_pass(self.cls_b, lds_impl)
         if len(self.cls_c):
-            self._screen_pass(self.cls_c, "lds")
+            self._screen_pass(self.cls_c, lds_impl)
         return self
 
     def _wait_qx(self):
@@ -415,7 +423,7 @@ class _KnnCall:
 
     def _screen_pass(self, idx, impl):
         torch = _torch()
-        if impl != "x1" and self.qlo is None:
+        if impl not in ("x1", "lds1") and self.qlo is None:
             self._prep_on_device()  # 3-term class / escalation after a host-prepared x1 pass
         L = _lib.lib()
         ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
@@ -445,7 +453,8 @@ class _KnnCall:
                                       L.dmlp_screen_stream_waves_per_cu(kcls), 1, cus)
         else:
             cap = (128 if kcls <= SCREEN_KMAX_A else 256 if kcls <= SCREEN_KMAX_B else 512)
-            S = _choose_slices(nq, L.dmlp_screen_waves(KT, cap), ds.n_tiles)
+            S = _choose_slices(nq, L.dmlp_screen_waves_hl(KT, cap, 1 if impl == "lds1" else 2),
+                               ds.n_tiles)
         if pre is None:
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
             cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
@@ -485,6 +494,21 @@ class _KnnCall:
                 _p(self.out_d), _p(self.out_i), self.ks, *fin), "refine_groups")
             _mark("refine_done")
             self._keep = (qidx, cand_ids, cand_cnt, cand_h)
+            return
+        if impl == "lds1":
+            # single term on the host's fp16 image + query fragments: nothing rendered on the
+            # device, the refine alone waits for the fp64 rows
+            x1_qhi, x1_qn = self.prepped
+            self._fill_outputs()
+            _lib.check(L.dmlp_screen_hl(KT, cap, 1, A, _p(ds.xfrag), _p(ds.xinit), ds.n_tiles,
+                                        _p(x1_qhi), None, _p(x1_qn), _p(qidx), _p(self.kdev_eff),
+                                        nq, _p(ds.xnmax_bits), _p(ds.bad), 0.0, S, _p(cand_ids),
+                                        _p(cand_cnt), s), "screen_hl")
+            self._wait_qx()
+            _lib.check(L.dmlp_refine(cap, _p(cand_ids), _p(cand_cnt), S, _p(ds.X), A,
+                                     _p(self.Qx), _p(qidx), _p(self.kdev_eff), nq, _p(self.out_d),
+                                     _p(self.out_i), self.ks, *fin), "refine")
+            self._keep = (qidx, cand_ids, cand_cnt)
             return
         if ds.hl != 2:
             self._wait_qx()  # the device image is rendered from the fp64 rows
@@ -531,15 +555,24 @@ class _KnnCall:
             # the refine kernels count overflowed queries into this call's counter slot: one
             # 4-byte read (and the call's one host sync) instead of a reduce over the status
             n_ovf = self._ovf.read(self._ovf_slot, self.stream)
-            if n_ovf and self.first_a == "x1" and (self.stream_ok or self.lds_ok):
+            esc_a = esc_bc = np.empty(0, np.int64)
+            if n_ovf and (self.first_a == "x1" or self.single_bc):
                 st = self.status.cpu().numpy()
-                esc = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
-                n_esc = len(esc)
-                if n_esc:
-                    self.cs_modified = True
-                    self._screen_pass(esc, "stream" if self.stream_ok else "lds")
-                    # (the escalation ran on this stream, which may not be the launch stream)
-                    n_ovf = self._ovf.read(self._ovf_slot, torch.cuda.current_stream())
+                if self.first_a == "x1" and (self.stream_ok or self.lds_ok):
+                    esc_a = np.nonzero(st)[0] if self.all_a else self.cls_a[st[self.cls_a] != 0]
+                if self.single_bc and not self.all_a:
+                    # single-term k > 32 classes: their overflows get the 3-term LDS screen
+                    esc_bc = np.concatenate([self.cls_b[st[self.cls_b] != 0],
+                                             self.cls_c[st[self.cls_c] != 0]])
+            n_esc = len(esc_a) + len(esc_bc)
+            if n_esc:
+                self.cs_modified = True
+                if len(esc_a):
+                    self._screen_pass(esc_a, "stream" if self.stream_ok else "lds")
+                if len(esc_bc):
+                    self._screen_pass(esc_bc, "lds")
+                # (the escalation ran on this stream, which may not be the launch stream)
+                n_ovf = self._ovf.read(self._ovf_slot, torch.cuda.current_stream())
         fb = (np.empty(0, np.int64) if self.all_a
               else np.nonzero(~self.on_screen & (kk >= 1))[0])
         if n_ovf:
@@ -1045,6 +1078,11 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         with torch.cuda.stream(ps):
             call.launch()
         main.wait_stream(ps)
+        # the call's one host sync (finish: the overflow count) goes on main, behind the report
+        # kernels and the report D2H that _pipelined_tail queues there: the call returns with
+        # its byte count and text complete (a sync on the part stream alone left them racing
+        # the caller's reads)
+        call.stream = main
     return ds, od, oi, ol, oc, calls
 
 

@@ -438,6 +438,37 @@ def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
 
 
+@pytest.mark.parametrize("A,dup,single", [(32, 0, True), (100, 0, True), (256, 0, True),
+                                          (32, 700, True), (64, 0, False)])
+def test_pipelined_single_term_lds(torch_cuda, A, dup, single, monkeypatch):
+    """k in (32, 256] on the single-term LDS screen over the host's fp16 operands (HL = 1) —
+    with `dup` copies of one point, the queries sitting on it overflow the single-term bound and
+    escalate to the 3-term LDS screen; single=False is the 3-term-only A/B path.  Bit-exact."""
+    torch = torch_cuda
+    monkeypatch.setattr(K, "LDS_SINGLE", single)
+    rng = np.random.default_rng(A + dup)
+    N, Q = 9000, 400
+    X = np.round(rng.uniform(0, 1000, (N, A)), 6)
+    if dup:
+        X[:dup] = X[0]
+    Qx = np.round(rng.uniform(0, 1000, (Q, A)), 6)
+    Qx[5] = X[0]
+    k = rng.integers(33, 257, Q).astype(np.int32)
+    labels = rng.integers(0, 9, N).astype(np.int32)
+    Xp = torch.from_numpy(X).pin_memory().numpy()
+    Qp = torch.from_numpy(Qx).pin_memory().numpy()
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, labels, (0, 9), Qp, k)
+    torch.cuda.synchronize()
+    d_ref, i_ref = K.knn_cpu(X, Qx, k, kstride=d.shape[1])
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, k, labels)
+    np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
+    np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
+    np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+    # (700 tied points may overflow the 3-term screen's buffers too: that query alone goes exact)
+    assert nfb <= (1 if dup else 0)
+
+
 @pytest.mark.parametrize("A,kmax", [(65, 16), (100, 32), (128, 16), (129, 16), (200, 30),
                                     (256, 16)])
 def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
