@@ -610,12 +610,8 @@ class KnnCore {
     uint16_t* qhi_h = (uint16_t*)hp; hp += up(b_qhi);
     float* qn_h = (float*)hp; hp += up(b_qn);
     double* mu_h = (double*)hp;
-    // the centre only tightens the screen's bound (any mu is exact): the mean of the first
-    // 4096 rows, as the Python pipeline takes it — a full pass over N rows cost 0.16 ms per call
-    // (profiles/r4l_dropin_trace.txt) on the critical path
-    const int64_t n_mu = std::min<int64_t>(N_, 4096);
-    if (Xr) dmlp_cpu_center_rows(Xr, n_mu, A_, mu_h);
-    else dmlp_cpu_center(X, n_mu, A_, mu_h);
+    if (Xr) dmlp_cpu_center_rows(Xr, N_, A_, mu_h);
+    else dmlp_cpu_center(X, N_, A_, mu_h);
     trace.mark("center");
     short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
     float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
