@@ -193,6 +193,26 @@ int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt, const 
                        const int* qidx, const int* qk, int nq, double* out_d, int* out_i,
                        int kstride, const int* labels, int label_lo, int label_hi,
                        int* out_label, uint64_t* out_cs, int* status, int* ovf_count, void* stream);
+// collect = 1: the lists of dmlp_screen_x1_collect (large k): k <= 256 over <= 512 filtered
+// members (fp16 host operands, hl = 1); collect = 0 is dmlp_refine_groups.
+int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
+                        int S, const double* X, int A, const double* Qx, const void* xfrag,
+                        const float* xinit, const void* qhi, int KT, int hl, int64_t n_points,
+                        const int* qidx, const int* qk, int nq, double* out_d, int* out_i,
+                        int kstride, const int* labels, int label_lo, int label_hi,
+                        int* out_label, uint64_t* out_cs, int* status, int* ovf_count,
+                        int collect, void* stream);
+
+// Large k on the single-term screen (screen_x1.hip): first-pass thresholds (S1 slices, k' =
+// ceil(k / S1)) -> per-query seeds (NaN: a slice overflowed), then the COLLECT pass at those
+// fixed thresholds into ccap group ids per (query, slice).
+int dmlp_x1_seed(const float* cand_h, const int* cand_cnt, int S1, int nq, float* hseed,
+                 void* stream);
+int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
+                           int64_t n_points, const void* qhi, const float* qn, const int* qidx,
+                           const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
+                           const float* hseed, int ccap, int S, int* cand_ids, int* cand_cnt,
+                           float* cand_h, void* stream);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

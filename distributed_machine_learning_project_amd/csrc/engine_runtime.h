@@ -412,7 +412,10 @@ struct LocalKnn {
     ~PinnedInts() {
       if (p && !host_arena().owns(p)) (void)hipHostFree(p);
     }
-  } kk_h_, ident_h_;
+  } kk_h_, ident_h_, kp_h_;
+  // the two-pass large-k x1 screen: first-pass lists / thresholds, per-query seeds, k'
+  DevBuf<int> k1_ids_, k1_cnt_, kp_d_;
+  DevBuf<float> k1_h_, k1_seed_;
   DevBuf<int> ident_, ovf_;
   int64_t ident_len_ = 0;
   int* identity(int64_t n) {  // device 0, 1, ..., n-1 (grow-only)
@@ -513,7 +516,8 @@ struct LocalKnn {
       const char* impl = std::getenv("KNN_SCREEN");
       const bool use_x1 = x1_ok && (!lds_ok || !(impl && std::string(impl) == "stream" && !hx));
       // impl: 0 x1 (single-term), 1 stream (3-term, k <= 32), 2 LDS-shared (3-term, k <= 256),
-      // 3 LDS-shared single-term on the host operands hx (k <= 256: no device image)
+      // 3 LDS-shared single-term on the host operands hx (k <= 256: no device image), 4 the
+      // two-pass single-term x1 screen on hx (k <= 256; ops/knn.py _x1k_pass)
       auto pass = [&](const std::vector<int>* idx, int impl, DevBuf<int>& qbuf) {
         const int nq = idx ? (int)idx->size() : (int)Q;
         int* qi;
@@ -553,6 +557,41 @@ struct LocalKnn {
                                      st));
           return;
         }
+        if (impl == 4) {
+          // pass 1: S1 slices at k' = ceil(k / S1) -> per-query seeds; pass 2: COLLECT at the
+          // seed into X1K_CCAP group ids per (query, slice); the large-k group refine
+          constexpr int kCcap = 1024, kS1 = 16;
+          const int S2 = slices_stream(nq, dmlp_screen_x1_cols(KT, 16), nt,
+                                       dmlp_screen_x1_waves_per_cu_kt(KT, 16),
+                                       dmlp_screen_x1_min_slices(nt));
+          const int S1 = std::max(kS1, S2);
+          int* kp = kp_h_.get(Q);
+          for (int64_t q = 0; q < Q; ++q) kp[q] = (std::max(kk[q], 1) + S1 - 1) / S1;
+          int kmax1 = 1;
+          for (int q : *idx) kmax1 = std::max(kmax1, kp[q]);
+          int* kpd = kp_d_.get(Q);
+          HIPCHK(hipMemcpyAsync(kpd, kp, Q * sizeof(int), hipMemcpyHostToDevice, st));
+          const int cap1 = dmlp_screen_x1_cap(kmax1);
+          int* i1 = k1_ids_.get((size_t)nq * S1 * cap1);
+          int* c1 = k1_cnt_.get((size_t)nq * S1);
+          float* h1 = k1_h_.get((size_t)nq * S1 * 2);
+          float* hs = k1_seed_.get(nq);
+          int* i2 = cand_ids.get((size_t)nq * S2 * kCcap);
+          int* c2 = cand_cnt.get((size_t)nq * S2);
+          float* h2 = cand_h.get((size_t)nq * S2 * 2);
+          DMLPCHK(dmlp_screen_x1(KT, 1, A, hx->xhi, hx->xin, nt, N, hx->qhi, hx->qn, qi, kpd, nq,
+                                 kmax1, hx->words, hx->words + 1, S1, i1, c1, h1, st));
+          DMLPCHK(dmlp_x1_seed(h1, c1, S1, nq, hs, st));
+          DMLPCHK(dmlp_screen_x1_collect(KT, A, hx->xhi, hx->xin, nt, N, hx->qhi, hx->qn, qi, kd,
+                                         nq, hx->words, hx->words + 1, hs, kCcap, S2, i2, c2, h2,
+                                         st));
+          wait_rows();
+          DMLPCHK(dmlp_refine_groups2(kCcap, i2, c2, h2, S2, X, A, Qx, hx->xhi, hx->xin, hx->qhi,
+                                      KT, 1, N, qi, kd, nq, out_d, out_i, kstride,
+                                      fin ? labels : nullptr, lab_lo, lab_hi, lab, cs, stat, ovf,
+                                      1, st));
+          return;
+        }
         if (impl == 3) {
           DMLPCHK(dmlp_screen_hl(KT, cap, 1, A, hx->xhi, hx->xin, nt, hx->qhi, nullptr, hx->qn, qi,
                                  kd, nq, hx->words, hx->words + 1, 0.0f, S, ci, cc, st));
@@ -579,8 +618,17 @@ struct LocalKnn {
       const char* ls = std::getenv("KNN_LDS_SINGLE");
       const int bc_impl = (hx && !(ls && std::string(ls) == "0") &&
                            dmlp_screen_waves_hl(KT, 128, 1) > 0) ? 3 : 2;
-      if (!b.empty()) pass(&b, bc_impl, qidx_b);
-      if (!c.empty()) pass(&c, bc_impl, qidx_c);
+      // ... and by the two-pass x1 screen on the same operands (KNN_X1K=0: the LDS screen)
+      const char* xk = std::getenv("KNN_X1K");
+      const bool x1k = bc_impl == 3 && x1_ok && !(xk && std::string(xk) == "0");
+      if (x1k && (!b.empty() || !c.empty())) {
+        std::vector<int> bc(b);
+        bc.insert(bc.end(), c.begin(), c.end());
+        pass(&bc, 4, qidx_b);
+      } else {
+        if (!b.empty()) pass(&b, bc_impl, qidx_b);
+        if (!c.empty()) pass(&c, bc_impl, qidx_c);
+      }
       // one host sync: the overflow count (4 bytes); the per-query status only when some
       // screened query overflowed
       int novf = 0;

@@ -119,14 +119,19 @@ struct GroupIn {
   int hl;
   int n_points;
   int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
+  int collect;            // lists of the COLLECT pass (large k): the threshold is always taken
+                          // over the lists (cand_h holds the fixed seed, not a final threshold)
 };
 
 // GROUPS = KT of the single-term screen (1, 2, 4 or 8) for group-mode input, 0 otherwise.  The group
 // variant sizes its LDS for k <= 32 (the screen's limit) and labels in [lo, lo + 256) (wider
 // label ranges take wave_vote's counting fallback), so more waves stay resident to hide the
 // gathers that dominate this kernel.
+// E = 8 with GROUPS: the large-k group variant (k <= 256 over <= 512 filtered members): its
+// top-k is one wave-wide bitonic sort of the members' exact keys, and labels are gathered at the
+// vote (no carry scratch).
 template <int E, int GROUPS, bool F16 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1 ? 8 : GROUPS ? 4 : 1))) void k_refine(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && E >= 8) ? 2 : GROUPS == 1 ? 8 : GROUPS ? 4 : 1))) void k_refine(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int S, int cap,
     const double* __restrict__ X, int A, const double* __restrict__ Qx,
     const int* __restrict__ qidx, const int* __restrict__ qk, int nq, double* __restrict__ out_d,
@@ -135,7 +140,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
     int* __restrict__ status, int* __restrict__ ovf_count, const GroupIn gin) {
   constexpr int P = E * 64;
   constexpr int SMAX = 256;
-  constexpr int KMAX = GROUPS ? 64 : 128;
+  constexpr bool GBIG = GROUPS && E >= 8;
+  constexpr int KMAX = GBIG ? 256 : GROUPS ? 64 : 128;
   constexpr int HCAP = GROUPS ? 256 : kHistCap;  // >= 256: the key histogram of the global threshold
   __shared__ double s_d[4][P];
   __shared__ int s_i[4][P];
@@ -226,8 +232,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
     };
     int* hist = s_hist[wave];
     const float eps = g_eps;
-    float hq = S == 1 ? g_h1 : -INFINITY;  // one slice: already global
-    if (S > 1 && M >= k && k >= 1) {
+    // one slice: its final threshold is already global; COLLECT lists: the fixed seed (a valid
+    // bound every slice shares), raised below to the k-th largest key over the lists
+    float hq = S == 1 || gin.collect ? g_h1 : -INFINITY;
+    if ((S > 1 || gin.collect) && M >= k && k >= 1) {
       int above = 0;
       int b1 = -1, b2 = -1;
 #pragma unroll 1
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
       }
       const unsigned T = ((unsigned)b1 << 24) | ((unsigned)b2 << 16);
       const unsigned tb = T ^ ((T >> 31) ? 0x80000000u : 0xffffffffu);  // ordered -> fp32 bits
-      hq = __uint_as_float(tb) - 2.0f * eps;
+      hq = fmaxf(hq, __uint_as_float(tb) - 2.0f * eps);
     }
     const unsigned tq = __float_as_uint(hq);
     const unsigned kh = (tq ^ ((unsigned)((int)tq >> 31) | 0x80000000u)) & 0xffff0000u;
@@ -339,12 +347,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GROUPS == 1
   // group mode: each candidate's label is gathered beside its row and travels with it (in the
   // slice-prefix scratch, dead after the member filter), so the vote reads LDS, not a final
   // dependent gather.  cl: candidates' labels [P], rl: the top-k's labels [KMAX].
-  const bool carry = GROUPS && labels != nullptr;
+  const bool carry = GROUPS && !GBIG && labels != nullptr;
   int* const cl = s_pre[wave];
   int* const rl = s_pre[wave] + P;
-  static_assert(!GROUPS || P + KMAX <= SMAX + 1, "label scratch must fit the prefix array");
+  static_assert(!GROUPS || GBIG || P + KMAX <= SMAX + 1, "label scratch must fit the prefix array");
   bool carried = false;
-  if (M <= P && k <= KMAX) {
+  if constexpr (GBIG) {
+    // M <= P filtered members (checked above): exact keys, one bitonic sort, the first k
+    double rd[E];
+    int ri[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const int j = r * 64 + lane;
+      rd[r] = INFINITY;
+      ri[r] = -1;
+      if (j < M) cand(j, rd[r], ri[r]);
+    }
+    dmlp::wave_sync();  // every member id read before the sorted keys overwrite the arrays
+    dmlp::wave_sort_keys<E>(rd, ri);
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      s_d[wave][r * 64 + lane] = rd[r];
+      s_i[wave][r * 64 + lane] = ri[r];
+    }
+    dmlp::wave_sync();
+    res_d = s_d[wave];
+    res_i = s_i[wave];
+  } else if (M <= P && k <= KMAX) {
     // rank select: keys are unique (distinct ids), so rank(i) = #{j : key_j < key_i} places
     // every member of the top-k directly at its sorted position.
     double* cd = s_d[wave];
@@ -1036,20 +1065,36 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   return 0;
 }
 
-extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt,
-                                  const float* cand_h, int S, const double* X, int A,
-                                  const double* Qx, const void* xfrag, const float* xinit,
-                                  const void* qhi, int KT, int hl, int64_t n_points, const int* qidx,
-                                  const int* qk, int nq, double* out_d, int* out_i, int kstride,
-                                  const int* labels, int label_lo, int label_hi, int* out_label,
-                                  uint64_t* out_cs, int* status, int* ovf_count, void* stream) {
+extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt,
+                                   const float* cand_h, int S, const double* X, int A,
+                                   const double* Qx, const void* xfrag, const float* xinit,
+                                   const void* qhi, int KT, int hl, int64_t n_points,
+                                   const int* qidx, const int* qk, int nq, double* out_d,
+                                   int* out_i, int kstride, const int* labels, int label_lo,
+                                   int label_hi, int* out_label, uint64_t* out_cs, int* status,
+                                   int* ovf_count, int collect, void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
   if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return -1;
   if (hl != 1 && hl != 2) return -1;
   const int64_t n_tiles = (n_points + 63) / 64;
   const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
-                    (int)((n_tiles + S - 1) / S)};
+                    (int)((n_tiles + S - 1) / S), collect ? 1 : 0};
+  // collect (the large-k lists, fp16 host operands only): k <= 256 over <= 512 filtered members
+  if (collect) {
+    if (hl != 1) return -1;
+#define DMLP_REFINE_GB(KTV)                                                                    \
+  hipLaunchKernelGGL((k_refine<8, KTV, true>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
+                     cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
+                     labels, label_lo, label_hi, out_label, out_cs, status, ovf_count, gin)
+    if (KT == 1) DMLP_REFINE_GB(1);
+    else if (KT == 2) DMLP_REFINE_GB(2);
+    else if (KT == 4) DMLP_REFINE_GB(4);
+    else DMLP_REFINE_GB(8);
+#undef DMLP_REFINE_GB
+    DMLP_LAUNCH_CHECK();
+    return 0;
+  }
 #define DMLP_REFINE_G(KTV, F16)                                                                \
   hipLaunchKernelGGL((k_refine<2, KTV, F16>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
@@ -1070,6 +1115,18 @@ extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_
 #undef DMLP_REFINE_G
   DMLP_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int dmlp_refine_groups(int cap, const int* cand_ids, const int* cand_cnt,
+                                  const float* cand_h, int S, const double* X, int A,
+                                  const double* Qx, const void* xfrag, const float* xinit,
+                                  const void* qhi, int KT, int hl, int64_t n_points, const int* qidx,
+                                  const int* qk, int nq, double* out_d, int* out_i, int kstride,
+                                  const int* labels, int label_lo, int label_hi, int* out_label,
+                                  uint64_t* out_cs, int* status, int* ovf_count, void* stream) {
+  return dmlp_refine_groups2(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xinit, qhi, KT,
+                             hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels, label_lo,
+                             label_hi, out_label, out_cs, status, ovf_count, 0, stream);
 }
 
 extern "C" int dmlp_exact_rows(const double* X, int64_t N, int A, const double* Qx,

@@ -35,7 +35,8 @@
 namespace {
 
 // profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
-// wrong results, timing only), 8 event counters (g_x1_dbg)
+// wrong results, timing only), 8 event counters (g_x1_dbg).  MODE 16 is not an ablation: the
+// COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
 
@@ -87,8 +88,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
     const unsigned* __restrict__ bad, float r1, float r2, float r3, int S, int tiles_per_slice,
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
-    float* __restrict__ cand_h) {
+    float* __restrict__ cand_h, const float* __restrict__ hseed, int ccap) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
+  // COLLECT (large k, second pass): the threshold is fixed at the query's seed hseed[p] (a
+  // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
+  // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
+  constexpr bool COLLECT = (MODE & 16) != 0;
   constexpr int CT = C::CT;
   constexpr int D = C::D;
   constexpr int NH = C::NCOL / 64;  // columns per lane in the lane-owns-column phases
@@ -142,7 +147,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const int q = valid ? qidx[p] : 0;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) bh[ct][kt] = qhi[(q * KT + kt) * 4 + kg];
-    h[ct] = valid ? -FLT_MAX : INFINITY;
+    // COLLECT: a NaN seed marks a query whose first pass failed (it reports overflow)
+    const float sd = COLLECT && valid ? hseed[p] : -FLT_MAX;
+    const bool sbad = COLLECT && sd != sd;
+    h[ct] = valid && !sbad ? (COLLECT ? fmaxf(sd, -FLT_MAX) : -FLT_MAX) : INFINITY;
     addr[ct] = (unsigned)(((ct * 16 + c) * C::CP + kg) * 4);
     lim[ct] = addr[ct] + (SUB - CHECK) * 16;
     if (lane < 16) {
@@ -152,7 +160,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       leps[col] = valid ? r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax +
                               r3 * (sqrtf(qn[q]) + sqrtf(xnmax)) + r3 * 0x1p-15f
                         : 0.0f;
-      lflag[col] = 0;
+      lflag[col] = sbad ? 1 : 0;
     }
   }
   // slice-local buffer resources: step j's fragments sit at j * KT * hl KiB (hi at +0, lo — when
@@ -170,6 +178,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // A column's entries are interleaved: slot s holds entry s >> 2 of sub-buffer s & 3, so the
   // lane reads its column as 16-byte vectors and re-deals the survivors by writing them back at
   // consecutive slots (slot s -> sub-buffer s & 3 again, i.e. round-robin).
+  int nout[NH];  // COLLECT: group entries this lane's column has flushed so far
+#pragma unroll
+  for (int hb = 0; hb < NH; ++hb) nout[hb] = 0;
   auto compact = [&](const bool final_pass) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = (int)(addr[ct] - (lim[ct] - (SUB - CHECK) * 16)) >> 4;
@@ -180,6 +191,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     unsigned* const colbuf = sbuf + j * C::CP;
     const int4 n4 = *(const int4*)(lcnt + j * 4);
     const int nm[4] = {n4.x, n4.y, n4.z, n4.w};
+    if constexpr (COLLECT) {
+      // flush: every buffered entry (appended at a group max >= the fixed seed) goes to the
+      // column's global list as (ordered 16-bit key << 16 | slice-relative group index)
+      const int pc = pbase + j;
+      bool ov = lflag[j] != 0;
+      int no = nout[hb];
+      int* const out = cand_ids + ((int64_t)pc * S + s) * ccap;
+      if (pc < nq && !ov) {
+#pragma unroll
+        for (int v = 0; v < SUB; ++v) {
+          const u32x4 raw = *(const u32x4*)(colbuf + 4 * v);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            if (v < nm[m]) {
+              if (no < ccap) out[no] = (int)((ord32(raw[m]) & 0xffff0000u) | (raw[m] & 0xffffu));
+              ++no;
+            }
+          }
+        }
+        ov = no > ccap;
+      }
+      nout[hb] = no;
+      if (!final_pass) {
+        *(int4*)(lcnt + j * 4) = int4{0, 0, 0, 0};
+        if (ov) { lh[j] = INFINITY; lflag[j] = 1; }  // stop appending: the query overflowed
+      } else if (pc < nq) {
+        cand_cnt[(int64_t)pc * S + s] = ov ? -1 : no;
+        cand_h[2 * ((int64_t)pc * S + s)] = lh[j];
+        cand_h[2 * ((int64_t)pc * S + s) + 1] = leps[j];
+      }
+      continue;
+    }
     const int kc = lk[j];
     const float epc = leps[j];
     const int flag = lflag[j];
@@ -433,7 +476,8 @@ template <int KT, int SUB, int DEPTH, int CHECK, int CTV, bool F16>
 int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, float r3, int S,
-              int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream) {
+              int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream,
+              const float* hseed = nullptr, int ccap = 0) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
@@ -443,9 +487,12 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
   hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M, F16>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
-                     n_qblocks, hl, cand_ids, cand_cnt, cand_h)
-  // ablation modes only for the A <= 64 variants (each mode is a full kernel instantiation)
-  if constexpr (KT <= 2) {
+                     n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap)
+  if (hseed) {  // the COLLECT pass (SUB = 16, CT = 4, fp16 only: see dmlp_screen_x1_collect)
+    if constexpr (SUB == 16 && CTV == 4 && F16) DMLP_X1_LAUNCH(16);
+    else return -3;
+  } else if constexpr (KT <= 2) {
+    // ablation modes only for the A <= 64 variants (each mode is a full kernel instantiation)
     switch (g_x1_mode) {
       case 1: DMLP_X1_LAUNCH(1); break;
       case 2: DMLP_X1_LAUNCH(2); break;
@@ -523,6 +570,66 @@ extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
     if (e != hipSuccess) return -(int)e;
   }
   return 0;
+}
+
+// ---- large k (32 < k <= 256) on the single-term screen, in two passes over the host's fp16
+// operands: (1) dmlp_screen_x1 over S1 data slices with k' = ceil(k / S1) <= 16 per query (the
+// cheap SUB = 16 variant) leaves each slice's final threshold h_s = a'_s - 2 eps (a'_s <= the
+// k'-th best approximate score of the slice); since S1 k' >= k, the k-th best exact score over all
+// slices is >= min_s (a'_s - eps), so hseed = min_s h_s keeps every true top-k member (any approx
+// score >= exact - eps).  (2) dmlp_screen_x1_collect re-screens everything at that fixed threshold
+// and flushes the passing 4-row groups to per-(query, slice) global lists; the group refine
+// (dmlp_refine_groups2, collect = 1) takes the k-th largest group key over the lists.
+__global__ __launch_bounds__(256) void k_x1_seed(const float* __restrict__ cand_h,
+                                                 const int* __restrict__ cand_cnt, int S1, int nq,
+                                                 float* __restrict__ hseed) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= nq) return;
+  float m = INFINITY;
+  bool bad = false;
+  for (int s = 0; s < S1; ++s) {
+    bad |= cand_cnt[(int64_t)p * S1 + s] < 0;  // overflowed: its threshold is lost
+    m = fminf(m, cand_h[2 * ((int64_t)p * S1 + s)]);
+  }
+  hseed[p] = bad ? __builtin_nanf("") : m;
+}
+
+extern "C" int dmlp_x1_seed(const float* cand_h, const int* cand_cnt, int S1, int nq,
+                            float* hseed, void* stream) {
+  if (nq <= 0) return 0;
+  if (S1 < 1) return -1;
+  hipLaunchKernelGGL(k_x1_seed, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, cand_h, cand_cnt, S1, nq, hseed);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+// The COLLECT pass over the host's fp16 image (hl = 1): hseed[p] per query position p (NaN: the
+// query reports overflow), ccap group ids per (query, slice); cand_cnt = -1 past ccap.
+extern "C" int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
+                                      int64_t n_tiles, int64_t n_points, const void* qhi,
+                                      const float* qn, const int* qidx, const int* qk, int nq,
+                                      const unsigned* xnmax_bits, const unsigned* bad,
+                                      const float* hseed, int ccap, int S, int* cand_ids,
+                                      int* cand_cnt, float* cand_h, void* stream) {
+  if (nq <= 0) return 0;
+  if (!hseed || ccap < 1 || S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 ||
+      n_points > n_tiles * 64)
+    return -1;
+  if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
+  if (!x1_kt_ok(KT) || A > KT * 32) return -3;
+  float r1, r2, r3;
+  dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
+  hipStream_t st = (hipStream_t)stream;
+#define DMLP_X1C(KTV)                                                                           \
+  return launch_x1<KTV, 16, 4, 2, 4, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx,   \
+                                          qk, nq, xnmax_bits, bad, r1, r2, r3, S, cand_ids,    \
+                                          cand_cnt, cand_h, st, hseed, ccap)
+  if (KT == 1) DMLP_X1C(1);
+  if (KT == 2) DMLP_X1C(2);
+  if (KT == 4) DMLP_X1C(4);
+  DMLP_X1C(8);
+#undef DMLP_X1C
 }
 
 extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit,

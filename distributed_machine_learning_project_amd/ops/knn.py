@@ -52,6 +52,12 @@ ROWS_I32 = os.environ.get("DMLP_ROWS_I32", "1") != "0"
 # fp16 operands when the host rendered them (no device hi/lo image, a third of the MFMA work);
 # its overflows escalate to the 3-term LDS screen.  DMLP_LDS_SINGLE=0: always 3-term (A/B)
 LDS_SINGLE = os.environ.get("DMLP_LDS_SINGLE", "1") != "0"
+# ... and, on the same operands, by the two-pass single-term x1 screen instead (screen_x1.hip:
+# per-query seeds from S1 slices at k' = ceil(k / S1), then one COLLECT pass at that fixed
+# threshold; refine over <= X1K_CCAP groups per query and slice).  DMLP_X1K=0: the LDS screen
+X1K = os.environ.get("DMLP_X1K", "1") != "0"
+X1K_S1 = 16        # first-pass slices: k' = ceil(k / 16) <= 16 for k <= 256 (the SUB = 16 variant)
+X1K_CCAP = 1024    # COLLECT group ids per (query, slice)
 
 
 def screen_kt(A: int) -> int:
@@ -382,6 +388,11 @@ class _KnnCall:
         self.single_bc = (LDS_SINGLE and ds.hl == 1 and self.prepped is not None
                           and L.dmlp_screen_waves_hl(KT, 128, 1) > 0)
         lds_impl = "lds1" if self.single_bc else "lds"
+        if self.single_bc and X1K and L.dmlp_screen_x1_qw(KT) > 0 and (len(self.cls_b)
+                                                                       or len(self.cls_c)):
+            # both k > 32 classes in one two-pass x1 screen
+            self._screen_pass(np.concatenate([self.cls_b, self.cls_c]), "x1k")
+            return self
         if len(self.cls_b):
             self._screen_pass(self.cls_b, lds_impl)
         if len(self.cls_c):
@@ -423,7 +434,7 @@ class _KnnCall:
 
     def _screen_pass(self, idx, impl):
         torch = _torch()
-        if impl not in ("x1", "lds1") and self.qlo is None:
+        if impl not in ("x1", "lds1", "x1k") and self.qlo is None:
             self._prep_on_device()  # 3-term class / escalation after a host-prepared x1 pass
         L = _lib.lib()
         ds, kk, A, KT, dev = self.ds, self.kk, self.A, self.ds.KT, self.dev
@@ -447,6 +458,8 @@ class _KnnCall:
             S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), ds.n_tiles,
                                       L.dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                       int(L.dmlp_screen_x1_min_slices(ds.n_tiles)), cus)
+        elif impl == "x1k":
+            cap = S = 0  # (_x1k_pass sizes its own buffers)
         elif impl == "stream":
             cap = L.dmlp_screen_stream_cap(kcls)
             S = _choose_slices_stream(nq, L.dmlp_screen_stream_qw(KT), ds.n_tiles,
@@ -455,7 +468,7 @@ class _KnnCall:
             cap = (128 if kcls <= SCREEN_KMAX_A else 256 if kcls <= SCREEN_KMAX_B else 512)
             S = _choose_slices(nq, L.dmlp_screen_waves_hl(KT, cap, 1 if impl == "lds1" else 2),
                                ds.n_tiles)
-        if pre is None:
+        if pre is None and impl != "x1k":
             cand_ids = torch.empty(nq * S * cap, dtype=torch.int32, device=dev)
             cand_cnt = torch.empty(nq * S, dtype=torch.int32, device=dev)
         fin = (_p(ds.labels) if self.want_fin else None, ds.label_lo, ds.label_hi, _p(self.lab),
@@ -495,6 +508,9 @@ class _KnnCall:
             _mark("refine_done")
             self._keep = (qidx, cand_ids, cand_cnt, cand_h)
             return
+        if impl == "x1k":
+            self._x1k_pass(idx, qidx, nq, kcls, cus, fin, s)
+            return
         if impl == "lds1":
             # single term on the host's fp16 image + query fragments: nothing rendered on the
             # device, the refine alone waits for the fp64 rows
@@ -531,6 +547,46 @@ class _KnnCall:
                                  _p(qidx), _p(self.kdev_eff), nq, _p(self.out_d), _p(self.out_i),
                                  self.ks, *fin), "refine")
         self._keep = (qidx, cand_ids, cand_cnt)
+
+    def _x1k_pass(self, idx, qidx, nq, kcls, cus, fin, s):
+        """k in (32, 256] on the single-term screen in two passes over the host's fp16 operands
+        (screen_x1.hip dmlp_x1_seed / dmlp_screen_x1_collect) and the large-k group refine;
+        overflowing queries report status 1 (finish() escalates them to the 3-term screen)."""
+        torch = _torch()
+        L = _lib.lib()
+        ds, A, KT, dev, N = self.ds, self.A, self.ds.KT, self.dev, self.ds.N
+        x1_qhi, x1_qn = self.prepped
+        n_tiles = ds.n_tiles
+        s_min = int(L.dmlp_screen_x1_min_slices(n_tiles))
+        S2 = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, 16), n_tiles,
+                                   L.dmlp_screen_x1_waves_per_cu_kt(KT, 16), s_min, cus)
+        S1 = max(X1K_S1, S2)
+        kp = -(-np.maximum(self.kk, 1) // S1)  # k' = ceil(k / S1) per query row (<= 16)
+        kp_dev = _h2d(kp.astype(np.int32), dev)
+        kmax1 = int(kp[idx].max()) if idx is not None else int(kp.max())
+        cap1 = L.dmlp_screen_x1_cap(kmax1)
+        ids1 = torch.empty(nq * S1 * cap1, dtype=torch.int32, device=dev)
+        cnt1 = torch.empty(nq * S1, dtype=torch.int32, device=dev)
+        h1 = torch.empty(nq * S1 * 2, dtype=torch.float32, device=dev)
+        hseed = torch.empty(nq, dtype=torch.float32, device=dev)
+        ids2 = torch.empty(nq * S2 * X1K_CCAP, dtype=torch.int32, device=dev)
+        cnt2 = torch.empty(nq * S2, dtype=torch.int32, device=dev)
+        h2 = torch.empty(nq * S2 * 2, dtype=torch.float32, device=dev)
+        self._fill_outputs()
+        _lib.check(L.dmlp_screen_x1(KT, 1, A, _p(ds.xfrag), _p(ds.xinit), n_tiles, N, _p(x1_qhi),
+                                    _p(x1_qn), _p(qidx), _p(kp_dev), nq, kmax1, _p(ds.xnmax_bits),
+                                    _p(ds.bad), S1, _p(ids1), _p(cnt1), _p(h1), s), "screen_x1 seed pass")
+        _lib.check(L.dmlp_x1_seed(_p(h1), _p(cnt1), S1, nq, _p(hseed), s), "x1_seed")
+        _lib.check(L.dmlp_screen_x1_collect(KT, A, _p(ds.xfrag), _p(ds.xinit), n_tiles, N,
+                                            _p(x1_qhi), _p(x1_qn), _p(qidx), _p(self.kdev_eff), nq,
+                                            _p(ds.xnmax_bits), _p(ds.bad), _p(hseed), X1K_CCAP, S2,
+                                            _p(ids2), _p(cnt2), _p(h2), s), "screen_x1_collect")
+        self._wait_qx()
+        _lib.check(L.dmlp_refine_groups2(
+            X1K_CCAP, _p(ids2), _p(cnt2), _p(h2), S2, _p(ds.X), A, _p(self.Qx), _p(ds.xfrag),
+            _p(ds.xinit), _p(x1_qhi), KT, 1, N, _p(qidx), _p(self.kdev_eff), nq, _p(self.out_d),
+            _p(self.out_i), self.ks, *fin[:-1], 1, fin[-1]), "refine_groups2")
+        self._keep = (qidx, kp_dev, ids1, cnt1, h1, hseed, ids2, cnt2, h2)
 
     # ------------------------------------------------------------------ finish (one sync)
     def finish(self) -> DeviceResult:

@@ -242,3 +242,8 @@ def test_fast_path_serves_any_k_and_escalates_per_query(tmp_path):
     phases = [l.split()[3] for l in err.splitlines() if l.startswith("[dmlp-trace]")]
     assert "h2d_operands" in phases and "knn" in phases, phases  # the fast path, not "compute"
     assert "distribute" not in phases
+    # k > 32 on the single-term LDS screen (KNN_X1K=0) and on the 3-term one only (A/B paths of
+    # the default two-pass x1 screen): the same bytes
+    for env in ({"KNN_X1K": "0"}, {"KNN_X1K": "0", "KNN_LDS_SINGLE": "0"}):
+        out, _ = _run(["--strategy", "farm"], path, env=env)
+        assert out == dmlp.format_report(cs)

@@ -438,14 +438,20 @@ def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
 
 
-@pytest.mark.parametrize("A,dup,single", [(32, 0, True), (100, 0, True), (256, 0, True),
-                                          (32, 700, True), (64, 0, False)])
-def test_pipelined_single_term_lds(torch_cuda, A, dup, single, monkeypatch):
-    """k in (32, 256] on the single-term LDS screen over the host's fp16 operands (HL = 1) —
-    with `dup` copies of one point, the queries sitting on it overflow the single-term bound and
-    escalate to the 3-term LDS screen; single=False is the 3-term-only A/B path.  Bit-exact."""
+@pytest.mark.parametrize("A,dup,single,x1k", [(32, 0, True, False), (100, 0, True, False),
+                                              (256, 0, True, False), (32, 700, True, False),
+                                              (64, 0, False, False), (32, 0, True, True),
+                                              (100, 0, True, True), (256, 0, True, True),
+                                              (32, 700, True, True)])
+def test_pipelined_single_term_lds(torch_cuda, A, dup, single, x1k, monkeypatch):
+    """k in (32, 256] on the single-term LDS screen over the host's fp16 operands (HL = 1), or
+    (x1k) the two-pass single-term x1 screen (seeds from 16 slices at k' = ceil(k / 16), one
+    COLLECT pass, the large-k group refine) — with `dup` copies of one point, the queries sitting
+    on it overflow the single-term bound and escalate to the 3-term LDS screen; single=False is
+    the 3-term-only A/B path.  Bit-exact."""
     torch = torch_cuda
     monkeypatch.setattr(K, "LDS_SINGLE", single)
+    monkeypatch.setattr(K, "X1K", x1k)
     rng = np.random.default_rng(A + dup)
     N, Q = 9000, 400
     X = np.round(rng.uniform(0, 1000, (N, A)), 6)
