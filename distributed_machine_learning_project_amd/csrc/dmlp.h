@@ -204,7 +204,7 @@ int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt, const
                         int collect, void* stream);
 
 // Large k on the single-term screen (screen_x1.hip): first-pass thresholds (S1 slices, k' =
-// ceil(k / S1)) -> per-query seeds (NaN: a slice overflowed), then the COLLECT pass at those
+// ceil(k / S1)) -> per-query seeds (+inf: a slice overflowed), then the COLLECT pass at those
 // fixed thresholds into ccap group ids per (query, slice).
 int dmlp_x1_seed(const float* cand_h, const int* cand_cnt, int S1, int nq, float* hseed,
                  void* stream);

@@ -35,7 +35,8 @@
 namespace {
 
 // profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
-// wrong results, timing only), 8 event counters (g_x1_dbg).  MODE 16 is not an ablation: the
+// wrong results, timing only), 8 event counters (g_x1_dbg), 32 appends without the any-hit
+// branch (A/B: a constant count of LDS ops per step, so no over-wait on lgkmcnt).  MODE 16 is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
@@ -147,9 +148,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const int q = valid ? qidx[p] : 0;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) bh[ct][kt] = qhi[(q * KT + kt) * 4 + kg];
-    // COLLECT: a NaN seed marks a query whose first pass failed (it reports overflow)
+    // COLLECT: a +inf seed marks a query whose first pass failed (it reports overflow; no real
+    // seed is +inf).  (Not NaN: this file is built with -fno-honor-nans.)
     const float sd = COLLECT && valid ? hseed[p] : -FLT_MAX;
-    const bool sbad = COLLECT && sd != sd;
+    const bool sbad = COLLECT && sd == INFINITY;
     h[ct] = valid && !sbad ? (COLLECT ? fmaxf(sd, -FLT_MAX) : -FLT_MAX) : INFINITY;
     addr[ct] = (unsigned)(((ct * 16 + c) * C::CP + kg) * 4);
     lim[ct] = addr[ct] + (SUB - CHECK) * 16;
@@ -342,14 +344,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   bf16x8 A[D][KT];
   f32x4 Xi[D];
   f32x4 acc[2][CT];
-#define DMLP_LOAD(J, R)                                                                         \
+#define DMLP_LOADA(J, R)                                                                        \
   do {                                                                                          \
     _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
       A[R][kt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(              \
           xr, lane * 16 + kt * ks, (J) * (KT * ks), 0));                                        \
+  } while (0)
+#define DMLP_LOADX(J, R)                                                                        \
+  do {                                                                                          \
     if (!(MODE & 4))                                                                            \
       Xi[R] = *(__attribute__((address_space(3))) const f32x4*)(size_t)(                        \
           xrb + (((J) >> 2) & 1) * 256 + ((J) & 3) * 64 + kg * 16);                             \
+  } while (0)
+#define DMLP_LOAD(J, R)                                                                         \
+  do {                                                                                          \
+    DMLP_LOADA(J, R);                                                                           \
+    DMLP_LOADX(J, R);                                                                           \
   } while (0)
 #define DMLP_MFMA(R, AB)                                                                        \
   do {                                                                                          \
@@ -372,7 +382,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     if (MODE & 8) {                                                                             \
       if (lane == 0) atomicAdd(&g_x1_dbg[0], 1ull);                                             \
     }                                                                                           \
-    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && __ballot(any_)) {                        \
+    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && ((MODE & 32) || __ballot(any_))) {        \
       if (MODE & 8) {                                                                           \
         int np_ = 0;                                                                            \
         _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += hit_[ct] ? 1 : 0;              \
@@ -437,12 +447,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
           xw = xwin((j0 >> 2) + 2);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
-        DMLP_LOAD(j + D, r);
+        // MODE 64 (A/B): the C-operand read after this step's appends, so the count-based
+        // lgkmcnt wait at the next step's top does not cover the appends issued after it
+        if (MODE & 64) DMLP_LOADA(j + D, r);
+        else DMLP_LOAD(j + D, r);
         if (MODE & 2) {  // ablation: keep every MFMA result alive, no epilogue at all
           _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[r & 1][ct]));
         } else if (j > 0) {
           DMLP_EPILOGUE((r + 1) & 1, j - 1);
         }
+        if (MODE & 64) DMLP_LOADX(j + D, r);
         if (r % CHECK == CHECK - 1) DMLP_CHECK();
       }
     }
@@ -451,6 +465,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     DMLP_EPILOGUE(jl & 1, jl);
   }
 #undef DMLP_LOAD
+#undef DMLP_LOADA
+#undef DMLP_LOADX
 #undef DMLP_MFMA
 #undef DMLP_EPILOGUE
 #undef DMLP_CHECK
@@ -499,6 +515,9 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 4: DMLP_X1_LAUNCH(4); break;
       case 6: DMLP_X1_LAUNCH(6); break;
       case 8: DMLP_X1_LAUNCH(8); break;
+      case 32: DMLP_X1_LAUNCH(32); break;  // A/B: appends without the any-hit branch
+      case 64: DMLP_X1_LAUNCH(64); break;  // A/B: C-operand LDS read after the appends
+      case 96: DMLP_X1_LAUNCH(96); break;
       default: DMLP_X1_LAUNCH(0); break;
     }
   } else {
@@ -591,7 +610,7 @@ __global__ __launch_bounds__(256) void k_x1_seed(const float* __restrict__ cand_
     bad |= cand_cnt[(int64_t)p * S1 + s] < 0;  // overflowed: its threshold is lost
     m = fminf(m, cand_h[2 * ((int64_t)p * S1 + s)]);
   }
-  hseed[p] = bad ? __builtin_nanf("") : m;
+  hseed[p] = bad ? INFINITY : m;  // +inf: the COLLECT pass reports the query as overflowed
 }
 
 extern "C" int dmlp_x1_seed(const float* cand_h, const int* cand_cnt, int S1, int nq,
@@ -604,7 +623,7 @@ extern "C" int dmlp_x1_seed(const float* cand_h, const int* cand_cnt, int S1, in
   return 0;
 }
 
-// The COLLECT pass over the host's fp16 image (hl = 1): hseed[p] per query position p (NaN: the
+// The COLLECT pass over the host's fp16 image (hl = 1): hseed[p] per query position p (+inf: the
 // query reports overflow), ccap group ids per (query, slice); cand_cnt = -1 past ccap.
 extern "C" int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
                                       int64_t n_tiles, int64_t n_points, const void* qhi,
