@@ -35,8 +35,7 @@
 namespace {
 
 // profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
-// wrong results, timing only), 8 event counters (g_x1_dbg), 32 appends without the any-hit
-// branch (A/B: a constant count of LDS ops per step, so no over-wait on lgkmcnt).  MODE 16 is not an ablation: the
+// wrong results, timing only), 8 event counters (g_x1_dbg).  MODE 16 is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
@@ -382,7 +381,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     if (MODE & 8) {                                                                             \
       if (lane == 0) atomicAdd(&g_x1_dbg[0], 1ull);                                             \
     }                                                                                           \
-    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && ((MODE & 32) || __ballot(any_))) {        \
+    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && __ballot(any_)) {                        \
       if (MODE & 8) {                                                                           \
         int np_ = 0;                                                                            \
         _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += hit_[ct] ? 1 : 0;              \
@@ -447,16 +446,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
           xw = xwin((j0 >> 2) + 2);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
-        // MODE 64 (A/B): the C-operand read after this step's appends, so the count-based
-        // lgkmcnt wait at the next step's top does not cover the appends issued after it
-        if (MODE & 64) DMLP_LOADA(j + D, r);
-        else DMLP_LOAD(j + D, r);
+        DMLP_LOAD(j + D, r);
         if (MODE & 2) {  // ablation: keep every MFMA result alive, no epilogue at all
           _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) asm volatile("" ::"v"(acc[r & 1][ct]));
         } else if (j > 0) {
           DMLP_EPILOGUE((r + 1) & 1, j - 1);
         }
-        if (MODE & 64) DMLP_LOADX(j + D, r);
         if (r % CHECK == CHECK - 1) DMLP_CHECK();
       }
     }
@@ -515,9 +510,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 4: DMLP_X1_LAUNCH(4); break;
       case 6: DMLP_X1_LAUNCH(6); break;
       case 8: DMLP_X1_LAUNCH(8); break;
-      case 32: DMLP_X1_LAUNCH(32); break;  // A/B: appends without the any-hit branch
-      case 64: DMLP_X1_LAUNCH(64); break;  // A/B: C-operand LDS read after the appends
-      case 96: DMLP_X1_LAUNCH(96); break;
+
       default: DMLP_X1_LAUNCH(0); break;
     }
   } else {
