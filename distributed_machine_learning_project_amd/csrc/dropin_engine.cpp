@@ -17,14 +17,9 @@
 //   * -DDEBUG build (engine.debug, Makefile:14-15 compiles this file with -DDEBUG as well):
 //     every query's sorted (distance, id) list and label go to the harness's reportResult, which
 //     prints the DEBUG listing itself (common.cpp:72-78).
-#include <fcntl.h>
 #include <mpi.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
 
 #include <atomic>
-#include <cstring>
 #include <chrono>
 #include <cstdio>
 #include <fstream>
@@ -160,62 +155,13 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
   if (bad) throw std::runtime_error("data point or query with wrong attribute count");
 }
 
-// The report is one contiguous block.  When stdout is a regular file (the reference's runner
-// redirects it: run_bench.sh:82-84) the render pool copies it into the file's pages through a
-// shared mapping of a second descriptor on the same file (page faults and page-cache copies on
-// every worker instead of one write() on this thread: ~0.8 ms for 6 MB otherwise), the blocks
-// reserved first so a full disk fails here instead of faulting; stdout's offset then moves past
-// it.  Anything else (a pipe, a terminal, O_APPEND, small reports, KNN_MMAP_STDOUT=0) and any
-// failure take std::cout.write: the bytes are the same either way.
-bool write_stdout_mapped(const char* text, size_t len) {
-  const char* env = getenv("KNN_MMAP_STDOUT");  // 0: never, force: any size (tests)
-  const std::string mode = env ? env : "";
-  if (mode == "0" || (len < (size_t(1) << 20) && mode != "force") || len == 0) return false;
-  struct stat st;
-  if (fstat(1, &st) != 0 || !S_ISREG(st.st_mode)) return false;
-  const int fl = fcntl(1, F_GETFL);
-  if (fl < 0 || (fl & O_APPEND)) return false;
-  std::cout.flush();
-  const off_t off = lseek(1, 0, SEEK_CUR);
-  if (off < 0) return false;
-  const int fd = open("/proc/self/fd/1", O_RDWR);
-  if (fd < 0) return false;
-  bool ok = posix_fallocate(fd, off, (off_t)len) == 0;
-  const off_t base = off & ~(off_t)4095;
-  const size_t span = (size_t)(off - base) + len;
-  char* m = nullptr;
-  if (ok) {
-    void* v = mmap(nullptr, span, PROT_WRITE, MAP_SHARED, fd, base);
-    ok = v != MAP_FAILED;
-    if (ok) m = (char*)v;
-  }
-  if (ok) {
-    char* dst = m + (off - base);
-    auto work = [&](int t, int nt) {
-      const size_t a = (len * t / nt) & ~size_t(4095), b = t + 1 == nt ? len : (len * (t + 1) / nt) & ~size_t(4095);
-      if (b > a) std::memcpy(dst + a, text + a, b - a);
-    };
-    using Work = decltype(work);
-    dmlp_host_pool_run([](void* c, int t, int nt) { (*(Work*)c)(t, nt); }, &work);
-    ok = munmap(m, span) == 0;
-  }
-  close(fd);
-  if (!ok) {
-    lseek(1, off, SEEK_SET);  // (nothing visible past off is trusted: rewrite it in one piece)
-    return false;
-  }
-  if (lseek(1, off + (off_t)len, SEEK_SET) != off + (off_t)len) return false;
-  if (getenv("KNN_TRACE")) fprintf(stderr, "[dmlp-io] report: %zu bytes by mapped write\n", len);
-  return true;
-}
-
 // The GPU report uses the query's index as its id; the harness numbers queries by index too
 // (common.cpp:110).  Any other numbering gets its ids rewritten line by line.
 void write_report(const char* text, size_t len, const std::vector<Query>& queries) {
   bool identity = true;
   for (size_t i = 0; i < queries.size() && identity; ++i) identity = queries[i].id == (int)i;
   if (identity) {
-    if (!write_stdout_mapped(text, len)) std::cout.write(text, (std::streamsize)len);
+    std::cout.write(text, (std::streamsize)len);
     return;
   }
   size_t pos = 0;

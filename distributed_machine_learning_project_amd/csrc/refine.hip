@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
         qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KTG * 4 + f]);
     }
     g_eps = gin.cand_h[2 * (int64_t)p * S + 1];
-    g_h1 = gin.cand_h[2 * (int64_t)p];
+    g_h1 = gin.cand_h[2 * (int64_t)p * S];  // slice 0's (COLLECT: every slice holds the seed)
     if (S == 1 && lane < cap) ebuf = (unsigned)cand_ids[(int64_t)p * cap + lane];
   }
   // prefix of candidate counts over slices (S <= SMAX)

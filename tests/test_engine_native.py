@@ -136,28 +136,6 @@ def test_dropin_engine_h_cpu(tmp_path):
         assert _run_dropin(exe, path, {"KNN_DEVICE": "cpu"}, np_=2) == dmlp.format_report(cs)
 
 
-def test_dropin_report_to_regular_file(tmp_path):
-    """stdout redirected to a regular file (as run_bench.sh does): the report goes through the
-    parallel mapped write (KNN_MMAP_STDOUT=force: any size) after bytes the harness already
-    wrote, and the file holds exactly the oracle's bytes; a pipe and KNN_MMAP_STDOUT=0 take
-    the plain write."""
-    path, inp, res, lab, cs = _case(tmp_path, N=900, Q=70)
-    exe = _dropin(tmp_path)
-    expect = dmlp.format_report(cs)
-    for mode in ("force", "0"):
-        out = tmp_path / f"out_{mode}.txt"
-        with open(out, "wb") as fo:
-            fo.write(b"prefix\n")  # stdout's offset is not 0 when the engine writes
-            fo.flush()
-            with open(path, "rb") as fin:
-                r = subprocess.run([exe], stdin=fin, stdout=fo, stderr=subprocess.PIPE,
-                                   timeout=180, env=dict(os.environ, KNN_DEVICE="cpu",
-                                                         KNN_MMAP_STDOUT=mode, KNN_TRACE="1"))
-        assert r.returncode == 0, r.stderr.decode()
-        assert out.read_bytes() == b"prefix\n" + expect
-        assert (b"by mapped write" in r.stderr) == (mode == "force"), r.stderr.decode()[-500:]
-
-
 def test_dropin_engine_h_debug_cpu(tmp_path):
     path, inp, res, lab, cs = _case(tmp_path, N=200, Q=9, kmax=7)
     out = _run_dropin(_dropin(tmp_path, debug=True), path, {"KNN_DEVICE": "cpu"})

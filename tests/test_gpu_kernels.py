@@ -475,6 +475,24 @@ def test_pipelined_single_term_lds(torch_cuda, A, dup, single, x1k, monkeypatch)
     assert nfb <= (1 if dup else 0)
 
 
+def test_pipelined_x1k_small_block(torch_cuda):
+    """Few k > 32 queries against a small dataset (N = 3000, A = 16): the two-pass x1 screen's
+    COLLECT lists span many data slices (S2 > 1), where the refine must take each query's own
+    seed (slice 0 of its lists) — reading another list's seed dropped true neighbours."""
+    torch = torch_cuda
+    inp = dmlp.parse_input(dmlp.generate_text(3000, 301, 16, 0, 1000, 1, 40, 5, seed=11))
+    for a, b in ((0, 151), (151, 301)):
+        Qx, k = np.ascontiguousarray(inp.Qx[a:b]), np.ascontiguousarray(inp.k[a:b])
+        Xp = torch.from_numpy(inp.X).pin_memory().numpy()
+        Qp = torch.from_numpy(Qx).pin_memory().numpy()
+        ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 5), Qp, k)
+        torch.cuda.synchronize()
+        d_ref, i_ref = K.knn_cpu(inp.X, Qx, k, kstride=d.shape[1])
+        _, cs_ref = K.finalize_cpu(i_ref, k, inp.labels)
+        np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
+        np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
 @pytest.mark.parametrize("A,kmax", [(65, 16), (100, 32), (128, 16), (129, 16), (200, 30),
                                     (256, 16)])
 def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
