@@ -127,9 +127,35 @@ def _torch():
     return torch
 
 
+_RAW_STREAM = []
+
+
 def _stream():
+    """The current stream's raw handle, without building a torch Stream object (a per-call hot
+    path: ~15 uses per pipelined call)."""
     torch = _torch()
+    if not _RAW_STREAM:
+        f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        _RAW_STREAM.append(f)
+    f = _RAW_STREAM[0]
+    if f is not None:
+        return f(torch.cuda.current_device())
     return torch.cuda.current_stream().cuda_stream
+
+
+_SCRATCH = {}
+
+
+def _scratch(name, numel, dtype, dev):
+    """Grow-only device scratch reused across calls (never returned to callers): every
+    pipelined call has completed on the device before it returns, so the next call may reuse
+    its buffers.  Saves the per-call allocator round trips of the operand images."""
+    torch = _torch()
+    key = (name, str(dev), dtype)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < numel:
+        t = _SCRATCH[key] = torch.empty(max(numel, 1), dtype=dtype, device=dev)
+    return t[:numel]
 
 
 def _p(t):
@@ -416,7 +442,7 @@ class _KnnCall:
                                        _p(self.qlo), _p(self.qn), _p(ds.bad), _stream()),
                    "prep_queries")
 
-    def x1_buffers(self):
+    def x1_buffers(self, slot: int = 0):
         """Candidate buffers + slice count of this call's all-queries x1 pass, for a screen that
         dmlp_host_ops_x1_parts queues natively; launch() then only adds the refine."""
         torch = _torch()
@@ -427,9 +453,10 @@ class _KnnCall:
         S = _choose_slices_stream(nq, L.dmlp_screen_x1_cols(KT, kcls), self.ds.n_tiles,
                                   L.dmlp_screen_x1_waves_per_cu_kt(KT, kcls),
                                   int(L.dmlp_screen_x1_min_slices(self.ds.n_tiles)), cus)
-        self.pre_screen = (torch.empty(nq * S * cap, dtype=torch.int32, device=self.dev),
-                           torch.empty(nq * S, dtype=torch.int32, device=self.dev),
-                           torch.empty(nq * S * 2, dtype=torch.float32, device=self.dev), S)
+        # (scratch: one all-queries x1 pass per pipelined call, complete before it returns)
+        self.pre_screen = (_scratch(f"x1_ids{slot}", nq * S * cap, torch.int32, self.dev),
+                           _scratch(f"x1_cnt{slot}", nq * S, torch.int32, self.dev),
+                           _scratch(f"x1_h{slot}", nq * S * 2, torch.float32, self.dev), S)
         return self.pre_screen
 
     def _screen_pass(self, idx, impl):
@@ -774,6 +801,13 @@ def io_bytes(reset: bool = False):
 
 _SIDE_STREAMS = {}
 _PIPE_DEBUG = os.environ.get("DMLP_PIPE_DEBUG") == "1"
+_HT = []  # DMLP_PIPE_DEBUG: host-side (phase, perf_counter) stamps of the current call
+_HT_PREV = [None]  # the previous call's "synced" stamp (the host gap between calls)
+
+
+def _ht(name):
+    if _PIPE_DEBUG:
+        _HT.append((name, time.perf_counter()))
 
 # DMLP_PIPE_EVENTS=1: GPU timestamps (hipEvents) at the phase boundaries of knn_gpu_pipelined,
 # read after the call's sync — a step timeline without a profiler (no host syncs added).
@@ -859,13 +893,20 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     by world) and one all-gather over xGMI completes the image before the screen; the max norm
     is max-reduced (+inf from a rank whose rows are outside the screen's range: every rank then
     takes the device path's exact fallbacks together, no rank-dependent branch).
-    Returns (DeviceDataset, dist, ids, label, checksum, n_fallback)."""
+    Returns (DeviceDataset, dist, ids, label, checksum, n_fallback); the DeviceDataset's device
+    arrays (operand images, fp64 rows) are scratch reused by the next pipelined call, the
+    result tensors are the caller's."""
     torch = _torch()
     L = _lib.lib()
     dev = torch.device("cuda", torch.cuda.current_device())
     main = torch.cuda.current_stream()
     copy = _side_stream("h2d")
     t_enter = time.perf_counter()
+    if _PIPE_DEBUG:
+        _HT.clear()
+        _HT.append(("enter", t_enter))
+        if _HT_PREV[0] is not None:
+            _HT.append(("since_prev_sync", t_enter - _HT_PREV[0] + t_enter))
     _ARENA.reset()
     copy.wait_stream(main)  # buffers recycled from the previous call
     _MARKS.clear()
@@ -908,18 +949,16 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
             t1 = min(t0 + tpr, n_tiles)
         else:
             tpr, t0, t1 = n_tiles, 0, n_tiles
-        with torch.cuda.stream(copy):
-            W = 64 * KT * 32
-            xhi = torch.empty((n_tiles if sh is None else sh[1] * tpr) * W, dtype=torch.int16,
-                              device=dev)
-            xin = torch.empty((n_tiles if sh is None else sh[1] * tpr) * 64, dtype=torch.float32,
-                              device=dev)
-            xhi_c, xin_c = ((xhi, xin) if sh is None else
-                            (torch.empty(tpr * W, dtype=torch.int16, device=dev),
-                             torch.empty(tpr * 64, dtype=torch.float32, device=dev)))
-            xnm = torch.empty(1, dtype=torch.int32, device=dev)
-            qhi = torch.empty(Q * KT * 32, dtype=torch.int16, device=dev)
-            qn = torch.empty(Q, dtype=torch.float32, device=dev)
+        # the operand images: device scratch reused across calls (internal, never returned)
+        W = 64 * KT * 32
+        xhi = _scratch("xhi", (n_tiles if sh is None else sh[1] * tpr) * W, torch.int16, dev)
+        xin = _scratch("xin", (n_tiles if sh is None else sh[1] * tpr) * 64, torch.float32, dev)
+        xhi_c, xin_c = ((xhi, xin) if sh is None else
+                        (_scratch("xhi_c", tpr * W, torch.int16, dev),
+                         _scratch("xin_c", tpr * 64, torch.float32, dev)))
+        xnm = _scratch("xnm", 1, torch.int32, dev)
+        qhi = _scratch("qhi", Q * KT * 32, torch.int16, dev)
+        qn = _scratch("qn", Q, torch.float32, dev)
         t_ops = t_ops0 = time.perf_counter()
         if split:
             def render_data(bad):
@@ -1064,14 +1103,16 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         bad = torch.zeros(1, dtype=torch.int32, device=dev)  # (sharded: the reduced verdict)
     # the dataset image first: its render and copy start before any of the Python set-up below
     # (~0.1 ms), which then runs while the image crosses PCIe
+    _ht("render_data")
     if render_data(bad):
         copy.synchronize()
         return None
     _mark("data_landed", copy)
-    with torch.cuda.stream(copy):
-        X = torch.empty((N, A), dtype=torch.float64, device=dev)
-        lab = (torch.empty(N, dtype=torch.int32, device=dev) if labels_host is not None else None)
-        Qd = torch.empty((Q, A), dtype=torch.float64, device=dev)
+    _ht("setup")
+    # the fp64 rows: device scratch reused across calls (internal, never returned)
+    X = _scratch("X", N * A, torch.float64, dev).view(N, A)
+    lab = _scratch("lab", N, torch.int32, dev) if labels_host is not None else None
+    Qd = _scratch("Qd", Q * A, torch.float64, dev).view(Q, A)
     if lab is not None and finalize:
         lo, hi = label_range
         lab_ds = lab
@@ -1102,12 +1143,13 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
             call = _KnnCall(ds, Qd[a:b], k_host[a:b], finalize, False, ks,
                             gpu_share=1.0 / parts, out=out, prepped=(qhi[a * W:b * W], qn[a:b]),
                             k_range=k_range)
-            bufs.append(call.x1_buffers())
+            bufs.append(call.x1_buffers(p))  # one scratch slot per query part
         calls.append(call)
     S = bufs[0][3]
     if any(bf[3] != S for bf in bufs):
         raise RuntimeError("query parts disagree on the slice count")
     arr = lambda xs: (ctypes.c_void_p * parts)(*xs)
+    _ht("query_render")
     rc = L.dmlp_host_ops_x1_parts(
         Qh.ctypes.data, Q, A, mu_h.ctypes.data, KT, hb[3].data_ptr(), hb[4].data_ptr(), _p(qhi),
         _p(qn), parts, copy.cuda_stream, arr([ps.cuda_stream for ps in pss]), _p(xhi), _p(xin),
@@ -1122,6 +1164,7 @@ def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstrid
         copy.synchronize()
         return None
     _mark("operands_landed", copy)
+    _ht("rows")
     with torch.cuda.stream(copy):
         if lab is not None:
             lab.copy_(torch.from_numpy(np.ascontiguousarray(labels_host, np.int32)),
@@ -1189,7 +1232,10 @@ def _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter, t_o
         else:
             report["copied"] = False
     t_launched = time.perf_counter()
+    _ht("finish")
     n_fb = sum(call.finish().n_fallback for call in calls)
+    _ht("synced")
+    _HT_PREV[0] = time.perf_counter()
     _close_marks()
     if report is not None:
         report["valid"] = spec is not None and not any(c.cs_modified for c in calls)
@@ -1197,6 +1243,9 @@ def _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter, t_o
     _ARENA.mark()
     if _PIPE_DEBUG:
         import sys
+        t0 = _HT[0][1] if _HT else t_enter
+        print("[dmlp-pipe] host stamps (ms): " + " ".join(f"{n}={1e3 * (t - t0):.3f}"
+                                                           for n, t in _HT), file=sys.stderr)
         print(f"[dmlp-pipe] host launch {1e3 * (t_launched - t_enter):.3f} ms (before host ops "
               f"{1e3 * (t_ops0 - t_enter):.3f} ms), finish "
               f"{1e3 * (time.perf_counter() - t_launched):.3f} ms, host ops "
