@@ -71,6 +71,10 @@ _SIGS = {
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_refine_groups2": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, vp]),
     "dmlp_x1_seed": (i32, [vp, vp, i32, i32, vp, vp]),
+    "dmlp_fast_step_events": (i32, [i32]),
+    "dmlp_fast_step_timeline": (i32, [vp, vp, i32]),
+    "dmlp_fast_step": (i32, [vp, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i64, i32, vp, i64,
+                             vp, vp, vp, vp]),
     "dmlp_screen_x1_collect": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
     "dmlp_set_x1_ct": (None, [i32]),

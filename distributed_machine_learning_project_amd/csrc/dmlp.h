@@ -214,6 +214,16 @@ int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
                            const float* hseed, int ccap, int S, int* cand_ids, int* cand_cnt,
                            float* cand_h, void* stream);
 
+// The single-GPU call for every k in [kmin, kmax] within [1, 32] in one native function
+// (fast_step.hip): host render + copies, screen, rows behind it, refine, report text into
+// report_dst, labels / checksums into the caller's device out_lab / out_cs, one sync.  Returns 0,
+// 1 (not this path's call: nothing observable written), 2 (a query overflowed: rerun on the
+// general path), or < 0 (HIP error).
+int dmlp_fast_step(const double* X, const int* labels, int64_t N, const double* Qx, const int* k,
+                   int64_t Q, int A, int kmin, int kmax, int label_lo, int label_hi,
+                   int64_t qid_base, int chunks, char* report_dst, int64_t report_cap,
+                   int64_t* report_len, int* out_lab, uint64_t* out_cs, void* stream);
+
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).
 int dmlp_exact_rows(const double* X, int64_t N, int A, const double* Qx, const int* qidx, int nq,

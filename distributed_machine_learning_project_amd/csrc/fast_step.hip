@@ -1,0 +1,309 @@
+// fast_step.hip — the single-GPU headline call in one native function (no Python between the
+// phases): the host-operand pipeline of ops/knn.py knn_gpu_pipelined (+ _pipelined_parts with one
+// part) for the common case, every k on the single-term class.  The Python path spends ~0.3 ms
+// of interpreter time per call on the critical path (profiles/r5m: 0.19 ms between calls, 0.12
+// ms before the first render, 0.12 ms of set-up between the data and query renders); here the
+// whole step is host C++ around the same kernels:
+//
+//   side stream: dataset image + query fragments rendered on the host pool and copied in slices
+//                (host_prep.cpp), k; then labels and the fp64 rows (lossless int32 when every
+//                value is a 6-decimal number) behind the screen
+//   main stream: single-term screen (screen_x1.hip) once the operands landed -> group refine
+//                (refine.hip, waits for the rows) -> report text (GPU) -> D2H of the text, the
+//                byte count and the overflow count -> one host sync
+//
+// Returns 0 (report and results written), 1 when the call is not this path's (k outside
+// [1, 32], data or queries outside the fp16 screen's range, no x1 variant for A: nothing the
+// caller can observe was written), 2 when some query's single-term candidates overflowed (the
+// caller reruns the call on the general path, whose per-query escalation handles it), < 0 on a
+// HIP error.  out_lab / out_cs (device, Q each) are the caller's: the labels and checksums stay
+// there; the report text goes to report_dst (page-locked, >= dmlp_format_bound(Q) bytes).  The
+// internal device and page-locked buffers are grow-only and reused by the next call.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "dmlp.h"
+
+namespace {
+
+template <typename T>
+struct DBuf {  // grow-only device buffer
+  T* p = nullptr;
+  size_t n = 0;
+  T* get(size_t m) {
+    if (m > n) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      n = 0;
+      if (hipMalloc((void**)&p, std::max<size_t>(m, 1) * sizeof(T)) != hipSuccess) return nullptr;
+      n = std::max<size_t>(m, 1);
+    }
+    return p;
+  }
+};
+
+template <typename T>
+struct HBuf {  // grow-only page-locked host buffer
+  T* p = nullptr;
+  size_t n = 0;
+  T* get(size_t m) {
+    if (m > n) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      n = 0;
+      if (hipHostMalloc((void**)&p, std::max<size_t>(m, 1) * sizeof(T), hipHostMallocDefault) !=
+          hipSuccess)
+        return nullptr;
+      n = std::max<size_t>(m, 1);
+    }
+    return p;
+  }
+};
+
+// phase marks of the step timeline (dmlp_fast_step_events(1): hipEvents, read after the sync)
+enum { M_ENTER, M_DATA, M_OPS, M_ROWS, M_SCREEN, M_REFINE, M_FORMAT, M_D2H, M_N };
+const char* const kMarkNames[M_N] = {"enter", "data_landed", "operands_landed", "rows_landed",
+                                     "screen_done", "refine_done", "format_done",
+                                     "report_d2h_done"};
+
+struct Workspace {
+  hipStream_t side = nullptr;
+  hipEvent_t ev_ops = nullptr, ev_rows = nullptr;
+  bool marks_on = false, marks_valid = false;
+  hipEvent_t marks[M_N] = {};
+  // device
+  DBuf<short> xhi, qhi;
+  DBuf<float> xin, qn, cand_h;
+  DBuf<unsigned> words;  // [0] xnmax bits, [1] bad (0: the host checked the ranges)
+  DBuf<int> kdev, ident, cand_ids, cand_cnt, status, ovf, lab_d, i32, out_i;
+  DBuf<double> X, Qd, out_d;
+  DBuf<int64_t> off;
+  DBuf<char> text;
+  // page-locked staging
+  HBuf<uint16_t> xhi_h, qhi_h;
+  HBuf<float> xin_h, qn_h;
+  HBuf<unsigned> xnm_h;
+  HBuf<int> k_h, i32_h, ident_h, small_h;  // small_h: [0] overflow count
+  HBuf<int64_t> len_h;
+  HBuf<double> mu_h;
+  int64_t ident_len = 0;
+};
+
+Workspace& ws() {
+  static Workspace w;
+  return w;
+}
+
+// Data slices of the single-term screen (ops/knn.py _choose_slices_stream).
+int slices(int nq, int qw, int64_t n_tiles, int waves_per_cu, int64_t s_lo) {
+  const int nqb = (nq + qw - 1) / qw;
+  const int slots = waves_per_cu * 256;
+  const int s_min = (int)std::max<int64_t>(std::max<int64_t>(1, s_lo),
+                                           (n_tiles * 64 + (1ll << 29) - 1) >> 29);
+  if (nqb >= slots) return s_min;
+  int best = s_min;
+  double best_eff = 0.0;
+  for (int S = s_min; S < s_min + 64 && S <= std::max<int64_t>(s_min, n_tiles / 4); ++S) {
+    const double w = (double)nqb * S;
+    const double eff = w / (double)(((int64_t)w + slots - 1) / slots * slots);
+    if (eff >= 0.9) return S;
+    if (eff > best_eff + 1e-9) {
+      best = S;
+      best_eff = eff;
+    }
+  }
+  return best;
+}
+
+}  // namespace
+
+extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, const double* Qx,
+                              const int* k, int64_t Q, int A, int kmin, int kmax, int label_lo,
+                              int label_hi, int64_t qid_base, int chunks, char* report_dst,
+                              int64_t report_cap, int64_t* report_len, int* out_lab,
+                              uint64_t* out_cs, void* stream) {
+#define FS_CHK(x)                                         \
+  do {                                                    \
+    const hipError_t e_ = (x);                            \
+    if (e_ != hipSuccess) return -(int)e_;                \
+  } while (0)
+#define FS_PTR(p)                                         \
+  do {                                                    \
+    if (!(p)) return -(int)hipErrorOutOfMemory;           \
+  } while (0)
+  if (N <= 0 || Q <= 0 || Q > (1 << 30) || A < 1 || kmin < 1 || kmax > 32 || kmax > N) return 1;
+  const int KT = dmlp_screen_kt(A);
+  if (dmlp_screen_x1_qw(KT) <= 0) return 1;
+  const int64_t nt = (N + 63) / 64;
+  if (report_cap < dmlp_format_bound((int)Q)) return 1;
+  Workspace& w = ws();
+  hipStream_t st = (hipStream_t)stream;
+  if (!w.side) {
+    FS_CHK(hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking));
+    FS_CHK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
+    FS_CHK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
+  }
+  w.marks_valid = false;
+  auto mark = [&](int i, hipStream_t s) -> hipError_t {
+    return w.marks_on ? hipEventRecord(w.marks[i], s) : hipSuccess;
+  };
+  FS_CHK(mark(M_ENTER, w.side));
+  const int64_t W = (int64_t)KT * 32;
+  // page-locked staging + device buffers (grow-only)
+  uint16_t* xhi_h = w.xhi_h.get(nt * 64 * W);
+  float* xin_h = w.xin_h.get(nt * 64);
+  unsigned* xnm_h = w.xnm_h.get(2);
+  uint16_t* qhi_h = w.qhi_h.get(Q * W);
+  float* qn_h = w.qn_h.get(Q);
+  double* mu = w.mu_h.get(A);
+  int* k_h = w.k_h.get(Q);
+  int* small_h = w.small_h.get(16);
+  int64_t* len_h = w.len_h.get(2);
+  short* xhi = w.xhi.get(nt * 64 * W);
+  float* xin = w.xin.get(nt * 64);
+  unsigned* words = w.words.get(2);
+  short* qhi = w.qhi.get(Q * W);
+  float* qn = w.qn.get(Q);
+  int* kd = w.kdev.get(Q);
+  FS_PTR(xhi_h); FS_PTR(xin_h); FS_PTR(xnm_h); FS_PTR(qhi_h); FS_PTR(qn_h); FS_PTR(mu);
+  FS_PTR(k_h); FS_PTR(small_h); FS_PTR(len_h); FS_PTR(xhi); FS_PTR(xin); FS_PTR(words);
+  FS_PTR(qhi); FS_PTR(qn); FS_PTR(kd);
+  // the previous call's work on the main stream is complete (it ended with a sync); the side
+  // stream may still hold nothing: no dependency needed
+  dmlp_cpu_center(X, std::min<int64_t>(N, 4096), A, mu);
+  // dataset image, then query fragments, rendered on the host pool and copied in slices (side);
+  // the query call renders no tiles and writes its (zero) norm word into words[1], the "bad"
+  // word, which the host-checked ranges leave at 0
+  const int ch = chunks < 1 ? 1 : chunks;
+  int rc = dmlp_host_ops_h2d_tiles(X, N, 0, nt, Qx, 0, A, mu, KT, xhi_h, xin_h, xnm_h, qhi_h,
+                                   qn_h, xhi, xin, words, qhi, qn, ch, w.side);
+  FS_CHK(mark(M_DATA, w.side));
+  rc |= dmlp_host_ops_h2d_tiles(X, N, nt, nt, Qx, Q, A, mu, KT, xhi_h, xin_h, xnm_h + 1, qhi_h,
+                                qn_h, xhi, xin, words + 1, qhi, qn, ch, w.side);
+  if (rc & 4) return -(int)hipErrorUnknown;
+  if (rc) {  // outside the fp16 screen's range: the caller's general path decides
+    FS_CHK(hipStreamSynchronize(w.side));
+    return 1;
+  }
+  FS_CHK(mark(M_OPS, w.side));
+  std::memcpy(k_h, k, (size_t)Q * sizeof(int));
+  FS_CHK(hipMemcpyAsync(kd, k_h, (size_t)Q * sizeof(int), hipMemcpyHostToDevice, w.side));
+  FS_CHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), w.side));
+  FS_CHK(hipEventRecord(w.ev_ops, w.side));
+  // identity query list (grow-only, written once)
+  if (w.ident_len < Q) {
+    const int64_t n = std::max<int64_t>(Q, 1 << 16);
+    int* h = w.ident_h.get(n);
+    int* d = w.ident.get(n);
+    FS_PTR(h); FS_PTR(d);
+    for (int64_t i = 0; i < n; ++i) h[i] = (int)i;
+    FS_CHK(hipMemcpyAsync(d, h, (size_t)n * sizeof(int), hipMemcpyHostToDevice, w.side));
+    FS_CHK(hipEventRecord(w.ev_ops, w.side));
+    w.ident_len = n;
+  }
+  // ---- main: the screen, as soon as the operands landed
+  const int S = slices((int)Q, dmlp_screen_x1_cols(KT, kmax), nt,
+                       dmlp_screen_x1_waves_per_cu_kt(KT, kmax), dmlp_screen_x1_min_slices(nt));
+  const int cap = dmlp_screen_x1_cap(kmax);
+  int* cand_ids = w.cand_ids.get((size_t)Q * S * cap);
+  int* cand_cnt = w.cand_cnt.get((size_t)Q * S);
+  float* cand_h = w.cand_h.get((size_t)Q * S * 2);
+  int* ovf = w.ovf.get(1);
+  FS_PTR(cand_ids); FS_PTR(cand_cnt); FS_PTR(cand_h); FS_PTR(ovf);
+  FS_CHK(hipStreamWaitEvent(st, w.ev_ops, 0));
+  FS_CHK(hipMemsetAsync(ovf, 0, sizeof(int), st));
+  {
+    const int e = dmlp_screen_x1(KT, 1, A, xhi, xin, nt, N, qhi, qn, w.ident.p, kd, (int)Q, kmax,
+                                 words, words + 1, S, cand_ids, cand_cnt, cand_h, st);
+    if (e) return e < 0 ? e : -1;
+  }
+  FS_CHK(mark(M_SCREEN, st));
+  // ---- side: labels and the fp64 rows behind the screen
+  int* lab_d = w.lab_d.get(N);
+  double* Xd = w.X.get((size_t)N * A);
+  double* Qd = w.Qd.get((size_t)Q * A);
+  FS_PTR(lab_d); FS_PTR(Xd); FS_PTR(Qd);
+  FS_CHK(hipMemcpyAsync(lab_d, labels, (size_t)N * sizeof(int), hipMemcpyHostToDevice, w.side));
+  {
+    const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
+    int* h32 = w.i32_h.get(at + nqa);
+    int* d32 = w.i32.get(at + nqa);
+    FS_PTR(h32); FS_PTR(d32);
+    auto rows = [&](const double* src, int64_t n, double* dst, int64_t off) -> int {
+      if (dmlp_cpu_rows_i32(src, n, h32 + off) == 0) {  // lossless 6-decimal: half the bytes
+        if (hipMemcpyAsync(d32 + off, h32 + off, (size_t)n * 4, hipMemcpyHostToDevice, w.side) !=
+            hipSuccess)
+          return -1;
+        return dmlp_rows_from_i32(d32 + off, n, dst, w.side);
+      }
+      return hipMemcpyAsync(dst, src, (size_t)n * 8, hipMemcpyHostToDevice, w.side) == hipSuccess
+                 ? 0 : -1;
+    };
+    if (rows(X, nx, Xd, 0) || rows(Qx, nqa, Qd, at)) return -(int)hipErrorUnknown;
+  }
+  FS_CHK(hipEventRecord(w.ev_rows, w.side));
+  FS_CHK(mark(M_ROWS, w.side));
+  // ---- main: exact re-rank (+ vote, checksum), report text, one sync
+  double* out_d = w.out_d.get((size_t)Q * kmax);
+  int* out_i = w.out_i.get((size_t)Q * kmax);
+  int* status = w.status.get(Q);
+  int64_t* off = w.off.get((size_t)dmlp_format_scratch((int)Q));
+  char* text = w.text.get((size_t)dmlp_format_bound((int)Q));
+  FS_PTR(out_d); FS_PTR(out_i); FS_PTR(out_lab); FS_PTR(out_cs); FS_PTR(status); FS_PTR(off);
+  FS_PTR(text);
+  FS_CHK(hipStreamWaitEvent(st, w.ev_rows, 0));
+  {
+    const int e = dmlp_refine_groups(cap, cand_ids, cand_cnt, cand_h, S, Xd, A, Qd, xhi, xin, qhi,
+                                     KT, 1, N, nullptr, kd, (int)Q, out_d, out_i, kmax, lab_d,
+                                     label_lo, label_hi, out_lab, out_cs, status, ovf, st);
+    if (e) return e < 0 ? e : -1;
+  }
+  FS_CHK(mark(M_REFINE, st));
+  {
+    const int e = dmlp_format_report(out_cs, (int)Q, (int)qid_base, off, text, st);
+    if (e) return e < 0 ? e : -1;
+  }
+  FS_CHK(mark(M_FORMAT, st));
+  const int64_t bound = dmlp_format_bound((int)Q);
+  FS_CHK(hipMemcpyAsync(report_dst, text, (size_t)bound, hipMemcpyDeviceToHost, st));
+  FS_CHK(hipMemcpyAsync(len_h, off + Q, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  FS_CHK(hipMemcpyAsync(small_h, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+  FS_CHK(mark(M_D2H, st));
+  FS_CHK(hipStreamSynchronize(st));
+  w.marks_valid = w.marks_on;
+  if (small_h[0]) return 2;  // some query's candidates overflowed: the general path escalates
+  *report_len = len_h[0];
+  return 0;
+#undef FS_CHK
+#undef FS_PTR
+}
+
+// Step-timeline marks of dmlp_fast_step (hipEvents with timing; off by default).
+extern "C" int dmlp_fast_step_events(int on) {
+  Workspace& w = ws();
+  if (on && !w.marks[0])
+    for (int i = 0; i < M_N; ++i)
+      if (hipEventCreate(&w.marks[i]) != hipSuccess) return -1;
+  w.marks_on = on != 0 && w.marks[0];
+  return 0;
+}
+
+// The last call's marks as ms since it entered (the previous call having synchronized, every
+// event is complete): names[i] / ms[i] for i < the returned count (0: no timeline).
+extern "C" int dmlp_fast_step_timeline(double* ms, const char** names, int cap) {
+  Workspace& w = ws();
+  if (!w.marks_valid) return 0;
+  int n = 0;
+  for (int i = 0; i < M_N && n < cap; ++i) {
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, w.marks[M_ENTER], w.marks[i]) != hipSuccess) continue;
+    ms[n] = t;
+    names[n] = kMarkNames[i];
+    ++n;
+  }
+  return n;
+}

@@ -822,6 +822,10 @@ def set_pipe_events(on: bool):
     global _EVENTS
     _EVENTS = bool(on)
     _PREV_END[0] = None
+    try:  # the native step's own marks (fast_step.hip)
+        _lib.lib().dmlp_fast_step_events(1 if on else 0)
+    except Exception:  # noqa: BLE001 (a library without the native step)
+        pass
 
 
 def _mark(name, stream=None):
@@ -1080,6 +1084,50 @@ def knn_gpu_pipelined(X_host, labels_host, label_range, Q_host, k_host, kstride=
     return _pipelined_tail(ds, od, oi, ol, oc, calls, report, Q, finalize, t_enter,
                            t_ops0 if host_ops else t_enter, t_ops if host_ops else 0.0,
                            prepped is not None)
+
+
+# the single-GPU call in one native function (fast_step.hip) when every k is on the single-term
+# class; DMLP_FAST_STEP=0: always the Python pipeline (knn_gpu_pipelined)
+FAST_STEP = os.environ.get("DMLP_FAST_STEP", "1") != "0"
+FAST_STEP_CALLS = [0]  # calls the native step served (tests, diagnostics)
+
+
+def fast_step(X_host, labels_host, label_range, Q_host, k_host, k_range, dst, qid_base=0):
+    """One rank's whole call natively (dmlp_fast_step): host render + copies, single-term screen,
+    fp64 rows behind it, exact re-rank, vote, checksum, report text into the page-locked `dst`,
+    one host sync.  Returns (label, checksum device tensors, report byte count), or None when
+    the call is not this path's (k outside [1, 32], data outside the fp16 screen's range, a
+    query that overflowed its single-term candidates): the caller then runs the general
+    pipeline (knn_gpu_pipelined), whose per-query dispatch and escalation handle it."""
+    torch = _torch()
+    L = _lib.lib()
+    Q, A = Q_host.shape
+    N = len(X_host)
+    if not FAST_STEP or Q == 0 or N == 0:
+        return None
+    dev = torch.device("cuda", torch.cuda.current_device())
+    lab = torch.empty(Q, dtype=torch.int32, device=dev)
+    cs = torch.empty(Q, dtype=torch.int64, device=dev)
+    n = np.zeros(1, np.int64)
+    rc = L.dmlp_fast_step(X_host.ctypes.data, labels_host.ctypes.data, N, Q_host.ctypes.data,
+                          k_host.ctypes.data, Q, A, int(k_range[0]), int(k_range[1]),
+                          int(label_range[0]), int(label_range[1]), qid_base, HOST_OPS_CHUNKS,
+                          dst.ctypes.data, len(dst), n.ctypes.data, _p(lab), _p(cs), _stream())
+    if rc in (1, 2):
+        return None
+    _lib.check(rc, "fast_step")
+    FAST_STEP_CALLS[0] += 1
+    if _EVENTS:
+        import ctypes
+        global _LAST_TIMELINE
+        ms = (ctypes.c_double * 16)()
+        names = (ctypes.c_char_p * 16)()
+        m = L.dmlp_fast_step_timeline(ms, names, 16)
+        _LAST_TIMELINE = [(names[i].decode(), round(ms[i], 4)) for i in range(m)]
+    _IO["h2d"] += ((N + 63) // 64 * 64 * (screen_kt(A) * 64 + 4) + Q * (screen_kt(A) * 64 + 4)
+                   + (N + Q) * A * 4 + N * 4)
+    _IO["d2h"] += L.dmlp_format_bound(Q)
+    return lab, cs, int(n[0])
 
 
 def _pipelined_parts(parts, X_host, labels_host, label_range, Qh, k_host, kstride, finalize,

@@ -292,6 +292,16 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
     bcast_data = mode == "bcast"
+    if (comm.world == 1 and not debug and be.on_gpu and not be.exact and pipeline
+            and getattr(inp, "out", None) is not None):
+        # one rank, every k on the single-term class: the whole call in one native function
+        # (ops/knn.py fast_step); anything else falls through to the pipeline below
+        from ..ops import knn as K
+        with tr.phase("h2d+compute"):
+            r = K.fast_step(inp.X, inp.labels, (lo, hi), inp.Qx, inp.k, inp.k_range_all, inp.out)
+        if r is not None:
+            lb, cs, n = r
+            return lb, cs, None, None, memoryview(inp.out)[:n].toreadonly()
     if not bcast_data and pipeline:
         # per-GPU H2D: the query chunks land while the earlier chunks already screen
         with tr.phase("h2d+compute"):

@@ -55,6 +55,28 @@ def test_shared_ingress_and_out_of_core(gpu, workload, monkeypatch, max_rows):
     eng.close()
 
 
+@pytest.mark.parametrize("kmax,fast", [(32, True), (40, False)])
+def test_native_fast_step(gpu, kmax, fast):
+    """One rank over the node-shared segment, every k on the single-term class: the whole call
+    runs in one native function (fast_step.hip) — report, labels and checksums == the oracle's,
+    three calls in a row (reused buffers); k > 32 falls through to the Python pipeline."""
+    from distributed_machine_learning_project_amd.utils.shm import share_input
+    inp = dmlp.generate(7000, 900, 32, 0.0, 1000.0, 1, kmax, 8, seed=kmax)
+    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    eng = _engine("farm")
+    sh = share_input(eng.comm, inp)
+    for _ in range(3):
+        n0 = K.FAST_STEP_CALLS[0]
+        out = eng.KNN(sh.params, sh, None)
+        assert bytes(eng.report(out)) == dmlp.format_report(cs)
+        np.testing.assert_array_equal(out.labels_np(), lab_ref)
+        np.testing.assert_array_equal(out.checksums_np(), cs)
+        assert (K.FAST_STEP_CALLS[0] == n0 + 1) == fast
+    sh.close()
+    eng.close()
+
+
 def test_debug_listing(gpu, workload):
     inp, _, d, i = workload
     eng = _engine("ring", debug=True)
