@@ -233,7 +233,7 @@ def main(argv=None):
             "vs_baseline": None,
             "vs_student_engine_cpu_np4": round(value / BASELINE_QPS, 1),
             "dtype": "fp64",
-            "screen": "none" if a.exact else "single-term bf16 MFMA screen (3-term escalation), "
+            "screen": "none" if a.exact else "single-term fp16 MFMA screen (3-term escalation), "
                                              "exact fp64 re-rank (results bit-identical to the "
                                              "fp64 reference)",
             "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",

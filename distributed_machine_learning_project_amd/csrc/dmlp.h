@@ -223,6 +223,10 @@ int dmlp_fast_step(const double* X, const int* labels, int64_t N, const double* 
                    int64_t Q, int A, int kmin, int kmax, int label_lo, int label_hi,
                    int64_t qid_base, int chunks, char* report_dst, int64_t report_cap,
                    int64_t* report_len, int* out_lab, uint64_t* out_cs, void* stream);
+// query parts of the following calls (1..4; <= 0: DMLP_FAST_PARTS, default 1); step timeline
+int dmlp_fast_step_events(int on);
+int dmlp_fast_step_timeline(double* ms, const char** names, int cap);
+void dmlp_fast_step_parts(int parts);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).
@@ -275,6 +279,10 @@ int64_t dmlp_format_bound(int nq);
 int64_t dmlp_format_scratch(int nq);
 int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off, char* out,
                        void* stream);
+// ... with the lines starting at byte *base of out (base: device int64, null = 0); line_off then
+// holds absolute offsets (line_off[nq] = the end of this run's text)
+int dmlp_format_report_at(const uint64_t* cs, int nq, int qid_base, int64_t* line_off, char* out,
+                          const int64_t* base, void* stream);
 
 // ---------------------------------------------------------------- host (CPU) implementations
 int dmlp_cpu_knn(const double* X, int64_t N, int A, const double* Qx, int64_t Q, const int* qk,

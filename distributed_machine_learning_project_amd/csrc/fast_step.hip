@@ -8,9 +8,10 @@
 //   side stream: dataset image + query fragments rendered on the host pool and copied in slices
 //                (host_prep.cpp), k; then labels and the fp64 rows (lossless int32 when every
 //                value is a 6-decimal number) behind the screen
-//   main stream: single-term screen (screen_x1.hip) once the operands landed -> group refine
-//                (refine.hip, waits for the rows) -> report text (GPU) -> D2H of the text, the
-//                byte count and the overflow count -> one host sync
+//   main stream: single-term screen (screen_x1.hip) of each query part once its operands landed
+//   tail stream: per part, group refine (refine.hip, waits for the rows and the part's screen)
+//                -> the part's report text (GPU, at the previous part's device-side end) -> D2H
+//                of its byte range; then the byte count and the overflow count -> one host sync
 //
 // Returns 0 (report and results written), 1 when the call is not this path's (k outside
 // [1, 32], data or queries outside the fp16 screen's range, no x1 variant for A: nothing the
@@ -23,6 +24,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -70,9 +73,34 @@ const char* const kMarkNames[M_N] = {"enter", "data_landed", "operands_landed", 
                                      "screen_done", "refine_done", "format_done",
                                      "report_d2h_done"};
 
+constexpr int kMaxParts = 4;
+
+// query parts of a call (DMLP_FAST_PARTS, 1..4; default 1): part p's screen starts as soon as its
+// operands landed, and its refine + report text + D2H run on the tail stream while the next
+// part screens
+int clamp_parts(int v) { return v < 1 ? 1 : v > kMaxParts ? kMaxParts : v; }
+int g_parts = -1;  // -1: DMLP_FAST_PARTS (read once)
+int fast_parts() {
+  if (g_parts < 0) {
+    const char* e = std::getenv("DMLP_FAST_PARTS");
+    g_parts = clamp_parts(e ? std::atoi(e) : 1);
+  }
+  return g_parts;
+}
+
+// sum of the decimal digit counts of v over [a, b)
+int64_t digits_sum(int64_t a, int64_t b) {
+  int64_t s = 0, lo = 0, hi = 10;
+  for (int d = 1; d <= 19 && lo < b; ++d, lo = hi, hi = hi > INT64_MAX / 10 ? INT64_MAX : hi * 10) {
+    const int64_t x = std::max(a, lo), y = std::min(b, hi);
+    if (y > x) s += (y - x) * d;
+  }
+  return s;
+}
+
 struct Workspace {
-  hipStream_t side = nullptr;
-  hipEvent_t ev_ops = nullptr, ev_rows = nullptr;
+  hipStream_t side = nullptr, tail = nullptr;
+  hipEvent_t ev_ops[kMaxParts] = {}, ev_scr[kMaxParts] = {}, ev_rows = nullptr, ev_k = nullptr;
   bool marks_on = false, marks_valid = false;
   hipEvent_t marks[M_N] = {};
   // device
@@ -144,8 +172,13 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   hipStream_t st = (hipStream_t)stream;
   if (!w.side) {
     FS_CHK(hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking));
-    FS_CHK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
+    FS_CHK(hipStreamCreateWithFlags(&w.tail, hipStreamNonBlocking));
+    for (int p = 0; p < kMaxParts; ++p) {
+      FS_CHK(hipEventCreateWithFlags(&w.ev_ops[p], hipEventDisableTiming));
+      FS_CHK(hipEventCreateWithFlags(&w.ev_scr[p], hipEventDisableTiming));
+    }
     FS_CHK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
+    FS_CHK(hipEventCreateWithFlags(&w.ev_k, hipEventDisableTiming));
   }
   w.marks_valid = false;
   auto mark = [&](int i, hipStream_t s) -> hipError_t {
@@ -175,25 +208,16 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   // the previous call's work on the main stream is complete (it ended with a sync); the side
   // stream may still hold nothing: no dependency needed
   dmlp_cpu_center(X, std::min<int64_t>(N, 4096), A, mu);
-  // dataset image, then query fragments, rendered on the host pool and copied in slices (side);
-  // the query call renders no tiles and writes its (zero) norm word into words[1], the "bad"
-  // word, which the host-checked ranges leave at 0
+  // dataset image, then the query fragments part by part, rendered on the host pool and copied
+  // in slices (side); a query call renders no tiles and writes its (zero) norm word into
+  // words[1], the "bad" word, which the host-checked ranges leave at 0
   const int ch = chunks < 1 ? 1 : chunks;
   int rc = dmlp_host_ops_h2d_tiles(X, N, 0, nt, Qx, 0, A, mu, KT, xhi_h, xin_h, xnm_h, qhi_h,
                                    qn_h, xhi, xin, words, qhi, qn, ch, w.side);
   FS_CHK(mark(M_DATA, w.side));
-  rc |= dmlp_host_ops_h2d_tiles(X, N, nt, nt, Qx, Q, A, mu, KT, xhi_h, xin_h, xnm_h + 1, qhi_h,
-                                qn_h, xhi, xin, words + 1, qhi, qn, ch, w.side);
   if (rc & 4) return -(int)hipErrorUnknown;
-  if (rc) {  // outside the fp16 screen's range: the caller's general path decides
-    FS_CHK(hipStreamSynchronize(w.side));
-    return 1;
-  }
-  FS_CHK(mark(M_OPS, w.side));
   std::memcpy(k_h, k, (size_t)Q * sizeof(int));
   FS_CHK(hipMemcpyAsync(kd, k_h, (size_t)Q * sizeof(int), hipMemcpyHostToDevice, w.side));
-  FS_CHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), w.side));
-  FS_CHK(hipEventRecord(w.ev_ops, w.side));
   // identity query list (grow-only, written once)
   if (w.ident_len < Q) {
     const int64_t n = std::max<int64_t>(Q, 1 << 16);
@@ -202,24 +226,50 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
     FS_PTR(h); FS_PTR(d);
     for (int64_t i = 0; i < n; ++i) h[i] = (int)i;
     FS_CHK(hipMemcpyAsync(d, h, (size_t)n * sizeof(int), hipMemcpyHostToDevice, w.side));
-    FS_CHK(hipEventRecord(w.ev_ops, w.side));
     w.ident_len = n;
   }
-  // ---- main: the screen, as soon as the operands landed
-  const int S = slices((int)Q, dmlp_screen_x1_cols(KT, kmax), nt,
-                       dmlp_screen_x1_waves_per_cu_kt(KT, kmax), dmlp_screen_x1_min_slices(nt));
+  // parts: multiples of 64 queries (whole screen query blocks)
+  const int P = (int)std::max<int64_t>(1, std::min<int64_t>(fast_parts(), (Q + 63) / 64));
+  int64_t q0s[kMaxParts + 1];
+  for (int p = 0; p <= P; ++p) q0s[p] = std::min<int64_t>(Q, (Q * p / P + 63) / 64 * 64);
+  q0s[P] = Q;
   const int cap = dmlp_screen_x1_cap(kmax);
-  int* cand_ids = w.cand_ids.get((size_t)Q * S * cap);
-  int* cand_cnt = w.cand_cnt.get((size_t)Q * S);
-  float* cand_h = w.cand_h.get((size_t)Q * S * 2);
+  int Sp[kMaxParts];
+  int64_t coff[kMaxParts + 1] = {0};  // candidate slots before part p
+  for (int p = 0; p < P; ++p) {
+    const int64_t qp = q0s[p + 1] - q0s[p];
+    Sp[p] = slices((int)qp, dmlp_screen_x1_cols(KT, kmax), nt,
+                   dmlp_screen_x1_waves_per_cu_kt(KT, kmax), dmlp_screen_x1_min_slices(nt));
+    coff[p + 1] = coff[p] + qp * Sp[p];
+  }
+  int* cand_ids = w.cand_ids.get((size_t)coff[P] * cap);
+  int* cand_cnt = w.cand_cnt.get((size_t)coff[P]);
+  float* cand_h = w.cand_h.get((size_t)coff[P] * 2);
   int* ovf = w.ovf.get(1);
   FS_PTR(cand_ids); FS_PTR(cand_cnt); FS_PTR(cand_h); FS_PTR(ovf);
-  FS_CHK(hipStreamWaitEvent(st, w.ev_ops, 0));
   FS_CHK(hipMemsetAsync(ovf, 0, sizeof(int), st));
-  {
-    const int e = dmlp_screen_x1(KT, 1, A, xhi, xin, nt, N, qhi, qn, w.ident.p, kd, (int)Q, kmax,
-                                 words, words + 1, S, cand_ids, cand_cnt, cand_h, st);
+  for (int p = 0; p < P; ++p) {
+    const int64_t q0 = q0s[p], qp = q0s[p + 1] - q0;
+    rc |= dmlp_host_ops_h2d_tiles(X, N, nt, nt, Qx + q0 * A, qp, A, mu, KT, xhi_h, xin_h,
+                                  xnm_h + 1, qhi_h + q0 * W, qn_h + q0, xhi, xin, words + 1,
+                                  qhi + q0 * W, qn + q0, ch, w.side);
+    if (rc & 4) return -(int)hipErrorUnknown;
+    if (rc) {  // outside the fp16 screen's range: the caller's general path decides
+      FS_CHK(hipStreamSynchronize(w.side));
+      FS_CHK(hipStreamSynchronize(st));
+      return 1;
+    }
+    if (p == P - 1) FS_CHK(mark(M_OPS, w.side));
+    FS_CHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), w.side));
+    FS_CHK(hipEventRecord(w.ev_ops[p], w.side));
+    // ---- main: the part's screen as soon as its operands landed
+    FS_CHK(hipStreamWaitEvent(st, w.ev_ops[p], 0));
+    const int e = dmlp_screen_x1(KT, 1, A, xhi, xin, nt, N, qhi + q0 * W, qn + q0, w.ident.p,
+                                 kd + q0, (int)qp, kmax, words, words + 1, Sp[p],
+                                 cand_ids + coff[p] * cap, cand_cnt + coff[p],
+                                 cand_h + coff[p] * 2, st);
     if (e) return e < 0 ? e : -1;
+    FS_CHK(hipEventRecord(w.ev_scr[p], st));
   }
   FS_CHK(mark(M_SCREEN, st));
   // ---- side: labels and the fp64 rows behind the screen
@@ -247,32 +297,48 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   }
   FS_CHK(hipEventRecord(w.ev_rows, w.side));
   FS_CHK(mark(M_ROWS, w.side));
-  // ---- main: exact re-rank (+ vote, checksum), report text, one sync
+  // ---- tail: per part, exact re-rank (+ vote, checksum), report text at the previous part's
+  // end (device word), D2H of the part's byte range; then one sync
   double* out_d = w.out_d.get((size_t)Q * kmax);
   int* out_i = w.out_i.get((size_t)Q * kmax);
   int* status = w.status.get(Q);
-  int64_t* off = w.off.get((size_t)dmlp_format_scratch((int)Q));
+  int64_t* off = w.off.get((size_t)dmlp_format_scratch((int)Q) + 2 * P);
   char* text = w.text.get((size_t)dmlp_format_bound((int)Q));
   FS_PTR(out_d); FS_PTR(out_i); FS_PTR(out_lab); FS_PTR(out_cs); FS_PTR(status); FS_PTR(off);
   FS_PTR(text);
-  FS_CHK(hipStreamWaitEvent(st, w.ev_rows, 0));
-  {
-    const int e = dmlp_refine_groups(cap, cand_ids, cand_cnt, cand_h, S, Xd, A, Qd, xhi, xin, qhi,
-                                     KT, 1, N, nullptr, kd, (int)Q, out_d, out_i, kmax, lab_d,
-                                     label_lo, label_hi, out_lab, out_cs, status, ovf, st);
-    if (e) return e < 0 ? e : -1;
-  }
-  FS_CHK(mark(M_REFINE, st));
-  {
-    const int e = dmlp_format_report(out_cs, (int)Q, (int)qid_base, off, text, st);
-    if (e) return e < 0 ? e : -1;
-  }
-  FS_CHK(mark(M_FORMAT, st));
+  FS_CHK(hipStreamWaitEvent(w.tail, w.ev_rows, 0));
   const int64_t bound = dmlp_format_bound((int)Q);
-  FS_CHK(hipMemcpyAsync(report_dst, text, (size_t)bound, hipMemcpyDeviceToHost, st));
-  FS_CHK(hipMemcpyAsync(len_h, off + Q, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  FS_CHK(hipMemcpyAsync(small_h, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
-  FS_CHK(mark(M_D2H, st));
+  int64_t lo = 0;           // a lower bound on the byte where part p's text starts
+  const int64_t* base = nullptr;
+  int64_t* off_p = off;     // part p's line offsets (scratch of its own: the next part reads its end)
+  for (int p = 0; p < P; ++p) {
+    const int64_t q0 = q0s[p], qp = q0s[p + 1] - q0;
+    FS_CHK(hipStreamWaitEvent(w.tail, w.ev_scr[p], 0));
+    int e = dmlp_refine_groups(cap, cand_ids + coff[p] * cap, cand_cnt + coff[p],
+                               cand_h + coff[p] * 2, Sp[p], Xd, A, Qd + q0 * A, xhi, xin,
+                               qhi + q0 * W, KT, 1, N, nullptr, kd + q0, (int)qp,
+                               out_d + q0 * kmax, out_i + q0 * kmax, kmax, lab_d, label_lo,
+                               label_hi, out_lab + q0, out_cs + q0, status + q0, ovf, w.tail);
+    if (e) return e < 0 ? e : -1;
+    if (p == P - 1) FS_CHK(mark(M_REFINE, w.tail));
+    e = dmlp_format_report_at(out_cs + q0, (int)qp, (int)(qid_base + q0), off_p, text, base,
+                              w.tail);
+    if (e) return e < 0 ? e : -1;
+    if (p == P - 1) FS_CHK(mark(M_FORMAT, w.tail));
+    // bytes [lo, the part's upper bound): lines of at most 48 bytes; [lo, previous end) is the
+    // previous part's text again (still intact on the device), copied after it in stream order
+    const int64_t hi = std::min<int64_t>(bound, 48 * (q0 + qp));
+    FS_CHK(hipMemcpyAsync(report_dst + lo, text + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost,
+                          w.tail));
+    // the next part starts at or after this part's shortest text: "Query " qid " checksum: " d "\n"
+    lo += 19 * qp + digits_sum(qid_base + q0, qid_base + q0 + qp);
+    base = off_p + qp;
+    off_p += qp + 1;  // (the next part's scratch: behind this part's offsets, below the bound)
+  }
+  FS_CHK(hipMemcpyAsync(len_h, base, sizeof(int64_t), hipMemcpyDeviceToHost, w.tail));
+  FS_CHK(hipMemcpyAsync(small_h, ovf, sizeof(int), hipMemcpyDeviceToHost, w.tail));
+  FS_CHK(mark(M_D2H, w.tail));
+  FS_CHK(hipStreamSynchronize(w.tail));
   FS_CHK(hipStreamSynchronize(st));
   w.marks_valid = w.marks_on;
   if (small_h[0]) return 2;  // some query's candidates overflowed: the general path escalates
@@ -281,6 +347,9 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
 #undef FS_CHK
 #undef FS_PTR
 }
+
+// Query parts of the following calls (1..4; <= 0: back to DMLP_FAST_PARTS / 1).
+extern "C" void dmlp_fast_step_parts(int parts) { g_parts = parts <= 0 ? -1 : clamp_parts(parts); }
 
 // Step-timeline marks of dmlp_fast_step (hipEvents with timing; off by default).
 extern "C" int dmlp_fast_step_events(int on) {

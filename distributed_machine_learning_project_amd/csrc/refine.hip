@@ -999,10 +999,12 @@ __device__ __forceinline__ void put_dec(char* txt, int end, uint64_t v) {
 __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__ cs, int nq,
                                                    int qid_base, int64_t* __restrict__ off,
                                                    const int64_t* __restrict__ blocksum,
+                                                   const int64_t* __restrict__ base,
                                                    char* __restrict__ out) {
   __shared__ char txt[1024 * 48 + 4];
   const int i = blockIdx.x * 1024 + threadIdx.x;
-  const int64_t g0 = blocksum[blockIdx.x], g1 = blocksum[blockIdx.x + 1];
+  const int64_t b0 = base ? *base : 0;  // byte offset of this run's first line in out
+  const int64_t g0 = b0 + blocksum[blockIdx.x], g1 = b0 + blocksum[blockIdx.x + 1];
   if (i < nq) {
     const int64_t qid = (int64_t)qid_base + i;
     const uint64_t v = cs[i];
@@ -1035,7 +1037,7 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
              ((unsigned)(unsigned char)txt[s + 3] << 24);
   }
   if (i < nq) off[i + 1] += g0;
-  if (i == 0) off[0] = 0;
+  if (i == 0) off[0] = b0;
 }
 
 }  // namespace
@@ -1242,6 +1244,13 @@ extern "C" int64_t dmlp_format_scratch(int nq) { return (int64_t)nq + 1 + (nq + 
 
 extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off,
                                   char* out, void* stream) {
+  return dmlp_format_report_at(cs, nq, qid_base, line_off, out, nullptr, stream);
+}
+
+// The same, the lines starting at byte *base of out (device word; null: 0): a report rendered in
+// query parts, each part's base = the previous part's line_off[nq] (its absolute end)
+extern "C" int dmlp_format_report_at(const uint64_t* cs, int nq, int qid_base, int64_t* line_off,
+                                     char* out, const int64_t* base, void* stream) {
   if (nq <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int nb = (nq + 1023) / 1024;
@@ -1251,7 +1260,7 @@ extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int6
   hipLaunchKernelGGL(k_fmt_scan_blocks, dim3(1), dim3(1024), 0, st, blocksum, nb);
   DMLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_fmt_write, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off,
-                     blocksum, out);
+                     blocksum, base, out);
   DMLP_LAUNCH_CHECK();
   return 0;
 }

@@ -1,4 +1,4 @@
-// screen_x1.hip — single-term bf16 MFMA screen with lane-parallel batched threshold compaction.
+// screen_x1.hip — single-term MFMA screen (fp16 host-rendered operands, bf16 device image) with lane-parallel batched threshold compaction.
 //
 // Same contract as screen_stream.hip (candidate ids per (query, slice), exact fp64 re-rank in
 // refine.hip), different balance:

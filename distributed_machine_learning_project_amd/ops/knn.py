@@ -33,7 +33,7 @@ SCREEN_KMAX_C = 256     # cap 512 class
 SCREEN_MAX_KT = 8       # A <= 256 on the screen path: the single-term screen and the LDS 3-term
 LDS_MAX_KT = 8          # screen (KT = 8 tiles stream through LDS as two 32 KiB stages)
 NUM_CUS = 256
-# "x1": single-term bf16 screen (default) | "stream": 3-term streaming screen | "lds": LDS-shared
+# "x1": single-term screen (fp16 operands on the host-operand path) (default) | "stream": 3-term streaming screen | "lds": LDS-shared
 SCREEN_IMPL = os.environ.get("DMLP_SCREEN", "x1")
 # slices of the host-rendered screen operands, each copied as soon as it is converted (1: measured
 # best on the bench shape — every extra slice costs ~20 us of copy-API time on the host)
