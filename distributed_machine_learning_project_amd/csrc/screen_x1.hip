@@ -35,7 +35,9 @@
 namespace {
 
 // profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
-// wrong results, timing only), 8 event counters (g_x1_dbg).  MODE 16 is not an ablation: the
+// wrong results, timing only), 8 event counters (g_x1_dbg), 32 / 64 fragment loads on every 2nd /
+// 4th step only (the others reuse stale ring registers: wrong results, timing only — what a
+// shared data ring would save on the texture path).  MODE 16 is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
@@ -345,6 +347,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   f32x4 acc[2][CT];
 #define DMLP_LOADA(J, R)                                                                        \
   do {                                                                                          \
+    if ((MODE & 32) && ((J) & 1)) break;                                                        \
+    if ((MODE & 64) && ((J) & 3)) break;                                                        \
     _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
       A[R][kt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(              \
           xr, lane * 16 + kt * ks, (J) * (KT * ks), 0));                                        \
@@ -510,6 +514,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 4: DMLP_X1_LAUNCH(4); break;
       case 6: DMLP_X1_LAUNCH(6); break;
       case 8: DMLP_X1_LAUNCH(8); break;
+      case 32: DMLP_X1_LAUNCH(32); break;
+      case 64: DMLP_X1_LAUNCH(64); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }
