@@ -227,6 +227,7 @@ int dmlp_fast_step(const double* X, const int* labels, int64_t N, const double* 
 int dmlp_fast_step_events(int on);
 int dmlp_fast_step_timeline(double* ms, const char** names, int cap);
 void dmlp_fast_step_parts(int parts);
+void dmlp_fast_step_rparts(int parts);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

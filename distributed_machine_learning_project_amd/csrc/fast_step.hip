@@ -12,6 +12,8 @@
 //   tail stream: per part, group refine (refine.hip, waits for the rows and the part's screen)
 //                -> the part's report text (GPU, at the previous part's device-side end) -> D2H
 //                of its byte range; then the byte count and the overflow count -> one host sync
+//                (one screen: the refine may run as R query ranges, DMLP_FAST_RPARTS, each
+//                range's D2H on a copy stream of its own under the next range's refine)
 //
 // Returns 0 (report and results written), 1 when the call is not this path's (k outside
 // [1, 32], data or queries outside the fp16 screen's range, no x1 variant for A: nothing the
@@ -87,6 +89,18 @@ int fast_parts() {
   }
   return g_parts;
 }
+// refine parts behind ONE screen (DMLP_FAST_RPARTS, 1..4; used when the screen is not split):
+// the refine runs as R launches over query ranges on the tail stream, and each range's report
+// text crosses PCIe on a stream of its own while the next range refines, so only the last
+// range's D2H stays on the critical path
+int g_rparts = -1;
+int fast_rparts() {
+  if (g_rparts < 0) {
+    const char* e = std::getenv("DMLP_FAST_RPARTS");
+    g_rparts = clamp_parts(e ? std::atoi(e) : 1);
+  }
+  return g_rparts;
+}
 
 // sum of the decimal digit counts of v over [a, b)
 int64_t digits_sum(int64_t a, int64_t b) {
@@ -99,8 +113,9 @@ int64_t digits_sum(int64_t a, int64_t b) {
 }
 
 struct Workspace {
-  hipStream_t side = nullptr, tail = nullptr;
+  hipStream_t side = nullptr, tail = nullptr, d2h = nullptr;
   hipEvent_t ev_ops[kMaxParts] = {}, ev_scr[kMaxParts] = {}, ev_rows = nullptr, ev_k = nullptr;
+  hipEvent_t ev_fmt[kMaxParts] = {};
   bool marks_on = false, marks_valid = false;
   hipEvent_t marks[M_N] = {};
   // device
@@ -173,9 +188,11 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   if (!w.side) {
     FS_CHK(hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking));
     FS_CHK(hipStreamCreateWithFlags(&w.tail, hipStreamNonBlocking));
+    FS_CHK(hipStreamCreateWithFlags(&w.d2h, hipStreamNonBlocking));
     for (int p = 0; p < kMaxParts; ++p) {
       FS_CHK(hipEventCreateWithFlags(&w.ev_ops[p], hipEventDisableTiming));
       FS_CHK(hipEventCreateWithFlags(&w.ev_scr[p], hipEventDisableTiming));
+      FS_CHK(hipEventCreateWithFlags(&w.ev_fmt[p], hipEventDisableTiming));
     }
     FS_CHK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     FS_CHK(hipEventCreateWithFlags(&w.ev_k, hipEventDisableTiming));
@@ -302,43 +319,60 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   double* out_d = w.out_d.get((size_t)Q * kmax);
   int* out_i = w.out_i.get((size_t)Q * kmax);
   int* status = w.status.get(Q);
-  int64_t* off = w.off.get((size_t)dmlp_format_scratch((int)Q) + 2 * P);
+  int64_t* off = w.off.get((size_t)dmlp_format_scratch((int)Q) + 2 * kMaxParts);
   char* text = w.text.get((size_t)dmlp_format_bound((int)Q));
   FS_PTR(out_d); FS_PTR(out_i); FS_PTR(out_lab); FS_PTR(out_cs); FS_PTR(status); FS_PTR(off);
   FS_PTR(text);
   FS_CHK(hipStreamWaitEvent(w.tail, w.ev_rows, 0));
   const int64_t bound = dmlp_format_bound((int)Q);
-  int64_t lo = 0;           // a lower bound on the byte where part p's text starts
+  // tail ranges: the screen parts, or (one screen) R query ranges of it
+  const int R = P > 1 ? P : (int)std::max<int64_t>(1, std::min<int64_t>(fast_rparts(), (Q + 63) / 64));
+  int64_t r0s[kMaxParts + 1];
+  for (int r = 0; r <= R; ++r)
+    r0s[r] = P > 1 ? q0s[r] : std::min<int64_t>(Q, (Q * r / R + 63) / 64 * 64);
+  r0s[R] = Q;
+  // the report bytes cross on their own stream when the refine is split (the next range refines
+  // meanwhile); one range keeps them on the tail stream
+  hipStream_t cp = R > 1 ? w.d2h : w.tail;
+  int64_t lo = 0;           // a lower bound on the byte where range r's text starts
   const int64_t* base = nullptr;
-  int64_t* off_p = off;     // part p's line offsets (scratch of its own: the next part reads its end)
-  for (int p = 0; p < P; ++p) {
-    const int64_t q0 = q0s[p], qp = q0s[p + 1] - q0;
-    FS_CHK(hipStreamWaitEvent(w.tail, w.ev_scr[p], 0));
-    int e = dmlp_refine_groups(cap, cand_ids + coff[p] * cap, cand_cnt + coff[p],
-                               cand_h + coff[p] * 2, Sp[p], Xd, A, Qd + q0 * A, xhi, xin,
-                               qhi + q0 * W, KT, 1, N, nullptr, kd + q0, (int)qp,
-                               out_d + q0 * kmax, out_i + q0 * kmax, kmax, lab_d, label_lo,
-                               label_hi, out_lab + q0, out_cs + q0, status + q0, ovf, w.tail);
+  int64_t* off_p = off;     // range r's line offsets (scratch of its own: the next reads its end)
+  for (int r = 0; r < R; ++r) {
+    const int64_t q0 = r0s[r], qp = r0s[r + 1] - q0;
+    const int sp = P > 1 ? r : 0;                              // the screen that served it
+    const int64_t c0 = P > 1 ? coff[r] : q0 * Sp[0];           // its first candidate slot
+    if (P > 1 || r == 0) FS_CHK(hipStreamWaitEvent(w.tail, w.ev_scr[sp], 0));
+    int e = dmlp_refine_groups(cap, cand_ids + c0 * cap, cand_cnt + c0, cand_h + c0 * 2, Sp[sp],
+                               Xd, A, Qd + q0 * A, xhi, xin, qhi + q0 * W, KT, 1, N, nullptr,
+                               kd + q0, (int)qp, out_d + q0 * kmax, out_i + q0 * kmax, kmax,
+                               lab_d, label_lo, label_hi, out_lab + q0, out_cs + q0, status + q0,
+                               ovf, w.tail);
     if (e) return e < 0 ? e : -1;
-    if (p == P - 1) FS_CHK(mark(M_REFINE, w.tail));
+    if (r == R - 1) FS_CHK(mark(M_REFINE, w.tail));
     e = dmlp_format_report_at(out_cs + q0, (int)qp, (int)(qid_base + q0), off_p, text, base,
                               w.tail);
     if (e) return e < 0 ? e : -1;
-    if (p == P - 1) FS_CHK(mark(M_FORMAT, w.tail));
-    // bytes [lo, the part's upper bound): lines of at most 48 bytes; [lo, previous end) is the
-    // previous part's text again (still intact on the device), copied after it in stream order
+    if (r == R - 1) FS_CHK(mark(M_FORMAT, w.tail));
+    if (cp != w.tail) {
+      FS_CHK(hipEventRecord(w.ev_fmt[r], w.tail));
+      FS_CHK(hipStreamWaitEvent(cp, w.ev_fmt[r], 0));
+    }
+    // bytes [lo, the range's upper bound): lines of at most 48 bytes; [lo, previous end) is the
+    // previous range's text again (still intact on the device), copied after it in stream order
+    // (bytes past this range's end that the next range's format may be writing meanwhile are
+    // copied again, complete, by the next range's copy, later on the same stream)
     const int64_t hi = std::min<int64_t>(bound, 48 * (q0 + qp));
-    FS_CHK(hipMemcpyAsync(report_dst + lo, text + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost,
-                          w.tail));
-    // the next part starts at or after this part's shortest text: "Query " qid " checksum: " d "\n"
+    FS_CHK(hipMemcpyAsync(report_dst + lo, text + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, cp));
+    // the next range starts at or after this range's shortest text: "Query " qid " checksum: " d "\n"
     lo += 19 * qp + digits_sum(qid_base + q0, qid_base + q0 + qp);
     base = off_p + qp;
-    off_p += qp + 1;  // (the next part's scratch: behind this part's offsets, below the bound)
+    off_p += qp + 1;  // (the next range's scratch: behind this range's offsets, below the bound)
   }
   FS_CHK(hipMemcpyAsync(len_h, base, sizeof(int64_t), hipMemcpyDeviceToHost, w.tail));
   FS_CHK(hipMemcpyAsync(small_h, ovf, sizeof(int), hipMemcpyDeviceToHost, w.tail));
-  FS_CHK(mark(M_D2H, w.tail));
+  FS_CHK(mark(M_D2H, cp));
   FS_CHK(hipStreamSynchronize(w.tail));
+  if (cp != w.tail) FS_CHK(hipStreamSynchronize(cp));
   FS_CHK(hipStreamSynchronize(st));
   w.marks_valid = w.marks_on;
   if (small_h[0]) return 2;  // some query's candidates overflowed: the general path escalates
@@ -350,6 +384,8 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
 
 // Query parts of the following calls (1..4; <= 0: back to DMLP_FAST_PARTS / 1).
 extern "C" void dmlp_fast_step_parts(int parts) { g_parts = parts <= 0 ? -1 : clamp_parts(parts); }
+// Refine ranges behind one screen (1..4; <= 0: back to DMLP_FAST_RPARTS / 1).
+extern "C" void dmlp_fast_step_rparts(int parts) { g_rparts = parts <= 0 ? -1 : clamp_parts(parts); }
 
 // Step-timeline marks of dmlp_fast_step (hipEvents with timing; off by default).
 extern "C" int dmlp_fast_step_events(int on) {

@@ -55,17 +55,22 @@ def test_shared_ingress_and_out_of_core(gpu, workload, monkeypatch, max_rows):
     eng.close()
 
 
-@pytest.mark.parametrize("kmax,fast,parts", [(32, True, 1), (32, True, 2), (24, True, 3),
-                                             (40, False, 1)])
-def test_native_fast_step(gpu, kmax, fast, parts):
+@pytest.mark.parametrize("kmax,fast,parts,rparts", [(32, True, 1, 1), (32, True, 2, 1),
+                                                    (24, True, 3, 1), (40, False, 1, 1),
+                                                    (32, True, 1, 2), (20, True, 1, 3)])
+def test_native_fast_step(gpu, kmax, fast, parts, rparts):
     """One rank over the node-shared segment, every k on the single-term class: the whole call
     runs in one native function (fast_step.hip) — report, labels and checksums == the oracle's,
     three calls in a row (reused buffers), in 1-3 query parts (each part's report text placed at
-    the previous part's device-side end); k > 32 falls through to the Python pipeline."""
+    the previous part's device-side end) or one screen with 2-3 refine ranges (each range's text
+    copied on the D2H stream while the next refines); k > 32 falls through to the Python
+    pipeline."""
     from distributed_machine_learning_project_amd import _lib
     from distributed_machine_learning_project_amd.utils.shm import share_input
     _lib.lib().dmlp_fast_step_parts(parts)
-    inp = dmlp.generate(7000, 9000 + 37 * parts, 32, 0.0, 1000.0, 1, kmax, 8, seed=kmax + parts)
+    _lib.lib().dmlp_fast_step_rparts(rparts)
+    inp = dmlp.generate(7000, 9000 + 37 * parts + 101 * rparts, 32, 0.0, 1000.0, 1, kmax, 8,
+                        seed=kmax + parts + 10 * rparts)
     d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
     lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
     eng = _engine("farm")
@@ -80,6 +85,7 @@ def test_native_fast_step(gpu, kmax, fast, parts):
     sh.close()
     eng.close()
     _lib.lib().dmlp_fast_step_parts(0)
+    _lib.lib().dmlp_fast_step_rparts(0)
 
 
 def test_debug_listing(gpu, workload):
