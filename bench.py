@@ -81,11 +81,12 @@ def main(argv=None):
     # sees the GPU working), and per-step jitter averages out
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--min-warmup-s", type=float, default=0.6,
+    ap.add_argument("--min-warmup-s", type=float, default=3.0,
                     help="keep running untimed warm-up steps (at least --warmup of them) until this "
-                         "much time has passed: the first ~0.5 s of a fresh process run up to 40 %% "
-                         "slower (clocks ramping; profiles/r3k_warmup.txt), which a 10-step warm-up "
-                         "does not cover")
+                         "much time has passed: a fresh process runs its first seconds up to 40 %% "
+                         "slower (profiles/r3k_warmup.txt; r6b: 2.77 ms/step after 0.6 s of warm-up "
+                         "vs 2.36 after 3 s on the same box), which a 10-step warm-up does not "
+                         "cover; the JSON's warmup_curve_ms shows the per-window means")
     ap.add_argument("--strategy", default="farm")
     ap.add_argument("--schedule", default="static", choices=["static", "dynamic"])
     ap.add_argument("--n-data", type=int, default=100_000)
@@ -166,6 +167,7 @@ def main(argv=None):
     import torch as _t
     t_w = time.perf_counter()
     warm = 0
+    curve, t_win, n_win = [], time.perf_counter(), 0  # mean ms/step of each ~0.25 s window
     while True:
         if warm >= a.warmup:
             # every rank takes the same decision (rank 0's clock), so all run the same step count
@@ -178,6 +180,11 @@ def main(argv=None):
                 break
         rep = step()
         warm += 1
+        n_win += 1
+        if time.perf_counter() - t_win >= 0.25:
+            now = time.perf_counter()
+            curve.append(round((now - t_win) / n_win * 1e3, 3))
+            t_win, n_win = now, 0
     comm.sync()
     comm.barrier()
     t0 = time.perf_counter()
@@ -226,6 +233,7 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "warmup_steps_run": warm,
+            "warmup_curve_ms": curve,
             "numa_node": Comm._numa,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,

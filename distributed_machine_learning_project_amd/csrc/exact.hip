@@ -106,7 +106,7 @@ __device__ __noinline__ void compact_rows(double* __restrict__ bd, int* __restri
   }
 }
 
-template <class C, bool PIPE>
+template <class C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C::WPE))) void k_exact_topk(const double* __restrict__ X, int64_t N, int A,
                                                     const double* __restrict__ Qx,
                                                     const int* __restrict__ qidx,
@@ -181,39 +181,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C::WPE))) v
       }
       // two attributes per step: 16-byte LDS reads; the sums stay in attribute order
       int a = 0;
-      if (PIPE && ac == AC) {
-        // a full chunk, unrolled, with the next attribute pair's LDS reads issued before the
-        // current pair's 3 RI PJ x 2 fp64 ops, so the reads' latency hides under VALU work
-        // instead of being exposed at the top of every pair (profiles/r4j: 33 % of wave
-        // cycles waiting)
-        double2 qv[2][RI], xv[2][PJ];
-#pragma unroll
-        for (int i = 0; i < RI; ++i) qv[0][i] = *(const double2*)&Qs[ty + 16 * i][0];
-#pragma unroll
-        for (int j = 0; j < PJ; ++j) xv[0][j] = *(const double2*)&Xs[tx + 16 * j][0];
-#pragma unroll
-        for (int s = 0; s < AC / 2; ++s) {
-          const int cb = s & 1, nb2 = cb ^ 1;
-          if (s + 1 < AC / 2) {
-#pragma unroll
-            for (int i = 0; i < RI; ++i)
-              qv[nb2][i] = *(const double2*)&Qs[ty + 16 * i][2 * s + 2];
-#pragma unroll
-            for (int j = 0; j < PJ; ++j)
-              xv[nb2][j] = *(const double2*)&Xs[tx + 16 * j][2 * s + 2];
-          }
-#pragma unroll
-          for (int i = 0; i < RI; ++i)
-#pragma unroll
-            for (int j = 0; j < PJ; ++j) {
-              const double d0 = __dsub_rn(qv[cb][i].x, xv[cb][j].x);
-              acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(d0, d0));
-              const double d1 = __dsub_rn(qv[cb][i].y, xv[cb][j].y);
-              acc[i][j] = __dadd_rn(acc[i][j], __dmul_rn(d1, d1));
-            }
-        }
-        a = ac;
-      }
       for (; a + 1 < ac; a += 2) {
         double2 qv[RI], xv[PJ];
 #pragma unroll
@@ -274,36 +241,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C::WPE))) v
                    kstride);
 }
 
-// software-pipelined inner loop (k_exact_topk<C, true>); DMLP_EXACT_PIPE=0 selects the plain one
-int g_exact_pipe = -1;
-bool exact_pipe() {
-  if (g_exact_pipe < 0) {
-    const char* e = getenv("DMLP_EXACT_PIPE");
-    g_exact_pipe = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_exact_pipe != 0;
-}
-
-template <class C, bool PIPE>
-int launch_exact_v(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
-                   const int* qk, int nb, double* out_d, int* out_i, int kstride, hipStream_t st) {
-  const int lds = C::LDS;
-  static const bool attr = hipFuncSetAttribute((const void*)&k_exact_topk<C, PIPE>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               lds) == hipSuccess;
-  if (!attr) return -5;
-  hipLaunchKernelGGL((k_exact_topk<C, PIPE>), dim3((unsigned)((nb + C::QB - 1) / C::QB)),
-                     dim3(256), lds, st, X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride);
-  DMLP_LAUNCH_CHECK();
-  return 0;
-}
-
 template <class C>
 int launch_exact(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
                  const int* qk, int nb, double* out_d, int* out_i, int kstride, hipStream_t st) {
-  return exact_pipe()
-             ? launch_exact_v<C, true>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st)
-             : launch_exact_v<C, false>(X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride, st);
+  const int lds = C::LDS;
+  static const bool attr = hipFuncSetAttribute((const void*)&k_exact_topk<C>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               lds) == hipSuccess;
+  if (!attr) return -5;
+  hipLaunchKernelGGL((k_exact_topk<C>), dim3((unsigned)((nb + C::QB - 1) / C::QB)), dim3(256),
+                     lds, st, X, N, A, Qx, qidx, qk, nb, out_d, out_i, kstride);
+  DMLP_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace

@@ -37,7 +37,8 @@ namespace {
 // profiling: 1 no candidate path, 2 no epilogue (MFMA + loads only), 4 no norm loads (C = 0:
 // wrong results, timing only), 8 event counters (g_x1_dbg), 32 / 64 fragment loads on every 2nd /
 // 4th step only (the others reuse stale ring registers: wrong results, timing only — what a
-// shared data ring would save on the texture path).  MODE 16 is not an ablation: the
+// shared data ring would save on the texture path), 128 no hit after the first compaction (the
+// threshold jumps to +inf: the step cost of a perfectly seeded threshold).  MODE 16 is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = 0;
 __device__ unsigned long long g_x1_dbg[8];
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * lcnt[(ct * 16 + c) * 4 + kg];
-        h[ct] = lh[ct * 16 + c];
+        h[ct] = (MODE & 128) ? INFINITY : lh[ct * 16 + c];
       }
       // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
       // pending after the conditional call and drains lgkmcnt at every following step
@@ -516,6 +517,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 8: DMLP_X1_LAUNCH(8); break;
       case 32: DMLP_X1_LAUNCH(32); break;
       case 64: DMLP_X1_LAUNCH(64); break;
+      case 128: DMLP_X1_LAUNCH(128); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }

@@ -53,15 +53,11 @@ for task in "$@"; do
       step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
     exact)
       step exact 300 python bench.py --exact --steps 5 --warmup 1 ;;
-    exactab)  # fused exact kernel: software-pipelined LDS reads (DMLP_EXACT_PIPE=1) vs plain, interleaved
-      for r in 1 2; do
-        for v in 0 1; do
-          DMLP_EXACT_PIPE=$v step "exact_pipe${v}_$r" 300 python bench.py --exact --steps 5 \
-              --warmup 1 --no-busbw --diag-steps 0
-        done
-      done
-      DMLP_EXACT_PIPE=1 step exact_pipe1_verify 300 python bench.py --exact --steps 2 --warmup 1 \
-          --no-busbw --diag-steps 0 --verify ;;
+    x1modes)  # k_screen_x1 ablations: production / no hits after the first compaction / MFMA+loads only / event counters
+      step x1modes 300 rocprofv3 --kernel-trace --stats -d "$OUT/x1modes" -o run --output-format csv \
+          -- python3 tools/quick_gpu_bench.py --q 131072 --iters 5 --check 0 --modes 0,128,2,0,128,8
+      grep -h "mode\|per call" "$OUT/x1modes.log"
+      find "$OUT/x1modes" -name '*kernel_stats.csv' -exec sh -c 'grep k_screen_x1 "$1" | cut -c1-200' _ {} \; ;;
     rparts)  # native step: 1 / 2 / 3 refine ranges behind one screen (DMLP_FAST_RPARTS), interleaved
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step rparts_ab 600 bash tools/kernel_ab.sh \
           r1:DMLP_FAST_RPARTS=1 r2:DMLP_FAST_RPARTS=2 r3:DMLP_FAST_RPARTS=3 ;;
