@@ -187,12 +187,16 @@ def main(argv=None):
             t_win, n_win = now, 0
     comm.sync()
     comm.barrier()
+    thr0 = _cgroup_cpu_stat()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    marks = [0.0] * a.steps  # host return time of each step (a perf_counter read per step)
+    for j in range(a.steps):
         rep = step()
+        marks[j] = time.perf_counter()
     comm.sync()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    thr1 = _cgroup_cpu_stat()
     elapsed_mine = elapsed
     # max over ranks
     el = torch.tensor([elapsed], dtype=torch.float64, device=comm.device)
@@ -204,6 +208,20 @@ def main(argv=None):
     my_ms = elapsed_mine / max(1, a.steps) * 1e3  # this rank's own clock
 
     extra = _world_report(comm, host_plane, a)
+    # the timed steps' spread and the CPU quota throttling the cgroup saw meanwhile: a slow run
+    # with uniformly slow steps points at the device side, one with a few very slow steps and
+    # throttled time at the host's CPU quota (the render pool + main thread spinning)
+    if a.steps:
+        st = np.diff(np.array([t0] + marks)) * 1e3
+        extra["timed_step_ms"] = {"p10": round(float(np.percentile(st, 10)), 4),
+                                  "p50": round(float(np.percentile(st, 50)), 4),
+                                  "p90": round(float(np.percentile(st, 90)), 4),
+                                  "max": round(float(st.max()), 4)}
+    if thr0 and thr1:
+        extra["cgroup_cpu_during_timed"] = {
+            "usage_ms": round((thr1.get("usage_usec", 0) - thr0.get("usage_usec", 0)) / 1e3, 1),
+            "nr_throttled": thr1.get("nr_throttled", 0) - thr0.get("nr_throttled", 0),
+            "throttled_ms": round((thr1.get("throttled_usec", 0) - thr0.get("throttled_usec", 0)) / 1e3, 1)}
     if a.diag_steps > 0:
         extra.update(_diagnostics(comm, eng, step, a.diag_steps, my_ms))
     if world > 1 and comm.backend == "nccl" and not a.no_busbw:
@@ -263,6 +281,25 @@ def main(argv=None):
         inp.close()
     eng.close()
     return 0
+
+
+def _cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters of this process's cgroup (usage_usec, nr_throttled,
+    throttled_usec), or {} when unreadable."""
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = next((ln.split(":", 2)[2].strip() for ln in f if ln.startswith("0::")), None)
+        for path in ([f"/sys/fs/cgroup{rel}/cpu.stat"] if rel else []) + [
+                "/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"]:  # v2, then v1
+            if os.path.exists(path):
+                with open(path) as f:
+                    d = {k: int(v) for k, v in (ln.split() for ln in f if len(ln.split()) == 2)}
+                if "throttled_time" in d:  # v1: ns
+                    d["throttled_usec"] = d["throttled_time"] // 1000
+                return d
+    except (OSError, ValueError, StopIteration):
+        pass
+    return {}
 
 
 def _world_report(comm, host_plane, a):

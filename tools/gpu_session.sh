@@ -49,6 +49,8 @@ for task in "$@"; do
           --timeout-method thread -k "${KTESTS:?KTESTS}" ;;
     bench)
       step bench 300 python bench.py ;;
+    bench3)  # three headline runs in a row (run-to-run spread: timed_step_ms, cgroup throttling)
+      for r in 1 2 3; do step bench_$r 300 python bench.py; done ;;
     verify)
       step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
     exact)
