@@ -74,6 +74,7 @@ _SIGS = {
     "dmlp_fast_step_events": (i32, [i32]),
     "dmlp_fast_step_parts": (None, [i32]),
     "dmlp_fast_step_rparts": (None, [i32]),
+    "dmlp_fast_step_early": (None, [i32]),
     "dmlp_fast_step_timeline": (i32, [vp, vp, i32]),
     "dmlp_fast_step": (i32, [vp, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i64, i32, vp, i64,
                              vp, vp, vp, vp]),

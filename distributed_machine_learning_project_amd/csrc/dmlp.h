@@ -213,6 +213,14 @@ int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
                            const int* qk, int nq, const unsigned* xnmax_bits, const unsigned* bad,
                            const float* hseed, int ccap, int S, int* cand_ids, int* cand_cnt,
                            float* cand_h, void* stream);
+// The single-term screen (fp16 host image, S = 1) started while the image is still crossing
+// PCIe: rdy[i] != 0 once tiles [i rdy_tiles, (i + 1) rdy_tiles) and their max norm xnm_sl[i]
+// landed; the screen waits per slice and grows each column's eps with the slices it has seen.
+int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
+                         int64_t n_points, const void* qhi, const float* qn, const int* qidx,
+                         const int* qk, int nq, int kmax, const unsigned* bad, const unsigned* rdy,
+                         int rdy_tiles, int rdy_n, const unsigned* xnm_sl, int* cand_ids,
+                         int* cand_cnt, float* cand_h, void* stream);
 
 // The single-GPU call for every k in [kmin, kmax] within [1, 32] in one native function
 // (fast_step.hip): host render + copies, screen, rows behind it, refine, report text into
@@ -228,6 +236,7 @@ int dmlp_fast_step_events(int on);
 int dmlp_fast_step_timeline(double* ms, const char** names, int cap);
 void dmlp_fast_step_parts(int parts);
 void dmlp_fast_step_rparts(int parts);
+void dmlp_fast_step_early(int on);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

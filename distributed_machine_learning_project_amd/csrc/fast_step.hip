@@ -102,6 +102,19 @@ int fast_rparts() {
   return g_rparts;
 }
 
+// early start (DMLP_FAST_EARLY=1; one part, one screen slice): the query operands cross first and
+// the screen starts on them while the dataset image follows in kEarlySlices slices, each with a
+// ready word the screen waits on (screen_x1.hip dmlp_screen_x1_early)
+constexpr int kEarlySlices = 4;
+int g_early = -1;
+bool fast_early() {
+  if (g_early < 0) {
+    const char* e = std::getenv("DMLP_FAST_EARLY");
+    g_early = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_early != 0;
+}
+
 // sum of the decimal digit counts of v over [a, b)
 int64_t digits_sum(int64_t a, int64_t b) {
   int64_t s = 0, lo = 0, hi = 10;
@@ -206,7 +219,7 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   // page-locked staging + device buffers (grow-only)
   uint16_t* xhi_h = w.xhi_h.get(nt * 64 * W);
   float* xin_h = w.xin_h.get(nt * 64);
-  unsigned* xnm_h = w.xnm_h.get(2);
+  unsigned* xnm_h = w.xnm_h.get(2 + kEarlySlices);
   uint16_t* qhi_h = w.qhi_h.get(Q * W);
   float* qn_h = w.qn_h.get(Q);
   double* mu = w.mu_h.get(A);
@@ -215,7 +228,7 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   int64_t* len_h = w.len_h.get(2);
   short* xhi = w.xhi.get(nt * 64 * W);
   float* xin = w.xin.get(nt * 64);
-  unsigned* words = w.words.get(2);
+  unsigned* words = w.words.get(2 + 2 * kEarlySlices);  // + early start: ready words, max norms
   short* qhi = w.qhi.get(Q * W);
   float* qn = w.qn.get(Q);
   int* kd = w.kdev.get(Q);
@@ -229,10 +242,7 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
   // in slices (side); a query call renders no tiles and writes its (zero) norm word into
   // words[1], the "bad" word, which the host-checked ranges leave at 0
   const int ch = chunks < 1 ? 1 : chunks;
-  int rc = dmlp_host_ops_h2d_tiles(X, N, 0, nt, Qx, 0, A, mu, KT, xhi_h, xin_h, xnm_h, qhi_h,
-                                   qn_h, xhi, xin, words, qhi, qn, ch, w.side);
-  FS_CHK(mark(M_DATA, w.side));
-  if (rc & 4) return -(int)hipErrorUnknown;
+  int rc = 0;
   std::memcpy(k_h, k, (size_t)Q * sizeof(int));
   FS_CHK(hipMemcpyAsync(kd, k_h, (size_t)Q * sizeof(int), hipMemcpyHostToDevice, w.side));
   // identity query list (grow-only, written once)
@@ -259,6 +269,19 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
                    dmlp_screen_x1_waves_per_cu_kt(KT, kmax), dmlp_screen_x1_min_slices(nt));
     coff[p + 1] = coff[p] + qp * Sp[p];
   }
+  const bool early = fast_early() && P == 1 && Sp[0] == 1 && nt >= 2 && nt <= 4096;
+  const int NS = early ? (int)std::min<int64_t>(kEarlySlices, nt) : 0;
+  const int rt = early ? (int)((nt + NS - 1) / NS) : 1;  // image tiles per early slice
+  unsigned* const rdy = words + 2;                         // [NS] ready words
+  unsigned* const xnm_sl = words + 2 + kEarlySlices;       // [NS] slice max norms
+  if (!early) {
+    rc = dmlp_host_ops_h2d_tiles(X, N, 0, nt, Qx, 0, A, mu, KT, xhi_h, xin_h, xnm_h, qhi_h, qn_h,
+                                 xhi, xin, words, qhi, qn, ch, w.side);
+    FS_CHK(mark(M_DATA, w.side));
+    if (rc & 4) return -(int)hipErrorUnknown;
+  } else {
+    FS_CHK(hipMemsetAsync(rdy, 0, (size_t)NS * sizeof(unsigned), w.side));
+  }
   int* cand_ids = w.cand_ids.get((size_t)coff[P] * cap);
   int* cand_cnt = w.cand_cnt.get((size_t)coff[P]);
   float* cand_h = w.cand_h.get((size_t)coff[P] * 2);
@@ -281,12 +304,37 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
     FS_CHK(hipEventRecord(w.ev_ops[p], w.side));
     // ---- main: the part's screen as soon as its operands landed
     FS_CHK(hipStreamWaitEvent(st, w.ev_ops[p], 0));
-    const int e = dmlp_screen_x1(KT, 1, A, xhi, xin, nt, N, qhi + q0 * W, qn + q0, w.ident.p,
-                                 kd + q0, (int)qp, kmax, words, words + 1, Sp[p],
-                                 cand_ids + coff[p] * cap, cand_cnt + coff[p],
-                                 cand_h + coff[p] * 2, st);
+    const int e =
+        early ? dmlp_screen_x1_early(KT, A, xhi, xin, nt, N, qhi + q0 * W, qn + q0, w.ident.p,
+                                     kd + q0, (int)qp, kmax, words + 1, rdy, rt, NS, xnm_sl,
+                                     cand_ids + coff[p] * cap, cand_cnt + coff[p],
+                                     cand_h + coff[p] * 2, st)
+              : dmlp_screen_x1(KT, 1, A, xhi, xin, nt, N, qhi + q0 * W, qn + q0, w.ident.p,
+                               kd + q0, (int)qp, kmax, words, words + 1, Sp[p],
+                               cand_ids + coff[p] * cap, cand_cnt + coff[p],
+                               cand_h + coff[p] * 2, st);
     if (e) return e < 0 ? e : -1;
     FS_CHK(hipEventRecord(w.ev_scr[p], st));
+  }
+  if (early) {
+    // the dataset image behind the queries, slice by slice, each followed by its ready word (the
+    // running screen waits on it); every word is written even when a slice is out of the fp16
+    // range, so the screen always drains before the caller falls back
+    small_h[8] = 1;
+    for (int i = 0; i < NS; ++i) {
+      const int64_t a = (int64_t)i * rt, b = std::min<int64_t>(nt, a + rt);
+      rc |= dmlp_host_ops_h2d_tiles(X, N, a, b, Qx, 0, A, mu, KT, xhi_h, xin_h, xnm_h + 2 + i,
+                                    qhi_h, qn_h, xhi + a * 64 * W, xin + a * 64, xnm_sl + i, qhi,
+                                    qn, 1, w.side);
+      FS_CHK(hipMemcpyAsync(rdy + i, small_h + 8, sizeof(unsigned), hipMemcpyHostToDevice,
+                            w.side));
+    }
+    FS_CHK(mark(M_DATA, w.side));
+    if (rc) {  // hip error or data outside the fp16 screen's range
+      FS_CHK(hipStreamSynchronize(w.side));
+      FS_CHK(hipStreamSynchronize(st));
+      return (rc & 4) ? -(int)hipErrorUnknown : 1;
+    }
   }
   FS_CHK(mark(M_SCREEN, st));
   // ---- side: labels and the fp64 rows behind the screen
@@ -386,6 +434,8 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
 extern "C" void dmlp_fast_step_parts(int parts) { g_parts = parts <= 0 ? -1 : clamp_parts(parts); }
 // Refine ranges behind one screen (1..4; <= 0: back to DMLP_FAST_RPARTS / 1).
 extern "C" void dmlp_fast_step_rparts(int parts) { g_rparts = parts <= 0 ? -1 : clamp_parts(parts); }
+// Early start of the following calls (1 on, 0 off, < 0: back to DMLP_FAST_EARLY).
+extern "C" void dmlp_fast_step_early(int on) { g_early = on < 0 ? -1 : (on ? 1 : 0); }
 
 // Step-timeline marks of dmlp_fast_step (hipEvents with timing; off by default).
 extern "C" int dmlp_fast_step_events(int on) {

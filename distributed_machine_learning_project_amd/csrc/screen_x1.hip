@@ -99,7 +99,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
     const unsigned* __restrict__ bad, float r1, float r2, float r3, int S, int tiles_per_slice,
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
-    float* __restrict__ cand_h, const float* __restrict__ hseed, int ccap) {
+    float* __restrict__ cand_h, const float* __restrict__ hseed, int ccap,
+    const unsigned* __restrict__ rdy, int rdy_tiles, int rdy_n,
+    const unsigned* __restrict__ xnm_sl) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   // COLLECT (large k, second pass): the threshold is fixed at the query's seed hseed[p] (a
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
@@ -145,7 +147,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       if (pbase + col < nq) cand_cnt[(int64_t)(pbase + col) * S + s] = -1;
     return;
   }
-  const float xnmax = __uint_as_float(*xnmax_bits);
+  // EARLY START (rdy != nullptr, S == 1): the data image is still crossing PCIe in rdy_n slices
+  // of rdy_tiles tiles; rdy[i] turns nonzero once slice i (and its max norm xnm_sl[i]) landed.
+  // The wave waits for a slice before its ring loads reach it, and a column's eps only covers
+  // the slices scanned so far: it grows at each new slice (and its threshold drops by twice the
+  // growth), so every compaction's bound holds for the entries it judges.  A wait that times
+  // out marks the wave's queries overflowed (the caller reruns the call on its general path).
+  int have = 0;          // slices known landed (wave-uniform)
+  bool rdy_fail = false;
+  auto wait_slice = [&](int i) -> bool {
+    unsigned* const f = const_cast<unsigned*>(rdy + i);
+    for (int it = 0; it < (1 << 21); ++it) {
+      if (__builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u)
+        return true;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+  };
+  auto cum_xnm = [&](int upto) {
+    float m = 0.0f;
+    for (int i = 0; i <= upto; ++i) {
+      const unsigned* const f = xnm_sl + i;
+      m = fmaxf(m, __uint_as_float(__hip_atomic_load(const_cast<unsigned*>(f), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM)));
+    }
+    return m;
+  };
+  float xnmax;
+  if (rdy) {
+    const int need = min(2 / rdy_tiles, rdy_n - 1);  // tiles 0..2: the prologue and step 0's loads
+    for (int i = 0; i <= need; ++i) rdy_fail |= !wait_slice(i);
+    have = need + 1;
+    xnmax = cum_xnm(need);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  } else {
+    xnmax = __uint_as_float(*xnmax_bits);
+  }
 
   bf16x8 bh[CT][KT];
   float h[CT];
@@ -426,6 +464,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     trig = 0;                                                                                   \
   } while (0)
 
+  // EARLY START: a new slice's max norm raises the eps of every column (see above)
+  auto eps_of = [&](float qv, float xm) {
+    return r1 * sqrtf(qv) * sqrtf(xm) + r2 * xm + r3 * (sqrtf(qv) + sqrtf(xm)) + r3 * 0x1p-15f;
+  };
+  auto grow = [&](float xm) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int col = ct * 16 + c;
+      const int p = pbase + col;
+      if (p < nq) {
+        const float e_old = leps[col];
+        const float e_new = eps_of(qn[qidx[p]], xm);
+        if (h[ct] > -FLT_MAX && h[ct] < INFINITY) h[ct] -= 2.0f * (e_new - e_old);
+        dmlp::wave_sync();  // every lane has read e_old before lane c rewrites it
+        if (lane < 16) {
+          leps[col] = e_new;
+          lh[col] = h[ct];
+        }
+      }
+    }
+    dmlp::wave_sync();
+  };
+  if (rdy && rdy_fail) {  // the data never arrived: report overflow, stop appending
+    for (int col = lane; col < C::NCOL; col += 64) lflag[col] = 1;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) h[ct] = INFINITY;
+    have = rdy_n;
+    dmlp::wave_sync();
+  }
   unsigned long long trig = 0;  // wave-uniform: some lane's sub-buffer passed its limit
   // The C-operand ring: window w (steps 4w .. 4w + 3, 64 floats) sits in LDS slot w & 1; lane L
   // moves float L of a window (one dword per lane, 4 steps ahead of its first read).  16 lanes
@@ -451,6 +518,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       __builtin_amdgcn_sched_barrier(0);
     }
     for (int j0 = 0; j0 < nsteps; j0 += D) {
+      if (rdy && have < rdy_n) {
+        // this iteration's loads reach tile (j0 + 11) / 4 (C-operand window j0/4 + 2)
+        const int need = min(((j0 + 11) >> 2) / rdy_tiles, rdy_n - 1);
+        if (need >= have) {
+          bool ok = true;
+          for (int i = have; i <= need; ++i) ok &= wait_slice(i);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          have = need + 1;
+          if (ok) {
+            const float xm = cum_xnm(need);
+            if (xm > xnmax) {
+              grow(xm);
+              xnmax = xm;
+            }
+          } else {
+            for (int col = lane; col < C::NCOL; col += 64) lflag[col] = 1;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) h[ct] = INFINITY;
+            have = rdy_n;
+            dmlp::wave_sync();
+          }
+        }
+      }
 #pragma unroll
       for (int r = 0; r < D; ++r) {
         const int j = j0 + r;  // D = 4: j < nsteps (nsteps % 4 == 0); D = 8: guarded epilogue
@@ -505,7 +595,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, float r3, int S,
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream,
-              const float* hseed = nullptr, int ccap = 0) {
+              const float* hseed = nullptr, int ccap = 0, const unsigned* rdy = nullptr,
+              int rdy_tiles = 1, int rdy_n = 0, const unsigned* xnm_sl = nullptr) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
@@ -515,7 +606,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
   hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M, F16>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
-                     n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap)
+                     n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap, rdy, rdy_tiles,     \
+                     rdy_n, xnm_sl)
   if (hseed) {  // the COLLECT pass (SUB = 16, CT = 4, fp16 only: see dmlp_screen_x1_collect)
     if constexpr (SUB == 16 && CTV == 4 && F16) DMLP_X1_LAUNCH(16);
     else return -3;
@@ -706,4 +798,47 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
   DMLP_X1_PICK(false);
 #undef DMLP_X1_PICK
 #undef DMLP_X1_ARGS
+}
+
+// The single-term screen over the host's fp16 image while that image is still crossing PCIe
+// (fast_step.hip's early start): one data slice per workgroup (S = 1), rdy[i] != 0 once image
+// tiles [i rdy_tiles, (i + 1) rdy_tiles) and their max norm xnm_sl[i] (fp32 bits) landed.  The
+// result is the one dmlp_screen_x1(KT, 1, ...) gives with S = 1 once every slice landed.
+extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit,
+                                    int64_t n_tiles, int64_t n_points, const void* qhi,
+                                    const float* qn, const int* qidx, const int* qk, int nq,
+                                    int kmax, const unsigned* bad, const unsigned* rdy,
+                                    int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
+                                    int* cand_ids, int* cand_cnt, float* cand_h, void* stream) {
+  if (nq <= 0) return 0;
+  if (n_tiles < 1 || n_tiles > 4096 || n_points > n_tiles * 64 || !rdy || !xnm_sl ||
+      rdy_tiles < 1 || rdy_n < 1 || (int64_t)rdy_tiles * rdy_n < n_tiles)
+    return -1;
+  if (kmax > 32 || !x1_kt_ok(KT) || A > KT * 32) return -3;
+  float r1, r2, r3;
+  dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
+  hipStream_t st = (hipStream_t)stream;
+  const int sub = x1_sub(kmax), ct = x1_ct(kmax);
+#define DMLP_X1E(KTV, SUBV, CTV)                                                                \
+  return launch_x1<KTV, SUBV, 4, 2, CTV, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, \
+                                               qk, nq, bad, bad, r1, r2, r3, 1, cand_ids,      \
+                                               cand_cnt, cand_h, st, nullptr, 0, rdy, rdy_tiles, \
+                                               rdy_n, xnm_sl)
+  if (KT == 1) {
+    if (sub == 32) DMLP_X1E(1, 32, 4);
+    if (ct == 8) DMLP_X1E(1, 16, 8);
+    DMLP_X1E(1, 16, 4);
+  }
+  if (KT == 2) {
+    if (sub == 32) DMLP_X1E(2, 32, 4);
+    if (ct == 8) DMLP_X1E(2, 16, 8);
+    DMLP_X1E(2, 16, 4);
+  }
+  if (KT == 4) {
+    if (sub == 32) DMLP_X1E(4, 32, 4);
+    DMLP_X1E(4, 16, 4);
+  }
+  if (sub == 32) DMLP_X1E(8, 32, 4);
+  DMLP_X1E(8, 16, 4);
+#undef DMLP_X1E
 }

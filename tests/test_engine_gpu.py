@@ -88,6 +88,36 @@ def test_native_fast_step(gpu, kmax, fast, parts, rparts):
     _lib.lib().dmlp_fast_step_rparts(0)
 
 
+@pytest.mark.parametrize("n,kmax", [(2000, 16), (5000, 32)])
+def test_native_fast_step_early(gpu, n, kmax):
+    """Early start (DMLP_FAST_EARLY): the screen starts on the query operands while the dataset
+    image crosses PCIe in 4 slices with ready words, each column's eps growing with the slices
+    it has seen.  It needs one screen slice (>= 131072 queries fill the chip at S = 1); the
+    report, labels and checksums == the oracle's over three calls, and == the default path."""
+    from distributed_machine_learning_project_amd import _lib
+    from distributed_machine_learning_project_amd.utils.shm import share_input
+    inp = dmlp.generate(n, 131072 + 64 * 3, 32, 0.0, 1000.0, 1, kmax, 8, seed=n + kmax)
+    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    expect = dmlp.format_report(cs)
+    eng = _engine("farm")
+    sh = share_input(eng.comm, inp)
+    try:
+        for early in (1, 0, 1):
+            _lib.lib().dmlp_fast_step_early(early)
+            for _ in range(2 if early else 1):
+                n0 = K.FAST_STEP_CALLS[0]
+                out = eng.KNN(sh.params, sh, None)
+                assert bytes(eng.report(out)) == expect
+                np.testing.assert_array_equal(out.labels_np(), lab_ref)
+                np.testing.assert_array_equal(out.checksums_np(), cs)
+                assert K.FAST_STEP_CALLS[0] == n0 + 1
+    finally:
+        _lib.lib().dmlp_fast_step_early(-1)
+        sh.close()
+        eng.close()
+
+
 def test_debug_listing(gpu, workload):
     inp, _, d, i = workload
     eng = _engine("ring", debug=True)
