@@ -102,15 +102,16 @@ int fast_rparts() {
   return g_rparts;
 }
 
-// early start (DMLP_FAST_EARLY=1; one part, one screen slice): the query operands cross first and
-// the screen starts on them while the dataset image follows in kEarlySlices slices, each with a
-// ready word the screen waits on (screen_x1.hip dmlp_screen_x1_early)
-constexpr int kEarlySlices = 4;
+// early start (default on, DMLP_FAST_EARLY=0 off; one part, one screen slice): the query operands
+// cross first and the screen starts on them while the dataset image follows in kEarlySlices
+// slices, each with a ready word the screen waits on (screen_x1.hip dmlp_screen_x1_early).
+// profiles/r6f: 2.23-2.24 vs 2.35-2.38 ms/step (4 slices, interleaved on one box)
+constexpr int kEarlySlices = 8;
 int g_early = -1;
 bool fast_early() {
   if (g_early < 0) {
     const char* e = std::getenv("DMLP_FAST_EARLY");
-    g_early = (e && e[0] == '1') ? 1 : 0;
+    g_early = (e && e[0] == '0') ? 0 : 1;
   }
   return g_early != 0;
 }

@@ -38,8 +38,8 @@ namespace {
 // wrong results, timing only), 8 event counters (g_x1_dbg), 32 / 64 fragment loads on every 2nd /
 // 4th step only (the others reuse stale ring registers: wrong results, timing only — what a
 // shared data ring would save on the texture path), 128 no hit after the first compaction (the
-// threshold jumps to +inf: the step cost of a perfectly seeded threshold), 256 per-tile append
-// branches in the taken path (correct results: an A/B variant).  MODE 16 is not an ablation: the
+// threshold jumps to +inf: the step cost of a perfectly seeded threshold; profiles/r6c).  MODE 16
+// is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = -1;  // -1: DMLP_X1_MODE (read once; default 0)
 int x1_mode() {
@@ -107,7 +107,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
   // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
   constexpr bool COLLECT = (MODE & 16) != 0;
-  constexpr bool TILEBR = (MODE & 256) != 0;  // per-tile append branches (A/B, DMLP_X1_MODE=256)
   constexpr int CT = C::CT;
   constexpr int D = C::D;
   constexpr int NH = C::NCOL / 64;  // columns per lane in the lane-owns-column phases
@@ -446,9 +445,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       unsigned gl_ = (unsigned)((J) * 4 + kg);                                                  \
       asm volatile("" : "+v"(gl_)); /* one VGPR: each key is a single v_and_or / v_bfi */       \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
-        /* TILEBR: a wave-uniform branch per tile, so a taken step appends only the tiles     \
-           some lane of which hit (past the saturated head of the scan usually one of 4) */    \
-        if (TILEBR && !__ballot(hit_[ct])) continue;                                            \
         *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                       \
             (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                      \
         addr[ct] += hit_[ct] ? 16u : 0u;                                                        \
@@ -622,7 +618,6 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 32: DMLP_X1_LAUNCH(32); break;
       case 64: DMLP_X1_LAUNCH(64); break;
       case 128: DMLP_X1_LAUNCH(128); break;
-      case 256: DMLP_X1_LAUNCH(256); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }
