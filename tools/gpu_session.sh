@@ -60,6 +60,12 @@ for task in "$@"; do
           -- python3 tools/quick_gpu_bench.py --q 131072 --iters 5 --check 0 --modes 0,128,2,0,128,8
       grep -h "mode\|per call" "$OUT/x1modes.log"
       find "$OUT/x1modes" -name '*kernel_stats.csv' -exec sh -c 'grep k_screen_x1 "$1" | cut -c1-200' _ {} \; ;;
+    early)  # native step early start (default) -- its tests, verify, interleaved step A/B against DMLP_FAST_EARLY=0
+      step early_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+          --timeout-method thread -k "fast_step"
+      step early_verify 300 python bench.py --steps 20 --warmup 2 --verify
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step early_ab 900 bash tools/kernel_ab.sh base:DMLP_FAST_EARLY=0 \
+          early:DMLP_FAST_EARLY=1 ;;
     rparts)  # native step: 1 / 2 / 3 refine ranges behind one screen (DMLP_FAST_RPARTS), interleaved
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step rparts_ab 600 bash tools/kernel_ab.sh \
           r1:DMLP_FAST_RPARTS=1 r2:DMLP_FAST_RPARTS=2 r3:DMLP_FAST_RPARTS=3 ;;
