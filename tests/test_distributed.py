@@ -255,6 +255,10 @@ def test_bench_launches_its_ranks(ingress):
     assert res["collective_check"]["ok"]
     if ingress == "root":  # broadcast / scatter / gather on every rank
         assert all(c > 0 for c in res["collective_check"]["calls_per_rank"])
+    # the timed steps' spread and the warm-up curve travel with the mean
+    ts = res["timed_step_ms"]
+    assert 0 < ts["p10"] <= ts["p50"] <= ts["p90"] <= ts["max"]
+    assert isinstance(res["warmup_curve_ms"], list)
 
 
 def test_collective_log_compare():
