@@ -116,6 +116,16 @@ bool fast_early() {
   return g_early != 0;
 }
 
+// query render slices under the early start (DMLP_FAST_QCHUNKS; default: the caller's count): the
+// query operands are the whole front of the step there, so their last slice's copy is exposed
+int early_qchunks(int ch) {
+  static const int q = [] {
+    const char* e = std::getenv("DMLP_FAST_QCHUNKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return q > 0 ? std::min(q, 16) : ch;
+}
+
 // sum of the decimal digit counts of v over [a, b)
 int64_t digits_sum(int64_t a, int64_t b) {
   int64_t s = 0, lo = 0, hi = 10;
@@ -293,7 +303,7 @@ extern "C" int dmlp_fast_step(const double* X, const int* labels, int64_t N, con
     const int64_t q0 = q0s[p], qp = q0s[p + 1] - q0;
     rc |= dmlp_host_ops_h2d_tiles(X, N, nt, nt, Qx + q0 * A, qp, A, mu, KT, xhi_h, xin_h,
                                   xnm_h + 1, qhi_h + q0 * W, qn_h + q0, xhi, xin, words + 1,
-                                  qhi + q0 * W, qn + q0, ch, w.side);
+                                  qhi + q0 * W, qn + q0, early ? early_qchunks(ch) : ch, w.side);
     if (rc & 4) return -(int)hipErrorUnknown;
     if (rc) {  // outside the fp16 screen's range: the caller's general path decides
       FS_CHK(hipStreamSynchronize(w.side));

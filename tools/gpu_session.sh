@@ -66,6 +66,9 @@ for task in "$@"; do
       step early_verify 300 python bench.py --steps 20 --warmup 2 --verify
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step early_ab 900 bash tools/kernel_ab.sh base:DMLP_FAST_EARLY=0 \
           early:DMLP_FAST_EARLY=1 ;;
+    qchunks)  # early start: query render slices 2 / 4 / 6 (DMLP_FAST_QCHUNKS), interleaved
+      AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step qchunks_ab 900 bash tools/kernel_ab.sh \
+          q2:DMLP_FAST_QCHUNKS=2 q4:DMLP_FAST_QCHUNKS=4 q6:DMLP_FAST_QCHUNKS=6 ;;
     rparts)  # native step: 1 / 2 / 3 refine ranges behind one screen (DMLP_FAST_RPARTS), interleaved
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step rparts_ab 600 bash tools/kernel_ab.sh \
           r1:DMLP_FAST_RPARTS=1 r2:DMLP_FAST_RPARTS=2 r3:DMLP_FAST_RPARTS=3 ;;
