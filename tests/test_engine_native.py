@@ -247,3 +247,28 @@ def test_fast_path_serves_any_k_and_escalates_per_query(tmp_path):
     for env in ({"KNN_X1K": "0"}, {"KNN_X1K": "0", "KNN_LDS_SINGLE": "0"}):
         out, _ = _run(["--strategy", "farm"], path, env=env)
         assert out == dmlp.format_report(cs)
+
+
+# ---------------------------------------------------------------- the reference runner's `make`
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_make_engine_targets_cpu(tmp_path):
+    """run_bench.sh:74,84 runs `make` and then `mpirun ./engine < input`: the top-level Makefile's
+    engine / engine.debug targets (the reference's unmodified common.cpp + the drop-in) build and
+    print the fp64 oracle's bytes at np 1 and 2, release and DEBUG listing."""
+    if build.reference_harness() is None:
+        pytest.skip("reference common.cpp not present")
+    r = subprocess.run(["make", "-C", ROOT, "engine", "engine.debug"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    path, inp, res, lab, cs = _case(tmp_path, N=800, Q=50, kmax=30, seed=4)
+    rel, dbg = os.path.join(ROOT, "engine"), os.path.join(ROOT, "engine.debug")
+    assert _run_dropin(rel, path, {"KNN_DEVICE": "cpu"}) == dmlp.format_report(cs)
+    assert _run_dropin(dbg, path, {"KNN_DEVICE": "cpu"}) == _debug_expect(inp, res, lab)
+    if os.path.exists(MPIEXEC):
+        assert _run_dropin(rel, path, {"KNN_DEVICE": "cpu"}, np_=2) == dmlp.format_report(cs)
+    # up to date: a second `make` rebuilds nothing
+    r = subprocess.run(["make", "-C", ROOT, "-q", "engine", "engine.debug"], capture_output=True,
+                       timeout=60)
+    assert r.returncode == 0

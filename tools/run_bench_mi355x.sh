@@ -6,13 +6,18 @@
 # are compared like run_bench.sh:29-72.  Inputs are generated (the reference's inputs.zip is
 # absent) and cached under inputs/.
 #
-#   tools/run_bench_mi355x.sh <1|2|3|4|debug|all> [native|python]
+#   tools/run_bench_mi355x.sh <1|2|3|4|debug|all> [native|python|dropin]
+#
+# IMPL: native = knn_engine (this framework's own harness and parser); python = the torchrun
+# front end; dropin = the reference's own harness: `make engine engine.debug` (top-level Makefile:
+# the reference's unmodified common.cpp linked with include/engine.h + dropin_engine.cpp), then
+# `mpiexec -n P ./engine < input` exactly as run_bench.sh:74,84 runs it (strategy from KNN_STRATEGY).
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 CONFIG="${1:-}"
 IMPL="${2:-native}"
 if [[ ! "$CONFIG" =~ ^(1|2|3|4|debug|all)$ ]]; then
-  echo "Usage: $0 <1|2|3|4|debug|all> [native|python]"
+  echo "Usage: $0 <1|2|3|4|debug|all> [native|python|dropin]"
   echo "  1 - shard_gather (bench_1) on 1 GPU      2 - shard_reduce (bench_2) on 2 GPUs"
   echo "  3 - shard_reduce batched (bench_3) on 4  4 - farm (bench_4) on 8 GPUs"
   echo "  debug - serial KD-tree (bench.debug) on the CPU"
@@ -20,6 +25,7 @@ if [[ ! "$CONFIG" =~ ^(1|2|3|4|debug|all)$ ]]; then
 fi
 cd "$ROOT"
 python3 -m distributed_machine_learning_project_amd.build >/dev/null
+[[ "$IMPL" == "dropin" ]] && make -s engine engine.debug >/dev/null
 mkdir -p inputs outputs
 gen() {  # name N Q A kmin kmax
   [[ -f inputs/$1.in ]] || python3 tools/generate_input.py --fast --num_data $2 --num_queries $3 \
@@ -37,7 +43,14 @@ run() {  # config strategy gpus input [--debug]
   fi
   local launch=(/opt/conda/bin/mpiexec -n $np)
   [[ $np -eq 1 ]] && launch=()
-  if [[ "$IMPL" == "native" ]]; then
+  if [[ "$IMPL" == "dropin" ]]; then
+    local exe=./engine
+    [[ -n "$dbg" ]] && exe=./engine.debug
+    # every rank opens the input as its stdin (only rank 0 reads it, common.cpp:93; MPICH's stdin
+    # forwarding to rank 0 can die with SIGPIPE on large inputs)
+    KNN_STRATEGY=$strat timeout 300 "${launch[@]}" sh -c "exec $exe < $in" \
+        > outputs/tmp_$cfg.out 2> outputs/tmp_$cfg.err
+  elif [[ "$IMPL" == "native" ]]; then
     timeout 300 "${launch[@]}" distributed_machine_learning_project_amd/knn_engine \
         --strategy $strat $dbg < $in > outputs/tmp_$cfg.out 2> outputs/tmp_$cfg.err
   else
