@@ -37,8 +37,6 @@ _SIGS = {
     "dmlp_cpu_gather_rows": (None, [vp, i64, i32, vp]),
     "dmlp_cpu_rows_i32": (i32, [vp, i64, vp]),
     "dmlp_rows_from_i32": (i32, [vp, i64, vp, vp]),
-    "dmlp_host_ops_x1_parts": (i32, [vp, i64, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp,
-                                     i64, i64, vp, vp, i32, vp, vp, i32, vp, vp, vp, i32]),
     "dmlp_host_ops_h2d_tiles": (i32, [vp, i64, i64, i64, vp, i64, i32, vp, i32, vp, vp, vp, vp, vp,
                                       vp, vp, vp, vp, vp, i32, vp]),
     "dmlp_screen_kmax": (i32, [i32]),
@@ -71,13 +69,16 @@ _SIGS = {
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_refine_groups2": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, vp]),
     "dmlp_x1_seed": (i32, [vp, vp, i32, i32, vp, vp]),
-    "dmlp_fast_step_events": (i32, [i32]),
-    "dmlp_fast_step_parts": (None, [i32]),
-    "dmlp_fast_step_rparts": (None, [i32]),
-    "dmlp_fast_step_early": (None, [i32]),
-    "dmlp_fast_step_timeline": (i32, [vp, vp, i32]),
-    "dmlp_fast_step": (i32, [vp, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i64, i32, vp, i64,
-                             vp, vp, vp, vp]),
+    "dmlp_arena_reserve": (i32, [i64, i64]),
+    "dmlp_knn_local": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp]),
+    "dmlp_step": (i32, [vp]),
+    "dmlp_step_emit": (i32, [vp, i64, vp]),
+    "dmlp_step_early": (None, [i32]),
+    "dmlp_step_early_delay": (None, [i32]),
+    "dmlp_step_events": (i32, [i32]),
+    "dmlp_step_timeline": (i32, [vp, vp, i32]),
+    "dmlp_pipeline_set": (i32, [C.c_char_p, i32]),
+    "dmlp_pipeline_stats": (None, [vp]),
     "dmlp_screen_x1_collect": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
     "dmlp_set_x1_ct": (None, [i32]),

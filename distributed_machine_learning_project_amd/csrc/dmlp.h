@@ -78,15 +78,6 @@ int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, i
                       const double* mu, int KT, uint16_t* xhi_h, float* xin_h, unsigned* xnm_h,
                       uint16_t* qhi_h, float* qn_h, void* xhi_d, void* xin_d, void* xnm_d,
                       void* qhi_d, void* qn_d, int chunks, void* stream);
-// Query parts of a pipelined call: render + copy part p, then queue its single-term screen
-// (fp16 host image) on part_streams[p] behind the copy (prep.hip).  0, | 2 out of range, | 4 error.
-int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const double* mu, int KT,
-                           uint16_t* qhi_h, float* qn_h, void* qhi_d, void* qn_d, int parts,
-                           void* copy, void* const* part_streams, const void* xfrag,
-                           const float* xinit, int64_t n_tiles, int64_t n_points, const int* qidx,
-                           const int* const* kdev, int kmax, const unsigned* xnmax_bits,
-                           const unsigned* bad, int S, int* const* cand_ids, int* const* cand_cnt,
-                           float* const* cand_h, int chunks);
 // Same, the dataset part restricted to tiles [t0, t1) (device image pointers at tile t0's slot;
 // *xnm = +inf when the range is outside the screen's range): the per-rank shard of a sharded render.
 int dmlp_host_ops_h2d_tiles(const double* X, int64_t N, int64_t t0, int64_t t1, const double* Qx,
@@ -215,28 +206,82 @@ int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
                            float* cand_h, void* stream);
 // The single-term screen (fp16 host image, S = 1) started while the image is still crossing
 // PCIe: rdy[i] != 0 once tiles [i rdy_tiles, (i + 1) rdy_tiles) and their max norm xnm_sl[i]
-// landed; the screen waits per slice and grows each column's eps with the slices it has seen.
+// landed; the screen waits per slice (bounded by DMLP_EARLY_TIMEOUT_MS of wall clock, default 50:
+// a timed-out wave reports its queries overflowed) and grows each column's eps with the slices
+// it has seen.  estats (nullable, device, zeroed by the caller): [0] waits that had to spin,
+// [1] eps growths, [2] timeouts, summed over the waves.
 int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
                          int64_t n_points, const void* qhi, const float* qn, const int* qidx,
                          const int* qk, int nq, int kmax, const unsigned* bad, const unsigned* rdy,
                          int rdy_tiles, int rdy_n, const unsigned* xnm_sl, int* cand_ids,
-                         int* cand_cnt, float* cand_h, void* stream);
+                         int* cand_cnt, float* cand_h, unsigned* estats, void* stream);
 
-// The single-GPU call for every k in [kmin, kmax] within [1, 32] in one native function
-// (fast_step.hip): host render + copies, screen, rows behind it, refine, report text into
-// report_dst, labels / checksums into the caller's device out_lab / out_cs, one sync.  Returns 0,
-// 1 (not this path's call: nothing observable written), 2 (a query overflowed: rerun on the
-// general path), or < 0 (HIP error).
-int dmlp_fast_step(const double* X, const int* labels, int64_t N, const double* Qx, const int* k,
-                   int64_t Q, int A, int kmin, int kmax, int label_lo, int label_hi,
-                   int64_t qid_base, int chunks, char* report_dst, int64_t report_cap,
-                   int64_t* report_len, int* out_lab, uint64_t* out_cs, void* stream);
-// query parts of the following calls (1..4; <= 0: DMLP_FAST_PARTS, default 1); step timeline
-int dmlp_fast_step_events(int on);
-int dmlp_fast_step_timeline(double* ms, const char** names, int cap);
-void dmlp_fast_step_parts(int parts);
-void dmlp_fast_step_rparts(int parts);
-void dmlp_fast_step_early(int on);
+// ---------------------------------------------------------------- the native pipeline (pipeline.hip)
+// Bump arenas for the pipeline's grow-only buffers, reserved once before any timed call (the
+// reference harness times ONE call per process: no hipMalloc may land inside it).  Past the
+// reservation allocations fall back to hipMalloc / hipHostMalloc.  Returns 0, | 1 / | 2 when
+// the device / host reservation failed.
+int dmlp_arena_reserve(int64_t dev_bytes, int64_t host_bytes);
+void* dmlp_dev_alloc(int64_t bytes);
+void dmlp_dev_free(void* p);
+void* dmlp_host_alloc(int64_t bytes);   // page-locked
+void dmlp_host_free(void* p);
+
+// Exact local k-NN of device-resident rows X [N][A], Qx [Q][A] with per-query k (host): the
+// per-query dispatch (single-term screen k <= 32, 3-term LDS screen k <= 256, exact fp64
+// otherwise, per-query escalation of overflows), lists out_d / out_i [Q][kstride] (kstride >= max
+// k; (+inf, -1) padding), and with labels (device) the vote + checksum.  exact = 1: the exact
+// paths only.  Synchronizes `stream` once (twice when a query escalates).
+int dmlp_knn_local(const double* X, int64_t N, int A, const double* Qx, int64_t Q, const int* k,
+                   int kstride, double* out_d, int* out_i, const int* labels, int label_lo,
+                   int label_hi, int* out_label, uint64_t* out_cs, int exact, void* stream);
+
+// One rank's whole Engine::KNN call from host rows (the call the reference times): host render of
+// the screen operands + copies on a side stream (early start when every k is in [1, 32]),
+// screens, fp64 rows behind them, exact re-rank, vote, checksum, the report text on the GPU ->
+// report_dst (report_mode 1) or kept on the device (report_mode 2: dmlp_step_emit), one host sync.
+typedef struct dmlp_step_args {
+  const double* X;            // [N][A] row-major, or
+  const double* const* Xr;    // [N] row pointers (the drop-in: the harness's own vectors)
+  int64_t N;
+  int A;
+  const int* labels;          // [N]; null: no vote / checksum / report
+  int label_lo, label_hi;     // labels in [lo, hi)
+  const double* Qx;           // [Q][A], or
+  const double* const* Qr;    // [Q] row pointers
+  const int* k;               // [Q]
+  int64_t Q;
+  int kmin, kmax;             // bounds of k (kmax < kmin: scanned here)
+  int64_t qid_base;           // the report's first query id
+  int exact;                  // 1: exact fp64 paths only
+  int* out_lab;               // device [Q] (null: internal)
+  uint64_t* out_cs;           // device [Q] (null: internal)
+  double* out_d;              // device [Q][kstride] lists (null: internal)
+  int* out_i;
+  int kstride;                // >= kmax (0: kmax)
+  int report_mode;            // 0 none, 1 -> report_dst, 2 kept on the device
+  char* report_dst;           // page-locked, >= dmlp_format_bound(Q) bytes (mode 1)
+  int64_t report_cap;
+  void* stream;
+  // results
+  int64_t report_len;
+  int path;                   // 0 host-rendered screen operands, 2 device image (range)
+  int early;                  // 1: the screen started before the dataset image landed
+  int n_escalated;            // queries redone after a screen overflow
+  int early_waits, early_grows, early_timeouts;
+} dmlp_step_args;
+int dmlp_step(dmlp_step_args* args);
+// The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
+int dmlp_step_emit(char* dst, int64_t bytes, void* stream);
+void dmlp_step_early(int on);          // 1 on, 0 off, < 0: DMLP_FAST_EARLY (default on)
+void dmlp_step_early_delay(int us);    // host sleep before each image slice (< 0: env)
+int dmlp_step_events(int on);          // hipEvent step timeline on / off
+int dmlp_step_timeline(double* ms, const char** names, int cap);
+// Tuning / A-B switches of the pipeline ("num_cus", "screen", "x1k", "host_ops"; pipeline.hip
+// Tuning): returns the previous value (-1: unknown key).  What the last call did: [0] exact-path
+// queries, [1] escalated queries, [2] path, [3] early start.
+int dmlp_pipeline_set(const char* key, int value);
+void dmlp_pipeline_stats(int64_t* out);
 
 // ---------------------------------------------------------------- device: exact rows (K2, fallback)
 // D[i][n] = exact dist(Qx[qidx[i]], X[n]) for i < nq, n < N; ldd = row stride of D (>= N).

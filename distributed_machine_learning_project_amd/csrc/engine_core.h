@@ -44,16 +44,15 @@ struct HostBuf {
     n = m;
     if (!m) return;
     pinned = false;
-    if (use_pinned()) {
-      p = (T*)host_arena().take(m * sizeof(T));
-      pinned = p != nullptr ||
-               hipHostMalloc((void**)&p, m * sizeof(T), hipHostMallocDefault) == hipSuccess;
+    if (use_pinned()) {  // the library's page-locked arena, else hipHostMalloc
+      p = (T*)dmlp_host_alloc((int64_t)(m * sizeof(T)));
+      pinned = p != nullptr;
     }
     if (!pinned) p = (T*)std::malloc(m * sizeof(T));
     if (!p) throw std::runtime_error("host allocation failed");
   }
   void release() {
-    if (p && !host_arena().owns(p)) { if (pinned) (void)hipHostFree(p); else std::free(p); }
+    if (p) { if (pinned) dmlp_host_free(p); else std::free(p); }
     p = nullptr; n = 0;
   }
   ~HostBuf() { release(); }
@@ -130,8 +129,6 @@ class KnnCore {
  public:
   KnnCore(Runtime& rt, std::string strategy, bool debug, bool exact, bool dynamic = false)
       : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact), dynamic_(dynamic) {
-    lk_.st = rt_.stream;
-    lk_.rt = &rt_;
     total_h_.resize(1);
     trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
@@ -148,8 +145,6 @@ class KnnCore {
   }
   ~KnnCore() {
     if (ctr_win_ != MPI_WIN_NULL) MPI_Win_free(&ctr_win_);
-    if (ev_rows_) (void)hipEventDestroy(ev_rows_);
-    if (ev_ops_) (void)hipEventDestroy(ev_ops_);
     if (wake_st_) (void)hipStreamDestroy(wake_st_);
     if (ring_ev_) (void)hipEventDestroy(ring_ev_);
     if (ring_done_) (void)hipEventDestroy(ring_done_);
@@ -159,7 +154,6 @@ class KnnCore {
       if (ooc_free_[b]) (void)hipEventDestroy(ooc_free_[b]);
     }
     if (ooc_st_) (void)hipStreamDestroy(ooc_st_);
-    if (side_) (void)hipStreamDestroy(side_);
   }
 
   // Engine::KNN — called on every rank; rank 0 holds `in` and receives `out`.
@@ -182,24 +176,22 @@ class KnnCore {
 
   void set_shared(const SharedIn& s) { sh_ = s; }
 
-  // The single-GPU fast path straight from tables of row pointers (the engine.h drop-in: the
+  // The single-GPU step straight from tables of row pointers (the engine.h drop-in: the
   // harness's per-point attribute vectors; `in` carries N, Q, A, labels and k, no rows).  Returns
-  // false, with nothing done, whenever that path does not apply (more ranks, another strategy,
-  // data outside the fp16 screen's range, ...): the caller then packs the rows and calls KNN.
+  // false, with nothing done, on more ranks or another strategy: the caller then packs the rows
+  // and calls KNN.
   bool KNN_rows(Input* in, const double* const* Xr, const double* const* Qr, Output* out) {
-    if (rt_.world != 1 || strategy_ != "farm" || dynamic_ || !fast_ || exact_ || !in) return false;
-    if (in->N == 0 || in->Q == 0 || in->Q > (1 << 30)) return false;
-    if (dmlp_screen_x1_qw(dmlp_screen_kt(in->A)) <= 0) return false;
+    if (rt_.world != 1 || strategy_ != "farm" || dynamic_ || !fast_ || !in) return false;
+    if (in->Q > (1 << 30)) return false;
     wake_d2h();
     N_ = in->N; Q_ = in->Q; A_ = in->A;
-    lo_ = *std::min_element(in->labels.begin(), in->labels.end());
-    hi_ = *std::max_element(in->labels.begin(), in->labels.end()) + 1;
-    kmax_ = std::max(1, *std::max_element(in->k.begin(), in->k.end()));
-    if (!side_) make_side();
-    FastOut fo;
-    if (fast_core(nullptr, in->labels.data(), nullptr, in->k.data(), Q_, fo, false, Xr, Qr) != 0)
-      return false;
-    render(out, fo.cs, fo.lb, fo.dd, fo.ii);  // synchronizes the stream
+    lo_ = 0; hi_ = 1;
+    if (N_) {
+      lo_ = *std::min_element(in->labels.begin(), in->labels.end());
+      hi_ = *std::max_element(in->labels.begin(), in->labels.end()) + 1;
+    }
+    kmax_ = Q_ ? std::max(1, *std::max_element(in->k.begin(), in->k.end())) : 1;
+    farm_step(in, Xr, Qr, out);
     trace.mark("report");
     return true;
   }
@@ -239,7 +231,6 @@ class KnnCore {
   MPI_Win ctr_win_ = MPI_WIN_NULL;
   int64_t* ctr_base_ = nullptr;
   DevBuf<int64_t> res_;
-  LocalKnn lk_;
   int64_t N_ = 0, Q_ = 0;
   int A_ = 0, lo_ = 0, hi_ = 1, kmax_ = 1;
   DevBuf<double> X_, Qx_, d_, dall_, stage_d_;
@@ -432,9 +423,9 @@ class KnnCore {
     HIPCHK(hipMemcpy(xd, x.data(), x.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(qd, qq.data(), qq.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ld, lab.data(), lab.size() * 4, hipMemcpyHostToDevice));
-    lk_.prepare(xd, n, a);
-    lk_.run(qd, q, k.data(), 64, d_.get(q * 64), ids_.get(q * 64), ld, 0, 3, labout_.get(q),
-            cs_.get(q));
+    A_ = a;
+    DMLPCHK(dmlp_knn_local(xd, n, a, qd, q, k.data(), 64, d_.get(q * 64), ids_.get(q * 64), ld, 0,
+                           3, labout_.get(q), cs_.get(q), exact_ ? 1 : 0, rt_.stream));
     int64_t* off = off_.get(dmlp_format_scratch(q));
     DMLPCHK(dmlp_format_report(cs_.p, q, 0, off, txt_.get(dmlp_format_bound(q)), rt_.stream));
     rt_.sync();
@@ -460,11 +451,11 @@ class KnnCore {
       rt_.sync();
     }
     const bool shm_ingress = getenv("KNN_INGRESS") && std::string(getenv("KNN_INGRESS")) == "shm";
-    if ((rt_.world == 1 || shm_ingress) && fast_ && !exact_) {
-      // the single-GPU fast path once on a tiny input: its side stream, event, staging and
-      // device buffers, the host pool's first job and the first copies on the side stream are
-      // all paid here (measured ~16 ms of first-use cost otherwise)
-      make_side();
+    if ((rt_.world == 1 || shm_ingress) && fast_) {
+      // the native step once on a tiny input, every k class (early start at k <= 32, the
+      // two-pass screen above): its side stream, events, staging and device buffers, the host
+      // pool's first job and the first copies on the side stream are all paid here (measured
+      // ~16 ms of first-use cost otherwise)
       Input w;
       w.N = 300; w.Q = 70; w.A = 8;
       w.labels.resize(w.N);
@@ -475,14 +466,15 @@ class KnnCore {
       for (int64_t i = 0; i < w.Q * w.A; ++i) w.Qx.data()[i] = (double)((i * 53) % 97);
       for (int64_t i = 0; i < w.N; ++i) w.labels[i] = (int)(i % 3);
       for (int64_t i = 0; i < w.Q; ++i) w.k[i] = 1 + (int)(i % 32);
-      N_ = w.N; Q_ = w.Q; A_ = w.A; lo_ = 0; hi_ = 3; kmax_ = 32;
-      if (rt_.world == 1) {
+      N_ = w.N; Q_ = w.Q; A_ = w.A; lo_ = 0; hi_ = 3;
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int64_t i = 0; i < w.Q; ++i) w.k[i] = 1 + (int)(i % (pass ? 60 : 32));
+        kmax_ = pass ? 60 : 32;
         Output o;
-        (void)farm_fast(&w, &o);
-      } else {  // the per-rank pipeline of the node-shared farm (no collectives here)
-        FastOut fo;
-        (void)fast_core(w.X.data(), w.labels.data(), w.Qx.data(), w.k.data(), w.Q, fo);
+        (void)step_host(w.X.data(), nullptr, w.labels.data(), w.Qx.data(), nullptr, w.k.data(),
+                        w.Q, 0, rt_.world == 1 ? 1 : 2, &o);
       }
+      step_calls_ = 0;
       rt_.sync();
     }
     MPI_Barrier(MPI_COMM_WORLD);
@@ -490,9 +482,9 @@ class KnnCore {
 
   void local_knn(const double* Xd, int64_t n, const double* Qd, int64_t nq, const int* kh,
                  double* od, int* oi, const int* labels, int* lab, uint64_t* cs) {
-    lk_.prepare(Xd, n, A_);
-    if (exact_) lk_.KT = 99;  // forces the exact fallback for every query
-    lk_.run(Qd, nq, kh, kmax_, od, oi, labels, lo_, hi_, lab, cs);
+    // the library's one dispatcher (pipeline.hip): per-query classes, escalation, exact paths
+    DMLPCHK(dmlp_knn_local(Xd, n, A_, Qd, nq, kh, kmax_, od, oi, labels, lo_, hi_, lab, cs,
+                           exact_ ? 1 : 0, rt_.stream));
   }
 
   // rank 0: the report (GPU formatter) or, with --debug, the host copies of the lists + labels
@@ -527,220 +519,102 @@ class KnnCore {
     out->report.clear();
   }
 
-  // ---------------------------------------------------------------- fast single-GPU farm
-  // The Python pipeline (ops/knn.py knn_gpu_pipelined) in native code, for one rank holding
-  // everything: the host renders the single-term screen's operands (host_prep.cpp: the
-  // dataset's fp16 hi-only tile image + norms, the queries' fp16 fragments + norms — 15.7 MB
-  // instead of 59 MB of fp64 rows at the bench shape) and copies them on the main stream; the
-  // fp64 rows, labels and queries cross PCIe on a second stream BEHIND the screen, and only the
-  // exact re-rank waits for them; the report is rendered straight into the page-locked output.
-  // Any k: LocalKnn::run serves 1 <= k <= 32 with the host operands, 32 < k <= 128 with the
-  // 3-term screen on a device image rendered from the landed rows, the rest exactly, and a query
-  // whose single-term candidates overflow escalates alone.  Returns false (nothing done) when
-  // the data or queries are outside the fp16 range (the device path then serves the call), or
-  // A > 64 (no x1 variant).
-  DevBuf<short> fx_hi_, fq_hi_, fx_hic_;
-  DevBuf<float> fx_in_, fq_n_, fx_inc_;
-  DevBuf<unsigned> f_words_;
-  HostBuf<char> f_stage_;
-  hipStream_t side_ = nullptr;
-  hipEvent_t ev_rows_ = nullptr;
-  // lossless int32 row transfer (KNN_ROWS_I32=0: always fp64): page-locked + device staging
-  const bool rows_i32_ = !(getenv("KNN_ROWS_I32") && std::string(getenv("KNN_ROWS_I32")) == "0");
-  template <typename T>
-  struct Pinned {
-    HostBuf<T> b;
-    T* get(int64_t n) {
-      if ((int64_t)b.size() < n) b.resize((size_t)n);
-      return b.data();
-    }
-  };
-  Pinned<int> f_i32_;
-  Pinned<double> f_f64_;  // fp64 rows gathered from a row table (inputs that are not 6-decimal)
-  DevBuf<int> f_i32d_;
+  // ---------------------------------------------------------------- the native step
+  // Every single-GPU call from host rows goes through the library's one pipeline (pipeline.hip
+  // dmlp_step, also behind the Python engine): host render of the screen operands, early start,
+  // fp64 rows behind the screen, exact re-rank, vote, checksum, report text on the GPU, per-query
+  // escalation.  Xr / Qr (non-null): tables of row pointers (the engine.h drop-in reads the
+  // harness's per-point vectors in place); else X / Qx row-major.  report_mode 1: the text into
+  // out->text (page-locked); 2: kept on the device for a multi-rank egress (dmlp_step_emit);
+  // lists mode (debug_): the sorted lists + labels into dd / ii / lb instead.
+  DevBuf<double> sd_;
+  DevBuf<int> si_, slb_;
+  DevBuf<uint64_t> scs_;
+  int64_t step_calls_ = 0;
 
-  bool farm_fast(Input* in, Output* out) {
-    // (debug_ = lists mode — the engine.h drop-in hands every list to the harness's reportResult
-    // — is served too: render() then copies the lists and labels instead of the report text)
-    if (rt_.world != 1 || exact_ || !in || N_ == 0 || Q_ == 0 || Q_ > (1 << 30)) return false;
-    const int KT = dmlp_screen_kt(A_);
-    if (dmlp_screen_x1_qw(KT) <= 0) return false;
-    FastOut fo;
-    if (fast_core(in->X.data(), in->labels.data(), in->Qx.data(), in->k.data(), Q_, fo) != 0)
-      return false;
-    render(out, fo.cs, fo.lb, fo.dd, fo.ii);  // synchronizes the stream
-    trace.mark("report");
-    return true;
+ public:
+  int64_t step_calls() const { return step_calls_; }
+  dmlp_step_args last_step_{};
+
+ private:
+  dmlp_step_args step_host(const double* X, const double* const* Xr, const int* labels,
+                           const double* Qx, const double* const* Qr, const int* k, int64_t nq,
+                           int64_t qid_base, int report_mode, Output* out) {
+    dmlp_step_args a{};
+    a.X = X; a.Xr = Xr; a.N = N_; a.A = A_;
+    a.labels = labels; a.label_lo = lo_; a.label_hi = hi_;
+    a.Qx = Qx; a.Qr = Qr; a.k = k; a.Q = nq;
+    a.kmin = 1; a.kmax = 0;  // scanned by the step (this rank's own block)
+    a.qid_base = qid_base;
+    a.exact = exact_ ? 1 : 0;
+    const int64_t qs = std::max<int64_t>(nq, 1);
+    a.out_lab = slb_.get(qs);
+    a.out_cs = scs_.get(qs);
+    a.kstride = kmax_;
+    if (debug_) {
+      a.out_d = sd_.get(qs * kmax_);
+      a.out_i = si_.get(qs * kmax_);
+    }
+    a.report_mode = debug_ ? 0 : report_mode;
+    if (a.report_mode == 1) {
+      const size_t bound = (size_t)dmlp_format_bound((int)nq);
+      if (out->text.size() < bound) out->text.resize(bound);
+      a.report_dst = out->text.data();
+      a.report_cap = (int64_t)out->text.size();
+    }
+    a.stream = rt_.stream;
+    trace.mark("step_enter");
+    DMLPCHK(dmlp_step(&a));
+    ++step_calls_;
+    last_step_ = a;
+    trace.mark("step");
+    return a;
   }
 
-  // The pipeline of farm_fast for nq queries (Qx / k: this rank's block) against the whole
-  // dataset X.  Returns 0 (results in fo, complete on the stream), or 1 when the data / queries
-  // are outside the fp16 screen's range (nothing left in flight).
-  struct FastOut {
-    double* dd = nullptr;
-    int* ii = nullptr;
-    int* lb = nullptr;
-    uint64_t* cs = nullptr;
-  };
-  // shard = true (node-shared farm, P > 1): this rank renders only its 1/P tile range of the
-  // dataset's screen image and one all-gather completes it; the data-range verdict and the max
-  // norm are agreed over MPI on the host first, so every rank takes the same branch.
-  // Xr / Qr (non-null): the rows come from tables of row pointers instead of X / Qx (the engine.h
-  // drop-in: the harness's per-point vectors, read in place — the render, the int32 pack and, if
-  // needed, an fp64 gather read them; nothing packs the AoS input first).
-  int fast_core(const double* X, const int* labels, const double* Qx, const int* k, int64_t nq,
-                FastOut& fo, bool shard = false, const double* const* Xr = nullptr,
-                const double* const* Qr = nullptr) {
-    const int KT = dmlp_screen_kt(A_);
-    hipStream_t st = rt_.stream;
-    const int64_t nt = (N_ + 63) / 64, W = (int64_t)KT * 32;
-    const int P = shard ? rt_.world : 1;
-    const int64_t tpr = (nt + P - 1) / P;  // tiles per rank (the last ranks' tails pad)
-    const int64_t t0 = shard ? std::min<int64_t>(rt_.rank * tpr, nt) : 0;
-    const int64_t t1 = shard ? std::min<int64_t>(t0 + tpr, nt) : nt;
-    // page-locked staging for the rendered operands (host_ops_h2d copies from it)
-    const size_t b_xhi = nt * 64 * W * 2, b_xin = nt * 64 * 4, b_qhi = nq * W * 2, b_qn = nq * 4;
-    auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t need = up(b_xhi) + up(b_xin) + 256 + up(b_qhi) + up(b_qn) + up(A_ * 8);
-    if (f_stage_.size() < need) f_stage_.resize(need);
-    char* hp = f_stage_.data();
-    uint16_t* xhi_h = (uint16_t*)hp; hp += up(b_xhi);
-    float* xin_h = (float*)hp; hp += up(b_xin);
-    unsigned* xnm_h = (unsigned*)hp; hp += 256;
-    uint16_t* qhi_h = (uint16_t*)hp; hp += up(b_qhi);
-    float* qn_h = (float*)hp; hp += up(b_qn);
-    double* mu_h = (double*)hp;
-    if (Xr) dmlp_cpu_center_rows(Xr, N_, A_, mu_h);
-    else dmlp_cpu_center(X, N_, A_, mu_h);
-    trace.mark("center");
-    short* xhi = fx_hi_.get((shard ? P * tpr : nt) * 64 * W);
-    float* xin = fx_in_.get((shard ? P * tpr : nt) * 64);
-    short* xhi_c = shard ? fx_hic_.get(tpr * 64 * W) : xhi;
-    float* xin_c = shard ? fx_inc_.get(tpr * 64) : xin;
-    unsigned* words = f_words_.get(2);  // [0] xnmax bits, [1] bad (0: the host checked ranges)
-    short* qhi = fq_hi_.get(std::max<int64_t>(nq, 1) * W);
-    float* qn = fq_n_.get(std::max<int64_t>(nq, 1));
-    int rc = Xr ? dmlp_host_ops_h2d_tiles_rows(Xr, N_, t0, t1, Qr, nq, A_, mu_h, KT, xhi_h, xin_h,
-                                              xnm_h, qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn,
-                                              host_slices_, st)
-                : dmlp_host_ops_h2d_tiles(X, N_, t0, t1, Qx, nq, A_, mu_h, KT, xhi_h, xin_h, xnm_h,
-                                          qhi_h, qn_h, xhi_c, xin_c, words, qhi, qn, host_slices_,
-                                          st);
-    if (rc & 4) throw std::runtime_error("host operand copy failed");
-    if (shard) {
-      // every rank's verdict and max norm (host values) before any device collective
-      unsigned v[2] = {(unsigned)(rc & 3), *xnm_h};
-      MPI_Allreduce(MPI_IN_PLACE, v, 2, MPI_UNSIGNED, MPI_MAX, MPI_COMM_WORLD);
-      if (v[0]) { rt_.sync(); return 1; }  // somewhere outside the screen's range
-      xnm_h[1] = v[1];  // (a second pinned word: the first one's copy may still be in flight)
-      HIPCHK(hipMemcpyAsync(words, xnm_h + 1, 4, hipMemcpyHostToDevice, st));
-      allgather_bytes(xhi_c, xhi, tpr * 64 * W * 2);
-      allgather_bytes(xin_c, xin, tpr * 64 * 4);
-    } else if (rc) {
-      rt_.sync();
-      return 1;  // outside the screen's range: the device path decides
+  // one rank holds everything: the whole call is one step
+  void farm_step(Input* in, const double* const* Xr, const double* const* Qr, Output* out) {
+    const dmlp_step_args a = step_host(Xr ? nullptr : in->X.data(), Xr, in->labels.data(),
+                                       Qr ? nullptr : in->Qx.data(), Qr, in->k.data(), Q_, 0, 1,
+                                       out);
+    out->kstride = kmax_;
+    if (!debug_) {
+      out->text_len = (size_t)a.report_len;
+      return;
     }
-    if (nq == 0) {  // a rank without queries (Q < P) took part in the collectives only
-      rt_.sync();
-      return 0;
-    }
-    HIPCHK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), st));
-    trace.mark("h2d_operands");
-    // fp64 rows + labels behind the screen, on the side stream — enqueued by LocalKnn::run right
-    // after the screen launch (everything the screen needs is queued by then), so no small copy
-    // of the main stream queues behind them on the copy engine
-    double* Xd = X_.get(N_ * A_);
-    int* Ld = lab_.get(N_);
-    double* Qd = Qx_.get(nq * A_);
-    auto issue_rows = [&]() {
-      // (no stream dependency: the previous call ended with a sync, nothing reads these yet)
-      HIPCHK(hipMemcpyAsync(Ld, labels, N_ * 4, hipMemcpyHostToDevice, side_));
-      // the host packs the rows while the screen runs: lossless int32 when every value is a
-      // 6-decimal number (half the PCIe bytes; the device divides back), else fp64
-      const int64_t nx = N_ * A_, nqa = nq * A_;
-      const int64_t qat = (nx + 3) & ~int64_t(3);  // (16-byte aligned for the decode kernel)
-      int* hx32 = rows_i32_ ? f_i32_.get(qat + nqa) : nullptr;
-      int* dx32 = rows_i32_ ? f_i32d_.get(qat + nqa) : nullptr;
-      auto rows = [&](const double* src, const double* const* tab, int64_t nr, double* dst,
-                      int64_t at) {
-        const int64_t n = nr * A_;
-        if (rows_i32_ && (tab ? dmlp_cpu_rows_i32_rows(tab, nr, A_, hx32 + at)
-                              : dmlp_cpu_rows_i32(src, n, hx32 + at)) == 0) {
-          HIPCHK(hipMemcpyAsync(dx32 + at, hx32 + at, n * 4, hipMemcpyHostToDevice, side_));
-          DMLPCHK(dmlp_rows_from_i32(dx32 + at, n, dst, side_));
-          return;
-        }
-        if (tab) {  // not 6-decimal: pack the fp64 rows from the table first
-          double* h = f_f64_.get(qat + nqa) + at;
-          dmlp_cpu_gather_rows(tab, nr, A_, h);
-          src = h;
-        }
-        HIPCHK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, side_));
-      };
-      trace.mark("screen_queued");
-      rows(X, Xr, N_, Xd, 0);
-      trace.mark("rows_x");
-      rows(Qx, Qr, nq, Qd, qat);
-      HIPCHK(hipEventRecord(ev_rows_, side_));
-      trace.mark("rows_q");
-    };
-    fo.dd = d_.get(nq * kmax_);
-    fo.ii = ids_.get(nq * kmax_);
-    fo.lb = labout_.get(nq);
-    fo.cs = cs_.get(nq);
-    LocalKnn::HostX1 hx;
-    hx.xhi = xhi; hx.xin = xin; hx.words = words; hx.qhi = qhi; hx.qn = qn;
-    lk_.X = Xd; lk_.N = N_; lk_.A = A_; lk_.KT = KT;
-    lk_.run(Qd, nq, k, kmax_, fo.dd, fo.ii, Ld, lo_, hi_, fo.lb, fo.cs, &hx, ev_rows_, issue_rows);
-    trace.mark("knn");
-    return 0;
+    out->label.resize(Q_);
+    out->dist.resize(Q_ * kmax_);
+    out->ids.resize(Q_ * kmax_);
+    HIPCHK(hipMemcpy(out->label.data(), a.out_lab, Q_ * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out->dist.data(), a.out_d, Q_ * kmax_ * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out->ids.data(), a.out_i, Q_ * kmax_ * 4, hipMemcpyDeviceToHost));
+    out->report.clear();
   }
 
-  // Farm over the node-shared segment, P > 1: every rank runs fast_core on its own query block
-  // straight from the segment (its own PCIe link), renders its report lines on its GPU and copies
-  // them into the segment's output region at its byte offset (one MPI_Allgather of the lengths).
-  // Every fallback decision is agreed by all ranks before anyone acts on it (MPI_Allreduce), so
-  // the general farm below runs on all of them or on none.
-  bool farm_fast_shared(Output* out) {
+  // Farm over the node-shared segment, P > 1: every rank runs the step on its own query block
+  // straight from the segment (its own PCIe link), keeps its report lines on its GPU, and copies
+  // them into the segment's output region at its byte offset once the lengths are known (one
+  // MPI_Allgather of 8 bytes); a barrier, and rank 0 holds the whole report.
+  bool farm_step_shared(Output* out) {
     const int P = rt_.world, r = rt_.rank;
-    if (exact_ || debug_ || N_ == 0 || Q_ == 0 || sh_.N != N_ || sh_.Q != Q_ || sh_.A != A_)
-      return false;
+    if (debug_ || sh_.N != N_ || sh_.Q != Q_ || sh_.A != A_) return false;
     std::vector<int64_t> cnt, off;
     block_partition(Q_, P, cnt, off);
-    const int64_t a = off[r], nl = cnt[r];
-    const int KT = dmlp_screen_kt(A_);
-    int ok = dmlp_screen_x1_qw(KT) > 0 && nl <= (1 << 30);
-    MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
-    if (!ok) return false;
-    if (!side_) make_side();
-    FastOut fo;
-    // (every rank enters fast_core, even with no queries: the image all-gather is collective)
-    int bad = fast_core(sh_.X, sh_.labels, sh_.Qx + a * A_, sh_.k + a, nl, fo, image_shard_);
+    const int64_t a0 = off[r], nl = cnt[r];
     int64_t len = 0;
-    char* txt = nullptr;
-    int64_t* off_d = nullptr;
-    if (!bad && nl) {
-      off_d = off_.get(dmlp_format_scratch((int)nl));
-      txt = txt_.get((size_t)dmlp_format_bound((int)nl));
-      DMLPCHK(dmlp_format_report(fo.cs, (int)nl, (int)a, off_d, txt, rt_.stream));
-      HIPCHK(hipMemcpyAsync(total_h_.data(), off_d + nl, 8, hipMemcpyDeviceToHost, rt_.stream));
-      rt_.sync();
-      len = total_h_.data()[0];
+    if (nl) {
+      const dmlp_step_args a = step_host(sh_.X, nullptr, sh_.labels, sh_.Qx + a0 * A_, nullptr,
+                                         sh_.k + a0, nl, a0, 2, out);
+      len = a.report_len;
     }
-    MPI_Allreduce(MPI_IN_PLACE, &bad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
-    if (bad) return false;  // every rank redoes the call on the general farm
-    trace.mark("format");
     std::vector<int64_t> lens(P);
     MPI_Allgather(&len, 1, MPI_INT64_T, lens.data(), 1, MPI_INT64_T, MPI_COMM_WORLD);
-    int64_t at = 0;
-    for (int i = 0; i < r; ++i) at += lens[i];
-    int64_t total = 0;
-    for (int i = 0; i < P; ++i) total += lens[i];
-    if (total > sh_.out_bytes) throw std::runtime_error("shared output region too small");
-    if (len) {
-      HIPCHK(hipMemcpyAsync(sh_.out + at, txt, len, hipMemcpyDeviceToHost, rt_.stream));
-      rt_.sync();
+    int64_t at = 0, total = 0;
+    for (int i = 0; i < P; ++i) {
+      if (i < r) at += lens[i];
+      total += lens[i];
     }
+    if (total > sh_.out_bytes) throw std::runtime_error("shared output region too small");
+    if (len) DMLPCHK(dmlp_step_emit(sh_.out + at, len, rt_.stream));
     MPI_Barrier(MPI_COMM_WORLD);  // every block is in the segment
     if (r == 0) {
       out->kstride = kmax_;
@@ -750,16 +624,7 @@ class KnnCore {
     trace.mark("report");
     return true;
   }
-  hipEvent_t ev_ops_ = nullptr;
-  void make_side() {
-    HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&ev_rows_, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&ev_ops_, hipEventDisableTiming));
-  }
   SharedIn sh_;
-  // KNN_IMAGE_SHARD=0: every rank renders the whole screen image (A/B)
-  bool image_shard_ = !(getenv("KNN_IMAGE_SHARD") && std::string(getenv("KNN_IMAGE_SHARD")) == "0");
-  int64_t qi_len_ = 0;
 
   // ---------------------------------------------------------------- farm (bench_4)
   // ---------------------------------------------------------------- out-of-core farm
@@ -886,8 +751,12 @@ class KnnCore {
   void farm(Input* in, Output* out) {
     const int P = rt_.world;
     if (ooc_rows_ > 0 && N_ > ooc_rows_) return farm_ooc(in, out);
-    if (P == 1 && fast_ && farm_fast(in, out)) return;
-    if (P > 1 && sh_.valid && fast_ && farm_fast_shared(out)) return;
+    if (P == 1 && fast_ && Q_ <= (1 << 30)) {
+      farm_step(in, nullptr, nullptr, out);
+      trace.mark("report");
+      return;
+    }
+    if (P > 1 && sh_.valid && fast_ && farm_step_shared(out)) return;
     std::vector<int64_t> cnt, off;
     block_partition(Q_, P, cnt, off);
     double* Xd = X_.get(N_ * A_);

@@ -426,58 +426,6 @@ extern "C" int dmlp_host_ops_h2d_tiles_rows(const double* const* Xr, int64_t N, 
                             xnm_h, qhi_h, qn_h, xhi_d, xin_d, xnm_d, qhi_d, qn_d, chunks, stream);
 }
 
-// Query parts of one pipelined local call: part p (rows [Q p / P, Q (p + 1) / P)) is rendered on
-// the host pool, copied on `copy`, and its single-term screen is queued on part_streams[p] behind
-// an event of that copy — part p's screen runs while the host renders part p + 1, so the GPU
-// starts after the dataset image plus 1/P of the query image instead of after all of it.  The
-// dataset image (xfrag / xinit / xnmax_bits) must already be queued on `copy`.  Per part: the
-// device k (kdev[p]), candidate buffers (cand_*[p], sized for S slices of the part); qidx is an
-// identity list of >= the largest part's rows.  Returns 0, or | 2 when a part holds a query
-// outside the screen's range (no later part is screened; the caller drains the part streams and
-// takes the device path), | 4 when a copy or launch failed.
-extern "C" int dmlp_host_ops_x1_parts(const double* Qx, int64_t Q, int A, const double* mu,
-                                      int KT, uint16_t* qhi_h, float* qn_h, void* qhi_d,
-                                      void* qn_d, int parts, void* copy,
-                                      void* const* part_streams, const void* xfrag,
-                                      const float* xinit, int64_t n_tiles, int64_t n_points,
-                                      const int* qidx, const int* const* kdev, int kmax,
-                                      const unsigned* xnmax_bits, const unsigned* bad, int S,
-                                      int* const* cand_ids, int* const* cand_cnt,
-                                      float* const* cand_h, int chunks) {
-  static std::vector<hipEvent_t> evs;  // one per part, re-recorded every call
-  while ((int)evs.size() < parts) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return 4;
-    evs.push_back(e);
-  }
-  hipStream_t cs = (hipStream_t)copy;
-  const int64_t W = (int64_t)KT * 32;
-  chunks = chunks < 1 ? 1 : chunks;
-  for (int p = 0; p < parts; ++p) {
-    const int64_t q0 = Q * p / parts, q1 = Q * (p + 1) / parts;
-    if (q1 <= q0) continue;
-    // the part in `chunks` slices: each slice's copy overlaps the render of the next
-    for (int c = 0; c < chunks; ++c) {
-      const int64_t a = q0 + (q1 - q0) * c / chunks, b = q0 + (q1 - q0) * (c + 1) / chunks;
-      if (b <= a) continue;
-      if (dmlp_cpu_prep_queries(Qx + a * A, b - a, A, mu, KT, qhi_h + a * W, qn_h + a)) return 2;
-      if (hipMemcpyAsync((char*)qhi_d + a * W * 2, qhi_h + a * W, (size_t)((b - a) * W * 2),
-                         hipMemcpyHostToDevice, cs) != hipSuccess ||
-          hipMemcpyAsync((float*)qn_d + a, qn_h + a, (size_t)((b - a) * 4),
-                         hipMemcpyHostToDevice, cs) != hipSuccess)
-        return 4;
-    }
-    hipStream_t ps = (hipStream_t)part_streams[p];
-    if (hipEventRecord(evs[p], cs) != hipSuccess || hipStreamWaitEvent(ps, evs[p], 0) != hipSuccess)
-      return 4;
-    if (dmlp_screen_x1(KT, 1, A, xfrag, xinit, n_tiles, n_points, (const char*)qhi_d + q0 * W * 2,
-                       (const float*)qn_d + q0, qidx, kdev[p], (int)(q1 - q0), kmax, xnmax_bits,
-                       bad, S, cand_ids[p], cand_cnt[p], cand_h[p], ps) != 0)
-      return 4;
-  }
-  return 0;
-}
-
 // The whole image (tiles [0, n_tiles)).
 extern "C" int dmlp_host_ops_h2d(const double* X, int64_t N, const double* Qx, int64_t Q, int A,
                                  const double* mu, int KT, uint16_t* xhi_h, float* xin_h,

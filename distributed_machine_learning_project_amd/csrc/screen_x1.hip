@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
     float* __restrict__ cand_h, const float* __restrict__ hseed, int ccap,
     const unsigned* __restrict__ rdy, int rdy_tiles, int rdy_n,
-    const unsigned* __restrict__ xnm_sl) {
+    const unsigned* __restrict__ xnm_sl, unsigned* __restrict__ estats, long long rdy_to) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   // COLLECT (large k, second pass): the threshold is fixed at the query's seed hseed[p] (a
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
@@ -151,18 +151,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // The wave waits for a slice before its ring loads reach it, and a column's eps only covers
   // the slices scanned so far: it grows at each new slice (and its threshold drops by twice the
   // growth), so every compaction's bound holds for the entries it judges.  A wait that times
-  // out marks the wave's queries overflowed (the caller reruns the call on its general path).
+  // out (rdy_to ticks of the constant-rate wall clock, a few ms) marks the wave's queries
+  // overflowed (the pipeline escalates them).  The ready word is written by a host-initiated copy:
+  // it is polled with relaxed system-scope loads and followed by a system-scope acquire fence
+  // before any image load.  Per wave: waits that had to spin, eps growths and timeouts go to
+  // estats[0..2] at the end (the pipeline reports them).
   int have = 0;          // slices known landed (wave-uniform)
   bool rdy_fail = false;
-  auto wait_slice = [&](int i) -> bool {
+  unsigned n_wait = 0, n_grow = 0, n_to = 0;
+  auto rdy_probe = [&](int i) -> bool {
     unsigned* const f = const_cast<unsigned*>(rdy + i);
-    for (int it = 0; it < (1 << 21); ++it) {
-      if (__builtin_amdgcn_readfirstlane(
-              __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u)
-        return true;
+    return __builtin_amdgcn_readfirstlane(
+               __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
+  };
+  auto wait_slice = [&](int i) -> bool {
+    if (rdy_probe(i)) return true;
+    ++n_wait;
+    const long long t0 = wall_clock64();
+    for (;;) {
       __builtin_amdgcn_s_sleep(2);
+      if (rdy_probe(i)) return true;
+      if (wall_clock64() - t0 > rdy_to) {
+        ++n_to;
+        return false;
+      }
     }
-    return false;
   };
   auto cum_xnm = [&](int upto) {
     float m = 0.0f;
@@ -176,10 +189,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   float xnmax;
   if (rdy) {
     const int need = min(2 / rdy_tiles, rdy_n - 1);  // tiles 0..2: the prologue and step 0's loads
-    for (int i = 0; i <= need; ++i) rdy_fail |= !wait_slice(i);
+    for (int i = 0; i <= need && !rdy_fail; ++i) rdy_fail |= !wait_slice(i);
     have = need + 1;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's DMA wrote them
     xnmax = cum_xnm(need);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   } else {
     xnmax = __uint_as_float(*xnmax_bits);
   }
@@ -519,14 +532,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
         const int need = min(((j0 + 11) >> 2) / rdy_tiles, rdy_n - 1);
         if (need >= have) {
           bool ok = true;
-          for (int i = have; i <= need; ++i) ok &= wait_slice(i);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          for (int i = have; i <= need && ok; ++i) ok &= wait_slice(i);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope (host DMA)
           have = need + 1;
           if (ok) {
             const float xm = cum_xnm(need);
             if (xm > xnmax) {
               grow(xm);
               xnmax = xm;
+              ++n_grow;
             }
           } else {
             for (int col = lane; col < C::NCOL; col += 64) lflag[col] = 1;
@@ -574,6 +588,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   }
   // final threshold over everything buffered, then the candidate ids
   compact(true);
+  if (rdy && estats && lane == 0 && (n_wait | n_grow | n_to)) {
+    atomicAdd(estats + 0, n_wait);
+    atomicAdd(estats + 1, n_grow);
+    atomicAdd(estats + 2, n_to);
+  }
 }
 
 int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
@@ -592,7 +611,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, float r3, int S,
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream,
               const float* hseed = nullptr, int ccap = 0, const unsigned* rdy = nullptr,
-              int rdy_tiles = 1, int rdy_n = 0, const unsigned* xnm_sl = nullptr) {
+              int rdy_tiles = 1, int rdy_n = 0, const unsigned* xnm_sl = nullptr,
+              unsigned* estats = nullptr, long long rdy_to = 0) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
@@ -603,7 +623,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap, rdy, rdy_tiles,     \
-                     rdy_n, xnm_sl)
+                     rdy_n, xnm_sl, estats, rdy_to)
   if (hseed) {  // the COLLECT pass (SUB = 16, CT = 4, fp16 only: see dmlp_screen_x1_collect)
     if constexpr (SUB == 16 && CTV == 4 && F16) DMLP_X1_LAUNCH(16);
     else return -3;
@@ -804,7 +824,8 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
                                     const float* qn, const int* qidx, const int* qk, int nq,
                                     int kmax, const unsigned* bad, const unsigned* rdy,
                                     int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
-                                    int* cand_ids, int* cand_cnt, float* cand_h, void* stream) {
+                                    int* cand_ids, int* cand_cnt, float* cand_h,
+                                    unsigned* estats, void* stream) {
   if (nq <= 0) return 0;
   if (n_tiles < 1 || n_tiles > 4096 || n_points > n_tiles * 64 || !rdy || !xnm_sl ||
       rdy_tiles < 1 || rdy_n < 1 || (int64_t)rdy_tiles * rdy_n < n_tiles)
@@ -814,11 +835,21 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
   dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
   hipStream_t st = (hipStream_t)stream;
   const int sub = x1_sub(kmax), ct = x1_ct(kmax);
+  // the wait bound: DMLP_EARLY_TIMEOUT_MS (default 50) of the constant-rate wall clock
+  static const long long rdy_to = [] {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;  // 100 MHz
+    const char* e = getenv("DMLP_EARLY_TIMEOUT_MS");
+    const double ms = e ? atof(e) : 50.0;
+    return (long long)(ms * khz);
+  }();
 #define DMLP_X1E(KTV, SUBV, CTV)                                                                \
   return launch_x1<KTV, SUBV, 4, 2, CTV, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, \
                                                qk, nq, bad, bad, r1, r2, r3, 1, cand_ids,      \
                                                cand_cnt, cand_h, st, nullptr, 0, rdy, rdy_tiles, \
-                                               rdy_n, xnm_sl)
+                                               rdy_n, xnm_sl, estats, rdy_to)
   if (KT == 1) {
     if (sub == 32) DMLP_X1E(1, 32, 4);
     if (ct == 8) DMLP_X1E(1, 16, 8);

@@ -51,31 +51,12 @@ class Backend:
             lab, cs = torch.from_numpy(l), torch.from_numpy(c.view(np.int64))
         return torch.from_numpy(d), torch.from_numpy(i), lab, cs
 
-    def knn_host(self, X_host, labels_host, label_range, Q_host, k_host: np.ndarray,
-                 kstride=None, gather=None, mu_rows=None, X_full_host=None, report=None,
-                 k_range=None, image_shard=None):
-        """knn() from host arrays: on the GPU the query H2D is chunked and overlapped with the
-        screen of earlier chunks (ops.knn.knn_gpu_pipelined).  gather(X, lab) -> (X, lab)
-        completes a dataset shard on the device (all-gather ingress); image_shard splits the
-        host render of the screen image over the ranks (ops.knn.knn_gpu_pipelined).  Returns
-        (dist, ids, label, checksum) like knn()."""
-        torch = _torch()
-        if self.on_gpu:
-            _, d, i, lab, cs, _ = K.knn_gpu_pipelined(X_host, labels_host, label_range, Q_host,
-                                                      k_host, kstride=kstride, exact=self.exact,
-                                                      gather=gather, mu_rows=mu_rows,
-                                                      X_full_host=X_full_host, report=report,
-                                                      k_range=k_range, image_shard=image_shard)
-            return d, i, lab, cs
-        if gather is not None:
-            X, lab = gather(torch.from_numpy(np.ascontiguousarray(X_host)),
-                            torch.from_numpy(np.ascontiguousarray(labels_host)))
-            return self.knn(X, torch.from_numpy(np.ascontiguousarray(Q_host)), k_host,
-                            labels=lab, label_range=label_range, kstride=kstride)
-        return self.knn(torch.from_numpy(np.ascontiguousarray(X_host)),
-                        torch.from_numpy(np.ascontiguousarray(Q_host)), k_host,
-                        labels=torch.from_numpy(np.ascontiguousarray(labels_host)),
-                        label_range=label_range, kstride=kstride)
+    def step(self, X_host, labels_host, label_range, Q_host, k_host, **kw):
+        """One rank's whole call from host rows on the GPU (ops.knn.step: libdmlp's native
+        pipeline, report text included)."""
+        if not self.on_gpu:
+            raise RuntimeError("the native step needs a GPU")
+        return K.step(X_host, labels_host, label_range, Q_host, k_host, exact=self.exact, **kw)
 
     def knn_streamed(self, X_host, labels_host, label_range, Qx, k_host: np.ndarray,
                      chunk_rows: int, kstride=None):

@@ -73,6 +73,15 @@ class Engine:
             Qx = self.be.tensor(w.Qx)
             self.be.knn(X, Qx, w.k, labels=lab, label_range=(0, 3))
             self.be.report(torch.zeros(4, dtype=torch.int64, device=self.comm.device))
+            # the native step (host render, early start, two-pass large-k screen, report
+            # egress): its streams, staging and first copies, untimed
+            from ..ops import knn as K
+            dst = torch.empty(64 * 48 + 64, dtype=torch.uint8).pin_memory().numpy()
+            for kmax in (32, 60):
+                k = (np.arange(64) % kmax + 1).astype(np.int32)
+                K.step(w.X, w.labels, (0, 3), w.Qx, k, report=dst)
+                K.step(w.X, w.labels, (0, 3), w.Qx, k, report="device")
+            K.step_stats(reset=True)
             self.comm.sync()
         self.comm.barrier()
 

@@ -221,123 +221,104 @@ def _farm_dynamic_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, call_id, chun
 
 
 def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
-    """Static farm over a node-shared input segment (utils/shm.py): every rank copies its own
-    query block host->GPU over its own PCIe link — no funnel through GPU 0.  The replicated
-    dataset (bench_4 @0xc199 broadcasts it) arrives by KNN_DATA_INGRESS:
-      allgather: each rank H2Ds 1/P of the rows, one RCCL all-gather over xGMI completes the
-                 replica — PCIe bytes per GPU drop from N*A*8 to N*A*8/P and the host memory
-                 reads from P*N*A*8 to N*A*8, but the all-gather's kernels wait for the screen;
-      h2d (default): every rank copies the whole dataset from the segment, behind the
-                 screen on the copy engines (the bf16 screen image: 1/P rendered per rank +
-                 one all-gather before the screen, KNN_IMAGE_SHARD);
-      bcast:     rank 0 copies it, one RCCL broadcast."""
+    """Static farm over a node-shared input segment (utils/shm.py): every rank runs the native
+    step (ops/knn.py step: libdmlp's one pipeline, csrc/pipeline.hip) on its own query block,
+    straight from the segment over its own PCIe link — no funnel through GPU 0; the replicated
+    dataset (bench_4 @0xc199 broadcasts it) is read by every rank from the segment.  Report lines:
+    one rank writes them straight into the segment's output region; with P ranks each keeps its
+    lines on its GPU, the lengths go through the segment's per-rank slots, and each rank copies
+    its lines to its byte offset (no RCCL collective, no per-call small collective).
+    KNN_DATA_INGRESS (A/B, P > 1): allgather — each rank H2Ds 1/P of the fp64 rows and one RCCL
+    all-gather over xGMI completes the replica; bcast — rank 0 H2Ds them and broadcasts; both then
+    run the device-rows pipeline (knn_gpu) on the rank's block."""
     import os
     torch = _torch()
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
-    # P > 1 default: every GPU copies the fp64 rows over its own link (DMA engines, behind the
-    # screen); an RCCL all-gather of them would need CUs the screen holds (it fills every SIMD's
-    # register file), so it would run after the screen, on the critical path.  The bf16 screen
-    # image is still sharded + all-gathered (before the screen, when the GPU is idle).
     mode = os.environ.get("KNN_DATA_INGRESS", "h2d") if comm.world > 1 else "h2d"
     max_rows = int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)
+    kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
     if max_rows and N > max_rows:
         # out-of-core: the replica does not fit the device budget, stream it from the segment
         with tr.phase("h2d"):
             Ql = be.tensor(inp.Qx[a:b])
-            kl_h = np.array(inp.k[a:b])
         with tr.phase("h2d+compute"):
-            d, i, lb, cs = be.knn_streamed(inp.X, inp.labels, (lo, hi), Ql, kl_h, max_rows,
-                                           kstride=kmax)
+            d, i, lb, cs = be.knn_streamed(inp.X, inp.labels, (lo, hi), Ql, np.array(kl_h),
+                                           max_rows, kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
-    pipeline = os.environ.get("KNN_PIPELINE", "1") == "1"
-    # the report lines are rendered right behind the re-rank (and, on one rank, copied straight
-    # into the segment's output region) before the call's one host sync
-    rep = {"qid_base": a}
-    if comm.world == 1 and not debug:
-        rep["dst"] = inp.out
-    if mode == "allgather":
-        nc, nd = block_partition(N, comm.world)
-        r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
-        kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
-        k_range = _lib_range(kl_h)  # this rank's own k bounds steer its dispatch
-
-        def gather(Xs, ls):
-            return (comm.allgather_rows(Xs, nc, (A,), torch.float64),
-                    comm.allgather_rows(ls, nc, (), torch.int32))
-        if pipeline:
-            # this rank's rows and its query chunks on the copy stream; the all-gather and the
-            # screen of the first chunk run while the later chunks are still crossing PCIe
-            with tr.phase("h2d+allgather+compute"):
-                # KNN_IMAGE_SHARD=0: every rank renders the whole screen image (A/B)
-                shard_img = (os.environ.get("KNN_IMAGE_SHARD", "1") == "1"
-                             and comm.on_gpu and comm.world > 1)
-                d, i, lb, cs = be.knn_host(inp.X[r0:r1], inp.labels[r0:r1], (lo, hi),
-                                           inp.Qx[a:b], kl_h, kstride=kmax, gather=gather,
-                                           mu_rows=inp.X[:4096], X_full_host=inp.X,
-                                           report=rep, k_range=k_range,
-                                           image_shard=(comm.rank, comm.world,
-                                                        comm.allgather_into,
-                                                        comm.allreduce_max_)
-                                           if shard_img else None)
-            return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug,
-                                     rep)
-        with tr.phase("h2d"):
-            Xs = be.tensor(inp.X[r0:r1])
-            ls = be.tensor(inp.labels[r0:r1])
-            Ql = be.tensor(inp.Qx[a:b])
-        with tr.phase("allgather_data"):
-            X, lab = gather(Xs, ls)
-        with tr.phase("compute"):
-            d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
-        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
-    bcast_data = mode == "bcast"
-    if (comm.world == 1 and not debug and be.on_gpu and not be.exact and pipeline
-            and getattr(inp, "out", None) is not None):
-        # one rank, every k on the single-term class: the whole call in one native function
-        # (ops/knn.py fast_step); anything else falls through to the pipeline below
-        from ..ops import knn as K
-        with tr.phase("h2d+compute"):
-            r = K.fast_step(inp.X, inp.labels, (lo, hi), inp.Qx, inp.k, inp.k_range_all, inp.out)
-        if r is not None:
-            lb, cs, n = r
-            return lb, cs, None, None, memoryview(inp.out)[:n].toreadonly()
-    if not bcast_data and pipeline:
-        # per-GPU H2D: the query chunks land while the earlier chunks already screen
-        with tr.phase("h2d+compute"):
-            kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
-            shard_img = (os.environ.get("KNN_IMAGE_SHARD", "1") == "1"
-                         and comm.on_gpu and comm.world > 1)
-            d, i, lb, cs = be.knn_host(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h,
-                                       kstride=kmax, report=rep,
-                                       k_range=(inp.k_range_all if comm.world == 1
-                                                else _lib_range(kl_h)),
-                                       image_shard=(comm.rank, comm.world, comm.allgather_into,
-                                                    comm.allreduce_max_)
-                                       if shard_img else None)
-        return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, rep)
+    if mode == "h2d" and be.on_gpu:
+        with tr.phase("step"):
+            k_range = inp.k_range_all if comm.world == 1 else _lib_range(kl_h)
+            rep = None if debug else (inp.out if comm.world == 1 else "device")
+            r = be.step(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h, k_range=k_range,
+                        qid_base=a, report=rep, lists=debug, kstride=kmax)
+        if debug:
+            return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, r.dist, r.ids, r.label,
+                                     r.checksum, True)
+        with tr.phase("report"):
+            text = _step_egress(comm, inp, r, a)
+        if comm.world == 1:
+            return r.label, r.checksum, None, None, text
+        if not comm.is_root:
+            return None
+        res = torch.from_numpy(inp.res)  # copies: the segment is reused by the next call
+        return res[:, 0].to(torch.int32), res[:, 1].contiguous(), None, None, text
     with tr.phase("h2d"):
-        X = lab = None
-        if not bcast_data or comm.is_root:
-            X = be.tensor(inp.X)
-            lab = be.tensor(inp.labels)
         Ql = be.tensor(inp.Qx[a:b])
-        kl_h = np.array(inp.k[a:b])
-    if bcast_data:
+        X = lab = None
+        if mode == "allgather":
+            nc, nd = block_partition(N, comm.world)
+            r0, r1 = nd[comm.rank], nd[comm.rank] + nc[comm.rank]
+            Xs, ls = be.tensor(inp.X[r0:r1]), be.tensor(inp.labels[r0:r1])
+        elif mode != "bcast" or comm.is_root:
+            X, lab = be.tensor(inp.X), be.tensor(inp.labels)
+    if mode == "allgather":
+        with tr.phase("allgather_data"):
+            X = comm.allgather_rows(Xs, nc, (A,), torch.float64)
+            lab = comm.allgather_rows(ls, nc, (), torch.int32)
+    elif mode == "bcast":
         with tr.phase("bcast_data"):
             X = comm.bcast(X, (N, A), torch.float64)
             lab = comm.bcast(lab, (N,), torch.int32)
     with tr.phase("compute"):
-        d, i, lb, cs = be.knn(X, Ql, kl_h, labels=lab, label_range=(lo, hi), kstride=kmax)
+        d, i, lb, cs = be.knn(X, Ql, np.array(kl_h), labels=lab, label_range=(lo, hi),
+                              kstride=kmax)
     return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
 
 
-def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, report=None):
+def _step_egress(comm, inp, r, qid_base):
+    """The native step's report lines into the segment's output region.  One rank: the step
+    already copied them to offset 0.  P ranks: each length goes through the segment's per-rank
+    slots, a segment barrier, each rank copies its lines (still on its GPU) to its byte offset
+    and its (label, checksum) rows to the results region, a second barrier; rank 0 gets a view
+    of the whole report."""
+    torch = _torch()
+    from ..ops import knn as K
+    n = r.report_len
+    if comm.world == 1:
+        comm.barrier()
+        return memoryview(inp.out)[:n].toreadonly()
+    inp.slots[comm.rank] = n
+    inp.barrier(comm.world)  # every length is in its slot
+    lens = [int(v) for v in inp.slots[:comm.world]]
+    off = sum(lens[:comm.rank])
+    if off + n > len(inp.out):
+        raise RuntimeError("shared output region too small")
+    K.step_emit(inp.out[off:off + n], n)
+    nq = r.checksum.shape[0]
+    if nq:
+        rows = torch.from_numpy(inp.res[qid_base:qid_base + nq])
+        rows.copy_(torch.stack([r.label.to(torch.int64), r.checksum], dim=1))
+    inp.barrier(comm.world)  # every block's text and rows are in the segment
+    return memoryview(inp.out)[:sum(lens)].toreadonly() if comm.is_root else None
+
+
+def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug):
     torch = _torch()
     text = None
     if not debug:
         with tr.phase("report"):
-            text = _shared_egress(comm, be, inp, cs, a, report, lb=lb)
+            text = _shared_egress(comm, be, inp, cs, a, lb=lb)
     if comm.world == 1:
         return lb, cs, d if debug else None, i if debug else None, text
     if not debug:
@@ -349,30 +330,21 @@ def _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug, r
     with tr.phase("gather"):
         packed = torch.stack([lb.to(torch.int64), cs], dim=1)
         allp = comm.gather_rows(packed, counts, (2,), torch.int64)
-        dd = ii = None
-        if debug:
-            dd = comm.gather_rows(d, counts, (kmax,), torch.float64)
-            ii = comm.gather_rows(i, counts, (kmax,), torch.int32)
+        dd = comm.gather_rows(d, counts, (kmax,), torch.float64)
+        ii = comm.gather_rows(i, counts, (kmax,), torch.int32)
     if not comm.is_root:
         return None
     return allp[:, 0].to(torch.int32), allp[:, 1].contiguous(), dd, ii, text
 
 
-def _shared_egress(comm, be, inp, cs, qid_base, report=None, lb=None):
-    """Every rank renders its block's report lines and copies them straight into the shared
-    segment's output region at its byte offset; rank 0 gets a view of the whole report.
-    report: knn_gpu_pipelined's speculative rendering (used when still valid).  P > 1: the
-    lengths go through the segment's per-rank slots and two segment barriers order the writes
-    (no RCCL collective, no extra device sync); with lb given, the block's (label, checksum)
-    rows are copied into the segment's results region in the same pass."""
+def _shared_egress(comm, be, inp, cs, qid_base, lb=None):
+    """Every rank renders its block's report lines (GPU formatter, or the host's on CPU) and
+    copies them straight into the shared segment's output region at its byte offset; rank 0 gets
+    a view of the whole report.  P > 1: the lengths go through the segment's per-rank slots and
+    two segment barriers order the writes; with lb given, the block's (label, checksum) rows are
+    copied into the segment's results region in the same pass."""
     torch = _torch()
-    if be.on_gpu and report is not None and report.get("valid"):
-        dev_text, n_h = report["text"]
-        n = int(n_h[0])
-        if report.get("copied"):  # one rank: the text already sits at offset 0
-            comm.barrier()
-            return memoryview(inp.out)[:n].toreadonly() if comm.is_root else None
-    elif be.on_gpu:
+    if be.on_gpu:
         from ..ops import knn as K
         dev_text, n = K.format_report_dev(cs, qid_base)
     else:
@@ -391,8 +363,6 @@ def _shared_egress(comm, be, inp, cs, qid_base, report=None, lb=None):
         dst = torch.from_numpy(inp.out[off:off + n])
         if be.on_gpu:
             dst.copy_(dev_text[:n], non_blocking=True)  # D2H into the page-locked segment
-            from ..ops import knn as K
-            K._IO["d2h"] += n
         else:
             dst.copy_(torch.frombuffer(bytearray(host), dtype=torch.uint8))
     if lb is not None and comm.world > 1 and nq:

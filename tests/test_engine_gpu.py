@@ -55,67 +55,83 @@ def test_shared_ingress_and_out_of_core(gpu, workload, monkeypatch, max_rows):
     eng.close()
 
 
-@pytest.mark.parametrize("kmax,fast,parts,rparts", [(32, True, 1, 1), (32, True, 2, 1),
-                                                    (24, True, 3, 1), (40, False, 1, 1),
-                                                    (32, True, 1, 2), (20, True, 1, 3)])
-def test_native_fast_step(gpu, kmax, fast, parts, rparts):
-    """One rank over the node-shared segment, every k on the single-term class: the whole call
-    runs in one native function (fast_step.hip) — report, labels and checksums == the oracle's,
-    three calls in a row (reused buffers), in 1-3 query parts (each part's report text placed at
-    the previous part's device-side end) or one screen with 2-3 refine ranges (each range's text
-    copied on the D2H stream while the next refines); k > 32 falls through to the Python
-    pipeline."""
-    from distributed_machine_learning_project_amd import _lib
+@pytest.mark.parametrize("kmax,A", [(32, 32), (24, 32), (40, 32), (200, 32), (16, 100)])
+def test_native_step(gpu, kmax, A):
+    """One rank over the node-shared segment: the whole call runs in libdmlp's native step
+    (pipeline.hip dmlp_step) for EVERY k — k <= 32 on the single-term screen, k in (32, 256] on
+    the two-pass single-term screen — report, labels and checksums == the oracle's, three calls in
+    a row (reused buffers), each served by the step."""
     from distributed_machine_learning_project_amd.utils.shm import share_input
-    _lib.lib().dmlp_fast_step_parts(parts)
-    _lib.lib().dmlp_fast_step_rparts(rparts)
-    inp = dmlp.generate(7000, 9000 + 37 * parts + 101 * rparts, 32, 0.0, 1000.0, 1, kmax, 8,
-                        seed=kmax + parts + 10 * rparts)
+    inp = dmlp.generate(7000, 9000 + kmax, A, 0.0, 1000.0, 1, kmax, 8, seed=kmax + A)
     d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
     lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
     eng = _engine("farm")
     sh = share_input(eng.comm, inp)
     for _ in range(3):
-        n0 = K.FAST_STEP_CALLS[0]
+        n0 = K.STEP_STATS["calls"]
         out = eng.KNN(sh.params, sh, None)
         assert bytes(eng.report(out)) == dmlp.format_report(cs)
         np.testing.assert_array_equal(out.labels_np(), lab_ref)
         np.testing.assert_array_equal(out.checksums_np(), cs)
-        assert (K.FAST_STEP_CALLS[0] == n0 + 1) == fast
+        assert K.STEP_STATS["calls"] == n0 + 1
+        assert K.pipeline_stats()["path"] == 0
     sh.close()
     eng.close()
-    _lib.lib().dmlp_fast_step_parts(0)
-    _lib.lib().dmlp_fast_step_rparts(0)
 
 
-@pytest.mark.parametrize("n,kmax", [(2000, 16), (5000, 32)])
-def test_native_fast_step_early(gpu, n, kmax):
-    """Early start (DMLP_FAST_EARLY): the screen starts on the query operands while the dataset
-    image crosses PCIe in 4 slices with ready words, each column's eps growing with the slices
-    it has seen.  It needs one screen slice (>= 131072 queries fill the chip at S = 1); the
-    report, labels and checksums == the oracle's over three calls, and == the default path."""
+def _early_inputs(n, A, kmax, Q, seed):
+    """Two different inputs of one shape (alternated through one engine, so a screen that read a
+    slice before its ready word, or a stale line, would read the OTHER input's bytes), each with
+    its farthest point in the last rows: the last image slice raises every column's eps."""
+    out = []
+    for s in (seed, seed + 1):
+        inp = dmlp.generate(n, Q, A, 0.0, 1000.0, 1, kmax, 8, seed=s)
+        inp.X[-1] = 1000.0 if s % 2 else 0.0  # a corner of the box: the largest |x - mu|
+        d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+        lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+        out.append((inp, lab_ref, cs, dmlp.format_report(cs)))
+    return out
+
+
+@pytest.mark.parametrize("n,A,kmax", [(2000, 32, 16), (5000, 32, 32), (3000, 128, 32),
+                                        (3000, 256, 32)])
+def test_native_step_early_start(gpu, n, A, kmax):
+    """Early start: the screen starts on the query operands while the dataset image crosses
+    PCIe in slices with ready words.  The host sleeps 400 us before each image slice
+    (dmlp_step_early_delay), so the screen provably waits mid-scan; the device counters then show
+    waits > 0, eps growths > 0 (the far point sits in the last slice) and no timeout.  Two
+    different inputs of equal shape alternate A, B, A, B (early on), then once with the early
+    start off; every report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
+    variant (one wave per SIMD, 404 of 512 registers).  A = 256 (KT = 8, all 512 registers): the
+    step refuses the early start there — its image copies (blit kernels) would find no free wave
+    slot beside the spinning screen — and the results stay exact.  One screen slice needs a full
+    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4)."""
     from distributed_machine_learning_project_amd import _lib
-    from distributed_machine_learning_project_amd.utils.shm import share_input
-    inp = dmlp.generate(n, 131072 + 64 * 3, 32, 0.0, 1000.0, 1, kmax, 8, seed=n + kmax)
-    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
-    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
-    expect = dmlp.format_report(cs)
-    eng = _engine("farm")
-    sh = share_input(eng.comm, inp)
+    L = _lib.lib()
+    Q = 131072 + 64 * 3 if A <= 64 else 65536 + 64
+    cases = _early_inputs(n, A, kmax, Q, seed=n + A + kmax)
+    dsts = []
+    import torch
+    for inp, _, _, _ in cases:
+        dsts.append(torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy())
     try:
-        for early in (1, 0, 1):
-            _lib.lib().dmlp_fast_step_early(early)
-            for _ in range(2 if early else 1):
-                n0 = K.FAST_STEP_CALLS[0]
-                out = eng.KNN(sh.params, sh, None)
-                assert bytes(eng.report(out)) == expect
-                np.testing.assert_array_equal(out.labels_np(), lab_ref)
-                np.testing.assert_array_equal(out.checksums_np(), cs)
-                assert K.FAST_STEP_CALLS[0] == n0 + 1
+        L.dmlp_step_early_delay(400)
+        for rnd, early in enumerate((1, 1, 1, 1, 0)):
+            L.dmlp_step_early(early)
+            inp, lab_ref, cs, expect = cases[rnd % 2]
+            dst = dsts[rnd % 2]
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
+            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
+            assert r.early == (early if A <= 128 else 0)
+            if r.early:
+                assert r.early_timeouts == 0
+                assert r.early_waits > 0, "the screen never waited for a slice"
+                assert r.early_grows > 0, "no column's eps grew with a later slice"
     finally:
-        _lib.lib().dmlp_fast_step_early(-1)
-        sh.close()
-        eng.close()
+        L.dmlp_step_early(-1)
+        L.dmlp_step_early_delay(-1)
 
 
 def test_debug_listing(gpu, workload):

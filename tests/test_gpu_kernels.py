@@ -165,12 +165,12 @@ def test_many_slices_small_q(torch_cuda):
 
 
 @pytest.mark.parametrize("impl", ["x1", "stream", "lds"])
-def test_screen_impls_bench_distribution(torch_cuda, impl, monkeypatch):
+def test_screen_impls_bench_distribution(torch_cuda, impl):
     """Every screen implementation is exact on the bench distribution (generate_input.py,
     A=32, k=16); the single-term screen needs no 3-term escalation there."""
-    monkeypatch.setattr(K, "SCREEN_IMPL", impl)
     inp = dmlp.generate(20000, 700, 32, 0.0, 1000.0, 16, 16, 10, seed=12)
-    r, refs = run_both(torch_cuda, inp)
+    with K.pipeline_options(screen=impl):
+        r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
     if impl == "x1":
         assert r.n_escalated == 0
@@ -178,9 +178,8 @@ def test_screen_impls_bench_distribution(torch_cuda, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("A,kmax", [(8, 16), (32, 32), (64, 16), (40, 30)])
-def test_x1_screen_shapes(torch_cuda, A, kmax, monkeypatch):
+def test_x1_screen_shapes(torch_cuda, A, kmax):
     """Single-term screen: KT 1/2, both sub-buffer depths (k <= 16 / <= 32), ragged tails."""
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
     inp = dmlp.generate(7777, 333, A, -100.0, 100.0, 1, kmax, 6, seed=A + kmax)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
@@ -192,38 +191,36 @@ def test_x1_screen_shapes(torch_cuda, A, kmax, monkeypatch):
                                                   (64, 1, 16, 9001, 260, -5.0, 5.0),
                                                   (32, 1, 1, 3000, 129, 0.0, 1000.0),
                                                   (20, 1, 12, 300000, 64, 0.0, 1000.0)])
-def test_single_term_screens(torch_cuda, A, kmin, kmax, N, Q, lo, hi, monkeypatch):
+def test_single_term_screens(torch_cuda, A, kmin, kmax, N, Q, lo, hi):
     """k <= 16 single-term class (screen_x1.hip, 16x16x32): KT 1/2, ragged query blocks and
     tiles, k = 1, and many slices (few queries, N = 3e5 > one slice's 16-bit group range)."""
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
     inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 6, seed=A + kmax + N)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
     assert_same(r, refs)
 
 
-def test_x1_escalates_tight_data(torch_cuda, monkeypatch):
+def test_x1_escalates_tight_data(torch_cuda):
     """Dense 1-D data: the single-term bound admits ~900 points per query (> its 60-group
     buffer), so queries escalate to the 3-term screen (or on to the exact path) and stay exact."""
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
-    monkeypatch.setattr(K, "NUM_CUS", 1)  # few slices: ~5000 points per query block and slice
     inp = dmlp.generate(20000, 100, 1, 0.0, 1000.0, 8, 16, 4, seed=2)
-    r, refs = run_both(torch_cuda, inp)
+    # few slices: ~5000 points per query block and slice
+    with K.pipeline_options(num_cus=1):
+        r, refs = run_both(torch_cuda, inp)
     assert r.n_escalated > 0
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("chunks,kmin", [(1, 1), (1, 0), (4, 1)])
-def test_pipelined_chunks_match(torch_cuda, chunks, kmin):
-    """Host-array entry == the exact CPU path: chunks=1 renders the screen's query operands on
-    the host and copies the fp64 rows behind the screen (kmin=0 takes the device-prep path),
-    chunks=4 screens query chunks as they land."""
+@pytest.mark.parametrize("kmin", [1, 0])
+def test_pipelined_chunks_match(torch_cuda, kmin):
+    """Host-array entry (the native step) == the exact CPU path: the host renders the screen's
+    operands and copies the fp64 rows behind the screen; kmin=0 adds k = 0 queries (no neighbour,
+    label -1) to the per-query dispatch."""
     torch = torch_cuda
     inp = dmlp.generate(30000, 9000, 32, 0.0, 1000.0, kmin, 24, 10, seed=21)
     Xp = torch.from_numpy(inp.X).pin_memory().numpy()
     Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
-    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k,
-                                                 chunks=chunks)
+    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k)
     torch.cuda.synchronize()
     d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
     lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
@@ -234,15 +231,15 @@ def test_pipelined_chunks_match(torch_cuda, chunks, kmin):
 
 
 @pytest.mark.parametrize("case", ["escalate", "slices", "ragged"])
-def test_pipelined_host_image_paths(torch_cuda, case, monkeypatch):
+def test_pipelined_host_image_paths(torch_cuda, case):
     """The host's fp16 hi-only dataset image (hl = 1) through the x1 screen and group refine:
     tight 1-D data escalates to the 3-term screen (device hi/lo image rendered on demand from
     the fp64 rows), few queries split the data into many slices, and A = 40 / N % 64 != 0
     exercises KT = 2 and a ragged last tile."""
     torch = torch_cuda
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
+    ncus = 256
     if case == "escalate":
-        monkeypatch.setattr(K, "NUM_CUS", 1)
+        ncus = 1
         inp = dmlp.generate(20000, 100, 1, 0.0, 1000.0, 8, 16, 4, seed=2)
     elif case == "slices":
         inp = dmlp.generate(60000, 64, 32, 0.0, 1000.0, 1, 32, 10, seed=4)
@@ -250,11 +247,13 @@ def test_pipelined_host_image_paths(torch_cuda, case, monkeypatch):
         inp = dmlp.generate(9001, 700, 40, -100.0, 100.0, 1, 30, 7, seed=6)
     Xp = torch.from_numpy(inp.X).pin_memory().numpy()
     Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
-    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, int(inp.labels.max()) + 1),
-                                                 Qp, inp.k)
+    with K.pipeline_options(num_cus=ncus):
+        ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels,
+                                                     (0, int(inp.labels.max()) + 1), Qp, inp.k)
     torch.cuda.synchronize()
-    if case != "escalate":
-        assert ds.hl == 1
+    assert ds.hl == 1
+    if case == "escalate":
+        assert ds.n_escalated > 0
     d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
     lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
     np.testing.assert_array_equal(i.cpu().numpy(), i_ref)
@@ -285,12 +284,20 @@ def test_host_data_image_matches_device(torch_cuda):
     ref = c.astype(np.float32).astype(np.float16).view(np.uint16)
     ref = ref.reshape(n_tiles, 4, 16, KT, 4, 8).transpose(0, 1, 3, 4, 2, 5).reshape(-1)
     np.testing.assert_array_equal(img, ref)
-    ds = K.prepare_dataset(torch.from_numpy(inp.X).cuda(), mu=torch.from_numpy(mu).cuda())
+    X = torch.from_numpy(inp.X).cuda()
+    mu_d = torch.from_numpy(mu).cuda()
+    xfrag = torch.empty(n_tiles * 64 * KT * 32 * 2, dtype=torch.int16, device="cuda")
+    xinit = torch.empty(n_tiles * 64, dtype=torch.float32, device="cuda")
+    xnmax = torch.zeros(1, dtype=torch.int32, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    _lib.check(L.dmlp_prep_data(X.data_ptr(), N, A, mu_d.data_ptr(), KT, xfrag.data_ptr(),
+                                xinit.data_ptr(), xnmax.data_ptr(), bad.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream), "prep_data")
     torch.cuda.synchronize()
-    np.testing.assert_allclose(ds.xinit.cpu().numpy()[:N], xin_h[:N], rtol=1e-6)
-    assert np.isneginf(ds.xinit.cpu().numpy()[N:]).all()
-    np.testing.assert_allclose(ds.xnmax_bits.cpu().numpy().view(np.float32),
-                               nm_h.view(np.float32), rtol=1e-6)
+    np.testing.assert_allclose(xinit.cpu().numpy()[:N], xin_h[:N], rtol=1e-6)
+    assert np.isneginf(xinit.cpu().numpy()[N:]).all()
+    np.testing.assert_allclose(xnmax.cpu().numpy().view(np.float32), nm_h.view(np.float32),
+                               rtol=1e-6)
 
 
 def test_host_prep_matches_device_prep(torch_cuda):
@@ -411,12 +418,11 @@ def test_format_report_gpu(torch_cuda):
     assert g == dmlp.format_report(cs, qid_base=7)
 
 
-def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
+def test_pipelined_host_operands_any_k(torch_cuda):
     """knn_gpu_pipelined keeps the host's fp16 x1 operands for the k <= 32 queries when other
     queries need the 3-term class (k in (32, 128]) or the exact path (k > 128), and when one
     query's candidates overflow (600 duplicate points): per-query dispatch, bit-exact."""
     torch = torch_cuda
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
     rng = np.random.default_rng(23)
     N, Q, A = 8000, 500, 32
     X = np.round(rng.uniform(0, 1000, (N, A)), 6)
@@ -438,20 +444,16 @@ def test_pipelined_host_operands_any_k(torch_cuda, monkeypatch):
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
 
 
-@pytest.mark.parametrize("A,dup,single,x1k", [(32, 0, True, False), (100, 0, True, False),
-                                              (256, 0, True, False), (32, 700, True, False),
-                                              (64, 0, False, False), (32, 0, True, True),
-                                              (100, 0, True, True), (256, 0, True, True),
-                                              (32, 700, True, True)])
-def test_pipelined_single_term_lds(torch_cuda, A, dup, single, x1k, monkeypatch):
-    """k in (32, 256] on the single-term LDS screen over the host's fp16 operands (HL = 1), or
-    (x1k) the two-pass single-term x1 screen (seeds from 16 slices at k' = ceil(k / 16), one
-    COLLECT pass, the large-k group refine) — with `dup` copies of one point, the queries sitting
-    on it overflow the single-term bound and escalate to the 3-term LDS screen; single=False is
-    the 3-term-only A/B path.  Bit-exact."""
+@pytest.mark.parametrize("A,dup,x1k", [(32, 0, False), (100, 0, False), (256, 0, False),
+                                        (32, 700, False), (32, 0, True), (100, 0, True),
+                                        (256, 0, True), (32, 700, True)])
+def test_pipelined_single_term_lds(torch_cuda, A, dup, x1k):
+    """k in (32, 256] on the two-pass single-term x1 screen over the host's fp16 operands (seeds
+    from 16 slices at k' = ceil(k / 16), one COLLECT pass, the large-k group refine) — with `dup`
+    copies of one point, the queries sitting on it overflow the single-term bound and escalate to
+    the 3-term LDS screen; x1k=False is the 3-term-only A/B path on the device image.
+    Bit-exact."""
     torch = torch_cuda
-    monkeypatch.setattr(K, "LDS_SINGLE", single)
-    monkeypatch.setattr(K, "X1K", x1k)
     rng = np.random.default_rng(A + dup)
     N, Q = 9000, 400
     X = np.round(rng.uniform(0, 1000, (N, A)), 6)
@@ -463,7 +465,8 @@ def test_pipelined_single_term_lds(torch_cuda, A, dup, single, x1k, monkeypatch)
     labels = rng.integers(0, 9, N).astype(np.int32)
     Xp = torch.from_numpy(X).pin_memory().numpy()
     Qp = torch.from_numpy(Qx).pin_memory().numpy()
-    ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, labels, (0, 9), Qp, k)
+    with K.pipeline_options(x1k=int(x1k)):
+        ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, labels, (0, 9), Qp, k)
     torch.cuda.synchronize()
     d_ref, i_ref = K.knn_cpu(X, Qx, k, kstride=d.shape[1])
     lab_ref, cs_ref = K.finalize_cpu(i_ref, k, labels)
@@ -495,10 +498,9 @@ def test_pipelined_x1k_small_block(torch_cuda):
 
 @pytest.mark.parametrize("A,kmax", [(65, 16), (100, 32), (128, 16), (129, 16), (200, 30),
                                     (256, 16)])
-def test_x1_wide_rows(torch_cuda, A, kmax, monkeypatch):
+def test_x1_wide_rows(torch_cuda, A, kmax):
     """Single-term screen for A > 64 (KT = 4 and 8, one wave per SIMD) with the group refine
     staging hi(q') in LDS."""
-    monkeypatch.setattr(K, "SCREEN_IMPL", "x1")
     inp = dmlp.generate(6000, 300, A, 0.0, 1000.0, 1, kmax, 6, seed=A + kmax)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
@@ -525,27 +527,32 @@ def test_wide_rows_every_class(torch_cuda, A):
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("case", ["parts", "out_of_range", "wide", "fp64_rows"])
-def test_pipelined_query_parts(torch_cuda, case, monkeypatch):
-    """The query-part front (HOST_OPS_PARTS): each part's screen is queued natively behind its
-    own operand copy on its own stream.  out_of_range puts one query of the last part outside
-    the fp16 range, so the parts already screened are drained and the call reruns on the
-    device path; wide runs KT = 8; fp64_rows has dataset values with more than 6 decimals, so
-    its rows cross as fp64 while the queries' cross as lossless int32."""
+@pytest.mark.parametrize("case", ["plain", "out_of_range", "data_out_of_range", "wide",
+                                  "fp64_rows"])
+def test_step_front_cases(torch_cuda, case):
+    """The native step's front: out_of_range puts one query outside the fp16 range (the step
+    takes the device image path for the whole call before anything is screened);
+    data_out_of_range puts one point of the last image slice outside it (with the early start
+    on, the screen already runs: it drains and the call continues on the device image path);
+    wide runs KT = 8; fp64_rows has dataset values with more than 6 decimals, so its rows cross
+    as fp64 while the queries' cross as lossless int32."""
     torch = torch_cuda
-    monkeypatch.setattr(K, "HOST_OPS_PARTS", 4)
     A = 256 if case == "wide" else 32
-    inp = dmlp.generate(8000 if case == "wide" else 20000, 32768, A, 0.0, 1000.0, 1, 32, 10,
-                        seed=31)
+    # (data_out_of_range: one full round of query waves, so the early start runs)
+    inp = dmlp.generate(8000 if case == "wide" else 20000,
+                        65536 + 64 if case == "data_out_of_range" else 32768, A, 0.0, 1000.0, 1,
+                        32, 10, seed=31)
     if case == "out_of_range":
         inp.Qx[-5, 3] = 1.0e6
+    if case == "data_out_of_range":
+        inp.X[-3, 3] = 1.0e7
     if case == "fp64_rows":
         inp.X[7, 5] += 1e-9
     Xp = torch.from_numpy(inp.X).pin_memory().numpy()
     Qp = torch.from_numpy(inp.Qx).pin_memory().numpy()
     ds, d, i, lab, cs, nfb = K.knn_gpu_pipelined(Xp, inp.labels, (0, 10), Qp, inp.k)
     torch.cuda.synchronize()
-    assert ds.hl == (2 if case == "out_of_range" else 1)
+    assert ds.hl == (2 if "out_of_range" in case else 1)
     d_ref, i_ref = K.knn_cpu(inp.X, inp.Qx, inp.k, kstride=d.shape[1])
     lab_ref, cs_ref = K.finalize_cpu(i_ref, inp.k, inp.labels)
     np.testing.assert_array_equal(i.cpu().numpy(), i_ref)

@@ -164,39 +164,35 @@ def case_x1(tmp_path_factory):
 
 
 @pytest.mark.parametrize("np_", [2, 3])
-def test_python_sharded_image_render(case_x1, np_):
-    """Static farm over the node-shared segment: each rank renders 1/np of the screen image on
-    the host and one all-gather completes it (KNN_IMAGE_SHARD=1, the default), == oracle bytes
-    and == the whole-image-per-rank render; with out-of-range data in one shard every rank
-    takes the fallback together (max-reduced +inf norm, no divergent collective)."""
+def test_python_shared_step_farm(case_x1, np_):
+    """Static farm over the node-shared segment: each rank runs libdmlp's native step on its own
+    query block straight from the segment, keeps its report lines on its GPU and copies them to
+    its byte offset in the segment (lengths through the segment's slots) == oracle bytes; with
+    out-of-range data each rank's step takes the device-image path by itself (no collective);
+    KNN_DATA_INGRESS=allgather (fp64 replica all-gathered over the data plane, then the
+    device-rows pipeline) == oracle bytes too."""
     (path, expect), (bad_path, bad_expect) = case_x1
     env = {"KNN_INGRESS": "shm"}
     assert _python(path, np_, "farm", env) == expect
-    assert _python(path, np_, "farm", dict(env, KNN_IMAGE_SHARD="0")) == expect
     assert _python(bad_path, np_, "farm", env) == bad_expect
+    assert _python(path, np_, "farm", dict(env, KNN_DATA_INGRESS="allgather")) == expect
 
 
 @pytest.mark.parametrize("np_", [2, 3])
 def test_native_shared_ingress_farm(case, case_x1, np_):
     """knn_engine KNN_INGRESS=shm: the parsed input in an MPI-3 node-shared window, every rank
-    runs the host-operand fast path on its own query block over its own link and writes its
-    report lines into the window; out-of-range data in one shard, or k > 32, sends every rank
-    to the general farm together.  == oracle bytes in all cases."""
+    runs the library's native step on its own query block over its own link and writes its
+    report lines into the window (one 8-byte all-gather of the lengths); out-of-range data and
+    k > 32 stay in the step too (device-image path / two-pass screen).  == oracle bytes in all
+    cases, and the general farm (its "distribute" phase) never runs."""
     (path, expect), (bad_path, bad_expect) = case_x1
     env = {"KNN_INGRESS": "shm", "KNN_TRACE": "1"}
-    out, err = _native(path, np_, "farm", env_extra=env, want_err=True)
-    assert out == expect
-    # the per-rank fast path ran on every rank (its phases), not the general farm's
-    for r in range(np_):
-        assert f"rank {r} h2d_operands".encode() in err, err.decode()[-2000:]
-    assert b"distribute" not in err
-    out, err = _native(bad_path, np_, "farm", env_extra=env, want_err=True)
-    assert out == bad_expect
-    assert b"distribute" in err  # the general farm, on every rank
-    gpath, gexpect = case
-    assert _native(gpath, np_, "farm", env_extra=env) == gexpect
-    # every rank renders the whole screen image instead of its 1/np (A/B switch)
-    assert _native(path, np_, "farm", env_extra=dict(env, KNN_IMAGE_SHARD="0")) == expect
+    for p, e in ((path, expect), (bad_path, bad_expect), case):
+        out, err = _native(p, np_, "farm", env_extra=env, want_err=True)
+        assert out == e
+        for r in range(np_):  # the step ran on every rank
+            assert f"rank {r} step ".encode() in err, err.decode()[-2000:]
+        assert b"distribute" not in err
 
 
 @pytest.mark.parametrize("np_", [2, 3])

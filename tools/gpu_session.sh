@@ -19,7 +19,6 @@
 #   exact      bench.py --exact (fp64-only path)
 #   harness    bench.py --harness native (knn_engine through the reference contract)
 #   dropin     bench.py --harness dropin (engine.h drop-in linked with the reference's common.cpp)
-#   parts      bench.py with 4 / 2 / 1 query parts of the host-operand pipeline (+ --verify at 4)
 #   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
@@ -62,16 +61,13 @@ for task in "$@"; do
       find "$OUT/x1modes" -name '*kernel_stats.csv' -exec sh -c 'grep k_screen_x1 "$1" | cut -c1-200' _ {} \; ;;
     early)  # native step early start (default) -- its tests, verify, interleaved step A/B against DMLP_FAST_EARLY=0
       step early_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
-          --timeout-method thread -k "fast_step"
+          --timeout-method thread -k "native_step"
       step early_verify 300 python bench.py --steps 20 --warmup 2 --verify
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step early_ab 900 bash tools/kernel_ab.sh base:DMLP_FAST_EARLY=0 \
           early:DMLP_FAST_EARLY=1 ;;
     qchunks)  # early start: query render slices 2 / 4 / 6 (DMLP_FAST_QCHUNKS), interleaved
       AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step qchunks_ab 900 bash tools/kernel_ab.sh \
           q2:DMLP_FAST_QCHUNKS=2 q4:DMLP_FAST_QCHUNKS=4 q6:DMLP_FAST_QCHUNKS=6 ;;
-    rparts)  # native step: 1 / 2 / 3 refine ranges behind one screen (DMLP_FAST_RPARTS), interleaved
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step rparts_ab 600 bash tools/kernel_ab.sh \
-          r1:DMLP_FAST_RPARTS=1 r2:DMLP_FAST_RPARTS=2 r3:DMLP_FAST_RPARTS=3 ;;
     warm)  # the headline bench after a 3 s warm-up instead of 0.6 s (box-to-box host variance)
       step bench_warm3 300 python bench.py --min-warmup-s 3 ;;
     prof)
@@ -130,11 +126,6 @@ for task in "$@"; do
       done
       cmp /tmp/dropin.out /tmp/native.out && echo "dropin == native report bytes"
       tail -n 12 "$OUT/dropin_trace_3.txt" "$OUT/dropin_trace_fp64rows.txt" "$OUT/native_trace_2.txt" ;;
-    parts)
-      DMLP_HOST_OPS_PARTS=4 step parts_verify 300 python bench.py --steps 5 --warmup 1 --verify
-      for P in 4 2 1; do
-        DMLP_HOST_OPS_PARTS=$P step parts_$P 300 python bench.py --steps 100 --warmup 10
-      done ;;
     split)
       for q in 131072 65536 32768; do
         step split_$q 240 rocprofv3 --kernel-trace --stats -d "$OUT/split_$q" -o run --output-format csv \
