@@ -24,7 +24,6 @@ is_initialized = _d.is_initialized
 get_rank = _d.get_rank
 get_world_size = _d.get_world_size
 get_backend = _d.get_backend
-new_group = _d.new_group
 destroy_process_group = _d.destroy_process_group
 broadcast_object_list = _d.broadcast_object_list
 
@@ -54,13 +53,25 @@ def coll_log():
     return list(_LOG or [])
 
 
+# sub-groups by creation order: dist.new_group is collective (every rank creates every group in
+# the same order), so the index is the same on every rank, unlike id(group)
+_GROUPS = {}
+
+
+def new_group(ranks=None, **kw):
+    g = _d.new_group(ranks, **kw)
+    _GROUPS[id(g)] = (len(_GROUPS), tuple(ranks) if ranks is not None else None)
+    return g
+
+
 def _members(group):
     if group is None or not _d.is_initialized():
         return None  # the world
     try:
         return tuple(_d.get_process_group_ranks(group))
     except Exception:  # noqa: BLE001 - older torch: no rank listing
-        return ("group", id(group))
+        idx, ranks = _GROUPS.get(id(group), (-1, None))
+        return ranks if ranks is not None else ("group", idx)
 
 
 def _rec(op, t, group=None, peer=None, nbytes=None):
@@ -227,12 +238,15 @@ def send(t, dst, group=None):
 
 
 def recv(t, src=None, group=None):
-    _rec("recv", t, None, peer=src)
+    # logged with the rank the message really came from (src=None receives from any rank: its
+    # pair must match the sender's (sender, me) entry)
     if not staged(t):
-        return _d.recv(t, src, group=group)
-    h = torch.empty(t.shape, dtype=t.dtype)
-    r = _d.recv(h, src, group=group)
-    t.copy_(h)
+        r = _d.recv(t, src, group=group)
+    else:
+        h = torch.empty(t.shape, dtype=t.dtype)
+        r = _d.recv(h, src, group=group)
+        t.copy_(h)
+    _rec("recv", t, None, peer=src if src is not None else r)
     return r
 
 
