@@ -250,7 +250,7 @@ int64_t digits_sum(int64_t a, int64_t b) {
 // ---------------------------------------------------------------- per-device workspace
 enum { M_ENTER, M_OPS, M_DATA, M_ROWS, M_SCREEN, M_REFINE, M_FORMAT, M_D2H, M_N };
 const char* const kMarkNames[M_N] = {"enter", "operands_landed", "data_landed", "rows_landed",
-                                     "screen_queued", "knn_done", "format_done",
+                                     "screen_done", "knn_done", "format_done",
                                      "report_d2h_done"};
 
 struct Ctx {
@@ -871,6 +871,8 @@ struct Step {
       L.rows = w.ev_rows;
       if (rows_pending) {
         L.issue_rows = [&]() {
+          // (called right after the first screen launch: this mark completes when it does)
+          CK(mark(M_SCREEN, st));
           if (with_hx && hx.rdy) {
             // the dataset image behind the queries, slice by slice, each followed by its ready
             // word (the running screen waits on it); every word is written even when a slice is
@@ -904,7 +906,6 @@ struct Step {
       a->early = 0;
       Lp = run_local(false, false);
     }
-    CK(mark(M_SCREEN, st));
     // ---- the report behind the re-rank, then the one host sync
     int* small = w.small_h.get(8);
     auto render = [&]() {
