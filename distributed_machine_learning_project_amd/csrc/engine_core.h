@@ -568,6 +568,13 @@ class KnnCore {
     ++step_calls_;
     last_step_ = a;
     trace.mark("step");
+    if (trace.on) {
+      int64_t st[4];
+      dmlp_pipeline_stats(st);
+      std::fprintf(stderr, "[dmlp-step] rank %d path %d early %d escalated %d exact %lld "
+                   "early_waits %d early_timeouts %d\n", rt_.rank, a.path, a.early,
+                   a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts);
+    }
     return a;
   }
 

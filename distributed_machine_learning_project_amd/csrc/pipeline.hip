@@ -198,7 +198,16 @@ struct Tuning {
   int x1k = 1;
   int host_ops = 1;
 };
-Tuning g_tune;
+Tuning make_tuning() {
+  Tuning t;
+  // environment defaults (A/B runs of the binaries): KNN_SCREEN=stream|lds, KNN_X1K=0
+  if (const char* e = std::getenv("KNN_SCREEN"))
+    t.screen = std::string(e) == "stream" ? 1 : std::string(e) == "lds" ? 2 : 0;
+  if (env_off("KNN_X1K") || env_off("DMLP_X1K")) t.x1k = 0;
+  if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
+  return t;
+}
+Tuning g_tune = make_tuning();
 // what the last call did (dmlp_pipeline_stats)
 struct Stats {
   int64_t n_exact = 0, n_escalated = 0, path = 0, early = 0;

@@ -240,11 +240,15 @@ def test_fast_path_serves_any_k_and_escalates_per_query(tmp_path):
     out, err = _run(["--strategy", "farm"], path, env={"KNN_TRACE": "1"})
     assert out == dmlp.format_report(cs)
     phases = [l.split()[3] for l in err.splitlines() if l.startswith("[dmlp-trace]")]
-    assert "h2d_operands" in phases and "knn" in phases, phases  # the fast path, not "compute"
-    assert "distribute" not in phases
-    # k > 32 on the single-term LDS screen (KNN_X1K=0) and on the 3-term one only (A/B paths of
-    # the default two-pass x1 screen): the same bytes
-    for env in ({"KNN_X1K": "0"}, {"KNN_X1K": "0", "KNN_LDS_SINGLE": "0"}):
+    assert "step" in phases, phases  # the library's native step, not the general farm
+    assert "distribute" not in phases and "compute" not in phases
+    st = [l.split() for l in err.splitlines() if l.startswith("[dmlp-step]")][0]
+    assert st[st.index("path") + 1] == "0"            # host-rendered operands
+    assert int(st[st.index("escalated") + 1]) >= 1    # the tied query escalated alone
+    # k > 32 on the 3-term LDS screen over the device image instead of the default two-pass
+    # single-term screen (KNN_X1K=0), and the 3-term streaming first screen (KNN_SCREEN=stream):
+    # the same bytes
+    for env in ({"KNN_X1K": "0"}, {"KNN_SCREEN": "stream"}):
         out, _ = _run(["--strategy", "farm"], path, env=env)
         assert out == dmlp.format_report(cs)
 
