@@ -453,15 +453,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
         if (lane == 0) { atomicAdd(&g_x1_dbg[1], 1ull);                                         \
                          atomicAdd(&g_x1_dbg[2], (unsigned long long)np_); }                    \
       }                                                                                         \
-      /* branch-free: every lane writes its entry to the next free slot and advances only on  \
-         a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
       unsigned gl_ = (unsigned)((J) * 4 + kg);                                                  \
       asm volatile("" : "+v"(gl_)); /* one VGPR: each key is a single v_and_or / v_bfi */       \
+      if (MODE & 256) {                                                                         \
+        /* per tile, only the lanes that hit (exec-masked) store and advance: ~1/64 of the     \
+           lane-tiles of a taken step hit (215 appends per query over 6250 steps), so the      \
+           branch-free form spent most of its VALU on misses */                                 \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                     \
+          if (hit_[ct]) {                                                                       \
+            *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                   \
+                (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                  \
+            addr[ct] += 16u;                                                                    \
+          }                                                                                     \
+          trig |= __ballot(addr[ct] > lim[ct]);                                                 \
+        }                                                                                       \
+      } else {                                                                                  \
+      /* branch-free: every lane writes its entry to the next free slot and advances only on  \
+         a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */     \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
         *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                       \
             (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                      \
         addr[ct] += hit_[ct] ? 16u : 0u;                                                        \
         trig |= __ballot(addr[ct] > lim[ct]);                                                   \
+      }                                                                                         \
       }                                                                                         \
     }                                                                                           \
   } while (0)
@@ -638,6 +652,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 32: DMLP_X1_LAUNCH(32); break;
       case 64: DMLP_X1_LAUNCH(64); break;
       case 128: DMLP_X1_LAUNCH(128); break;
+      case 256: DMLP_X1_LAUNCH(256); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }
