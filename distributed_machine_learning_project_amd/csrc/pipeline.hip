@@ -10,8 +10,8 @@
 //
 //   dmlp_knn_local  rows already on the device (the sharded strategies' shards, the ring's
 //                   travelling shards, the out-of-core chunks): per-query classes
-//                     1 <= k <= 32         single-term MFMA screen (screen_x1.hip) + group refine
-//                     32 < k <= 256        3-term LDS screen (screen.hip) + refine
+//                     1 <= k <= 64         single-term MFMA screen (screen_x1.hip) + group refine
+//                     64 < k <= 256        3-term LDS screen (screen.hip) + refine
 //                     k > 256, A > 256     exact fp64 paths (exact.hip / fallback.hip)
 //                   on a device-rendered bf16 image (prep.hip); a query whose screen candidates
 //                   overflow escalates alone (3-term screen, then exact).
@@ -21,13 +21,13 @@
 //                   renders the single-term screen's fp16 operands (host_prep.cpp) and copies them
 //                   on a side stream; the screen starts on them while the fp64 rows (lossless
 //                   int32 when every value is a 6-decimal number) cross PCIe behind it; k in
-//                   (32, 256] takes the two-pass single-term screen on the same operands; then
+//                   (64, 256] takes the two-pass single-term screen on the same operands; then
 //                   exact re-rank + vote + FNV checksum, the report text rendered on the GPU and
 //                   copied into the caller's page-locked buffer (or kept on the device for a
 //                   multi-rank egress, dmlp_step_emit).  One host sync in the common case; an
 //                   overflowed query escalates natively (no call is ever re-run elsewhere).
 //
-// Early start (dmlp_step, every k in [1, 32], one screen slice): the query operands cross first
+// Early start (dmlp_step, every k in [1, 64], one screen slice): the query operands cross first
 // and the screen starts on them while the dataset image follows in slices, each with a ready word
 // the screen waits on (screen_x1.hip k_screen_x1 rdy): the wait is bounded by elapsed time, its
 // waits / eps growths / timeouts are counted on the device and returned in dmlp_step_args, and
@@ -603,16 +603,17 @@ struct Local {
     x1_ok = dmlp_screen_x1_qw(KT) > 0 && !exact;
     const bool screen = (lds_ok || x1_ok) && N > 0;
     all_a = screen && x1_ok;
+    const int ka = dmlp_screen_x1_kmax();  // the single-term one-pass class: k <= 64
     for (int64_t q = 0; q < Q; ++q) {
       kk[q] = (int)std::min<int64_t>(k_host[q], N);
-      all_a = all_a && k_host[q] >= 1 && k_host[q] <= 32 && k_host[q] <= N;
+      all_a = all_a && k_host[q] >= 1 && k_host[q] <= ka && k_host[q] <= N;
     }
     for (int64_t q = 0; q < Q && !all_a; ++q) {
       if (kk[q] < 1) {
         rest.push_back((int)q);
         continue;
       }
-      if (screen && kk[q] <= 32 && x1_ok) a.push_back((int)q);
+      if (screen && kk[q] <= ka && x1_ok) a.push_back((int)q);
       else if (screen && lds_ok && kk[q] <= 128) b.push_back((int)q);
       else if (screen && lds_ok && kk[q] <= 256) c.push_back((int)q);
       else f.push_back((int)q);
@@ -661,11 +662,14 @@ struct Local {
     CK(hipStreamSynchronize(st));
     std::vector<int> esc, esc_bc, fq;
     const bool stream_ok = dmlp_screen_stream_qw(KT) > 0 && stream_screen_on();
+    const int ka = dmlp_screen_x1_kmax(), ks = dmlp_screen_stream_kmax();
     for (int64_t q = 0; q < Q; ++q) {
       if (!sh[q]) continue;
-      // a single-term screen's overflow escalates to a 3-term screen; a 3-term screen's goes exact
-      if (kk[q] <= 32 && first_a == 0 && (stream_ok || lds_ok)) esc.push_back((int)q);
-      else if (kk[q] > 32 && kk[q] <= 256 && bc_single) esc_bc.push_back((int)q);
+      // a single-term screen's overflow escalates to a 3-term screen (the streaming one for
+      // k <= 32, the LDS one above); a 3-term screen's goes exact
+      const bool single = (kk[q] <= ka && first_a == 0) || (kk[q] > ka && kk[q] <= 256 && bc_single);
+      if (single && kk[q] <= ks && stream_ok) esc.push_back((int)q);
+      else if (single && lds_ok) esc_bc.push_back((int)q);
       else fq.push_back((int)q);
     }
     // a 3-term screen's own overflow goes to the exact path (escalated twice: no third screen)
@@ -676,7 +680,7 @@ struct Local {
       for (int q : esc_bc) CK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
       const HostOps* keep = hx;
       hx = nullptr;  // the 3-term screens run on the device image
-      if (!esc.empty()) pass(&esc, stream_ok ? 1 : 2, w.qidx_e, w.le_h);
+      if (!esc.empty()) pass(&esc, 1, w.qidx_e, w.le_h);
       if (!esc_bc.empty()) pass(&esc_bc, 2, w.qidx_e2, w.le2_h);
       hx = keep;
       int n2 = 0;
@@ -794,7 +798,7 @@ struct Step {
     }
     const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
                           g_tune.host_ops && g_tune.screen == 0 && !env_off("DMLP_HOST_OPS");
-    const bool all_a = kmin >= 1 && kmax <= 32 && kmax <= N;
+    const bool all_a = kmin >= 1 && kmax <= dmlp_screen_x1_kmax() && kmax <= N;
     // KT <= 4 only: the early screen's waves spin while the image copies land, and on this
     // runtime host->device copies are blit KERNELS that need a free wave slot beside them.  The
     // KT <= 4 variants leave registers for one (KT 1: 211 VGPRs x 2 waves/SIMD, KT 4 / k <= 32:

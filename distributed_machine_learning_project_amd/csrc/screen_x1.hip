@@ -692,7 +692,9 @@ extern "C" void dmlp_screen_x1_bound(int A, float* r1, float* r2) {
   float r3;
   dmlp_screen_x1_bound2(A, 2, r1, r2, &r3);
 }
-extern "C" int dmlp_screen_x1_kmax(void) { return 32; }
+// k <= 64 on one pass: the SUB = 32 buffers keep up to 120 group entries per column after a
+// compaction (k + the 2 eps slack), and the group refine ranks up to 64 (KMAX) of <= 128 members
+extern "C" int dmlp_screen_x1_kmax(void) { return 64; }
 static bool x1_kt_ok(int KT) { return KT == 1 || KT == 2 || KT == 4 || KT == 8; }
 extern "C" int dmlp_screen_x1_qw(int KT) { return x1_kt_ok(KT) ? 64 : 0; }
 // queries per wave (= workgroup) of the variant that serves kmax
@@ -795,7 +797,7 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
   if (nq <= 0) return 0;
   if (S < 1 || n_tiles < 0 || n_tiles > 0x7fffffff / 64 || n_points > n_tiles * 64) return -1;
   if ((n_tiles + S - 1) / S > 4096) return -4;  // 16-bit group index per slice
-  if (kmax > 32 || !x1_kt_ok(KT) || A > KT * 32) return -3;
+  if (kmax > 64 || !x1_kt_ok(KT) || A > KT * 32) return -3;
   if (hl != 1 && hl != 2) return -1;
   float r1, r2, r3;
   dmlp_screen_x1_bound2(A, hl, &r1, &r2, &r3);
@@ -845,7 +847,7 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
   if (n_tiles < 1 || n_tiles > 4096 || n_points > n_tiles * 64 || !rdy || !xnm_sl ||
       rdy_tiles < 1 || rdy_n < 1 || (int64_t)rdy_tiles * rdy_n < n_tiles)
     return -1;
-  if (kmax > 32 || !x1_kt_ok(KT) || A > KT * 32) return -3;
+  if (kmax > 64 || !x1_kt_ok(KT) || A > KT * 32) return -3;
   float r1, r2, r3;
   dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
   hipStream_t st = (hipStream_t)stream;

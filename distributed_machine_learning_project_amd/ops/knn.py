@@ -3,7 +3,7 @@
 GPU: libdmlp's ONE native pipeline (csrc/pipeline.hip), which the standalone knn_engine and the
 engine.h drop-in run as well — no part of a call is orchestrated from Python:
   knn_gpu  (dmlp_knn_local)  rows already on the device (shards, ring shards, out-of-core chunks):
-           per-query classes — single-term MFMA screen (k <= 32), 3-term LDS screen (k <= 256),
+           per-query classes — single-term MFMA screen (k <= 64), 3-term LDS screen (k <= 256),
            exact fp64 (k > 256, A > 256) — a device-rendered bf16 image, exact re-rank (reference
            order, no FMA), per-query escalation of overflowed screens, fused vote + FNV checksum
   step     (dmlp_step)       one rank's whole Engine::KNN call from host rows: the host renders
@@ -27,7 +27,7 @@ import numpy as np
 
 from .. import _lib
 
-SCREEN_KMAX_A = 32      # single-term screen class
+SCREEN_KMAX_A = 64      # single-term one-pass screen class
 SCREEN_KMAX_B = 128     # 3-term cap-256 class
 SCREEN_KMAX_C = 256     # 3-term cap-512 class: larger k take the exact path
 SCREEN_MAX_KT = 8       # A <= 256 on the screens

@@ -55,11 +55,11 @@ def test_shared_ingress_and_out_of_core(gpu, workload, monkeypatch, max_rows):
     eng.close()
 
 
-@pytest.mark.parametrize("kmax,A", [(32, 32), (24, 32), (40, 32), (200, 32), (16, 100)])
+@pytest.mark.parametrize("kmax,A", [(32, 32), (24, 32), (40, 32), (64, 32), (200, 32), (16, 100)])
 def test_native_step(gpu, kmax, A):
     """One rank over the node-shared segment: the whole call runs in libdmlp's native step
-    (pipeline.hip dmlp_step) for EVERY k — k <= 32 on the single-term screen, k in (32, 256] on
-    the two-pass single-term screen — report, labels and checksums == the oracle's, three calls in
+    (pipeline.hip dmlp_step) for EVERY k — k <= 64 on the one-pass single-term screen, k in
+    (64, 256] on the two-pass single-term screen — report, labels and checksums == the oracle's, three calls in
     a row (reused buffers), each served by the step."""
     from distributed_machine_learning_project_amd.utils.shm import share_input
     inp = dmlp.generate(7000, 9000 + kmax, A, 0.0, 1000.0, 1, kmax, 8, seed=kmax + A)

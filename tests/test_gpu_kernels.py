@@ -177,9 +177,9 @@ def test_screen_impls_bench_distribution(torch_cuda, impl):
     assert_same(r, refs)
 
 
-@pytest.mark.parametrize("A,kmax", [(8, 16), (32, 32), (64, 16), (40, 30)])
+@pytest.mark.parametrize("A,kmax", [(8, 16), (32, 32), (64, 16), (40, 30), (32, 64), (20, 48)])
 def test_x1_screen_shapes(torch_cuda, A, kmax):
-    """Single-term screen: KT 1/2, both sub-buffer depths (k <= 16 / <= 32), ragged tails."""
+    """Single-term screen: KT 1/2, both sub-buffer depths (k <= 16 / <= 64), ragged tails."""
     inp = dmlp.generate(7777, 333, A, -100.0, 100.0, 1, kmax, 6, seed=A + kmax)
     r, refs = run_both(torch_cuda, inp)
     assert r.n_fallback == 0
@@ -560,3 +560,30 @@ def test_step_front_cases(torch_cuda, case):
     np.testing.assert_array_equal(d.cpu().numpy(), d_ref)
     np.testing.assert_array_equal(lab.cpu().numpy(), lab_ref)
     np.testing.assert_array_equal(cs.cpu().numpy().view(np.uint64), cs_ref)
+
+
+@pytest.mark.parametrize("A", [32, 100])
+def test_step_mixed_k_one_pass(torch_cuda, A):
+    """The generator's k distribution (minK = 1, maxK = 64: generate_input.py:19) screened in ONE
+    single-term pass with per-column k (no class split, no second scan), one query sitting on
+    600 duplicate points (its candidates overflow the single-term bound: it alone escalates
+    inside the native step) — report, labels, checksums == the oracle's, served by the step."""
+    torch = torch_cuda
+    rng = np.random.default_rng(A)
+    N, Q = 9000, 4000
+    X = np.round(rng.uniform(0, 1000, (N, A)), 6)
+    X[:600] = X[0]
+    Qx = np.round(rng.uniform(0, 1000, (Q, A)), 6)
+    Qx[11] = X[0]
+    k = rng.integers(1, 65, Q).astype(np.int32)
+    k[11] = 40
+    labels = rng.integers(0, 6, N).astype(np.int32)
+    _, i_ref = K.knn_cpu(X, Qx, k)
+    lab_ref, cs_ref = K.finalize_cpu(i_ref, k, labels)
+    dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
+    n0 = K.STEP_STATS["calls"]
+    r = K.step(X, labels, (0, 6), Qx, k, report=dst)
+    assert K.STEP_STATS["calls"] == n0 + 1
+    assert bytes(dst[:r.report_len]) == dmlp.format_report(cs_ref)
+    np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+    assert r.path == 0 and r.n_escalated >= 1
