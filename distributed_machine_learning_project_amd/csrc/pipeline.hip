@@ -240,10 +240,16 @@ int slices_lds(int nq, int waves, int64_t n_tiles) {
   while ((int64_t)nqb * S < 2 * g_tune.num_cus && S * 2 <= std::max<int64_t>(1, n_tiles) && S < 256) S *= 2;
   return S;
 }
-// data slices of the single-term x1 pass over nq queries of class bound kcls
+// data slices of the single-term x1 pass over nq queries of class bound kcls.  Every (query,
+// slice) keeps its slice's own top-k groups (all k may sit in one slice) in <= 120 entries, so a
+// slice must hold many more groups than k: for k > 32 at least 32 k points per slice (a slice of
+// a few hundred groups would keep most of them within 2 eps of its k-th key and overflow)
 int x1_slices(int nq, int KT, int kcls, int64_t nt) {
-  return slices_stream(nq, dmlp_screen_x1_cols(KT, kcls), nt,
-                       dmlp_screen_x1_waves_per_cu_kt(KT, kcls), dmlp_screen_x1_min_slices(nt));
+  const int64_t smin = dmlp_screen_x1_min_slices(nt);
+  int S = slices_stream(nq, dmlp_screen_x1_cols(KT, kcls), nt,
+                        dmlp_screen_x1_waves_per_cu_kt(KT, kcls), smin);
+  if (kcls > 32) S = (int)std::max<int64_t>(smin, std::min<int64_t>(S, nt * 64 / (32 * kcls)));
+  return std::max(S, 1);
 }
 
 // sum of the decimal digit counts of v over [a, b)
@@ -955,7 +961,6 @@ struct Step {
     const int novf = small[0];
     if (novf) {
       a->n_escalated = Lp->finish(novf);
-      a->path = 1;
       w.marks_valid = false;
       render();
       CK(hipStreamSynchronize(st));
