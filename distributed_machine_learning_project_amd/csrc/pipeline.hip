@@ -614,12 +614,20 @@ struct Local {
       kk[q] = (int)std::min<int64_t>(k_host[q], N);
       all_a = all_a && k_host[q] >= 1 && k_host[q] <= ka && k_host[q] <= N;
     }
+    // the first screen of class a: the single-term one (k <= 64), or on the device image the
+    // 3-term streaming screen (k <= 32; the A/B switch "screen") or LDS screen
+    first_a = hx || g_tune.screen == 0 ? 0
+              : g_tune.screen == 1 && dmlp_screen_stream_qw(KT) > 0 ? 1 : 2;
+    const int ka_eff = first_a == 0 ? ka : first_a == 1 ? dmlp_screen_stream_kmax() : 32;
+    if (ka_eff < ka) {
+      for (int64_t q = 0; q < Q && all_a; ++q) all_a = k_host[q] <= ka_eff;
+    }
     for (int64_t q = 0; q < Q && !all_a; ++q) {
       if (kk[q] < 1) {
         rest.push_back((int)q);
         continue;
       }
-      if (screen && kk[q] <= ka && x1_ok) a.push_back((int)q);
+      if (screen && kk[q] <= ka_eff && x1_ok) a.push_back((int)q);
       else if (screen && lds_ok && kk[q] <= 128) b.push_back((int)q);
       else if (screen && lds_ok && kk[q] <= 256) c.push_back((int)q);
       else f.push_back((int)q);
@@ -636,8 +644,6 @@ struct Local {
     if (!all_a || !hx) fill();
     if (all_a || !a.empty() || !b.empty() || !c.empty()) {
       if (!hx) need_dev();  // the device operands of every screen
-      first_a = hx || g_tune.screen == 0 ? 0
-                : g_tune.screen == 1 && dmlp_screen_stream_qw(KT) > 0 ? 1 : 2;
       if (all_a || !a.empty()) pass(all_a ? nullptr : &a, first_a, w.qidx_a, w.la_h);
       if (!b.empty() || !c.empty()) {
         bc_single = hx && x1_ok && g_tune.x1k;
@@ -923,6 +929,7 @@ struct Step {
       CK(hipStreamSynchronize(w.side));
       CK(hipStreamSynchronize(st));
       a->early = 0;
+      use_hx = false;
       Lp = run_local(false, false);
     }
     // ---- the report behind the re-rank, then the one host sync
