@@ -274,6 +274,7 @@ struct Ctx {
   hipEvent_t ev_ops = nullptr, ev_rows = nullptr;
   bool marks_on = false, marks_valid = false;
   hipEvent_t marks[M_N] = {};
+  unsigned marks_rec = 0;  // marks recorded in the last call (a path may skip some)
   // Local: device image, query fragments, candidates, class lists, exact workspace
   DBuf<double> mu;
   DBuf<char> xfrag;
@@ -725,7 +726,9 @@ struct Step {
   explicit Step(Ctx& c_, dmlp_step_args* a_) : w(c_), a(a_), st((hipStream_t)a_->stream) {}
 
   hipError_t mark(int i, hipStream_t s) {
-    return w.marks_on ? hipEventRecord(w.marks[i], s) : hipSuccess;
+    if (!w.marks_on) return hipSuccess;
+    w.marks_rec |= 1u << i;
+    return hipEventRecord(w.marks[i], s);
   }
 
   // labels + fp64 rows (X, then Qx) on the side stream: lossless int32 when every value is a
@@ -774,6 +777,7 @@ struct Step {
     a->n_escalated = 0;
     a->early_waits = a->early_grows = a->early_timeouts = 0;
     w.marks_valid = false;
+    w.marks_rec = 0;
     if (Q < 0 || N < 0 || A < 1 || Q > (1 << 30)) return -1;
     if ((a->X == nullptr && a->Xr == nullptr && N > 0) || (a->Qx == nullptr && a->Qr == nullptr && Q > 0) ||
         (Q > 0 && !a->k))
@@ -1150,8 +1154,12 @@ extern "C" int dmlp_step_timeline(double* ms, const char** names, int cap) {
     if (!w.marks_valid) return 0;
     int n = 0;
     for (int i = 0; i < M_N && n < cap; ++i) {
+      if (!(w.marks_rec & (1u << i))) continue;  // (never recorded: would leave a sticky error)
       float t = 0.0f;
-      if (hipEventElapsedTime(&t, w.marks[M_ENTER], w.marks[i]) != hipSuccess) continue;
+      if (hipEventElapsedTime(&t, w.marks[M_ENTER], w.marks[i]) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
       ms[n] = t;
       names[n] = kMarkNames[i];
       ++n;
