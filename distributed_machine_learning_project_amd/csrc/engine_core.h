@@ -227,7 +227,6 @@ class KnnCore {
   // KNN_FAST=0 disables the single-GPU host-operand pipeline (A/B against the device path)
   bool fast_ = !(getenv("KNN_FAST") && std::string(getenv("KNN_FAST")) == "0");
   // host render + H2D of the screen operands in pipelined slices (the Python default too)
-  int host_slices_ = getenv("KNN_HOST_OPS_CHUNKS") ? std::max(1, std::atoi(getenv("KNN_HOST_OPS_CHUNKS"))) : 2;
   MPI_Win ctr_win_ = MPI_WIN_NULL;
   int64_t* ctr_base_ = nullptr;
   DevBuf<int64_t> res_;

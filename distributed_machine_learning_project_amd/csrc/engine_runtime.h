@@ -167,6 +167,13 @@ struct Runtime {
     if (ndev == 0) throw std::runtime_error("no HIP device");
     device = local % ndev;
     HIPCHK(hipSetDevice(device));
+    // ranks of this node on the same GPU (a host-plane rehearsal): the native step's early start
+    // stays off for them (pipeline.hip early_on; profiles/r7h_host_budget.md)
+    {
+      int same = 0;
+      for (int r = 0; r < local_world; ++r) same += r % ndev == device;
+      setenv("DMLP_DEVICE_RANKS", std::to_string(std::max(1, same)).c_str(), 1);
+    }
     numa = bind_numa(device, local_world, ndev);  // before the arenas: pages land next to the GPU
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     reserve_arenas();

@@ -151,11 +151,17 @@ int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e && *e ? std::atoi(e) : dflt;
 }
-// early start of dmlp_step (DMLP_FAST_EARLY=0: off; dmlp_step_early); off for the rest of the
-// process after a wait timed out
+// early start of dmlp_step (DMLP_FAST_EARLY=0: off, =1: on; dmlp_step_early); off for the rest
+// of the process after a wait timed out.  Default: on, unless several ranks share this GPU
+// (DMLP_DEVICE_RANKS > 1, set by both front ends): one rank's screen spinning on its slices
+// then holds the CUs the other ranks' copies need — P = 3 on one MI355X measured 20.8 ms/step
+// with it against 7.3 ms without (profiles/r7h_host_budget.md).
 int g_early = -1;
 bool early_on() {
-  if (g_early < 0) g_early = env_off("DMLP_FAST_EARLY") ? 0 : 1;
+  if (g_early < 0) {
+    const char* e = std::getenv("DMLP_FAST_EARLY");
+    g_early = e && *e ? (std::string(e) != "0") : env_int("DMLP_DEVICE_RANKS", 1) <= 1;
+  }
   return g_early != 0;
 }
 constexpr int kEarlySlices = 8;  // dataset image slices behind the query operands (profiles/r6f)
@@ -191,7 +197,7 @@ bool stream_screen_on() {
 // wide slices), the first screen of the k <= 32 class on the device image (0 single-term, 1 3-term
 // streaming, 2 3-term LDS), the two-pass single-term screen for k in (32, 256] on the host
 // operands (0: the 3-term LDS screen on the device image), the host-rendered operands (0: the
-// device image path for every step).
+// device image path for every step, 1: when the render pool has >= 2 threads, 2: always).
 struct Tuning {
   int num_cus = 256;
   int screen = 0;
@@ -204,7 +210,12 @@ Tuning make_tuning() {
   if (const char* e = std::getenv("KNN_SCREEN"))
     t.screen = std::string(e) == "stream" ? 1 : std::string(e) == "lds" ? 2 : 0;
   if (env_off("KNN_X1K") || env_off("DMLP_X1K")) t.x1k = 0;
+  // DMLP_HOST_OPS=0: the device path; =1: the host operands whatever the pool size; unset: the
+  // host operands when the render pool has at least 2 threads (Step::run: with 1 the device path
+  // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
+  // 3.74: profiles/r7h_host_budget.md)
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
+  else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
 }
 Tuning g_tune = make_tuning();
@@ -813,7 +824,8 @@ struct Step {
       return 0;
     }
     const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
-                          g_tune.host_ops && g_tune.screen == 0 && !env_off("DMLP_HOST_OPS");
+                          g_tune.screen == 0 &&
+                          (g_tune.host_ops >= 2 || (g_tune.host_ops == 1 && dmlp_host_threads() >= 2));
     const bool all_a = kmin >= 1 && kmax <= dmlp_screen_x1_kmax() && kmax <= N;
     // KT <= 4 only: the early screen's waves spin while the image copies land, and on this
     // runtime host->device copies are blit KERNELS that need a free wave slot beside them.  The
@@ -900,8 +912,9 @@ struct Step {
       L.rows = w.ev_rows;
       if (rows_pending) {
         L.issue_rows = [&]() {
-          // (called right after the first screen launch: this mark completes when it does)
-          CK(mark(M_SCREEN, st));
+          // (host operands: called right after the first screen launch, so this mark completes
+          // when it does; the device path calls it before its image is built: no mark)
+          if (with_hx) CK(mark(M_SCREEN, st));
           if (with_hx && hx.rdy) {
             // the dataset image behind the queries, slice by slice, each followed by its ready
             // word (the running screen waits on it); every word is written even when a slice is

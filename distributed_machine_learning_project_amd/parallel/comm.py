@@ -145,6 +145,11 @@ class Comm:
         if use_gpu:
             ndev = torch.cuda.device_count()
             torch.cuda.set_device(local_rank % max(1, ndev))
+            # ranks of this node on the same GPU (DMLP_DATA_PLANE=host rehearsals): the native
+            # step's early start stays off for them (csrc/pipeline.hip early_on)
+            lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            same = sum(1 for r in range(max(1, lw)) if r % max(1, ndev) == local_rank % max(1, ndev))
+            os.environ["DMLP_DEVICE_RANKS"] = str(max(1, same))
             dev = torch.device("cuda", torch.cuda.current_device())
             Comm._numa = Comm.bind_numa(dev.index, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
         else:

@@ -141,3 +141,62 @@ def test_debug_listing(gpu, workload):
     lab, _ = K.finalize_cpu(i, inp.k, inp.labels)
     assert bytes(eng.report(out)) == dmlp.format_debug(d, i, inp.k, lab)
     eng.close()
+
+
+_POLICY_CHILD = r"""
+import sys
+import numpy as np
+import distributed_machine_learning_project_amd as dmlp
+from distributed_machine_learning_project_amd import _lib
+from distributed_machine_learning_project_amd.ops import knn as K
+inp = dmlp.generate(3000, 4096, 32, 0.0, 1000.0, 1, 16, 8, seed=5)
+_, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+_, cs = K.finalize_cpu(i, inp.k, inp.labels)
+r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report="device")
+ok = np.array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
+print("POLICY", _lib.lib().dmlp_host_threads(), r.path, int(ok))
+"""
+
+
+def test_step_policy_host_budget_and_shared_device(gpu, monkeypatch):
+    """The step's automatic choices (profiles/r7h_host_budget.md): (1) ranks sharing one GPU
+    (DMLP_DEVICE_RANKS > 1, set by Comm.init / knn_engine) run without the early start, which
+    made P = 3 on one MI355X 2.8x slower; DMLP_FAST_EARLY=1 still forces it.  (2) A render pool
+    of one thread takes the device-image path (measured faster there); DMLP_HOST_OPS=1 forces the
+    host operands.  Results == the oracle's either way."""
+    import os
+    import subprocess
+    import sys
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    (inp, lab_ref, cs, expect), _ = _early_inputs(2000, 32, 16, 131072 + 64, seed=77)
+    import torch
+    dst = torch.empty(48 * len(inp.k) + 64, dtype=torch.uint8).pin_memory().numpy()
+    monkeypatch.delenv("DMLP_FAST_EARLY", raising=False)
+    try:
+        for ranks, force, want in (("2", None, 0), ("1", None, 1), ("3", "1", 1)):
+            monkeypatch.setenv("DMLP_DEVICE_RANKS", ranks)
+            if force:
+                monkeypatch.setenv("DMLP_FAST_EARLY", force)
+            L.dmlp_step_early(-1)  # re-read the environment
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert bytes(dst[:r.report_len]) == expect
+            assert r.early == want, (ranks, force)
+    finally:
+        monkeypatch.delenv("DMLP_DEVICE_RANKS", raising=False)
+        monkeypatch.delenv("DMLP_FAST_EARLY", raising=False)
+        L.dmlp_step_early(-1)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for env, want_path in (({"DMLP_HOST_THREADS": "1"}, 2),
+                           ({"DMLP_HOST_THREADS": "1", "DMLP_HOST_OPS": "1"}, 0),
+                           ({"DMLP_HOST_THREADS": "2"}, 0)):
+        e = dict(os.environ, **env)
+        e.pop("DMLP_HOST_OPS", None) if "DMLP_HOST_OPS" not in env else None
+        out = subprocess.run([sys.executable, "-c", _POLICY_CHILD], cwd=root, env=e,
+                             capture_output=True, text=True, timeout=100)
+        line = [x for x in out.stdout.splitlines() if x.startswith("POLICY")]
+        assert line, out.stderr[-2000:]
+        _, threads, path, ok = line[-1].split()
+        assert int(threads) == int(env["DMLP_HOST_THREADS"])
+        assert int(path) == want_path, env
+        assert ok == "1"
