@@ -22,6 +22,20 @@ extern "C" {
 // mu[A] = mean of the first min(N, 4096) rows (centering offset for the screen; any value is
 // correct, a good one only tightens the screen).
 int dmlp_center(const double* X, int64_t N, int A, double* mu, void* stream);
+// The exact path's fp64 MFMA screen (screen_f64.hip) + exact group re-rank: k <= 64, A <= 32,
+// results bit-identical to dmlp_exact_topk; overflowing queries get status[q] = 1 (nothing
+// written) and are counted into *ovf_count (device).  ws: dmlp_exact_f64_bytes bytes.
+int dmlp_exact_f64_amax(void);
+int dmlp_exact_f64_kmax(void);
+int64_t dmlp_exact_f64_bytes(int64_t N, int A, int nq, int kmax);
+int dmlp_exact_f64(const double* X, int64_t N, int A, const double* Qx, const int* qidx,
+                   const int* qk, int nq, int kmax, double* out_d, int* out_i, int kstride,
+                   int* status, int* ovf_count, void* ws, int64_t ws_bytes, void* stream);
+int dmlp_refine_groups_exact(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
+                             int S, int64_t tiles_per_slice, const double* X, int A,
+                             const double* Qx, int64_t n_points, const int* qidx, const int* qk,
+                             int nq, double* out_d, int* out_i, int kstride, int* status,
+                             int* ovf_count, void* stream);
 
 // X [N][A] fp64 -> fragment-native bf16 hi/lo tiles (64 points x 32*KT attrs per tile),
 // xinit[n_tiles*64] = -(|x-mu|^2)/2 (fp32; -inf for padding), xnmax_bits = max |x-mu|^2 (fp32
@@ -278,8 +292,9 @@ void dmlp_step_early_delay(int us);    // host sleep before each image slice (< 
 int dmlp_step_events(int on);          // hipEvent step timeline on / off
 int dmlp_step_timeline(double* ms, const char** names, int cap);
 // Tuning / A-B switches of the pipeline ("num_cus", "screen", "x1k", "host_ops"; pipeline.hip
-// Tuning): returns the previous value (-1: unknown key).  What the last call did: [0] exact-path
-// queries, [1] escalated queries, [2] path, [3] early start.
+// Tuning): returns the previous value (-1: unknown key).  What the last call did (6 slots): [0]
+// exact-path queries, [1] escalated queries, [2] path, [3] early start, [4] exact-path queries on
+// the fp64 MFMA screen, [5] of those handed to the fused VALU kernel (overflow).
 int dmlp_pipeline_set(const char* key, int value);
 void dmlp_pipeline_stats(int64_t* out);
 

@@ -568,7 +568,7 @@ class KnnCore {
     last_step_ = a;
     trace.mark("step");
     if (trace.on) {
-      int64_t st[4];
+      int64_t st[6];
       dmlp_pipeline_stats(st);
       std::fprintf(stderr, "[dmlp-step] rank %d path %d early %d escalated %d exact %lld "
                    "early_waits %d early_timeouts %d\n", rt_.rank, a.path, a.early,

@@ -222,6 +222,7 @@ Tuning g_tune = make_tuning();
 // what the last call did (dmlp_pipeline_stats)
 struct Stats {
   int64_t n_exact = 0, n_escalated = 0, path = 0, early = 0;
+  int64_t n_exact_f64 = 0, n_exact_f64_redo = 0;  // exact-path queries on the fp64 MFMA screen
 };
 Stats g_stats;
 
@@ -294,10 +295,11 @@ struct Ctx {
   DBuf<short> qhi, qlo;
   DBuf<float> qn, cand_h, k1_h, k1_seed;
   DBuf<int> qidx_a, qidx_b, qidx_c, qidx_e, qidx_e2, qidx_f, qidx_r, kdev, kfull, cand_ids,
-      cand_cnt, status, ovf, ident, k1_ids, k1_cnt, kp_d;
-  DBuf<char> fb_ws;
+      cand_cnt, status, ovf, ident, k1_ids, k1_cnt, kp_d, qidx_f2, f64_stat, f64_ovf;
+  DBuf<char> fb_ws, f64_ws;
   // page-locked staging of the per-call host lists (one per list: no copy waits for a reuse)
-  HBuf<int> kk_h, kp_h, kfull_h, ident_h, small_h, la_h, lb_h, lc_h, le_h, le2_h, lf_h, lr_h;
+  HBuf<int> kk_h, kp_h, kfull_h, ident_h, small_h, la_h, lb_h, lc_h, le_h, le2_h, lf_h, lr_h,
+      lf2_h, f64_h, f64_st_h;
   int64_t ident_len = 0;
   // dmlp_step: host-rendered operands (staging + device), rows, labels, outputs, report
   HBuf<uint16_t> sx_hi, sq_hi;
@@ -571,8 +573,49 @@ struct Local {
     CK(hipMemcpyAsync(qi, h, fq.size() * sizeof(int), hipMemcpyHostToDevice, st));
     base = 0;
     if (!fused.empty()) {
-      CKL(dmlp_exact_topk(X, N, A, Qx, qi, kd, (int)fused.size(), kfmax, out_d, out_i, kstride,
-                          st));
+      // A <= 32, 1 <= k <= 64: the fp64 MFMA screen + exact group re-rank (screen_f64.hip); its
+      // overflows (pathological ties) go to the fused VALU kernel.  DMLP_EXACT_F64=0: never.
+      int kfmin = kfmax;
+      for (int q : fused) kfmin = std::min(kfmin, kk[q]);
+      const bool f64 = !env_off("DMLP_EXACT_F64") && A <= dmlp_exact_f64_amax() && kfmin >= 1 &&
+                       kfmax <= dmlp_exact_f64_kmax();
+      std::vector<int> redo;
+      if (f64) {
+        const int64_t wb = dmlp_exact_f64_bytes(N, A, (int)fused.size(), kfmax);
+        char* fws = w.f64_ws.get(wb);
+        int* fst = w.f64_stat.get(Q);
+        int* fov = w.f64_ovf.get(1);
+        int* oh = w.f64_h.get(1);
+        CK(hipMemsetAsync(fov, 0, sizeof(int), st));
+        CKL(dmlp_exact_f64(X, N, A, Qx, qi, kd, (int)fused.size(), kfmax, out_d, out_i, kstride,
+                           fst, fov, fws, wb, st));
+        CK(hipMemcpyAsync(oh, fov, sizeof(int), hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        if (*oh > 0) {
+          int* sh = w.f64_st_h.get(Q);
+          CK(hipMemcpyAsync(sh, fst, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+          CK(hipStreamSynchronize(st));
+          for (int q : fused)
+            if (sh[q]) redo.push_back(q);
+        }
+        g_stats.n_exact_f64 += (int64_t)fused.size();
+        g_stats.n_exact_f64_redo += (int64_t)redo.size();
+      }
+      if (!f64 || !redo.empty()) {
+        const int* ql = qi;
+        int n = (int)fused.size(), km = kfmax;
+        if (f64) {
+          int* q2 = w.qidx_f2.get(redo.size());
+          int* h2 = w.lf2_h.get(redo.size());
+          std::memcpy(h2, redo.data(), redo.size() * sizeof(int));
+          CK(hipMemcpyAsync(q2, h2, redo.size() * sizeof(int), hipMemcpyHostToDevice, st));
+          ql = q2;
+          n = (int)redo.size();
+          km = 0;
+          for (int q : redo) km = std::max(km, kk[q]);
+        }
+        CKL(dmlp_exact_topk(X, N, A, Qx, ql, kd, n, km, out_d, out_i, kstride, st));
+      }
       base += fused.size();
     }
     for (int pz = 0; pz < 2; ++pz) {
@@ -614,6 +657,7 @@ struct Local {
   }
 
   void launch() {
+    g_stats.n_exact_f64 = g_stats.n_exact_f64_redo = 0;
     if (Q == 0) return;
     KT = dmlp_screen_kt(A);
     kk = w.kk_h.get(Q);
@@ -1203,4 +1247,6 @@ extern "C" void dmlp_pipeline_stats(int64_t* out) {
   out[1] = g_stats.n_escalated;
   out[2] = g_stats.path;
   out[3] = g_stats.early;
+  out[4] = g_stats.n_exact_f64;
+  out[5] = g_stats.n_exact_f64_redo;
 }

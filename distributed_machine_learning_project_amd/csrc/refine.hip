@@ -121,6 +121,8 @@ struct GroupIn {
   int tiles_per_slice;    // the screen's slicing: group base = (s * tps * 64) + 4 * index
   int collect;            // lists of the COLLECT pass (large k): the threshold is always taken
                           // over the lists (cand_h holds the fixed seed, not a final threshold)
+  int rescore = 1;        // 0 (screen_f64.hip's fp64 keys): every member of a group at or above
+                          // the threshold goes to the exact re-rank (no image to rescore from)
 };
 
 // GROUPS = KT of the single-term screen (1, 2, 4 or 8) for group-mode input, 0 otherwise.  The group
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
   float g_eps = 0.0f, g_h1 = 0.0f;
   unsigned ebuf = 0;  // S == 1: entry `lane` of the query's single slice
   if (GROUPS) {
-    if (KTG == 1) {  // (KT = 2: 32 registers held this long would spill; loaded at first use)
+    if (KTG == 1 && gin.rescore) {  // (KT = 2: 32 registers held this long would spill; loaded at first use)
 #pragma unroll
       for (int f = 0; f < KTG * 4; ++f)
         qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KTG * 4 + f]);
@@ -265,10 +267,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
     u32x4* const qs = (u32x4*)s_hist[wave];  // (the histogram is dead once hq is known)
     if constexpr (QLDS) {
       static_assert(KT * 4 * 16 <= HCAP * 4, "query fragments must fit the histogram scratch");
-      for (int f = lane; f < KT * 4; f += 64)
+      for (int f = lane; f < KT * 4 && gin.rescore; f += 64)
         qs[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
       dmlp::wave_sync();
-    } else if (KT != 1) {
+    } else if (KT != 1 && gin.rescore) {
 #pragma unroll
       for (int f = 0; f < KT * 4; ++f)
         qraw[f] = __builtin_bit_cast(u32x4, gin.qhi[(int64_t)q * KT * 4 + f]);
@@ -294,7 +296,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
       if (g < M) {
         const int lo = slice_of(g);
         id = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4 + (jm & 3);
-        if (e >= kh && id < gin.n_points) {
+        if (e >= kh && id < gin.n_points && !gin.rescore) {
+          keep = true;
+        } else if (e >= kh && id < gin.n_points) {
           const int64_t t = id >> 6;
           const int pl = id & 63;
           const u32x4* fr = gin.xfrag + t * (int64_t)(4 * KT * gin.hl * 64) + (pl & 15);
@@ -1115,6 +1119,27 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
     else DMLP_REFINE_G(8, false);
   }
 #undef DMLP_REFINE_G
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+// The exact path's fp64 screen (screen_f64.hip): group ids of 4-point groups in slices of
+// tiles_per_slice 64-point tiles, no rescoring image — every member of a group at or above the
+// global threshold is re-ranked exactly (<= 512 members, k <= 256: the E = 8 variant).  Writes
+// out_d / out_i only (no vote).
+extern "C" int dmlp_refine_groups_exact(int cap, const int* cand_ids, const int* cand_cnt,
+                                        const float* cand_h, int S, int64_t tiles_per_slice,
+                                        const double* X, int A, const double* Qx, int64_t n_points,
+                                        const int* qidx, const int* qk, int nq, double* out_d,
+                                        int* out_i, int kstride, int* status, int* ovf_count,
+                                        void* stream) {
+  if (nq <= 0) return 0;
+  if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff || tiles_per_slice < 1) return -1;
+  GroupIn gin{cand_h, nullptr, nullptr, nullptr, 1, 1, (int)n_points, (int)tiles_per_slice, 0};
+  gin.rescore = 0;
+  hipLaunchKernelGGL((k_refine<8, 1, true>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride,
+                     nullptr, 0, 1, nullptr, nullptr, status, ovf_count, gin);
   DMLP_LAUNCH_CHECK();
   return 0;
 }

@@ -151,10 +151,13 @@ def pipeline_options(**kw):
 
 
 def pipeline_stats():
-    """What the last native call did: {"n_exact", "n_escalated", "path", "early"}."""
-    out = (C.c_int64 * 4)()
+    """What the last native call did: {"n_exact", "n_escalated", "path", "early", "n_exact_f64",
+    "n_exact_f64_redo"} (the last two: exact-path queries on the fp64 MFMA screen, and those of
+    them that overflowed to the fused VALU kernel)."""
+    out = (C.c_int64 * 6)()
     _lib.lib().dmlp_pipeline_stats(out)
-    return {"n_exact": out[0], "n_escalated": out[1], "path": out[2], "early": out[3]}
+    return {"n_exact": out[0], "n_escalated": out[1], "path": out[2], "early": out[3],
+            "n_exact_f64": out[4], "n_exact_f64_redo": out[5]}
 
 
 # ---------------------------------------------------------------- rows on the device

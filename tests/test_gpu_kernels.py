@@ -152,7 +152,45 @@ def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, monkeypatch
     every k (DMLP_EXACT_FUSED=2): at these small N the dispatch would pick rows + select for
     k > 64."""
     monkeypatch.setenv("DMLP_EXACT_FUSED", "2")
+    monkeypatch.setenv("DMLP_EXACT_F64", "0")  # (A <= 32, k <= 64 would take the fp64 screen)
     inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 5, seed=N + A)
+    r, refs = run_both(torch_cuda, inp, exact=True)
+    assert_same(r, refs)
+    assert K.pipeline_stats()["n_exact_f64"] == 0
+
+
+@pytest.mark.parametrize("N,Q,A,kmin,kmax,lo,hi", [
+    (3000, 130, 32, 1, 16, 0, 1000),        # SUB 16, 2 query blocks, many slices
+    (4097, 70, 7, 17, 64, -5, 5),           # SUB 32, odd A (padded to 8), ragged last tile
+    (20000, 700, 32, 1, 64, 0, 1000),       # mixed k in one wave
+    (9000, 64, 16, 16, 16, 1e6, 1e6 + 1),   # offset data: centring keeps the keys tight
+    (700, 33, 3, 1, 40, 0, 2),              # heavy exact ties: overflow -> VALU kernel
+    (1000, 20, 1, 1, 64, 0, 10),            # A = 1
+])
+def test_exact_f64_screen(torch_cuda, N, Q, A, kmin, kmax, lo, hi):
+    """The exact path's fp64 MFMA screen (screen_f64.hip) + exact group re-rank == the CPU path
+    bit for bit; queries whose candidates overflow (ties) are re-ranked by exact.hip, and the
+    stats say how many took which."""
+    inp = dmlp.generate(N, Q, A, lo, hi, kmin, kmax, 5, seed=N + A + kmax)
+    r, refs = run_both(torch_cuda, inp, exact=True)
+    assert_same(r, refs)
+    st = K.pipeline_stats()
+    assert st["n_exact_f64"] == Q
+    if hi - lo > 100:
+        assert st["n_exact_f64_redo"] == 0
+
+
+def test_exact_f64_huge_and_duplicates(torch_cuda):
+    """Magnitudes past the fp32 key range and all-identical points: every query overflows the
+    fp64 screen and the VALU kernel answers it, still exact."""
+    inp = dmlp.generate(1000, 50, 8, 0.0, 1.0, 1, 16, 3, seed=6)
+    inp.X[3, 2] = 1e200
+    r, refs = run_both(torch_cuda, inp, exact=True)
+    assert_same(r, refs)
+    assert K.pipeline_stats()["n_exact_f64_redo"] == 50
+    X = np.ones((5000, 4))
+    labels = (np.arange(5000) % 3).astype(np.int32)
+    inp = dmlp.KNNInput(labels, X, np.full(17, 16, np.int32), np.zeros((17, 4)))
     r, refs = run_both(torch_cuda, inp, exact=True)
     assert_same(r, refs)
 
