@@ -1044,6 +1044,191 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
   if (i == 0) off[0] = b0;
 }
 
+
+// Group refine, TWO queries per wave (32 lanes each): the one-slice single-term screen on the
+// host's fp16 operands (S = 1, hl = 1, KT <= 2), k <= 64, labels given.  k_refine (one query per
+// wave) is bound by its chain of dependent gathers — group entries -> member fragments -> exact
+// rows -> labels — at 8 waves per SIMD, i.e. 8 queries in flight per SIMD; here each wave keeps
+// two queries' chains in flight with about the same registers per lane.  Members are scored two
+// per lane per batch (64 per query), so the usual ~72 members take 2 batches.  More than PM
+// surviving members hand the query back (status 1, as k_refine does past its P).
+template <int KT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? 6 : 4))) void k_refine_pair(
+    const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int cap,
+    const float* __restrict__ cand_h, const double* __restrict__ X, int A,
+    const double* __restrict__ Qx, const int* __restrict__ qidx, const int* __restrict__ qk,
+    int nq, const u32x4* __restrict__ xfrag, const float* __restrict__ xinit,
+    const bf16x8* __restrict__ qhi, int n_points, double* __restrict__ out_d,
+    int* __restrict__ out_i, int kstride, const int* __restrict__ labels,
+    int* __restrict__ out_label, uint64_t* __restrict__ out_cs, int* __restrict__ status,
+    int* __restrict__ ovf_count) {
+  constexpr int PM = 64;   // surviving members per query
+  constexpr int KM = 64;   // k
+  constexpr int EC = 4;    // group entries held per lane (cap <= 128)
+  __shared__ int s_i[8][PM];
+  __shared__ double s_d[8][PM];
+  __shared__ int s_l[8][PM];
+  __shared__ double s_rd[8][KM];
+  __shared__ int s_ri[8][KM];
+  __shared__ int s_rl[8][KM];
+  __shared__ __attribute__((aligned(16))) float s_qf[8][32 * KT];  // hi(q') as fp32
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, hl = lane & 31;
+  const int slot = wave * 2 + half;
+  const int p = blockIdx.x * 8 + slot;
+  bool act = p < nq;
+  const int q = act ? (qidx ? qidx[p] : p) : 0;
+  const int k = act ? qk[q] : 0;
+  const int n = act ? cand_cnt[p] : 0;
+  const float hq = act ? cand_h[2 * (int64_t)p] : 0.0f;
+  unsigned ent[EC];
+#pragma unroll
+  for (int u = 0; u < EC; ++u) {
+    const int j = hl + 32 * u;
+    ent[u] = act && j < n && j < cap ? (unsigned)cand_ids[(int64_t)p * cap + j] : 0u;
+  }
+  // hi(q') as fp32 in LDS, read at each use (held in registers it pushed the kernel into spills)
+  {
+    const unsigned short* qh = (const unsigned short*)(qhi + (int64_t)q * KT * 4);
+    for (int a = hl; a < 32 * KT; a += 32)
+      s_qf[slot][a] = act ? (float)__builtin_bit_cast(_Float16, qh[a]) : 0.0f;
+  }
+  if (act)
+    for (int i = k + hl; i < kstride; i += 32) {
+      out_d[(int64_t)q * kstride + i] = INFINITY;
+      out_i[(int64_t)q * kstride + i] = -1;
+    }
+  if (act && n < 0) {
+    if (hl == 0) {
+      status[q] = 1;
+      atomicAdd(ovf_count, 1);
+    }
+    act = false;
+  } else if (act && hl == 0) {
+    status[q] = 0;
+  }
+  const int M = act ? n : 0;
+  const unsigned tq = __float_as_uint(hq);
+  const unsigned kh = (tq ^ ((unsigned)((int)tq >> 31) | 0x80000000u)) & 0xffff0000u;
+  // ---- members: two per lane per batch; keep those whose single-term score reaches hq
+  int Mw = M;  // wave-uniform trip count: the larger half's
+  Mw = max(Mw, __shfl_xor(Mw, 32));
+  int nm = 0;
+  dmlp::wave_sync();  // s_qf written
+  for (int j0 = 0; j0 < 4 * Mw; j0 += 64) {
+    __asm__ volatile("" ::: "memory");  // keep the s_qf reads in the loop
+    int id[2];
+    bool pass[2];
+    u32x4 w[2][KT * 4];
+    float sc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int jm = j0 + 32 * u + hl;
+      const int g = jm >> 2;
+      const int src = half * 32 + (g & 31);
+      unsigned e = 0;
+#pragma unroll
+      for (int c = 0; c < EC; ++c) {
+        const unsigned v = (unsigned)__shfl((int)ent[c], src);
+        if ((g >> 5) == c) e = v;
+      }
+      id[u] = (int)(e & 0xffffu) * 4 + (jm & 3);
+      pass[u] = g < M && e >= kh && id[u] < n_points;
+      const int pt = pass[u] ? id[u] : 0;
+      const u32x4* fr = xfrag + (int64_t)(pt >> 6) * (4 * KT * 64) + (pt & 15);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int kq = 0; kq < 4; ++kq)
+          w[u][kt * 4 + kq] = pass[u] ? fr[(int64_t)((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq]
+                                      : u32x4{0, 0, 0, 0};
+      sc[u] = pass[u] ? xinit[pt] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int f = 0; f < KT * 4; ++f) {
+        const float4 q0 = *(const float4*)&s_qf[slot][8 * f];
+        const float4 q1 = *(const float4*)&s_qf[slot][8 * f + 4];
+        const float qf[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+          const unsigned xw = w[u][f][q2];
+          // fp16 x fp16 products are exact in fp32: fma == multiply-then-add here
+          sc[u] = __builtin_fmaf(qf[2 * q2], (float)__builtin_bit_cast(_Float16, (unsigned short)(xw & 0xffffu)), sc[u]);
+          sc[u] = __builtin_fmaf(qf[2 * q2 + 1], (float)__builtin_bit_cast(_Float16, (unsigned short)(xw >> 16)), sc[u]);
+        }
+      }
+      const bool keep = pass[u] && sc[u] >= hq;
+      const unsigned long long bm = __ballot(keep);
+      const unsigned hm = (unsigned)(bm >> (32 * half));
+      const int pos = nm + __popc(hm & ((1u << hl) - 1u));
+      if (keep && pos < PM) s_i[slot][pos] = id[u];
+      nm += __popc(hm);
+    }
+  }
+  if (act && nm > PM) {  // pathological ties: hand the query back
+    if (hl == 0) {
+      status[q] = 1;
+      atomicAdd(ovf_count, 1);
+    }
+    act = false;
+  }
+  const int Ms = act ? nm : 0;
+  dmlp::wave_sync();
+  // ---- exact distances (reference order) and labels of the survivors
+  const double* qv = Qx + (int64_t)q * A;
+  for (int j = hl; j < Ms; j += 32) {
+    const int id = s_i[slot][j];
+    s_d[slot][j] = exact_dist_row(qv, X + (int64_t)id * A, A);
+    s_l[slot][j] = labels[id];
+  }
+  for (int i = hl; i < KM; i += 32) {
+    s_rd[slot][i] = INFINITY;
+    s_ri[slot][i] = -1;
+    s_rl[slot][i] = 0;
+  }
+  dmlp::wave_sync();
+  // ---- rank select: keys are unique, rank = #{ keys before } places the top-k directly
+  for (int j = hl; j < Ms; j += 32) {
+    const double dj = s_d[slot][j];
+    const int ij = s_i[slot][j];
+    int r = 0;
+    for (int i = 0; i < Ms; ++i) r += dmlp::key_less(s_d[slot][i], s_i[slot][i], dj, ij) ? 1 : 0;
+    if (r < k) {
+      s_rd[slot][r] = dj;
+      s_ri[slot][r] = ij;
+      s_rl[slot][r] = s_l[slot][j];
+    }
+  }
+  dmlp::wave_sync();
+  if (act)
+    for (int i = hl; i < k; i += 32) {
+      out_d[(int64_t)q * kstride + i] = s_rd[slot][i];
+      out_i[(int64_t)q * kstride + i] = s_ri[slot][i];
+    }
+  // ---- vote (max count, tie -> larger label; padding ids < 0 not counted) + FNV checksum
+  long long best = -1;
+  for (int i = hl; i < k; i += 32) {
+    if (s_ri[slot][i] < 0) continue;
+    const int li = s_rl[slot][i];
+    int c = 0;
+    for (int j = 0; j < k; ++j) c += (s_ri[slot][j] >= 0 && s_rl[slot][j] == li) ? 1 : 0;
+    const long long key = ((long long)c << 32) | (long long)((unsigned)li ^ 0x80000000u);
+    best = key > best ? key : best;
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    const long long o = __shfl_xor(best, off);
+    best = o > best ? o : best;
+  }
+  if (act && hl == 0) {
+    const int label = best < 0 ? -1 : (int)((unsigned)(best & 0xffffffffll) ^ 0x80000000u);
+    out_label[q] = label;
+    out_cs[q] = dmlp::fnv_checksum(label, s_ri[slot], k);
+  }
+}
+
 }  // namespace
 
 extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, int S,
@@ -1098,6 +1283,24 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
     else if (KT == 4) DMLP_REFINE_GB(4);
     else DMLP_REFINE_GB(8);
 #undef DMLP_REFINE_GB
+    DMLP_LAUNCH_CHECK();
+    return 0;
+  }
+  // one slice of the host's fp16 operands, k <= 64, labels: two queries per wave
+  // (k_refine_pair; DMLP_REFINE_PAIR=0: the one-query-per-wave kernel)
+  static const bool pair_on = !(getenv("DMLP_REFINE_PAIR") && getenv("DMLP_REFINE_PAIR")[0] == '0');
+  if (pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128) {
+    const dim3 grid((unsigned)((nq + 7) / 8));
+    if (KT == 1)
+      hipLaunchKernelGGL((k_refine_pair<1>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
+                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
+                         (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
+                         out_cs, status, ovf_count);
+    else
+      hipLaunchKernelGGL((k_refine_pair<2>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
+                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
+                         (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
+                         out_cs, status, ovf_count);
     DMLP_LAUNCH_CHECK();
     return 0;
   }

@@ -93,8 +93,8 @@ def _early_inputs(n, A, kmax, Q, seed):
     return out
 
 
-@pytest.mark.parametrize("n,A,kmax", [(2000, 32, 16), (5000, 32, 32), (3000, 128, 32),
-                                        (3000, 256, 32)])
+@pytest.mark.parametrize("n,A,kmax", [(2000, 32, 16), (5000, 32, 32), (3000, 64, 64),
+                                        (3000, 128, 32), (3000, 256, 32)])
 def test_native_step_early_start(gpu, n, A, kmax):
     """Early start: the screen starts on the query operands while the dataset image crosses
     PCIe in slices with ready words.  The host sleeps 400 us before each image slice
