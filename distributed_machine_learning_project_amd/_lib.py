@@ -100,6 +100,8 @@ _SIGS = {
     "dmlp_exact_f64_kmax": (i32, []),
     "dmlp_exact_f64_bytes": (i64, [i64, i32, i32, i32]),
     "dmlp_exact_f64": (i32, [vp, i64, i32, vp, vp, vp, i32, i32, vp, vp, i32, vp, vp, vp, i64, vp]),
+    "dmlp_exact_f64_probe": (i32, [vp, i64, i32, vp, vp, vp, i64, vp]),
+    "dmlp_exact_f64_layout": (None, [i64, i32, i32, i32, vp]),
     "dmlp_fallback_select_bytes": (i64, [i32, i64]),
     "dmlp_fallback_select": (i32, [vp, i64, i32, vp, vp, vp, i32, vp, i64, vp, vp, i32, vp]),
     "dmlp_fallback_topk": (i32, [vp, i64, i32, vp, vp, vp, i32, vp, i64, vp, vp, i32, vp]),

@@ -420,7 +420,64 @@ F64Ws f64_ws(char* base, int64_t N, int A, int nq, int kmax) {
   return w;
 }
 
+// Layout probe (tests): scores of queries Qx[0..16) against points [0, 16) computed exactly as
+// k_screen_f64 does (image, C operand, f64 MFMA chain, result rows g + 4r -> point 4g + r),
+// written out[query * 16 + point].  NM = A padded / 4 (<= 8).
+__global__ void k_f64_probe(const double2* __restrict__ frag, const double* __restrict__ xi,
+                            const double* __restrict__ Qx, int A, const double* __restrict__ mu,
+                            int NM, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63, c = lane & 15, kg = lane >> 4;
+  f64x4 a;
+  for (int r = 0; r < 4; ++r) a[r] = xi[4 * kg + r];
+  for (int m = 0; m < NM; ++m) {
+    const double2 v = frag[(m >> 1) * 64 + lane];
+    const double av = (m & 1) ? v.y : v.x;
+    const int at = 4 * m + kg;
+    const double bv = at < A ? __dsub_rn(Qx[c * A + at], mu[at]) : 0.0;
+    a = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, a, 0, 0, 0);
+  }
+  for (int r = 0; r < 4; ++r) out[c * 16 + 4 * kg + r] = a[r];
+}
+
 }  // namespace
+
+extern "C" int dmlp_exact_f64_probe(const double* X, int64_t N, int A, const double* Qx,
+                                    double* out16x16, void* ws, int64_t ws_bytes, void* stream) {
+  const int NM = f64_nm(A);
+  if (NM == 0 || N < 16) return -3;
+  F64Ws w = f64_ws((char*)ws, N, A, 64, 16);
+  if (!ws || ws_bytes < w.bytes) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n_tiles = (N + 63) / 64;
+  int rc = dmlp_center(X, N, A, w.mu, stream);
+  if (rc) return rc;
+  if (hipMemsetAsync(w.xnmax, 0, 8, st) != hipSuccess) return -1;
+  const int64_t n_steps = n_tiles * 4;
+  const int64_t nimg = n_steps * (NM / 2) * 64;
+  hipLaunchKernelGGL(k_f64_image, dim3((unsigned)((nimg + 255) / 256)), dim3(256), 0, st, X, N, A,
+                     w.mu, NM, n_steps, w.frag);
+  hipLaunchKernelGGL(k_f64_norms, dim3((unsigned)((n_tiles * 64 + 255) / 256)), dim3(256), 0, st,
+                     X, N, A, w.mu, n_tiles * 64, w.xi, w.xnmax);
+  hipLaunchKernelGGL(k_f64_probe, dim3(1), dim3(64), 0, st, w.frag, w.xi, Qx, A, w.mu, NM, out16x16);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+// Workspace layout (debugging): [0] S, [1] tiles per slice, [2] ids per (query, slice), byte
+// offsets of [3] cand_ids, [4] cand_cnt, [5] cand_h, [6] xnmax, [7] mu.
+extern "C" void dmlp_exact_f64_layout(int64_t N, int A, int nq, int kmax, int64_t* out) {
+  F64Ws w = f64_ws(nullptr, N, A, nq, kmax);
+  const int64_t n_tiles = (N + 63) / 64;
+  const int S = f64_slices(nq, n_tiles);
+  out[0] = S;
+  out[1] = (n_tiles + S - 1) / S;
+  out[2] = 4 * (f64_sub(kmax) - 1);
+  out[3] = (int64_t)(size_t)w.cand_ids;
+  out[4] = (int64_t)(size_t)w.cand_cnt;
+  out[5] = (int64_t)(size_t)w.cand_h;
+  out[6] = (int64_t)(size_t)w.xnmax;
+  out[7] = (int64_t)(size_t)w.mu;
+}
+
 
 extern "C" int dmlp_refine_groups_exact(int cap, const int* cand_ids, const int* cand_cnt,
                                         const float* cand_h, int S, int64_t tiles_per_slice,
@@ -476,6 +533,7 @@ extern "C" int dmlp_exact_f64(const double* X, int64_t N, int A, const double* Q
   else DMLP_F64(8);
 #undef DMLP_F64
   if (rc) return rc;
+  if (getenv("DMLP_EXACT_F64_SCREEN_ONLY")) return 0;  // debugging: the candidates stay in ws
   return dmlp_refine_groups_exact(4 * (sub - 1), w.cand_ids, w.cand_cnt, w.cand_h, S,
                                   (n_tiles + S - 1) / S, X, A, Qx, N, qidx, qk, nq, out_d, out_i,
                                   kstride, status, ovf_count, stream);

@@ -159,6 +159,30 @@ def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, monkeypatch
     assert K.pipeline_stats()["n_exact_f64"] == 0
 
 
+@pytest.mark.parametrize("A", [32, 7, 1])
+def test_exact_f64_mfma_layout(torch_cuda, A):
+    """The fp64 screen's operand / result maps (v_mfma_f64_16x16x4_f64, screen_f64.hip) on exact
+    integer data: 16 queries x the first 16 points, every score q'.x' - |x'|^2/2 exact."""
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    torch = torch_cuda
+    rng = np.random.default_rng(A)
+    X = rng.integers(-8, 9, size=(64, A)).astype(np.float64)
+    Qh = rng.integers(-8, 9, size=(16, A)).astype(np.float64)
+    mu = X.mean(0)  # dyadic (N = 64): exact, as dmlp_center computes it
+    xs, qs = X - mu, Qh - mu
+    expect = qs @ xs[:16].T - 0.5 * (xs[:16] ** 2).sum(1)[None, :]
+    dX, dQ = torch.from_numpy(X).cuda(), torch.from_numpy(Qh).cuda()
+    out = torch.zeros(256, dtype=torch.float64, device="cuda")
+    nb = int(L.dmlp_exact_f64_bytes(64, A, 64, 16))
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    rc = L.dmlp_exact_f64_probe(dX.data_ptr(), 64, A, dQ.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                nb, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().reshape(16, 16), expect)
+
+
 @pytest.mark.parametrize("N,Q,A,kmin,kmax,lo,hi", [
     (3000, 130, 32, 1, 16, 0, 1000),        # SUB 16, 2 query blocks, many slices
     (4097, 70, 7, 17, 64, -5, 5),           # SUB 32, odd A (padded to 8), ragged last tile

@@ -27,9 +27,10 @@ echo "dropin: $(grep -o '"time_ms_median": [0-9.]*' $OUT/dropin.log | tr '\n' ' 
 timeout -k 10 600 python bench.py --harness native --steps 20 --warmup 2 > $OUT/native.log 2>&1 || { tail -5 $OUT/native.log; exit 1; }
 echo "native: $(grep -o '"time_ms_median": [0-9.]*' $OUT/native.log | tr '\n' ' ')"
 # copy engine A/B: the step's H2D/D2H run as __amd_rocclr_copyBuffer blit kernels by default
-for E in "BASE=1" "HSA_ENABLE_SDMA=1" "GPU_FORCE_BLIT_COPY_SIZE=0" "HSA_ENABLE_SDMA=0"; do
-  env $E timeout -k 10 200 python bench.py --steps 100 > $OUT/copy_${E%%=*}.log 2>&1 || { tail -5 $OUT/copy_${E%%=*}.log; exit 1; }
-  echo "copy $E: $(grep -o '"ms_per_step": [0-9.]*' $OUT/copy_${E%%=*}.log | head -1)"
+for E in "BASE=1" "DMLP_REFINE_PAIR=0" "HSA_ENABLE_SDMA=1" "GPU_FORCE_BLIT_COPY_SIZE=0" "HSA_ENABLE_SDMA=0" "BASE=2" "DMLP_REFINE_PAIR=0"; do
+  T=$(echo $E | tr '=' '_')
+  env $E timeout -k 10 200 python bench.py --steps 100 > $OUT/ab_$T.log 2>&1 || { tail -5 $OUT/ab_$T.log; exit 1; }
+  echo "ab $E: $(grep -o '"ms_per_step": [0-9.]*' $OUT/ab_$T.log | head -1) $(grep -o '"step_timeline_ms": {[^}]*}' $OUT/ab_$T.log)"
 done
 cd /tmp
 HSA_ENABLE_SDMA=1 timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_sdma -o prof -- python3 $R/bench.py --steps 20 --warmup 2 --min-warmup-s 0 > $R/$OUT/prof_sdma.log 2>&1 || { echo "prof sdma failed"; exit 1; }
