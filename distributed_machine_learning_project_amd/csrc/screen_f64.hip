@@ -411,7 +411,7 @@ F64Ws f64_ws(char* base, int64_t N, int A, int nq, int kmax) {
   w.mu = (double*)(base + o); o += al(8 * (int64_t)A);
   w.xnmax = (unsigned long long*)(base + o); o += al(8);
   w.ovf = (int*)(base + o); o += al(4);
-  w.frag = (double2*)(base + o); o += al(n_tiles * 64 * (int64_t)NM * 8);
+  w.frag = (double2*)(base + o); o += al(n_tiles * 64 * (int64_t)NM * 4 * 8);  // 4 NM fp64 per point
   w.xi = (double*)(base + o); o += al(n_tiles * 64 * 8);
   w.cand_ids = (int*)(base + o); o += al((int64_t)nq * S * idcap * 4);
   w.cand_cnt = (int*)(base + o); o += al((int64_t)nq * S * 4);
