@@ -173,6 +173,7 @@ class KnnCore {
   hipStream_t wake_st_ = nullptr;
   HostBuf<char> wake_h_;
   bool wake_ = !(getenv("KNN_WAKE_D2H") && std::string(getenv("KNN_WAKE_D2H")) == "0");
+  bool step_events_ = false;
 
   void set_shared(const SharedIn& s) { sh_ = s; }
 
@@ -562,6 +563,7 @@ class KnnCore {
       a.report_cap = (int64_t)out->text.size();
     }
     a.stream = rt_.stream;
+    if (trace.on && !step_events_) step_events_ = dmlp_step_events(1) == 0;
     trace.mark("step_enter");
     DMLPCHK(dmlp_step(&a));
     ++step_calls_;
@@ -573,6 +575,13 @@ class KnnCore {
       std::fprintf(stderr, "[dmlp-step] rank %d path %d early %d escalated %d exact %lld "
                    "early_waits %d early_timeouts %d\n", rt_.rank, a.path, a.early,
                    a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts);
+      // KNN_TRACE: the step's own hipEvent timeline (ms from step entry)
+      double ms[16];
+      const char* nm[16];
+      const int n = dmlp_step_timeline(ms, nm, 16);
+      std::fprintf(stderr, "[dmlp-step] rank %d timeline", rt_.rank);
+      for (int i = 0; i < n; ++i) std::fprintf(stderr, " %s %.3f", nm[i], ms[i]);
+      std::fprintf(stderr, "\n");
     }
     return a;
   }
