@@ -1052,8 +1052,11 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
 // two queries' chains in flight with about the same registers per lane.  Members are scored two
 // per lane per batch (64 per query), so the usual ~72 members take 2 batches.  More than PM
 // surviving members hand the query back (status 1, as k_refine does past its P).
+#ifndef DMLP_PAIR_WPE
+#define DMLP_PAIR_WPE 5  // 288 vs 297 us at 6 (14 VGPRs spilled), profiles/r7n_refine_ab.txt
+#endif
 template <int KT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? 6 : 4))) void k_refine_pair(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? DMLP_PAIR_WPE : 4))) void k_refine_pair(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int cap,
     const float* __restrict__ cand_h, const double* __restrict__ X, int A,
     const double* __restrict__ Qx, const int* __restrict__ qidx, const int* __restrict__ qk,
@@ -1061,7 +1064,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? 6
     const bf16x8* __restrict__ qhi, int n_points, double* __restrict__ out_d,
     int* __restrict__ out_i, int kstride, const int* __restrict__ labels,
     int* __restrict__ out_label, uint64_t* __restrict__ out_cs, int* __restrict__ status,
-    int* __restrict__ ovf_count) {
+    int* __restrict__ ovf_count, int abl) {
   constexpr int PM = 64;   // surviving members per query
   constexpr int KM = 64;   // k
   constexpr int EC = 4;    // group entries held per lane (cap <= 128)
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? 6
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int kq = 0; kq < 4; ++kq)
-          w[u][kt * 4 + kq] = pass[u] ? fr[(int64_t)((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq]
+          w[u][kt * 4 + kq] = pass[u] && !(abl & 2) ? fr[(int64_t)((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq]
                                       : u32x4{0, 0, 0, 0};
       sc[u] = pass[u] ? xinit[pt] : 0.0f;
     }
@@ -1176,12 +1179,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? 6
   }
   const int Ms = act ? nm : 0;
   dmlp::wave_sync();
-  // ---- exact distances (reference order) and labels of the survivors
-  const double* qv = Qx + (int64_t)q * A;
-  for (int j = hl; j < Ms; j += 32) {
-    const int id = s_i[slot][j];
-    s_d[slot][j] = exact_dist_row(qv, X + (int64_t)id * A, A);
-    s_l[slot][j] = labels[id];
+  // ---- exact distances of the survivors in the reference's order (engine.cpp:12-18), 16 lanes
+  // per row: lane t loads attributes 2t, 2t+1 (+ 32 u) of the row — one row is two cache lines
+  // read by one instruction, where a lane-per-row gather touched a line per lane per load (the
+  // rows were half of this kernel's time: profiles/r7m_refine_ablation.txt) — squares their
+  // differences (each product rounded, no FMA), and the left-to-right sum travels from lane to
+  // lane by a DPP row rotate, so lane 15 ends with exactly the reference's sum.
+  {
+    const int t16 = hl & 15, rsel = hl >> 4;
+    double qa[KT][2];
+#pragma unroll
+    for (int u = 0; u < KT; ++u) {
+      const int a0 = 32 * u + 2 * t16;
+      qa[u][0] = a0 < A ? Qx[(int64_t)q * A + a0] : 0.0;
+      qa[u][1] = a0 + 1 < A ? Qx[(int64_t)q * A + a0 + 1] : 0.0;
+    }
+    int Msw = Ms;
+    Msw = max(Msw, __shfl_xor(Msw, 32));
+    for (int r0 = 0; r0 < Msw; r0 += 2) {
+      const int j = r0 + rsel;
+      const bool rv = j < Ms;
+      const int id = rv ? s_i[slot][j] : 0;
+      const double* xr = X + (int64_t)id * A;
+      double pr[KT][2];
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const int a0 = 32 * u + 2 * t16;
+        const double x0 = rv && a0 < A && !(abl & 1) ? xr[a0] : 0.0;
+        const double x1 = rv && a0 + 1 < A && !(abl & 1) ? xr[a0 + 1] : 0.0;
+        const double d0 = a0 < A ? __dsub_rn(qa[u][0], x0) : 0.0;
+        const double d1 = a0 + 1 < A ? __dsub_rn(qa[u][1], x1) : 0.0;
+        pr[u][0] = __dmul_rn(d0, d0);
+        pr[u][1] = __dmul_rn(d1, d1);
+      }
+      double sm = 0.0;
+#pragma unroll
+      for (int u = 0; u < KT; ++u)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          // lane t's turn: its predecessor's partial sum arrives by the rotate (lane 0 gets lane
+          // 15's: 0 at the start, the previous 32-attribute chunk's total after it)
+          const long long b = __double_as_longlong(sm);
+          const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x121, 0xf, 0xf, false);
+          const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x121, 0xf, 0xf, false);
+          const double in = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+          sm = t16 == t ? __dadd_rn(__dadd_rn(in, pr[u][0]), pr[u][1]) : sm;
+        }
+      if (rv && t16 == 15) {
+        s_d[slot][j] = (abl & 1) ? (double)id : sm;
+        s_l[slot][j] = labels[id];
+      }
+    }
   }
   for (int i = hl; i < KM; i += 32) {
     s_rd[slot][i] = INFINITY;
@@ -1289,18 +1337,20 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
   // one slice of the host's fp16 operands, k <= 64, labels: two queries per wave
   // (k_refine_pair; DMLP_REFINE_PAIR=0: the one-query-per-wave kernel)
   static const bool pair_on = !(getenv("DMLP_REFINE_PAIR") && getenv("DMLP_REFINE_PAIR")[0] == '0');
+  // DMLP_REFINE_ABL (timing ablations, wrong results): 1 no exact-row gathers, 2 no member loads
+  static const int pair_abl = getenv("DMLP_REFINE_ABL") ? atoi(getenv("DMLP_REFINE_ABL")) : 0;
   if (pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128) {
     const dim3 grid((unsigned)((nq + 7) / 8));
     if (KT == 1)
       hipLaunchKernelGGL((k_refine_pair<1>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
                          cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
                          (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
-                         out_cs, status, ovf_count);
+                         out_cs, status, ovf_count, pair_abl);
     else
       hipLaunchKernelGGL((k_refine_pair<2>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
                          cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
                          (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
-                         out_cs, status, ovf_count);
+                         out_cs, status, ovf_count, pair_abl);
     DMLP_LAUNCH_CHECK();
     return 0;
   }
