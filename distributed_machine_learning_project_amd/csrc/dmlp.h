@@ -260,7 +260,7 @@ typedef struct dmlp_step_args {
   int64_t N;
   int A;
   const int* labels;          // [N]; null: no vote / checksum / report
-  int label_lo, label_hi;     // labels in [lo, hi)
+  int label_lo, label_hi;     // labels in [lo, hi) (hi <= lo: scanned here)
   const double* Qx;           // [Q][A], or
   const double* const* Qr;    // [Q] row pointers
   const int* k;               // [Q]
@@ -365,6 +365,7 @@ int dmlp_kdtree_knn(const double* X, int64_t N, int A, const double* Qx, int64_t
                     const int* qk, int kstride, double* out_d, int* out_i);
 // Text report, host side.  Returns bytes written (buffer must hold 48*Q bytes).
 void dmlp_cpu_i32_range(const int* a, int64_t n, int* lo, int* hi);
+void dmlp_host_i32_range(const int* a, int64_t n, int* lo, int* hi);  // on the render pool
 int64_t dmlp_atomic_fetch_add_i64(int64_t* p, int64_t v);
 void dmlp_atomic_store_i64(int64_t* p, int64_t v);
 int64_t dmlp_cpu_format_report(const uint64_t* cs, int64_t Q, int64_t qid_base, char* out);

@@ -202,6 +202,36 @@ inline uint16_t f16_rn(float f) {
 
 extern "C" int dmlp_host_threads(void) { return pool().size(); }
 
+// (min, max) of an int32 array on the render pool (the native step's label / k scans: ~15 us
+// single-threaded at the bench shape, on the step's critical path); (0, -1) when empty.
+extern "C" void dmlp_host_i32_range(const int* a, int64_t n, int* lo, int* hi) {
+  if (n <= 0) {
+    *lo = 0;
+    *hi = -1;
+    return;
+  }
+  int mn[64], mx[64];
+  const int parts = n < (1 << 16) ? 1 : std::min(pool().size(), 64);
+  std::function<void(int, int)> job = [&](int part, int np) {
+    if (part >= parts) return;
+    const int64_t b = n * part / std::min(np, parts), e = n * (part + 1) / std::min(np, parts);
+    int l = INT32_MAX, h = INT32_MIN;
+    for (int64_t i = b; i < e; ++i) {
+      l = std::min(l, a[i]);
+      h = std::max(h, a[i]);
+    }
+    mn[part] = l;
+    mx[part] = h;
+  };
+  for (int i = 0; i < parts; ++i) { mn[i] = INT32_MAX; mx[i] = INT32_MIN; }
+  if (parts == 1) job(0, 1);
+  else pool().run(job);
+  int l = INT32_MAX, h = INT32_MIN;
+  for (int i = 0; i < parts; ++i) { l = std::min(l, mn[i]); h = std::max(h, mx[i]); }
+  *lo = l;
+  *hi = h;
+}
+
 // fn(ctx, part, parts) on every worker of the render pool and the caller (parts = the pool's
 // size); returns when all parts are done.  For host passes of other modules (the drop-in's
 // index of the harness's vectors) that should not pay a thread start each.

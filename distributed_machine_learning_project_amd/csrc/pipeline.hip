@@ -845,10 +845,16 @@ struct Step {
     CK(hipEventRecord(w.ev_ops, st));
     CK(hipStreamWaitEvent(w.side, w.ev_ops, 0));
     int kmin = a->kmin, kmax = a->kmax;
-    if (Q > 0 && kmax < kmin) {
-      dmlp_cpu_i32_range(a->k, Q, &kmin, &kmax);
+    if (Q > 0 && kmax < kmin) {  // k bounds not given: one pass on the render pool
+      dmlp_host_i32_range(a->k, Q, &kmin, &kmax);
       a->kmin = kmin;
       a->kmax = kmax;
+    }
+    if (a->labels && a->label_hi <= a->label_lo) {  // label range not given: the same
+      int lmin = 0, lmax = -1;
+      if (N > 0) dmlp_host_i32_range(a->labels, N, &lmin, &lmax);
+      a->label_lo = N > 0 ? lmin : 0;
+      a->label_hi = N > 0 ? lmax + 1 : 1;
     }
     const int kst = a->kstride > 0 ? a->kstride : std::max(1, Q ? kmax : 1);
     if (Q > 0 && kmax > kst) return -3;

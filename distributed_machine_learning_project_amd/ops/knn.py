@@ -299,10 +299,13 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     labels_host = None if labels_host is None else np.ascontiguousarray(labels_host, np.int32)
     N, A = X_host.shape
     Q = Q_host.shape[0]
-    if Q and k_range is None:
-        k_range = _lib.i32_range(k_host)
-    kmin, kmax = (int(k_range[0]), int(k_range[1])) if Q else (1, 1)
-    ks = kstride or max(1, kmax)
+    if Q and k_range is None and lists and not kstride:
+        k_range = _lib.i32_range(k_host)  # (the lists' stride)
+    if k_range is None:  # the native step scans k on its render pool
+        kmin, kmax = (1, 0) if Q else (1, 1)
+    else:
+        kmin, kmax = (int(k_range[0]), int(k_range[1])) if Q else (1, 1)
+    ks = kstride or (max(1, kmax) if kmax >= kmin else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
     lab = torch.empty(max(Q, 1), dtype=torch.int32, device=dev)[:Q]
     cs = torch.empty(max(Q, 1), dtype=torch.int64, device=dev)[:Q]
@@ -313,7 +316,8 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     a = StepArgs()
     a.X, a.N, a.A = _np_ptr(X_host), N, A
     a.labels = _np_ptr(labels_host)
-    a.label_lo, a.label_hi = (int(label_range[0]), int(label_range[1])) if label_range else (0, 1)
+    # (label_range None: the native step scans the labels on its render pool)
+    a.label_lo, a.label_hi = (int(label_range[0]), int(label_range[1])) if label_range else (0, 0)
     a.Qx, a.k, a.Q = _np_ptr(Q_host), _np_ptr(k_host), Q
     a.kmin, a.kmax = kmin, kmax
     a.qid_base = int(qid_base)

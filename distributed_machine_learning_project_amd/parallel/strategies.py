@@ -100,6 +100,13 @@ def _k_host(comm, k_dev_or_none, Q):
 # ============================================================================ farm (bench_4)
 def farm(comm, be, inp, tr, schedule="static", chunks_per_rank=4, call_id=0, debug=False, **_):
     torch = _torch()
+    import os
+    if (getattr(inp, "shared", False) and schedule == "static" and comm.world == 1 and not debug
+            and be.on_gpu and not int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)):
+        # one rank, the whole call in the native step: it scans the label and k ranges itself
+        # (on its render pool, ~2 us instead of ~30 us of host scans on the critical path)
+        N, A = inp.X.shape
+        return _farm_shared(comm, be, inp, tr, N, inp.Qx.shape[0], A, None, None, None, debug)
     N, Q, A, lo, hi, kmax, shared = _meta(comm, inp, with_shared=True)
     if shared and schedule == "static":
         return _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug)
@@ -248,10 +255,12 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
     if mode == "h2d" and be.on_gpu:
         with tr.phase("step"):
-            k_range = inp.k_range_all if comm.world == 1 else _lib_range(kl_h)
+            # lo / hi / kmax None (one rank, farm()): the native step scans them
+            k_range = (None if kmax is None else inp.k_range_all if comm.world == 1
+                       else _lib_range(kl_h))
             rep = None if debug else (inp.out if comm.world == 1 else "device")
-            r = be.step(inp.X, inp.labels, (lo, hi), inp.Qx[a:b], kl_h, k_range=k_range,
-                        qid_base=a, report=rep, lists=debug, kstride=kmax)
+            r = be.step(inp.X, inp.labels, None if lo is None else (lo, hi), inp.Qx[a:b], kl_h,
+                        k_range=k_range, qid_base=a, report=rep, lists=debug, kstride=kmax)
         if debug:
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, r.dist, r.ids, r.label,
                                      r.checksum, True)
