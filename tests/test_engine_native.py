@@ -242,7 +242,8 @@ def test_fast_path_serves_any_k_and_escalates_per_query(tmp_path):
     phases = [l.split()[3] for l in err.splitlines() if l.startswith("[dmlp-trace]")]
     assert "step" in phases, phases  # the library's native step, not the general farm
     assert "distribute" not in phases and "compute" not in phases
-    st = [l.split() for l in err.splitlines() if l.startswith("[dmlp-step]")][-1]  # (the call)
+    st = [l.split() for l in err.splitlines()
+          if l.startswith("[dmlp-step]") and " path " in l][-1]  # (the call; not its timeline)
     assert st[st.index("path") + 1] == "0"            # host-rendered operands
     assert int(st[st.index("escalated") + 1]) >= 1    # the tied query escalated alone
     # k > 32 on the 3-term LDS screen over the device image instead of the default two-pass
