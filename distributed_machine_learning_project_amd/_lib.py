@@ -66,6 +66,8 @@ _SIGS = {
                                      C.POINTER(C.c_float)]),
     "dmlp_screen_x1": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
+    "dmlp_screen_x1_early": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp,
+                                   i32, i32, vp, vp, vp, vp, vp, vp]),
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_refine_groups2": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, vp]),
     "dmlp_x1_seed": (i32, [vp, vp, i32, i32, vp, vp]),

@@ -177,22 +177,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       }
     }
   };
-  auto cum_xnm = [&](int upto) {
-    float m = 0.0f;
-    for (int i = 0; i <= upto; ++i) {
+  // m folded with the max norms of slices [lo, hi] (system-scope loads: ~1-2 us each, so the
+  // words of slices already seen are not read again)
+  auto fold_xnm = [&](float m, int lo, int hi) {
+    for (int i = lo; i <= hi; ++i) {
       const unsigned* const f = xnm_sl + i;
       m = fmaxf(m, __uint_as_float(__hip_atomic_load(const_cast<unsigned*>(f), __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_SYSTEM)));
     }
     return m;
   };
+  // Once the last slice's word is set every slice has landed (the copies and their words run in
+  // slice order on one stream): a wave that sees it takes the rest of the image at once instead
+  // of probing slice by slice — each probe is a system-scope round trip on the wave's critical
+  // path (the per-slice probes cost the screen ~0.075 ms: profiles/r7n_refine_ab.txt, r7s)
+  auto widen = [&](int need) { return need < rdy_n - 1 && rdy_probe(rdy_n - 1) ? rdy_n - 1 : need; };
   float xnmax;
   if (rdy) {
-    const int need = min(2 / rdy_tiles, rdy_n - 1);  // tiles 0..2: the prologue and step 0's loads
+    // tiles 0..2: the prologue and step 0's loads
+    const int need = widen(min(2 / rdy_tiles, rdy_n - 1));
     for (int i = 0; i <= need && !rdy_fail; ++i) rdy_fail |= !wait_slice(i);
     have = need + 1;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's DMA wrote them
-    xnmax = cum_xnm(need);
+    xnmax = fold_xnm(0.0f, 0, need);
   } else {
     xnmax = __uint_as_float(*xnmax_bits);
   }
@@ -543,14 +550,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     for (int j0 = 0; j0 < nsteps; j0 += D) {
       if (rdy && have < rdy_n) {
         // this iteration's loads reach tile (j0 + 11) / 4 (C-operand window j0/4 + 2)
-        const int need = min(((j0 + 11) >> 2) / rdy_tiles, rdy_n - 1);
+        int need = min(((j0 + 11) >> 2) / rdy_tiles, rdy_n - 1);
         if (need >= have) {
+          const int need1 = widen(need);
           bool ok = true;
-          for (int i = have; i <= need && ok; ++i) ok &= wait_slice(i);
+          if (need1 == need)  // (all landed: no per-slice probes)
+            for (int i = have; i <= need && ok; ++i) ok &= wait_slice(i);
+          need = need1;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope (host DMA)
+          const int from = have;
           have = need + 1;
           if (ok) {
-            const float xm = cum_xnm(need);
+            const float xm = fold_xnm(xnmax, from, need);
             if (xm > xnmax) {
               grow(xm);
               xnmax = xm;

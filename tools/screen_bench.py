@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--early", type=int, default=0,
+                    help="1: the early-start entry (dmlp_screen_x1_early) with every slice ready")
     a = ap.parse_args()
     L = _lib.lib()
     inp = dmlp.generate(a.n, a.q, a.a, 0.0, 1000.0, a.k, a.k, 10, seed=42)
@@ -67,10 +69,24 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     wp = d_words.data_ptr()
 
+    NS = 8
+    rt = (nt + NS - 1) // NS
+    rdy = torch.ones(NS, dtype=torch.int32, device=dev)  # every slice "landed"
+    xsl = torch.from_numpy(np.full(NS, xnm[0], np.uint32).view(np.int32)).to(dev)
+    est = torch.zeros(4, dtype=torch.int32, device=dev)
+
     def launch():
-        rc = L.dmlp_screen_x1(KT, 1, A, d_xhi.data_ptr(), d_xin.data_ptr(), nt, N,
-                              d_qhi.data_ptr(), d_qn.data_ptr(), d_qi.data_ptr(), d_k.data_ptr(),
-                              Q, a.k, wp, wp + 4, S, ci.data_ptr(), cc.data_ptr(), ch.data_ptr(), s)
+        if a.early:
+            rc = L.dmlp_screen_x1_early(KT, A, d_xhi.data_ptr(), d_xin.data_ptr(), nt, N,
+                                        d_qhi.data_ptr(), d_qn.data_ptr(), d_qi.data_ptr(),
+                                        d_k.data_ptr(), Q, a.k, wp + 4, rdy.data_ptr(), rt, NS,
+                                        xsl.data_ptr(), ci.data_ptr(), cc.data_ptr(),
+                                        ch.data_ptr(), est.data_ptr(), s)
+        else:
+            rc = L.dmlp_screen_x1(KT, 1, A, d_xhi.data_ptr(), d_xin.data_ptr(), nt, N,
+                                  d_qhi.data_ptr(), d_qn.data_ptr(), d_qi.data_ptr(),
+                                  d_k.data_ptr(), Q, a.k, wp, wp + 4, S, ci.data_ptr(),
+                                  cc.data_ptr(), ch.data_ptr(), s)
         assert rc == 0, rc
 
     modes = [int(m) for m in a.modes.split(",")]
