@@ -307,7 +307,9 @@ struct Ctx {
   HBuf<unsigned> sx_nm;
   HBuf<double> s_mu, s_f64;
   HBuf<int> s_i32, s_lab;
-  HBuf<int64_t> s_len;
+  HBuf<int64_t> s_len, small64_h;
+  DBuf<int64_t> small64_d;
+  hipEvent_t ev_done = nullptr;
   DBuf<short> dx_hi, dq_hi;
   DBuf<float> dx_in, dq_n;
   DBuf<unsigned> dwords;  // [0] xnmax, [1] bad, [2, 2+S) ready words, [2+S, 2+2S) slice norms,
@@ -331,8 +333,37 @@ Ctx& ctx() {
     CK(hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking));
     CK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
   }
   return w;
+}
+
+// The step's small results in one word block: [0] report length, [1] overflowed queries,
+// [2..4] early-start waits / eps growths / timeouts.
+__global__ void k_pack_small(const int64_t* __restrict__ len, const int* __restrict__ ovf,
+                             const unsigned* __restrict__ estats, int64_t* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    out[0] = len ? *len : 0;
+    out[1] = *ovf;
+    out[2] = estats ? estats[0] : 0;
+    out[3] = estats ? estats[1] : 0;
+    out[4] = estats ? estats[2] : 0;
+  }
+}
+
+// Wait for the step's last event by polling it (the host thread spins for the ~2 ms a step takes
+// instead of sleeping in the runtime's blocking wait, whose wake-up sat on every step's tail).
+void spin_wait(hipEvent_t e) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) {
+      (void)hipGetLastError();
+      CK(hipEventSynchronize(e));  // (reports the error)
+      return;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 int* identity(Ctx& w, int64_t n, hipStream_t st) {  // device 0, 1, ..., n-1 (grow-only)
@@ -999,40 +1030,47 @@ struct Step {
       use_hx = false;
       Lp = run_local(false, false);
     }
-    // ---- the report behind the re-rank, then the one host sync
-    int* small = w.small_h.get(8);
+    // ---- the report behind the re-rank, then the one host sync.  The small results (report
+    // length, overflow count, early-start counters) are packed on the device and cross in ONE
+    // copy: each separate small D2H cost a copy command's latency on the step's tail.
+    int64_t* small = w.small64_h.get(8);
+    int64_t* small_d = w.small64_d.get(8);
     auto render = [&]() {
-      if (!want_report) return;
-      int64_t* off = w.d_off.get((size_t)dmlp_format_scratch((int)Q));
-      char* text = w.d_text.get((size_t)dmlp_format_bound((int)Q));
-      CKL(dmlp_format_report(ocs, (int)Q, (int)a->qid_base, off, text, st));
-      CK(mark(M_FORMAT, st));
-      int64_t* len_h = w.s_len.get(2);
-      CK(hipMemcpyAsync(len_h, off + Q, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      if (a->report_mode == 1)
-        CK(hipMemcpyAsync(a->report_dst, text, (size_t)dmlp_format_bound((int)Q),
+      const int64_t* len_src = nullptr;
+      if (want_report) {
+        int64_t* off = w.d_off.get((size_t)dmlp_format_scratch((int)Q));
+        char* text = w.d_text.get((size_t)dmlp_format_bound((int)Q));
+        CKL(dmlp_format_report(ocs, (int)Q, (int)a->qid_base, off, text, st));
+        CK(mark(M_FORMAT, st));
+        len_src = off + Q;
+      }
+      hipLaunchKernelGGL(k_pack_small, dim3(1), dim3(64), 0, st, len_src, Lp->ovf,
+                         a->early ? estats : nullptr, small_d);
+      CK(hipGetLastError());
+      CK(hipMemcpyAsync(small, small_d, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (want_report && a->report_mode == 1)
+        CK(hipMemcpyAsync(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q),
                           hipMemcpyDeviceToHost, st));
     };
     CK(mark(M_REFINE, st));
     render();
-    CK(hipMemcpyAsync(small, Lp->ovf, sizeof(int), hipMemcpyDeviceToHost, st));
-    if (a->early) CK(hipMemcpyAsync(small + 4, estats, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
     CK(mark(M_D2H, st));
-    CK(hipStreamSynchronize(st));
+    CK(hipEventRecord(w.ev_done, st));
+    spin_wait(w.ev_done);
     CK(hipStreamSynchronize(w.side));
     w.marks_valid = w.marks_on;
     if (a->early) {
-      a->early_waits = small[4];
-      a->early_grows = small[5];
-      a->early_timeouts = small[6];
-      if (small[6] && g_early != 0) {
+      a->early_waits = (int)small[2];
+      a->early_grows = (int)small[3];
+      a->early_timeouts = (int)small[4];
+      if (small[4] && g_early != 0) {
         std::fprintf(stderr, "[dmlp] early start: %d screen wave(s) timed out waiting for the "
                      "dataset image (overflowed queries were escalated); early start is off for "
-                     "the rest of this process\n", small[6]);
+                     "the rest of this process\n", (int)small[4]);
         g_early = 0;
       }
     }
-    const int novf = small[0];
+    const int novf = (int)small[1];
     if (novf) {
       a->n_escalated = Lp->finish(novf);
       w.marks_valid = false;
@@ -1040,7 +1078,7 @@ struct Step {
       CK(hipStreamSynchronize(st));
     }
     if (want_report) {
-      a->report_len = w.s_len.p[0];
+      a->report_len = small[0];
       w.text_len = a->report_len;
     }
     if (!use_hx) a->path = 2;
