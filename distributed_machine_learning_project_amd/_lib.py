@@ -118,6 +118,7 @@ _SIGS = {
     "dmlp_kdtree_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp]),
     "dmlp_cpu_format_report": (i64, [vp, i64, i64, vp]),
     "dmlp_cpu_i32_range": (None, [vp, i64, i32p, i32p]),
+    "dmlp_host_i32_range": (None, [vp, i64, i32p, i32p]),
     "dmlp_atomic_fetch_add_i64": (i64, [vp, i64]),
     "dmlp_atomic_store_i64": (None, [vp, i64]),
     "dmlp_cpu_format_debug": (i64, [vp, vp, i32, vp, vp, i64, vp, i64]),

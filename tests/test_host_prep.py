@@ -215,3 +215,21 @@ def test_row_table_render_matches_flat():
     L.dmlp_cpu_gather_rows(tab, N, A, g.ctypes.data)
     assert np.array_equal(g.reshape(N, A), np.stack(rows))
     del keep
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 65535, 65536, 300001])
+def test_host_i32_range_matches_numpy(n):
+    """The native step's label / k scans (dmlp_host_i32_range: on the render pool above 64K
+    values) == numpy's min / max, negative values and both ends included; (0, -1) when empty."""
+    import ctypes as C
+    from distributed_machine_learning_project_amd import _lib
+    rng = np.random.default_rng(n)
+    a = rng.integers(-(2 ** 31), 2 ** 31 - 1, size=n, dtype=np.int64).astype(np.int32)
+    if n > 2:
+        a[0], a[-1] = np.int32(2 ** 31 - 1), np.int32(-(2 ** 31))
+    lo, hi = C.c_int(), C.c_int()
+    _lib.lib().dmlp_host_i32_range(a.ctypes.data, a.size, C.byref(lo), C.byref(hi))
+    if n == 0:
+        assert (lo.value, hi.value) == (0, -1)
+    else:
+        assert (lo.value, hi.value) == (int(a.min()), int(a.max()))
