@@ -1052,8 +1052,12 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
 // two queries' chains in flight with about the same registers per lane.  Members are scored two
 // per lane per batch (64 per query), so the usual ~72 members take 2 batches.  More than PM
 // surviving members hand the query back (status 1, as k_refine does past its P).
+#ifndef DMLP_PAIR_U
+#define DMLP_PAIR_U 1  // members per lane per batch (1 at 8 waves/SIMD: 239 us vs 289 us for 2 at 5, r7w)
+#endif
+constexpr int PAIR_U = DMLP_PAIR_U;
 #ifndef DMLP_PAIR_WPE
-#define DMLP_PAIR_WPE 5  // 288 vs 297 us at 6 (14 VGPRs spilled), profiles/r7n_refine_ab.txt
+#define DMLP_PAIR_WPE 8  // (U = 2: 5, 288 us; profiles/r7n_refine_ab.txt)
 #endif
 template <int KT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? DMLP_PAIR_WPE : 4))) void k_refine_pair(
@@ -1118,14 +1122,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
   Mw = max(Mw, __shfl_xor(Mw, 32));
   int nm = 0;
   dmlp::wave_sync();  // s_qf written
-  for (int j0 = 0; j0 < 4 * Mw; j0 += 64) {
+  for (int j0 = 0; j0 < 4 * Mw; j0 += 32 * PAIR_U) {
     __asm__ volatile("" ::: "memory");  // keep the s_qf reads in the loop
-    int id[2];
-    bool pass[2];
-    u32x4 w[2][KT * 4];
-    float sc[2];
+    int id[PAIR_U];
+    bool pass[PAIR_U];
+    u32x4 w[PAIR_U][KT * 4];
+    float sc[PAIR_U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PAIR_U; ++u) {
       const int jm = j0 + 32 * u + hl;
       const int g = jm >> 2;
       const int src = half * 32 + (g & 31);
@@ -1148,7 +1152,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       sc[u] = pass[u] ? xinit[pt] : 0.0f;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < PAIR_U; ++u) {
 #pragma unroll
       for (int f = 0; f < KT * 4; ++f) {
         const float4 q0 = *(const float4*)&s_qf[slot][8 * f];
