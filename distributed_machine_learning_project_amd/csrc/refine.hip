@@ -1056,6 +1056,9 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
 #define DMLP_PAIR_U 1  // members per lane per batch (1 at 8 waves/SIMD: 239 us vs 289 us for 2 at 5, r7w)
 #endif
 constexpr int PAIR_U = DMLP_PAIR_U;
+#ifndef DMLP_PAIR_RL
+#define DMLP_PAIR_RL 8  // lanes per exact row in the survivors' phase: 8 (218 us) or 16 (239 us), r8c
+#endif
 #ifndef DMLP_PAIR_WPE
 #define DMLP_PAIR_WPE 8  // (U = 2: 5, 288 us; profiles/r7n_refine_ab.txt)
 #endif
@@ -1189,6 +1192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
   // rows were half of this kernel's time: profiles/r7m_refine_ablation.txt) — squares their
   // differences (each product rounded, no FMA), and the left-to-right sum travels from lane to
   // lane by a DPP row rotate, so lane 15 ends with exactly the reference's sum.
+#if DMLP_PAIR_RL == 16
   {
     const int t16 = hl & 15, rsel = hl >> 4;
     double qa[KT][2];
@@ -1235,6 +1239,72 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       }
     }
   }
+#else
+  // 8 lanes per row (four rows per round): lane t holds attributes 4t .. 4t+3 (+ 32 u), adds its
+  // four products to its predecessor's partial sum in order, and the sum moves on by a DPP row
+  // shift — half the rounds and half the chain steps of the 16-lane form
+  {
+    const int t8 = hl & 7, rsel = hl >> 3;
+    double qa[KT][4];
+#pragma unroll
+    for (int u = 0; u < KT; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int a = 32 * u + 4 * t8 + e;
+        qa[u][e] = a < A ? Qx[(int64_t)q * A + a] : 0.0;
+      }
+    int Msw = Ms;
+    Msw = max(Msw, __shfl_xor(Msw, 32));
+    for (int r0 = 0; r0 < Msw; r0 += 4) {
+      const int j = r0 + rsel;
+      const bool rv = j < Ms;
+      const int id = rv ? s_i[slot][j] : 0;
+      const double* xr = X + (int64_t)id * A;
+      double pr[KT][4];
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const int a0 = 32 * u + 4 * t8;
+        double x[4];
+        if (rv && !(abl & 1) && a0 + 3 < A && (A & 1) == 0) {  // 16-byte aligned pairs
+          const double2 v0 = *(const double2*)(xr + a0);
+          const double2 v1 = *(const double2*)(xr + a0 + 2);
+          x[0] = v0.x; x[1] = v0.y; x[2] = v1.x; x[3] = v1.y;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = rv && !(abl & 1) && a0 + e < A ? xr[a0 + e] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const double d = a0 + e < A ? __dsub_rn(qa[u][e], x[e]) : 0.0;
+          pr[u][e] = __dmul_rn(d, d);
+        }
+      }
+      double sm = 0.0;
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        // lane 0 of the group continues from lane 7's total of the previous 32 attributes
+        const double t7 = u == 0 ? 0.0 : __shfl(sm, (lane & ~7) | 7);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          double in = t7;
+          if (t > 0) {
+            const long long b = __double_as_longlong(sm);
+            const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x111, 0xf, 0xf, false);
+            const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xf, 0xf, false);
+            in = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+          }
+          sm = t8 == t ? __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(in, pr[u][0]), pr[u][1]), pr[u][2]),
+                                   pr[u][3])
+                       : sm;
+        }
+      }
+      if (rv && t8 == 7) {
+        s_d[slot][j] = (abl & 1) ? (double)id : sm;
+        s_l[slot][j] = labels[id];
+      }
+    }
+  }
+#endif
   for (int i = hl; i < KM; i += 32) {
     s_rd[slot][i] = INFINITY;
     s_ri[slot][i] = -1;

@@ -7,7 +7,7 @@ import statistics as st
 import sys
 
 base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab"
-pats = {"screen": "k_screen_x", "refine": "k_refine<2, 1>", "fmt": "k_fmt_write"}
+pats = {"screen": "k_screen_x", "refine": "k_refine<2, 1>", "pair": "k_refine_pair", "fmt": "k_fmt_write"}
 for d in sorted(glob.glob(os.path.join(base, "*.*/"))):
     f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     if not f:
