@@ -1059,6 +1059,10 @@ constexpr int PAIR_U = DMLP_PAIR_U;
 #ifndef DMLP_PAIR_RL
 #define DMLP_PAIR_RL 8  // lanes per exact row in the survivors' phase: 8 (218 us) or 16 (239 us), r8c
 #endif
+#ifndef DMLP_PAIR_DOT2
+#define DMLP_PAIR_DOT2 1  // member scores by v_dot2c_f32_f16 (219 -> 212 us, 0 spills; r8h) or cvt + fma
+#endif
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 #ifndef DMLP_PAIR_WPE
 #define DMLP_PAIR_WPE 8  // (U = 2: 5, 288 us; profiles/r7n_refine_ab.txt)
 #endif
@@ -1081,7 +1085,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
   __shared__ double s_rd[8][KM];
   __shared__ int s_ri[8][KM];
   __shared__ int s_rl[8][KM];
+#if DMLP_PAIR_DOT2
+  __shared__ __attribute__((aligned(16))) unsigned s_qh[8][16 * KT];  // hi(q') as fp16 pairs
+#else
   __shared__ __attribute__((aligned(16))) float s_qf[8][32 * KT];  // hi(q') as fp32
+#endif
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int half = lane >> 5, hl = lane & 31;
   const int slot = wave * 2 + half;
@@ -1100,8 +1108,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
   // hi(q') as fp32 in LDS, read at each use (held in registers it pushed the kernel into spills)
   {
     const unsigned short* qh = (const unsigned short*)(qhi + (int64_t)q * KT * 4);
+#if DMLP_PAIR_DOT2
+    for (int a = hl; a < 16 * KT; a += 32)
+      s_qh[slot][a] = act ? (unsigned)qh[2 * a] | ((unsigned)qh[2 * a + 1] << 16) : 0u;
+#else
     for (int a = hl; a < 32 * KT; a += 32)
       s_qf[slot][a] = act ? (float)__builtin_bit_cast(_Float16, qh[a]) : 0.0f;
+#endif
   }
   if (act)
     for (int i = k + hl; i < kstride; i += 32) {
@@ -1158,6 +1171,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
     for (int u = 0; u < PAIR_U; ++u) {
 #pragma unroll
       for (int f = 0; f < KT * 4; ++f) {
+#if DMLP_PAIR_DOT2
+        // v_dot2c_f32_f16: two exact fp16 products added into the fp32 score per instruction (at
+        // most two roundings per pair, A in all: inside the screen bound like the MFMA's chain;
+        // fp16 subnormal inputs are not flushed: tools/probe/dot2_probe.hip).  The words are taken
+        // out of the vectors first: w[u][f][q2] inside the builtin's operand compiled to word 0
+        // of each fragment for every q2 (one dword load per fragment, wrong scores)
+        const uint4 qv = *(const uint4*)&s_qh[slot][4 * f];
+        const u32x4 xv = w[u][f];
+        const unsigned qw[4] = {qv.x, qv.y, qv.z, qv.w};
+        const unsigned xw[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2)
+          sc[u] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2v, qw[q2]),
+                                         __builtin_bit_cast(f16x2v, xw[q2]), sc[u], false);
+#else
         const float4 q0 = *(const float4*)&s_qf[slot][8 * f];
         const float4 q1 = *(const float4*)&s_qf[slot][8 * f + 4];
         const float qf[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
@@ -1168,6 +1196,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
           sc[u] = __builtin_fmaf(qf[2 * q2], (float)__builtin_bit_cast(_Float16, (unsigned short)(xw & 0xffffu)), sc[u]);
           sc[u] = __builtin_fmaf(qf[2 * q2 + 1], (float)__builtin_bit_cast(_Float16, (unsigned short)(xw >> 16)), sc[u]);
         }
+#endif
       }
       const bool keep = pass[u] && sc[u] >= hq;
       const unsigned long long bm = __ballot(keep);
@@ -1240,41 +1269,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
     }
   }
 #else
-  // 8 lanes per row (four rows per round): lane t holds attributes 4t .. 4t+3 (+ 32 u), adds its
-  // four products to its predecessor's partial sum in order, and the sum moves on by a DPP row
-  // shift — half the rounds and half the chain steps of the 16-lane form
+  // 8 lanes per row (four rows per round; DMLP_PAIR_RL=4: 4 lanes, eight rows): lane t holds
+  // attributes E t .. E t + E-1 (+ 32 u), adds its E products to its predecessor's partial sum in
+  // order, and the sum moves on by a DPP row shift — fewer rounds and chain steps than 16 lanes
   {
-    const int t8 = hl & 7, rsel = hl >> 3;
-    double qa[KT][4];
+    constexpr int RL = DMLP_PAIR_RL, E = 32 / RL;
+    const int t8 = hl & (RL - 1), rsel = hl / RL;
+    double qa[KT][E];
 #pragma unroll
     for (int u = 0; u < KT; ++u)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int a = 32 * u + 4 * t8 + e;
+      for (int e = 0; e < E; ++e) {
+        const int a = 32 * u + E * t8 + e;
         qa[u][e] = a < A ? Qx[(int64_t)q * A + a] : 0.0;
       }
     int Msw = Ms;
     Msw = max(Msw, __shfl_xor(Msw, 32));
-    for (int r0 = 0; r0 < Msw; r0 += 4) {
+    for (int r0 = 0; r0 < Msw; r0 += 32 / RL) {
       const int j = r0 + rsel;
       const bool rv = j < Ms;
       const int id = rv ? s_i[slot][j] : 0;
       const double* xr = X + (int64_t)id * A;
-      double pr[KT][4];
+      double pr[KT][E];
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
-        const int a0 = 32 * u + 4 * t8;
-        double x[4];
-        if (rv && !(abl & 1) && a0 + 3 < A && (A & 1) == 0) {  // 16-byte aligned pairs
-          const double2 v0 = *(const double2*)(xr + a0);
-          const double2 v1 = *(const double2*)(xr + a0 + 2);
-          x[0] = v0.x; x[1] = v0.y; x[2] = v1.x; x[3] = v1.y;
+        const int a0 = 32 * u + E * t8;
+        double x[E];
+        if (rv && !(abl & 1) && a0 + E - 1 < A && (A & 1) == 0) {  // 16-byte aligned pairs
+#pragma unroll
+          for (int e = 0; e < E; e += 2) {
+            const double2 v = *(const double2*)(xr + a0 + e);
+            x[e] = v.x;
+            x[e + 1] = v.y;
+          }
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = rv && !(abl & 1) && a0 + e < A ? xr[a0 + e] : 0.0;
+          for (int e = 0; e < E; ++e) x[e] = rv && !(abl & 1) && a0 + e < A ? xr[a0 + e] : 0.0;
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < E; ++e) {
           const double d = a0 + e < A ? __dsub_rn(qa[u][e], x[e]) : 0.0;
           pr[u][e] = __dmul_rn(d, d);
         }
@@ -1282,23 +1315,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       double sm = 0.0;
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
-        // lane 0 of the group continues from lane 7's total of the previous 32 attributes
-        const double t7 = u == 0 ? 0.0 : __shfl(sm, (lane & ~7) | 7);
+        // lane 0 of the group continues from the last lane's total of the previous 32 attributes
+        const double tl = u == 0 ? 0.0 : __shfl(sm, (lane & ~(RL - 1)) | (RL - 1));
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          double in = t7;
+        for (int t = 0; t < RL; ++t) {
+          double in = tl;
           if (t > 0) {
             const long long b = __double_as_longlong(sm);
             const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x111, 0xf, 0xf, false);
             const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xf, 0xf, false);
             in = __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
           }
-          sm = t8 == t ? __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(in, pr[u][0]), pr[u][1]), pr[u][2]),
-                                   pr[u][3])
-                       : sm;
+          double v = in;
+#pragma unroll
+          for (int e = 0; e < E; ++e) v = __dadd_rn(v, pr[u][e]);
+          sm = t8 == t ? v : sm;
         }
       }
-      if (rv && t8 == 7) {
+      if (rv && t8 == RL - 1) {
         s_d[slot][j] = (abl & 1) ? (double)id : sm;
         s_l[slot][j] = labels[id];
       }
