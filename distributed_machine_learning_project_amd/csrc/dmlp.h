@@ -207,6 +207,16 @@ int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt, const
                         int kstride, const int* labels, int label_lo, int label_hi,
                         int* out_label, uint64_t* out_cs, int* status, int* ovf_count,
                         int collect, void* stream);
+// dmlp_refine_groups with the image also point-major (xrow, from dmlp_x1_rowmajor; nullptr: none)
+int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
+                          int S, const double* X, int A, const double* Qx, const void* xfrag,
+                          const void* xrow, const float* xinit, const void* qhi, int KT, int hl,
+                          int64_t n_points, const int* qidx, const int* qk, int nq, double* out_d,
+                          int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
+                          int* out_label, uint64_t* out_cs, int* status, int* ovf_count,
+                          void* stream);
+// the host-rendered fp16 tile image (n_tiles x 64 points x 64 KT bytes) copied point-major
+int dmlp_x1_rowmajor(const void* xfrag, int64_t n_tiles, int KT, void* xrow, void* stream);
 
 // Large k on the single-term screen (screen_x1.hip): first-pass thresholds (S1 slices, k' =
 // ceil(k / S1)) -> per-query seeds (+inf: a slice overflowed), then the COLLECT pass at those

@@ -166,6 +166,12 @@ bool early_on() {
 }
 constexpr int kEarlySlices = 8;  // dataset image slices behind the query operands (profiles/r6f)
 // query render slices under the early start (profiles/r6i: 4 is best)
+// DMLP_PAIR_ROWMAJOR=1: the pair refine reads its members from a point-major copy of the fp16
+// image (one 64-byte run per member) instead of the tile image (A/B, off by default)
+bool rowmajor_on() {
+  static const bool on = getenv("DMLP_PAIR_ROWMAJOR") && getenv("DMLP_PAIR_ROWMAJOR")[0] == '1';
+  return on;
+}
 int early_qchunks() {
   static const int q = std::min(16, std::max(1, env_int("DMLP_FAST_QCHUNKS", 4)));
   return q;
@@ -311,6 +317,7 @@ struct Ctx {
   DBuf<int64_t> small64_d;
   hipEvent_t ev_done = nullptr;
   DBuf<short> dx_hi, dq_hi;
+  DBuf<short> dx_row;  // the fp16 image point-major (dmlp_x1_rowmajor) for the pair refine
   DBuf<float> dx_in, dq_n;
   DBuf<unsigned> dwords;  // [0] xnmax, [1] bad, [2, 2+S) ready words, [2+S, 2+2S) slice norms,
                           // [2+2S, 2+2S+4) early-start stats
@@ -391,6 +398,7 @@ struct HostOps {
   int rdy_tiles = 1, rdy_n = 0;
   const unsigned* xnm_sl = nullptr;
   unsigned* estats = nullptr;
+  const void* xrow = nullptr;  // xhi point-major (set once its copy kernel is queued), or none
 };
 
 // ---------------------------------------------------------------- the dispatcher
@@ -513,9 +521,9 @@ struct Local {
                            cc, ch, st));
       }
       wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
-      CKL(dmlp_refine_groups(cap, ci, cc, ch, S, X, A, Qx, xf, xi, qh, KT, hl, N,
-                             idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
-                             fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, st));
+      CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
+                                qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
+                                fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, st));
       return;
     }
     if (impl == 4) {
@@ -1012,6 +1020,13 @@ struct Step {
               CK(hipMemcpyAsync(rdy + i, one, sizeof(unsigned), hipMemcpyHostToDevice, w.side));
             }
             CK(mark(M_DATA, w.side));
+          }
+          if (with_hx && KT <= 2 && rowmajor_on()) {
+            // the pair refine's point-major image, behind the whole image on the side stream
+            // (the re-rank waits for the rows' event recorded after it)
+            short* xr = w.dx_row.get(nt * 64 * W);
+            CKL(dmlp_x1_rowmajor(hx.xhi, nt, KT, xr, w.side));
+            hx.xrow = xr;
           }
           issue_rows_now(Xd, Qd, lab_d);
         };

@@ -1071,11 +1071,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int cap,
     const float* __restrict__ cand_h, const double* __restrict__ X, int A,
     const double* __restrict__ Qx, const int* __restrict__ qidx, const int* __restrict__ qk,
-    int nq, const u32x4* __restrict__ xfrag, const float* __restrict__ xinit,
-    const bf16x8* __restrict__ qhi, int n_points, double* __restrict__ out_d,
-    int* __restrict__ out_i, int kstride, const int* __restrict__ labels,
-    int* __restrict__ out_label, uint64_t* __restrict__ out_cs, int* __restrict__ status,
-    int* __restrict__ ovf_count, int abl) {
+    int nq, const u32x4* __restrict__ xfrag, const u32x4* __restrict__ xrow,
+    const float* __restrict__ xinit, const bf16x8* __restrict__ qhi, int n_points,
+    double* __restrict__ out_d, int* __restrict__ out_i, int kstride,
+    const int* __restrict__ labels, int* __restrict__ out_label, uint64_t* __restrict__ out_cs,
+    int* __restrict__ status, int* __restrict__ ovf_count, int abl) {
   constexpr int PM = 64;   // surviving members per query
   constexpr int KM = 64;   // k
   constexpr int EC = 4;    // group entries held per lane (cap <= 128)
@@ -1158,13 +1158,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       id[u] = (int)(e & 0xffffu) * 4 + (jm & 3);
       pass[u] = g < M && e >= kh && id[u] < n_points;
       const int pt = pass[u] ? id[u] : 0;
-      const u32x4* fr = xfrag + (int64_t)(pt >> 6) * (4 * KT * 64) + (pt & 15);
+      if (xrow) {  // the point's 64 * KT bytes in one run (k_x1_rowmajor): one line per member
+        const u32x4* fr = xrow + (int64_t)pt * (4 * KT);
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt)
+        for (int f = 0; f < 4 * KT; ++f)
+          w[u][f] = pass[u] && !(abl & 2) ? fr[f] : u32x4{0, 0, 0, 0};
+      } else {
+        const u32x4* fr = xfrag + (int64_t)(pt >> 6) * (4 * KT * 64) + (pt & 15);
 #pragma unroll
-        for (int kq = 0; kq < 4; ++kq)
-          w[u][kt * 4 + kq] = pass[u] && !(abl & 2) ? fr[(int64_t)((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq]
-                                      : u32x4{0, 0, 0, 0};
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+          for (int kq = 0; kq < 4; ++kq)
+            w[u][kt * 4 + kq] = pass[u] && !(abl & 2) ? fr[(int64_t)((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq]
+                                        : u32x4{0, 0, 0, 0};
+      }
       sc[u] = pass[u] ? xinit[pt] : 0.0f;
     }
 #pragma unroll
@@ -1412,14 +1419,14 @@ extern "C" int dmlp_refine(int cap, const int* cand_ids, const int* cand_cnt, in
   return 0;
 }
 
-extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt,
-                                   const float* cand_h, int S, const double* X, int A,
-                                   const double* Qx, const void* xfrag, const float* xinit,
-                                   const void* qhi, int KT, int hl, int64_t n_points,
-                                   const int* qidx, const int* qk, int nq, double* out_d,
-                                   int* out_i, int kstride, const int* labels, int label_lo,
-                                   int label_hi, int* out_label, uint64_t* out_cs, int* status,
-                                   int* ovf_count, int collect, void* stream) {
+static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
+                              const float* cand_h, int S, const double* X, int A, const double* Qx,
+                              const void* xfrag, const void* xrow, const float* xinit,
+                              const void* qhi, int KT, int hl, int64_t n_points, const int* qidx,
+                              const int* qk, int nq, double* out_d, int* out_i, int kstride,
+                              const int* labels, int label_lo, int label_hi, int* out_label,
+                              uint64_t* out_cs, int* status, int* ovf_count, int collect,
+                              void* stream) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
   if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return -1;
@@ -1451,13 +1458,15 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
     const dim3 grid((unsigned)((nq + 7) / 8));
     if (KT == 1)
       hipLaunchKernelGGL((k_refine_pair<1>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
-                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
-                         (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
+                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
+                         (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
+                         kstride, labels, out_label,
                          out_cs, status, ovf_count, pair_abl);
     else
       hipLaunchKernelGGL((k_refine_pair<2>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
-                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag, xinit,
-                         (const bf16x8*)qhi, (int)n_points, out_d, out_i, kstride, labels, out_label,
+                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
+                         (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
+                         kstride, labels, out_label,
                          out_cs, status, ovf_count, pair_abl);
     DMLP_LAUNCH_CHECK();
     return 0;
@@ -1501,6 +1510,60 @@ extern "C" int dmlp_refine_groups_exact(int cap, const int* cand_ids, const int*
   hipLaunchKernelGGL((k_refine<8, 1, true>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride,
                      nullptr, 0, 1, nullptr, nullptr, status, ovf_count, gin);
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt,
+                                   const float* cand_h, int S, const double* X, int A,
+                                   const double* Qx, const void* xfrag, const float* xinit,
+                                   const void* qhi, int KT, int hl, int64_t n_points,
+                                   const int* qidx, const int* qk, int nq, double* out_d,
+                                   int* out_i, int kstride, const int* labels, int label_lo,
+                                   int label_hi, int* out_label, uint64_t* out_cs, int* status,
+                                   int* ovf_count, int collect, void* stream) {
+  return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, nullptr, xinit,
+                            qhi, KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
+                            label_lo, label_hi, out_label, out_cs, status, ovf_count, collect,
+                            stream);
+}
+
+extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* cand_cnt,
+                                     const float* cand_h, int S, const double* X, int A,
+                                     const double* Qx, const void* xfrag, const void* xrow,
+                                     const float* xinit, const void* qhi, int KT, int hl,
+                                     int64_t n_points, const int* qidx, const int* qk, int nq,
+                                     double* out_d, int* out_i, int kstride, const int* labels,
+                                     int label_lo, int label_hi, int* out_label, uint64_t* out_cs,
+                                     int* status, int* ovf_count, void* stream) {
+  return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xrow, xinit, qhi,
+                            KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
+                            label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream);
+}
+
+// The host-rendered fp16 image (tile layout of the screen's MFMA A operand: point p's 8-element
+// chunk f at u32x4 index tile * 256 KT + ((p & 63) >> 4) KT 64 + (f >> 2) 64 + 16 (f & 3) +
+// (p & 15)) copied point-major, xrow[p][f]: the pair refine's member loads then read one 64 KT
+// byte run per member instead of 4 KT separate lines
+__global__ __launch_bounds__(256) void k_x1_rowmajor(const u32x4* __restrict__ xfrag,
+                                                     int64_t n_items, int KT,
+                                                     u32x4* __restrict__ xrow) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // = p * 4 KT + f
+  if (i >= n_items) return;
+  const int nf = 4 * KT;
+  const int64_t pt = i / nf;
+  const int f = (int)(i - pt * nf), kt = f >> 2, kq = f & 3;
+  xrow[i] = xfrag[(pt >> 6) * (4 * KT * 64) + ((((pt & 63) >> 4) * KT + kt) * 64) + 16 * kq +
+                  (pt & 15)];
+}
+
+extern "C" int dmlp_x1_rowmajor(const void* xfrag, int64_t n_tiles, int KT, void* xrow,
+                                void* stream) {
+  if (n_tiles <= 0) return 0;
+  if (KT < 1 || KT > 8) return -1;
+  const int64_t n = n_tiles * 64 * 4 * KT;
+  hipLaunchKernelGGL(k_x1_rowmajor, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const u32x4*)xfrag, n, KT, (u32x4*)xrow);
   DMLP_LAUNCH_CHECK();
   return 0;
 }
