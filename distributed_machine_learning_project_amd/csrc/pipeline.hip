@@ -166,10 +166,11 @@ bool early_on() {
 }
 constexpr int kEarlySlices = 8;  // dataset image slices behind the query operands (profiles/r6f)
 // query render slices under the early start (profiles/r6i: 4 is best)
-// DMLP_PAIR_ROWMAJOR=1: the pair refine reads its members from a point-major copy of the fp16
-// image (one 64-byte run per member) instead of the tile image (A/B, off by default)
+// The pair refine reads its members from a point-major copy of the fp16 image (one 64-byte run
+// per member: k_refine_pair 211 -> 177 us, profiles/r7n_refine_ab.txt r8i); DMLP_PAIR_ROWMAJOR=0
+// keeps the tile image
 bool rowmajor_on() {
-  static const bool on = getenv("DMLP_PAIR_ROWMAJOR") && getenv("DMLP_PAIR_ROWMAJOR")[0] == '1';
+  static const bool on = !(getenv("DMLP_PAIR_ROWMAJOR") && getenv("DMLP_PAIR_ROWMAJOR")[0] == '0');
   return on;
 }
 int early_qchunks() {
