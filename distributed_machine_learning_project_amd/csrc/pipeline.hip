@@ -165,7 +165,6 @@ bool early_on() {
   return g_early != 0;
 }
 constexpr int kEarlySlices = 8;  // dataset image slices behind the query operands (profiles/r6f)
-// query render slices under the early start (profiles/r6i: 4 is best)
 // The pair refine reads its members from a point-major copy of the fp16 image (one 64-byte run
 // per member: k_refine_pair 211 -> 177 us, profiles/r7n_refine_ab.txt r8i); DMLP_PAIR_ROWMAJOR=0
 // keeps the tile image
@@ -173,6 +172,7 @@ bool rowmajor_on() {
   static const bool on = !(getenv("DMLP_PAIR_ROWMAJOR") && getenv("DMLP_PAIR_ROWMAJOR")[0] == '0');
   return on;
 }
+// query render slices under the early start (profiles/r6i: 4 is best)
 int early_qchunks() {
   static const int q = std::min(16, std::max(1, env_int("DMLP_FAST_QCHUNKS", 4)));
   return q;
