@@ -126,6 +126,16 @@ _SIGS = {
     "dmlp_parse_body": (i64, [vp, i64, i64, i64, i64, i32, vp, vp, vp, vp, i32]),
     "dmlp_version": (C.c_char_p, []),
     "dmlp_device_count": (i32, []),
+    "dmlp_plane_slices": (i32, []),
+    "dmlp_plane_bytes": (i64, [i64, i32, i32]),
+    "dmlp_plane_init": (i32, [vp, i64, i64, i32, i32]),
+    "dmlp_plane_slice": (i32, [i64, i32, i32, i64p, i64p]),
+    "dmlp_plane_regions": (i32, [vp, i64, i32, vp, vp, vp, vp]),
+    "dmlp_plane_put_mu": (i32, [vp, i32, vp]),
+    "dmlp_plane_get_mu": (i32, [vp, i32, vp]),
+    "dmlp_plane_render": (i32, [vp, vp, vp, i64, i32, vp, i32, i32]),
+    "dmlp_plane_wait": (i32, [vp, i32, i32, i32p, C.POINTER(C.c_float)]),
+    "dmlp_plane_ready": (i32, [vp, i32, i32]),
     "dmlp_host_register": (i32, [vp, i64]),
     "dmlp_host_unregister": (i32, [vp]),
 }

@@ -208,12 +208,13 @@ int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand_cnt, const
                         int* out_label, uint64_t* out_cs, int* status, int* ovf_count,
                         int collect, void* stream);
 // dmlp_refine_groups with the image also point-major (xrow, from dmlp_x1_rowmajor; nullptr: none)
+// and kmax = the largest k of the list (the two-queries-per-wave kernel serves kmax <= 32 only)
 int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* cand_cnt, const float* cand_h,
                           int S, const double* X, int A, const double* Qx, const void* xfrag,
                           const void* xrow, const float* xinit, const void* qhi, int KT, int hl,
                           int64_t n_points, const int* qidx, const int* qk, int nq, double* out_d,
                           int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
-                          int* out_label, uint64_t* out_cs, int* status, int* ovf_count,
+                          int* out_label, uint64_t* out_cs, int* status, int* ovf_count, int kmax,
                           void* stream);
 // the host-rendered fp16 tile image (n_tiles x 64 points x 64 KT bytes) copied point-major
 int dmlp_x1_rowmajor(const void* xfrag, int64_t n_tiles, int KT, void* xrow, void* stream);
@@ -239,6 +240,38 @@ int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit, i
                          const int* qk, int nq, int kmax, const unsigned* bad, const unsigned* rdy,
                          int rdy_tiles, int rdy_n, const unsigned* xnm_sl, int* cand_ids,
                          int* cand_cnt, float* cand_h, unsigned* estats, void* stream);
+
+// ---------------------------------------------------------------- node render plane (plane.cpp)
+// P ranks of a node stepping against ONE dataset render it once: slice i of the dataset (image
+// tiles + xinit + max norm, and its rows as lossless int32 / fp64) is rendered by rank
+// i % renderers into a node-shared page-locked segment and published by a generation flag; every
+// rank's dmlp_step (args.plane) copies the slices from there.  The callers separate calls by a
+// barrier of all plane ranks.
+typedef struct dmlp_plane {
+  void* base;       // node-shared segment of >= dmlp_plane_bytes(N, A, with_f64) bytes, set up by
+                    // dmlp_plane_init once, page-locked by every rank (dmlp_host_register)
+  int64_t bytes;
+  int rank;         // this rank among the plane's ranks
+  int renderers;    // ranks [0, renderers) render the slices, round-robin (1: rank 0 alone)
+  int with_f64;     // fp64 rows region for slices failing the int32 check (else: the node-shared X)
+  int pad_;
+  int64_t gen;      // this call's generation (> 0, equal on every rank, increasing per call)
+  double wait_s;    // bound on a wait for another rank's slice (0: 60 s)
+} dmlp_plane;
+int dmlp_plane_slices(void);
+int64_t dmlp_plane_bytes(int64_t N, int A, int with_f64);
+int dmlp_plane_init(void* base, int64_t bytes, int64_t N, int A, int with_f64);
+int dmlp_plane_slice(int64_t N, int A, int i, int64_t* t0, int64_t* t1);  // -> slice count
+int dmlp_plane_regions(const dmlp_plane* p, int64_t N, int A, void** img, void** xin, void** r32,
+                       void** r64);
+int dmlp_plane_put_mu(const dmlp_plane* p, int A, const double* mu);
+int dmlp_plane_get_mu(const dmlp_plane* p, int A, double* mu);
+int dmlp_plane_render(const dmlp_plane* p, const double* X, const double* const* Xr, int64_t N,
+                      int A, const double* mu, int what, int i);
+int dmlp_plane_wait(const dmlp_plane* p, int what, int i, int* bits, float* nmax);
+int dmlp_plane_ready(const dmlp_plane* p, int what, int i);
+int dmlp_plane_rows_f64(const dmlp_plane* p, int64_t N, int A, int i, const double* X,
+                        double* dst);
 
 // ---------------------------------------------------------------- the native pipeline (pipeline.hip)
 // Bump arenas for the pipeline's grow-only buffers, reserved once before any timed call (the
@@ -287,6 +320,8 @@ typedef struct dmlp_step_args {
   char* report_dst;           // page-locked, >= dmlp_format_bound(Q) bytes (mode 1)
   int64_t report_cap;
   void* stream;
+  const dmlp_plane* plane;    // node render plane (null: this rank renders the whole dataset);
+                              // consumers (rank >= renderers) may pass X = Xr = null
   // results
   int64_t report_len;
   int path;                   // 0 host-rendered screen operands, 2 device image (range)

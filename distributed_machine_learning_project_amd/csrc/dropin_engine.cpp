@@ -9,8 +9,16 @@
 //
 // Engine::KNN (timed): on one rank, hands the fast path tables of pointers to the harness's own
 // attribute vectors (KnnCore::KNN_rows: the host render and the int32 row pack read them in
-// place); otherwise, or when that path does not apply, packs the AoS vectors (K1) into
-// page-locked rows with a thread pool and runs KnnCore::KNN.  Then it emits the report:
+// place).  At P > 1 on one node (the farm, run_bench.sh config 4's `mpirun ./engine`), the node
+// window: an MPI-3 shared-memory window every rank joined and page-locked in the MPI_Init hook
+// (untimed).  Rank 0 puts labels, k and the other ranks' query rows into it, and its native step
+// renders the dataset's screen image and rows into the window's render plane (plane.cpp) from
+// the harness's vectors; every rank runs the native step (pipeline.hip dmlp_step) on its own
+// query block straight from the window over its own PCIe link and copies its report lines into
+// the window at its byte offset — no funnel through GPU 0, no dataset broadcast.  Otherwise, or
+// when that path does not apply (the DEBUG listing, other strategies, KNN_WINDOW=0), it packs
+// the AoS vectors (K1) into page-locked rows with a thread pool and runs KnnCore::KNN.  Then it
+// emits the report:
 //   * release build: the "Query <id> checksum: <u64>" lines are rendered on the GPU and written
 //     to std::cout in one piece — the stream reportResult writes to (common.cpp:70), so stdout
 //     is byte-identical to Q reportResult calls without 131072 iostream formats on the host;
@@ -32,9 +40,85 @@
 
 namespace {
 
+// The node window (P > 1, every rank on one node): [control 64 KiB | labels | k | query rows |
+// report text | render plane], rank 0's MPI-3 shared allocation, mapped and page-locked by every
+// rank.  Sized once in the MPI_Init hook (KNN_WINDOW_MB, default 512) and grown collectively when
+// a call's input does not fit.
+struct NodeWindow {
+  MPI_Comm node = MPI_COMM_NULL;
+  MPI_Win win = MPI_WIN_NULL;
+  char* base = nullptr;
+  int64_t bytes = 0;
+  bool registered = false, gpu = false;
+  int64_t gen = 0;  // calls through the window (every rank counts the same calls)
+  struct Layout {
+    int64_t labels, k, qx, out, plane, plane_bytes, total;
+  };
+  static int64_t up(int64_t b) { return (b + 4095) & ~int64_t(4095); }
+  static Layout layout(int64_t N, int64_t Q, int A) {
+    Layout L;
+    L.labels = 65536;
+    L.k = L.labels + up(N * 4);
+    L.qx = L.k + up(Q * 4);
+    L.out = L.qx + up(Q * A * 8);
+    L.plane = L.out + up(dmlp_format_bound((int)std::max<int64_t>(Q, 1)));
+    L.plane_bytes = std::max<int64_t>(0, dmlp_plane_bytes(N, A, 1));
+    L.total = L.plane + up(L.plane_bytes);
+    return L;
+  }
+  // control words: [0] the call's flag (labels, k and the plane header are in place), [8 + r]
+  // rank r's query rows are in place (both = the call's generation)
+  int64_t* ctrl() { return (int64_t*)base; }
+  bool valid() const { return base != nullptr; }
+  // collective over the node: a window of at least `want` bytes
+  void create(int rank, int64_t want, bool gpu_) {
+    gpu = gpu_;
+    if (node == MPI_COMM_NULL) MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0,
+                                                   MPI_INFO_NULL, &node);
+    char* mine = nullptr;
+    MPI_Win_allocate_shared(rank == 0 ? (MPI_Aint)want : 0, 1, MPI_INFO_NULL, node, &mine, &win);
+    MPI_Aint sz = 0;
+    int du = 1;
+    MPI_Win_shared_query(win, 0, &sz, &du, &base);
+    bytes = (int64_t)sz;
+    if (rank == 0) std::memset(base, 0, 65536);
+    MPI_Barrier(node);
+    // page-locked on every rank: each GPU's copies from it run as DMA over its own link
+    if (gpu) registered = dmlp_host_register(base, bytes) == 0;
+  }
+  void destroy() {
+    if (registered) dmlp_host_unregister(base);
+    registered = false;
+    if (win != MPI_WIN_NULL) MPI_Win_free(&win);
+    base = nullptr;
+    bytes = 0;
+  }
+  void free_all() {
+    destroy();
+    if (node != MPI_COMM_NULL) MPI_Comm_free(&node);
+  }
+};
+
+int64_t load_acq(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+void store_rel(int64_t* p, int64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+// spin until *p == v (bounded: KNN_TIMEOUT_S, default 600 s)
+void wait_word(const int64_t* p, int64_t v, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const double lim = getenv("KNN_TIMEOUT_S") ? std::atof(getenv("KNN_TIMEOUT_S")) : 600.0;
+  for (int spin = 0; load_acq(p) != v; ++spin) {
+    if (spin < 4096) continue;
+    std::this_thread::yield();
+    if ((spin & 4095) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim)
+      throw std::runtime_error(std::string("node window: timed out waiting for ") + what);
+  }
+}
+
 struct DropinState {
   dmlp_rt::Runtime rt;
   std::unique_ptr<dmlp_rt::KnnCore> core;
+  NodeWindow win;
+  bool use_window = false, cpu_window = false;
   // the row index's tables, kept across calls: fresh vectors every call cost ~1 ms of page
   // faults and zero-fills at the bench shape (profiles/r4l_dropin_trace.txt "index")
   std::vector<int> labels, k;
@@ -69,12 +153,38 @@ void start_engine() {
   const char* ex = getenv("KNN_EXACT");
   s->rt.init(strategy != "serial");
   dmlp_rt::HostBuf<double>::use_pinned() = s->rt.gpu;
-  s->core.reset(new dmlp_rt::KnnCore(s->rt, strategy, kListsMode, ex && std::string(ex) == "1"));
+  // the node window (P > 1, farm, release build, every rank on one node); KNN_DEVICE=cpu with
+  // KNN_STRATEGY=farm runs the same window protocol on the CPU (tests at np 2 / 3)
+  const bool farm_env = st && std::string(st) == "farm";
+  const bool want_window = s->rt.world > 1 && !kListsMode && !(getenv("KNN_WINDOW") &&
+                           std::string(getenv("KNN_WINDOW")) == "0") &&
+                           ((s->rt.gpu && strategy == "farm") || (cpu && farm_env));
+  if (want_window) {
+    int all_here = 0;
+    {
+      MPI_Comm node;
+      MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+      int nsize = 0;
+      MPI_Comm_size(node, &nsize);
+      MPI_Comm_free(&node);
+      all_here = nsize == s->rt.world;
+      MPI_Allreduce(MPI_IN_PLACE, &all_here, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+    }
+    if (all_here) {
+      const char* mb = getenv("KNN_WINDOW_MB");
+      const int64_t want = (mb ? std::max(1L, std::atol(mb)) : 512L) << 20;
+      s->win.create(s->rt.rank, want, s->rt.gpu);
+      s->use_window = true;
+      s->cpu_window = !s->rt.gpu;
+    }
+  }
+  s->core.reset(new dmlp_rt::KnnCore(s->rt, strategy, kListsMode, ex && std::string(ex) == "1",
+                                     false, s->use_window));
   // the one-rank fast path's row index tables, allocated and faulted in here (untimed, before
   // the harness parses its input): built fresh inside the timed KNN call, their first-touch
   // page faults cost ~0.5 ms at the bench shape.  KNN_INDEX_RESERVE rows each (default 2^20;
   // a larger input grows them in the call as before).
-  if (s->rt.world == 1) {
+  if (s->rt.world == 1 || s->use_window) {
     const char* rv = getenv("KNN_INDEX_RESERVE");
     const size_t n = rv ? (size_t)std::max(0L, std::atol(rv)) : (size_t(1) << 20);
     s->labels.assign(n, 0);
@@ -89,6 +199,7 @@ void stop_engine() {
   DropinState* s = state();
   if (!s) return;
   s->core.reset();
+  s->win.free_all();
   s->rt.finalize();
   delete s;
   state() = nullptr;
@@ -189,6 +300,105 @@ void write_report(const char* text, size_t len, const std::vector<Query>& querie
   }
 }
 
+// ---------------------------------------------------------------- the node-window call (P > 1)
+// Every rank, after the meta broadcast.  Rank 0 (root) holds the harness's vectors; returns on
+// rank 0 the report bytes' location in the window.
+void window_call(DropinState* s, const std::vector<Query>* queries, dmlp_rt::Input* in,
+                 const int64_t meta[6], const char** text, size_t* text_len) {
+  const int P = s->rt.world, r = s->rt.rank;
+  const int64_t N = meta[0], Q = meta[1];
+  const int A = (int)meta[2];
+  NodeWindow& W = s->win;
+  const NodeWindow::Layout L = NodeWindow::layout(N, Q, A);
+  if (L.total > W.bytes) {  // collective (every rank computed the same size): grow
+    W.destroy();
+    W.create(r, L.total, W.gpu);
+  }
+  const int64_t gen = ++W.gen;
+  char* b = W.base;
+  int* labels = (int*)(b + L.labels);
+  int* kk = (int*)(b + L.k);
+  double* qx = (double*)(b + L.qx);
+  std::vector<int64_t> cnt, off;
+  dmlp_rt::block_partition(Q, P, cnt, off);
+  dmlp_plane pl{};
+  pl.base = b + L.plane;
+  pl.bytes = L.plane_bytes;
+  pl.rank = r;
+  pl.renderers = 1;  // only rank 0 holds the dataset (common.cpp:93-117)
+  pl.with_f64 = 1;   // the other ranks have no rows to fall back on
+  pl.gen = gen;
+  if (r == 0) {
+    if (dmlp_plane_init(pl.base, pl.bytes, N, A, 1) != 0) throw std::runtime_error("plane init");
+    std::memcpy(labels, in->labels.data(), N * sizeof(int));
+    std::memcpy(kk, in->k.data(), Q * sizeof(int));
+    store_rel(W.ctrl(), gen);
+    // the other ranks' query rows, rank by rank (each released as soon as it is in place)
+    for (int t = 1; t < P; ++t) {
+      if (cnt[t]) dmlp_cpu_gather_rows(s->qr.data() + off[t], cnt[t], A, qx + off[t] * A);
+      store_rel(W.ctrl() + 8 + t, gen);
+    }
+  } else {
+    wait_word(W.ctrl(), gen, "the call's labels and k");
+    wait_word(W.ctrl() + 8 + r, gen, "this rank's query rows");
+  }
+  const int64_t a0 = off[r], nl = cnt[r];
+  const int lo = (int)meta[3], hi = (int)meta[4], kmax = (int)meta[5];
+  int64_t len = 0;
+  std::vector<char> cpu_text;
+  if (!s->cpu_window) {
+    // the native step: rank 0 renders the dataset into the plane from the harness's vectors
+    len = s->core->step_block(r == 0 ? s->xr.data() : nullptr, N, A, labels, lo, hi, kmax,
+                              r == 0 ? nullptr : qx + a0 * A, r == 0 ? s->qr.data() : nullptr,
+                              kk + a0, nl, a0, &pl);
+  } else {
+    // the same protocol on the CPU: rank 0 renders the plane's rows, every rank rebuilds the
+    // dataset from them and runs the exact brute force on its block
+    int64_t t0 = 0, t1 = 0;
+    const int ns = N > 0 ? dmlp_plane_slice(N, A, 0, &t0, &t1) : 0;
+    if (r == 0)
+      for (int i = 0; i < ns; ++i)
+        if (dmlp_plane_render(&pl, nullptr, s->xr.data(), N, A, nullptr, 2, i) < 0)
+          throw std::runtime_error("plane render");
+    std::vector<double> X((size_t)N * A);
+    for (int i = 0; i < ns; ++i)
+      if (dmlp_plane_rows_f64(&pl, N, A, i, nullptr, X.data()) != 0)
+        throw std::runtime_error("node window: plane rows");
+    std::vector<double> qrow((size_t)std::max<int64_t>(nl, 1) * A);
+    if (r == 0) dmlp_cpu_gather_rows(s->qr.data(), nl, A, qrow.data());
+    else std::memcpy(qrow.data(), qx + a0 * A, sizeof(double) * nl * A);
+    const int ks = std::max(1, kmax);
+    std::vector<double> d((size_t)std::max<int64_t>(nl, 1) * ks);
+    std::vector<int> ids(d.size()), lab(std::max<int64_t>(nl, 1));
+    std::vector<uint64_t> cs(lab.size());
+    if (nl) {
+      dmlp_cpu_knn(X.data(), N, A, qrow.data(), nl, kk + a0, ks, d.data(), ids.data(), 0);
+      dmlp_cpu_finalize(d.data(), ids.data(), ks, kk + a0, nl, labels, lab.data(), cs.data());
+      cpu_text.resize((size_t)dmlp_format_bound((int)nl));
+      len = dmlp_cpu_format_report(cs.data(), nl, a0, cpu_text.data());
+    }
+  }
+  std::vector<int64_t> lens(P);
+  MPI_Allgather(&len, 1, MPI_INT64_T, lens.data(), 1, MPI_INT64_T, MPI_COMM_WORLD);
+  int64_t at = 0, total = 0;
+  for (int i = 0; i < P; ++i) {
+    if (i < r) at += lens[i];
+    total += lens[i];
+  }
+  if (total > dmlp_format_bound((int)std::max<int64_t>(Q, 1)))
+    throw std::runtime_error("node window: report region too small");
+  if (len) {
+    if (s->cpu_window) std::memcpy(b + L.out + at, cpu_text.data(), (size_t)len);
+    else s->core->emit_block(b + L.out + at, len);
+  }
+  MPI_Barrier(MPI_COMM_WORLD);  // every block is in the window (and the next call may reuse it)
+  if (r == 0) {
+    *text = b + L.out;
+    *text_len = (size_t)total;
+  }
+  (void)queries;
+}
+
 }  // namespace
 
 // MPI profiling interface: the engine starts right after the harness's MPI_Init (untimed) and
@@ -219,8 +429,43 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
   s->core->trace.begin();
   bool done = false;
   auto t1 = t0;
-  const bool own_tables = root && s->rt.world == 1;
-  if (own_tables) {
+  const bool own_tables = root && (s->rt.world == 1 || s->use_window);
+  const char* win_text = nullptr;
+  size_t win_len = 0;
+  if (s->use_window) {
+    // P > 1 through the node window: labels, k and the row tables on rank 0 (no pack pass)
+    int64_t meta[6] = {0, 0, 0, 0, 1, 1};
+    if (root) {
+      std::swap(in.labels, s->labels);
+      std::swap(in.k, s->k);
+      index_rows(dataset, queries, p.num_attrs, in, s->xr, s->qr);
+      meta[0] = in.N;
+      meta[1] = in.Q;
+      meta[2] = in.A;
+      if (in.N) {
+        int lo = 0, hi = -1;
+        dmlp_host_i32_range(in.labels.data(), in.N, &lo, &hi);
+        meta[3] = lo;
+        meta[4] = (int64_t)hi + 1;
+      }
+      if (in.Q) {
+        int lo = 0, hi = 0;
+        dmlp_host_i32_range(in.k.data(), in.Q, &lo, &hi);
+        meta[5] = std::max(1, hi);
+      }
+    }
+    s->core->trace.mark("index");
+    MPI_Bcast(meta, 6, MPI_INT64_T, 0, MPI_COMM_WORLD);
+    t1 = std::chrono::steady_clock::now();
+    if (meta[2] >= 1 && meta[2] <= 256 && meta[1] <= (1 << 30)) {
+      window_call(s, &queries, &in, meta, &win_text, &win_len);
+      done = true;
+      s->core->trace.mark("window");
+    } else if (root) {  // outside the plane's shapes: the strategy pipeline below
+      std::swap(in.labels, s->labels);
+      std::swap(in.k, s->k);
+    }
+  } else if (own_tables) {
     // one rank: the fast path reads the harness's vectors in place (no pack pass)
     std::swap(in.labels, s->labels);
     std::swap(in.k, s->k);
@@ -247,6 +492,8 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
           res[j] = {out.dist[(size_t)q * ks + j], out.ids[(size_t)q * ks + j]};
         reportResult(queries[q], res, out.label[q]);
       }
+    } else if (win_text) {
+      write_report(win_text, win_len, queries);
     } else if (out.shared_text) {
       write_report(out.shared_text, out.text_len, queries);
     } else if (out.text_len) {
@@ -256,7 +503,7 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     }
   }
   s->core->trace.mark("emit");
-  if (own_tables) {  // back to the state for the next call (allocated, already faulted in)
+  if (own_tables && (!s->use_window || done)) {  // back to the state for the next call
     std::swap(in.labels, s->labels);
     std::swap(in.k, s->k);
   }

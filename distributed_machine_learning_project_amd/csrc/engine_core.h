@@ -96,6 +96,8 @@ struct SharedIn {
   const int* k = nullptr;
   char* out = nullptr;
   int64_t out_bytes = 0;
+  void* plane = nullptr;  // the node render plane's region (dmlp_plane_bytes(N, A, 0)), or null
+  int64_t plane_bytes = 0;
 };
 
 inline std::vector<char> read_all(const char* path) {
@@ -127,8 +129,11 @@ inline Input parse(const std::vector<char>& buf) {
 
 class KnnCore {
  public:
-  KnnCore(Runtime& rt, std::string strategy, bool debug, bool exact, bool dynamic = false)
-      : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact), dynamic_(dynamic) {
+  // warm_step: warm the native step up even at P > 1 (the drop-in's node-window farm)
+  KnnCore(Runtime& rt, std::string strategy, bool debug, bool exact, bool dynamic = false,
+          bool warm_step = false)
+      : rt_(rt), strategy_(std::move(strategy)), debug_(debug), exact_(exact), dynamic_(dynamic),
+        warm_step_(warm_step) {
     total_h_.resize(1);
     trace.init(rt_.rank, rt_.gpu ? rt_.stream : nullptr);
     if (strategy_ != "farm" && strategy_ != "shard_gather" && strategy_ != "shard_reduce" &&
@@ -181,6 +186,23 @@ class KnnCore {
   // harness's per-point attribute vectors; `in` carries N, Q, A, labels and k, no rows).  Returns
   // false, with nothing done, on more ranks or another strategy: the caller then packs the rows
   // and calls KNN.
+  // One rank's block of a node-window call (the engine.h drop-in at P > 1, dropin_engine.cpp):
+  // the native step on this rank's queries, the dataset through the node render plane (plane
+  // rank 0 renders it from the harness's vectors Xr; the other ranks pass Xr = null), the report
+  // kept on the device for emit_block.  Returns the report's byte count.
+  int64_t step_block(const double* const* Xr, int64_t N, int A, const int* labels, int lo, int hi,
+                     int kmax, const double* Qx, const double* const* Qr, const int* k, int64_t nq,
+                     int64_t qid_base, const dmlp_plane* plane) {
+    N_ = N; A_ = A; lo_ = lo; hi_ = hi; kmax_ = std::max(1, kmax); Q_ = nq;
+    Output o;
+    const dmlp_step_args a = step_host(nullptr, Xr, labels, Qx, Qr, k, nq, qid_base, 2, &o, plane);
+    return a.report_len;
+  }
+  // the last step_block's report bytes -> dst (page-locked / registered), synchronously
+  void emit_block(char* dst, int64_t len) {
+    if (len) DMLPCHK(dmlp_step_emit(dst, len, rt_.stream));
+  }
+
   bool KNN_rows(Input* in, const double* const* Xr, const double* const* Qr, Output* out) {
     if (rt_.world != 1 || strategy_ != "farm" || dynamic_ || !fast_ || !in) return false;
     if (in->Q > (1 << 30)) return false;
@@ -224,7 +246,7 @@ class KnnCore {
  private:
   Runtime& rt_;
   std::string strategy_;
-  bool debug_, exact_, dynamic_;
+  bool debug_, exact_, dynamic_, warm_step_;
   // KNN_FAST=0 disables the single-GPU host-operand pipeline (A/B against the device path)
   bool fast_ = !(getenv("KNN_FAST") && std::string(getenv("KNN_FAST")) == "0");
   // host render + H2D of the screen operands in pipelined slices (the Python default too)
@@ -451,7 +473,7 @@ class KnnCore {
       rt_.sync();
     }
     const bool shm_ingress = getenv("KNN_INGRESS") && std::string(getenv("KNN_INGRESS")) == "shm";
-    if ((rt_.world == 1 || shm_ingress) && fast_) {
+    if ((rt_.world == 1 || shm_ingress || warm_step_) && fast_) {
       // the native step once on a tiny input, every k class (early start at k <= 32, the
       // two-pass screen above): its side stream, events, staging and device buffers, the host
       // pool's first job and the first copies on the side stream are all paid here (measured
@@ -539,8 +561,10 @@ class KnnCore {
  private:
   dmlp_step_args step_host(const double* X, const double* const* Xr, const int* labels,
                            const double* Qx, const double* const* Qr, const int* k, int64_t nq,
-                           int64_t qid_base, int report_mode, Output* out) {
+                           int64_t qid_base, int report_mode, Output* out,
+                           const dmlp_plane* plane = nullptr) {
     dmlp_step_args a{};
+    a.plane = plane;
     a.X = X; a.Xr = Xr; a.N = N_; a.A = A_;
     a.labels = labels; a.label_lo = lo_; a.label_hi = hi_;
     a.Qx = Qx; a.Qr = Qr; a.k = k; a.Q = nq;
@@ -616,9 +640,21 @@ class KnnCore {
     block_partition(Q_, P, cnt, off);
     const int64_t a0 = off[r], nl = cnt[r];
     int64_t len = 0;
-    if (nl) {
+    // the replicated dataset's image and rows rendered once for the node, 1/P by each rank, into
+    // the window's render plane (KNN_PLANE=0: every rank renders all of it)
+    dmlp_plane pl{};
+    const bool use_plane = sh_.plane && P > 1 && plane_on_;
+    if (use_plane) {
+      pl.base = sh_.plane;
+      pl.bytes = sh_.plane_bytes;
+      pl.rank = r;
+      pl.renderers = P;
+      pl.gen = ++plane_gen_;
+    }
+    // (a rank without queries still renders its share of the plane)
+    if (nl || use_plane) {
       const dmlp_step_args a = step_host(sh_.X, nullptr, sh_.labels, sh_.Qx + a0 * A_, nullptr,
-                                         sh_.k + a0, nl, a0, 2, out);
+                                         sh_.k + a0, nl, a0, 2, out, use_plane ? &pl : nullptr);
       len = a.report_len;
     }
     std::vector<int64_t> lens(P);
@@ -640,6 +676,8 @@ class KnnCore {
     return true;
   }
   SharedIn sh_;
+  int64_t plane_gen_ = 0;
+  bool plane_on_ = !(getenv("KNN_PLANE") && std::string(getenv("KNN_PLANE")) == "0");
 
   // ---------------------------------------------------------------- farm (bench_4)
   // ---------------------------------------------------------------- out-of-core farm

@@ -39,13 +39,16 @@ struct SharedWin {
     auto up = [](int64_t b) { return (b + 4095) & ~int64_t(4095); };
     const int64_t oX = 0, oL = up(N * A * 8), oQ = oL + up(N * 4), oK = oQ + up(Q * A * 8),
                   oO = oK + up(Q * 4), ob = up(dmlp_format_bound((int)std::max<int64_t>(Q, 1)));
-    bytes = oO + ob;
+    // + the node render plane (plane.cpp): the dataset's image and rows rendered once per call
+    const int64_t pb = std::max<int64_t>(0, dmlp_plane_bytes(N, (int)A, 0)), oP = oO + ob;
+    bytes = oP + up(pb);
     char* mine = nullptr;
     MPI_Win_allocate_shared(rt.rank == 0 ? (MPI_Aint)bytes : 0, 1, MPI_INFO_NULL, node, &mine,
                             &win);
     MPI_Aint sz = 0;
     int du = 1;
     MPI_Win_shared_query(win, 0, &sz, &du, &base);
+    if (rt.rank == 0 && pb > 0) dmlp_plane_init(base + oP, pb, N, (int)A, 0);
     if (in) {  // ingest: the parsed arrays into the segment (untimed, like the parse)
       std::memcpy(base + oX, in->X.data(), N * A * 8);
       std::memcpy(base + oL, in->labels.data(), N * 4);
@@ -63,6 +66,8 @@ struct SharedWin {
     s.k = (const int*)(base + oK);
     s.out = base + oO;
     s.out_bytes = ob;
+    s.plane = pb > 0 ? base + oP : nullptr;
+    s.plane_bytes = pb;
     eng.set_shared(s);
     MPI_Barrier(MPI_COMM_WORLD);
   }

@@ -80,6 +80,7 @@ T* need(T* p) {
 struct Arena {
   char* base = nullptr;
   size_t size = 0, used = 0;
+  int dev = -1;  // the device the (device) arena was reserved on
   std::mutex mu;
   void* take(size_t bytes) {
     std::lock_guard<std::mutex> g(mu);
@@ -96,7 +97,11 @@ struct Arena {
 Arena g_dev, g_host;
 
 void* dev_alloc(size_t bytes) {
-  void* p = g_dev.take(bytes);
+  // the arena lives on one device: a buffer for another device (a process driving two GPUs)
+  // comes from hipMalloc on the current one
+  int d = -1;
+  void* p = nullptr;
+  if (g_dev.base && hipGetDevice(&d) == hipSuccess && d == g_dev.dev) p = g_dev.take(bytes);
   if (!p && hipMalloc(&p, std::max<size_t>(bytes, 1)) != hipSuccess) p = nullptr;
   return p;
 }
@@ -524,7 +529,7 @@ struct Local {
       wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
       CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
                                 qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
-                                fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, st));
+                                fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls, st));
       return;
     }
     if (impl == 4) {
@@ -857,10 +862,68 @@ struct Step {
       }
       CK(hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, w.side));
     };
-    rows(a->X, a->Xr, N, Xd, 0);
-    rows(a->Qx, a->Qr, Q, Qd, at);
+    if (const dmlp_plane* pl = a->plane) {
+      // the dataset's rows through the node render plane: this rank renders its row slices into
+      // the segment, its own query rows privately, then copies every slice from the segment
+      plane_slices(2, [&](int i, int bits, float) {
+        int64_t t0 = 0, t1 = 0;
+        dmlp_plane_slice(N, (int)A, i, &t0, &t1);
+        const int64_t r0 = std::min<int64_t>(N, t0 * 64), r1 = std::min<int64_t>(N, t1 * 64);
+        const int64_t n = (r1 - r0) * A;
+        if (n <= 0) return;
+        void *r32 = nullptr, *r64 = nullptr;
+        CKL(dmlp_plane_regions(pl, N, (int)A, nullptr, nullptr, &r32, &r64));
+        if (bits & 2) {  // not 6-decimal: fp64 from the segment, or from the node-shared X
+          const double* src = r64 ? (const double*)r64 + r0 * A : a->X ? a->X + r0 * A : nullptr;
+          if (!src) throw Fail{-10};
+          CK(hipMemcpyAsync(Xd + r0 * A, src, n * 8, hipMemcpyHostToDevice, w.side));
+        } else {
+          int* d32 = w.d_i32.get(at + nqa) + r0 * A;
+          CK(hipMemcpyAsync(d32, (const int*)r32 + r0 * A, n * 4, hipMemcpyHostToDevice, w.side));
+          CKL(dmlp_rows_from_i32(d32, n, Xd + r0 * A, w.side));
+        }
+      }, [&]() { rows(a->Qx, a->Qr, Q, Qd, at); });
+    } else {
+      rows(a->X, a->Xr, N, Xd, 0);
+      rows(a->Qx, a->Qr, Q, Qd, at);
+    }
     CK(hipEventRecord(w.ev_rows, w.side));
     CK(mark(M_ROWS, w.side));
+  }
+
+  // The node render plane's slices of kind `what` (1 image, 2 rows): this rank renders its own
+  // (i % renderers == rank) and publishes each, then `between` (this rank's private work that
+  // needs no other rank), then consumes every slice in order — each as soon as its flag of this
+  // call is set (consume(i, bits, nmax): the copies out of the segment).  A wait bounded by the
+  // plane's wait_s that expires throws (the call fails; the other ranks' waits expire too).
+  template <class F, class G>
+  void plane_slices(int what, F&& consume, G&& between) {
+    const dmlp_plane* pl = a->plane;
+    int64_t t0 = 0, t1 = 0;
+    const int ns = dmlp_plane_slice(a->N, a->A, 0, &t0, &t1);
+    if (ns <= 0) throw Fail{-9};
+    int next = 0;
+    auto drain = [&](bool block) {
+      while (next < ns) {
+        if (!block && !dmlp_plane_ready(pl, what, next)) return;
+        int bits = 0;
+        float nm = 0.0f;
+        if (dmlp_plane_wait(pl, what, next, &bits, &nm) != 0) {
+          std::fprintf(stderr, "[dmlp] plane rank %d: no slice %d (kind %d) of call %lld from rank %d\n",
+                       pl->rank, next, what, (long long)pl->gen, next % std::max(1, pl->renderers));
+          throw Fail{-9};
+        }
+        consume(next, bits, nm);
+        ++next;
+      }
+    };
+    if (pl->rank < pl->renderers)
+      for (int i = pl->rank; i < ns; i += std::max(1, pl->renderers)) {
+        if (dmlp_plane_render(pl, a->X, a->Xr, a->N, a->A, w.s_mu.p, what, i) < 0) throw Fail{-9};
+        drain(false);
+      }
+    between();
+    drain(true);
   }
 
   int run() {
@@ -873,8 +936,16 @@ struct Step {
     a->early_waits = a->early_grows = a->early_timeouts = 0;
     w.marks_valid = false;
     w.marks_rec = 0;
+    w.text_len = 0;  // dmlp_step_emit copies only what THIS call rendered
     if (Q < 0 || N < 0 || A < 1 || Q > (1 << 30)) return -1;
-    if ((a->X == nullptr && a->Xr == nullptr && N > 0) || (a->Qx == nullptr && a->Qr == nullptr && Q > 0) ||
+    const dmlp_plane* pl = a->plane;
+    if (pl && (!pl->base || pl->rank < 0 || pl->renderers < 1 || pl->gen <= 0 ||
+               dmlp_plane_bytes(N, A, pl->with_f64) < 0 ||
+               pl->bytes < dmlp_plane_bytes(N, A, pl->with_f64)))
+      return -1;
+    // (a plane rank that renders no slice needs no dataset rows: the engine.h drop-in's ranks > 0)
+    const bool need_x = N > 0 && (!pl || pl->rank < pl->renderers);
+    if ((a->X == nullptr && a->Xr == nullptr && need_x) || (a->Qx == nullptr && a->Qr == nullptr && Q > 0) ||
         (Q > 0 && !a->k))
       return -1;
     const bool want_report = a->report_mode != 0 && a->labels;
@@ -908,14 +979,34 @@ struct Step {
     double* Xd = w.d_X.get((size_t)std::max<int64_t>(N, 1) * A);
     double* Qd = w.d_Q.get((size_t)std::max<int64_t>(Q, 1) * A);
     int* lab_d = a->labels ? w.d_lab.get(N) : nullptr;
+    // (with a plane every rank must take the same front: not a function of its own pool size)
+    const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
+                          g_tune.screen == 0 &&
+                          (g_tune.host_ops >= 2 ||
+                           (g_tune.host_ops == 1 && (pl || dmlp_host_threads() >= 2)));
     if (Q == 0) {
       a->report_len = 0;
       w.text_len = 0;
+      // no queries here, but this rank's share of the node render plane is still owed
+      if (pl && pl->rank < pl->renderers && N > 0) {
+        double* mu = w.s_mu.get(A);
+        if (x1_front) {
+          if (pl->rank == 0) {
+            if (a->Xr) dmlp_cpu_center_rows(a->Xr, std::min<int64_t>(N, 4096), A, mu);
+            else dmlp_cpu_center(a->X, std::min<int64_t>(N, 4096), A, mu);
+            CKL(dmlp_plane_put_mu(pl, A, mu));
+          } else if (dmlp_plane_get_mu(pl, A, mu) != 0) {
+            throw Fail{-9};
+          }
+        }
+        int64_t t0 = 0, t1 = 0;
+        const int ns = dmlp_plane_slice(N, A, 0, &t0, &t1);
+        for (int what = x1_front ? 1 : 2; what <= 2; ++what)
+          for (int i = pl->rank; i < ns; i += pl->renderers)
+            if (dmlp_plane_render(pl, a->X, a->Xr, N, A, mu, what, i) < 0) throw Fail{-9};
+      }
       return 0;
     }
-    const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
-                          g_tune.screen == 0 &&
-                          (g_tune.host_ops >= 2 || (g_tune.host_ops == 1 && dmlp_host_threads() >= 2));
     const bool all_a = kmin >= 1 && kmax <= dmlp_screen_x1_kmax() && kmax <= N;
     // KT <= 4 only: the early screen's waves spin while the image copies land, and on this
     // runtime host->device copies are blit KERNELS that need a free wave slot beside them.  The
@@ -944,8 +1035,13 @@ struct Step {
       float* xin = w.dx_in.get(nt * 64);
       short* qhi = w.dq_hi.get(Q * W);
       float* qn = w.dq_n.get(Q);
-      if (a->Xr) dmlp_cpu_center_rows(a->Xr, std::min<int64_t>(N, 4096), A, mu);
-      else dmlp_cpu_center(a->X, std::min<int64_t>(N, 4096), A, mu);
+      if (pl && pl->rank != 0) {
+        if (dmlp_plane_get_mu(pl, A, mu) != 0) throw Fail{-9};  // rank 0's centre, same bits
+      } else {
+        if (a->Xr) dmlp_cpu_center_rows(a->Xr, std::min<int64_t>(N, 4096), A, mu);
+        else dmlp_cpu_center(a->X, std::min<int64_t>(N, 4096), A, mu);
+        if (pl) CKL(dmlp_plane_put_mu(pl, A, mu));
+      }
       auto h2d_tiles = [&](int64_t t0, int64_t t1, const double* qx, const double* const* qr,
                            int64_t nq, unsigned* xnm_hw, void* xhi_d, void* xin_d, void* xnm_d,
                            void* qhi_d, void* qn_d, int chunks) {
@@ -964,6 +1060,16 @@ struct Step {
         CK(hipMemsetAsync(estats, 0, 4 * sizeof(unsigned), w.side));
         rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, words + 1, qhi, qn,
                        early_qchunks());
+      } else if (pl) {
+        // this rank's query operands, then the dataset image from the node render plane; the
+        // image's max norm (+inf when a slice is outside the fp16 range) into words[0]
+        rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, words + 1, qhi, qn,
+                       host_slices());
+        float mx = 0.0f;
+        if (plane_image(xhi, xin, nullptr, nullptr, &mx)) rc |= 1;
+        std::memcpy(xnm_h, &mx, 4);
+        CK(hipMemcpyAsync(words, xnm_h, 4, hipMemcpyHostToDevice, w.side));
+        CK(mark(M_DATA, w.side));
       } else {
         rc = h2d_tiles(0, nt, a->Qx, a->Qr, Q, xnm_h, xhi, xin, words, qhi, qn, host_slices());
         CK(mark(M_DATA, w.side));
@@ -1012,7 +1118,8 @@ struct Step {
             unsigned* one = w.sx_nm.get(2 + kEarlySlices);  // (slot 0 is free in early mode)
             one[0] = 1u;
             const int dly = early_delay_us();
-            for (int i = 0; i < NS; ++i) {
+            if (pl && plane_image(hx.xhi, hx.xin, rdy, xnm_sl, nullptr)) early_bad = true;
+            for (int i = 0; i < NS && !pl; ++i) {
               if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
               const int64_t t0 = (int64_t)i * rt, t1 = std::min<int64_t>(nt, t0 + rt);
               const int r2 = h2d_tiles_data(t0, t1, i);
@@ -1113,6 +1220,45 @@ struct Step {
     int64_t nt, W;
     int KT;
   } hx_data_ctx_{};
+  // The dataset image from the node render plane: every slice (rendered by this rank or another)
+  // copied from the segment into the device image xhi / xin on the side stream.  Early start
+  // (rdy != null): each slice's max norm -> xnm_sl[i], then its ready word.  Else the max over the
+  // slices -> *mx.  Returns 1 when some slice is outside the fp16 range.
+  int plane_image(const void* xhi, const float* xin, unsigned* rdy, unsigned* xnm_sl, float* mx) {
+    const dmlp_plane* pl = a->plane;
+    const int64_t N = a->N;
+    const int A = a->A;
+    const int64_t W = (int64_t)dmlp_screen_kt(A) * 32;
+    void *img = nullptr, *xi = nullptr;
+    CKL(dmlp_plane_regions(pl, N, A, &img, &xi, nullptr, nullptr));
+    unsigned* nh = w.sx_nm.get(2 + kEarlySlices);  // [0] the ready value, [2 + i] slice norms
+    nh[0] = 1u;
+    const int dly = rdy ? early_delay_us() : 0;
+    int bad = 0;
+    float m = 0.0f;
+    plane_slices(1, [&](int i, int bits, float nm) {
+      if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
+      int64_t t0 = 0, t1 = 0;
+      dmlp_plane_slice(N, A, i, &t0, &t1);
+      if (t1 > t0) {
+        CK(hipMemcpyAsync((short*)const_cast<void*>(xhi) + t0 * 64 * W,
+                          (const uint16_t*)img + t0 * 64 * W, (t1 - t0) * 64 * W * 2,
+                          hipMemcpyHostToDevice, w.side));
+        CK(hipMemcpyAsync(const_cast<float*>(xin) + t0 * 64, (const float*)xi + t0 * 64,
+                          (t1 - t0) * 64 * 4, hipMemcpyHostToDevice, w.side));
+      }
+      bad |= bits & 1;
+      m = std::max(m, nm);
+      if (rdy) {
+        std::memcpy(nh + 2 + i, &nm, 4);
+        CK(hipMemcpyAsync(xnm_sl + i, nh + 2 + i, 4, hipMemcpyHostToDevice, w.side));
+        CK(hipMemcpyAsync(rdy + i, nh, 4, hipMemcpyHostToDevice, w.side));
+      }
+    }, [] {});
+    if (mx) *mx = bad ? INFINITY : m;
+    return bad;
+  }
+
   int h2d_tiles_data(int64_t t0, int64_t t1, int i) {
     const HxData& d = hx_data_ctx_;
     double* mu = w.s_mu.p;
@@ -1149,6 +1295,7 @@ extern "C" int dmlp_arena_reserve(int64_t dev_bytes, int64_t host_bytes) {
     if (hipMalloc(&p, (size_t)dev_bytes) == hipSuccess) {
       g_dev.base = (char*)p;
       g_dev.size = (size_t)dev_bytes;
+      if (hipGetDevice(&g_dev.dev) != hipSuccess) g_dev.dev = -1;
     } else {
       rc |= 1;
     }
@@ -1191,6 +1338,9 @@ extern "C" int dmlp_knn_local(const double* X, int64_t N, int A, const double* Q
   try {
     if (Q < 0 || N < 0 || A < 1 || kstride < 1 || Q > (1 << 30)) return -1;
     if (Q == 0) return 0;
+    // every query's list (min(k, N) entries) must fit its row of out_d / out_i (as dmlp_step)
+    for (int64_t q = 0; q < Q; ++q)
+      if (std::min<int64_t>(k[q], N) > kstride) return -3;
     Ctx& w = ctx();
     wp = &w;
     Local L(w);

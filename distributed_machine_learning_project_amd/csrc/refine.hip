@@ -1426,7 +1426,7 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
                               const int* qk, int nq, double* out_d, int* out_i, int kstride,
                               const int* labels, int label_lo, int label_hi, int* out_label,
                               uint64_t* out_cs, int* status, int* ovf_count, int collect,
-                              void* stream) {
+                              void* stream, int kmax = 64) {
   if (nq <= 0) return 0;
   if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
   if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return -1;
@@ -1449,12 +1449,14 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
     DMLP_LAUNCH_CHECK();
     return 0;
   }
-  // one slice of the host's fp16 operands, k <= 64, labels: two queries per wave
-  // (k_refine_pair; DMLP_REFINE_PAIR=0: the one-query-per-wave kernel)
+  // one slice of the host's fp16 operands, k <= 32, labels: two queries per wave
+  // (k_refine_pair; DMLP_REFINE_PAIR=0: the one-query-per-wave kernel).  Its PM = 64 member slots
+  // leave >= 32 of slack above k only for k <= 32: at k near 64 any member inside the 2-eps band
+  // would hand the query back, so the class k in (32, 64] takes k_refine (P = 128 slots)
   static const bool pair_on = !(getenv("DMLP_REFINE_PAIR") && getenv("DMLP_REFINE_PAIR")[0] == '0');
   // DMLP_REFINE_ABL (timing ablations, wrong results): 1 no exact-row gathers, 2 no member loads
   static const int pair_abl = getenv("DMLP_REFINE_ABL") ? atoi(getenv("DMLP_REFINE_ABL")) : 0;
-  if (pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128) {
+  if (pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128 && kmax <= 32) {
     const dim3 grid((unsigned)((nq + 7) / 8));
     if (KT == 1)
       hipLaunchKernelGGL((k_refine_pair<1>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
@@ -1535,10 +1537,11 @@ extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* ca
                                      int64_t n_points, const int* qidx, const int* qk, int nq,
                                      double* out_d, int* out_i, int kstride, const int* labels,
                                      int label_lo, int label_hi, int* out_label, uint64_t* out_cs,
-                                     int* status, int* ovf_count, void* stream) {
+                                     int* status, int* ovf_count, int kmax, void* stream) {
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xrow, xinit, qhi,
                             KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
-                            label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream);
+                            label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream,
+                            kmax);
 }
 
 // The host-rendered fp16 image (tile layout of the screen's MFMA A operand: point p's 8-element

@@ -244,9 +244,17 @@ class StepArgs(C.Structure):
                 ("exact", C.c_int), ("out_lab", C.c_void_p), ("out_cs", C.c_void_p),
                 ("out_d", C.c_void_p), ("out_i", C.c_void_p), ("kstride", C.c_int),
                 ("report_mode", C.c_int), ("report_dst", C.c_void_p), ("report_cap", C.c_int64),
-                ("stream", C.c_void_p), ("report_len", C.c_int64), ("path", C.c_int),
+                ("stream", C.c_void_p), ("plane", C.c_void_p), ("report_len", C.c_int64),
+                ("path", C.c_int),
                 ("early", C.c_int), ("n_escalated", C.c_int), ("early_waits", C.c_int),
                 ("early_grows", C.c_int), ("early_timeouts", C.c_int)]
+
+
+class Plane(C.Structure):
+    """dmlp.h dmlp_plane: the node render plane (csrc/plane.cpp)."""
+    _fields_ = [("base", C.c_void_p), ("bytes", C.c_int64), ("rank", C.c_int),
+                ("renderers", C.c_int), ("with_f64", C.c_int), ("pad_", C.c_int),
+                ("gen", C.c_int64), ("wait_s", C.c_double)]
 
 
 @dataclass
@@ -281,7 +289,7 @@ def step_stats(reset: bool = False):
 
 
 def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_base=0,
-         exact=False, report=None, lists=False, kstride=None) -> StepResult:
+         exact=False, report=None, lists=False, kstride=None, plane=None) -> StepResult:
     """One rank's whole Engine::KNN call from host arrays (dmlp_step): X_host [N, A] /
     Q_host [Q, A] fp64, labels_host [N] int32 (page-locked or registered memory for real
     overlap; a node-shared segment is), k_host [Q] int32.
@@ -290,6 +298,8 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
               kept on the GPU for step_emit (the multi-rank egress).
       lists:  also return the sorted (dist, id) lists [Q, kstride] (the DEBUG listing).
       k_range: (a lower bound of min k, an upper bound of max k) when known, else scanned.
+      plane:  a Plane (node render plane): the dataset's image and rows are rendered once per
+              node, slice by slice, by the plane's renderers into a node-shared segment.
     Returns once everything is complete (one host sync in the common case)."""
     torch = _torch()
     L = _lib.lib()
@@ -335,6 +345,7 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
         a.report_mode = 1
         a.report_dst, a.report_cap = report.ctypes.data, report.nbytes
     a.stream = _stream()
+    a.plane = C.cast(C.pointer(plane), C.c_void_p) if plane is not None else None
     _lib.check(L.dmlp_step(C.byref(a)), "dmlp_step")
     st = pipeline_stats()
     STEP_STATS["calls"] += 1

@@ -259,8 +259,14 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             k_range = (None if kmax is None else inp.k_range_all if comm.world == 1
                        else _lib_range(kl_h))
             rep = None if debug else (inp.out if comm.world == 1 else "device")
+            # P > 1: the replicated dataset's image and rows are rendered once for the node, 1/P
+            # by each rank, into the segment's render plane (KNN_PLANE=0: every rank renders all)
+            # (the debug listing's gather is no barrier between calls: no plane there)
+            plane = (inp.plane(comm.rank, comm.world) if comm.world > 1 and not debug
+                     and os.environ.get("KNN_PLANE", "1") != "0" else None)
             r = be.step(inp.X, inp.labels, None if lo is None else (lo, hi), inp.Qx[a:b], kl_h,
-                        k_range=k_range, qid_base=a, report=rep, lists=debug, kstride=kmax)
+                        k_range=k_range, qid_base=a, report=rep, lists=debug, kstride=kmax,
+                        plane=plane)
         if debug:
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, r.dist, r.ids, r.label,
                                      r.checksum, True)

@@ -25,7 +25,9 @@ byte 64 (the dynamic farm's chunk claims, alternating per call), a barrier count
 a call generation at byte 80 (the dynamic farm: which counter a call claims from),
 per-rank int64 slots from byte 128 (report lengths), then labels i32[N], k i32[Q],
 X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), res i64[2*Q] (the dynamic farm's
-(label, checksum) per query), each section 4096-byte aligned.
+(label, checksum) per query), plane (the node render plane, csrc/plane.cpp: the dataset's fp16
+image and int32 rows, rendered once per call by all ranks together, 1/P each), each section
+4096-byte aligned.
 """
 from __future__ import annotations
 
@@ -44,11 +46,18 @@ def _up(x):
     return (x + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _plane_bytes(N, A):
+    """Bytes of the node render plane for this dataset (0: none — A beyond the screen's 256)."""
+    from .. import _lib
+    b = int(_lib.lib().dmlp_plane_bytes(N, A, 0))
+    return max(b, 0)
+
+
 def _layout(N, Q, A):
     off = {}
     o = _ALIGN
     for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A),
-                         ("out", 48 * Q + 64), ("res", 16 * Q)):
+                         ("out", 48 * Q + 64), ("res", 16 * Q), ("plane", _plane_bytes(N, A))):
         off[name] = o
         o += _up(max(nbytes, 1))
     return off, o
@@ -74,6 +83,19 @@ class SharedInput(KNNInput):
         self._nbar = 0  # barriers this process has entered
         self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
         self._pinned = False
+        self._plane_off, self._plane_bytes = off["plane"], _plane_bytes(N, A)
+        self._plane_gen = 0  # node render plane calls this process made (same on every rank)
+
+    def plane(self, rank: int, renderers: int):
+        """The node render plane for this call (ops.knn.Plane), or None when the segment has
+        none: every rank calls it once per farm call, so the generations agree."""
+        if not self._plane_bytes:
+            return None
+        from ..ops.knn import Plane
+        self._plane_gen += 1
+        return Plane(base=self._mm.ctypes.data + self._plane_off, bytes=self._plane_bytes,
+                     rank=rank, renderers=renderers, with_f64=0, gen=self._plane_gen,
+                     wait_s=float(os.environ.get("DMLP_PLANE_WAIT_S", "60")))
 
     @staticmethod
     def create(inp: KNNInput, directory: str = "/dev/shm", query_nodes=None) -> "SharedInput":
@@ -89,6 +111,10 @@ class SharedInput(KNNInput):
             _place(mm, off, N, Q, A, query_nodes)
         np.frombuffer(mm, np.int64, 4, 0)[:] = [_MAGIC, N, Q, A]
         s = SharedInput(mm, path, N, Q, A, owner=True)
+        if s._plane_bytes:
+            from .. import _lib
+            _lib.check(_lib.lib().dmlp_plane_init(mm.ctypes.data + off["plane"], s._plane_bytes,
+                                                  N, A, 0), "dmlp_plane_init")
         s.labels[:] = inp.labels
         s.k[:] = inp.k
         s.X[:] = inp.X
@@ -220,6 +246,7 @@ def _place(mm, off, N, Q, A, query_nodes):
         return
     if len(nodes) > 1:
         _mbind(base + off["X"], 8 * N * A, nodes, MPOL_INTERLEAVE)
+        _mbind(base + off["plane"], _plane_bytes(N, A), nodes, MPOL_INTERLEAVE)
     for a, b, n in query_nodes:
         if n >= 0 and b > a:
             _mbind(base + off["Qx"] + 8 * A * a, 8 * A * (b - a), [n], MPOL_PREFERRED)

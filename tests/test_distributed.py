@@ -72,6 +72,18 @@ def test_four_and_six_ranks(workload, strategy):
     assert _run(path, 6, strategy) == expect  # non-square grid (D1: heap overflow in engine.cpp)
 
 
+@pytest.mark.parametrize("strategy", ["farm", "shard_gather", "shard_reduce", "grid2d", "serial",
+                                      "ring"])
+def test_eight_ranks(workload, strategy):
+    """World size 8, the MI355X node's GPU count: grid2d is a 4 x 2 grid
+    (MPI_Dims_create), shards of 32 points against k up to 40 (N/P < k, defect D4), Q = 23 over 8
+    ranks; the dynamic farm at 8 claims from the shared counter."""
+    path, expect = workload
+    assert _run(path, 8, strategy) == expect
+    if strategy == "farm":
+        assert _run(path, 8, "farm", env_extra={"KNN_SCHEDULE": "dynamic"}) == expect
+
+
 def test_dynamic_farm(workload):
     path, expect = workload
     assert _run(path, 3, "farm", env_extra={"KNN_SCHEDULE": "dynamic"}) == expect

@@ -74,7 +74,12 @@ def test_native_step(gpu, kmax, A):
         np.testing.assert_array_equal(out.labels_np(), lab_ref)
         np.testing.assert_array_equal(out.checksums_np(), cs)
         assert K.STEP_STATS["calls"] == n0 + 1
-        assert K.pipeline_stats()["path"] == 0
+        st = K.pipeline_stats()
+        assert st["path"] == 0
+        if A == 32 and kmax <= 64:
+            # uniform data: no query may overflow the one-pass screen's refine (k near 64 once
+            # overflowed the two-queries-per-wave kernel's 64 member slots and escalated)
+            assert st["n_escalated"] == 0 and st["n_exact"] == 0, st
     sh.close()
     eng.close()
 
@@ -125,6 +130,8 @@ def test_native_step_early_start(gpu, n, A, kmax):
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
             assert r.early == (early if A <= 128 else 0)
+            if A <= 64:
+                assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
             if r.early:
                 assert r.early_timeouts == 0
                 assert r.early_waits > 0, "the screen never waited for a slice"

@@ -277,3 +277,50 @@ def test_make_engine_targets_cpu(tmp_path):
     r = subprocess.run(["make", "-C", ROOT, "-q", "engine", "engine.debug"], capture_output=True,
                        timeout=60)
     assert r.returncode == 0
+
+
+# ---------------------------------------------------------------- the drop-in's node window (P > 1)
+def _text_with_decimals(inp, decimals):
+    """The input as the reference's text format, attributes printed with `decimals` digits (9:
+    values the lossless int32 row transfer cannot carry, so the render plane ships fp64 rows)."""
+    f = f"%.{decimals}f"
+    lines = [f"{inp.X.shape[0]} {inp.Qx.shape[0]} {inp.X.shape[1]}"]
+    for lab, row in zip(inp.labels, inp.X):
+        lines.append(f"{int(lab)} " + " ".join(f % v for v in row))
+    for k, row in zip(inp.k, inp.Qx):
+        lines.append(f"Q {int(k)} " + " ".join(f % v for v in row))
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("np_", [2, 3])
+@pytest.mark.parametrize("decimals", [6, 9])
+def test_dropin_node_window_cpu(tmp_path, np_, decimals):
+    """engine.h drop-in at P > 1 through the node window (KNN_DEVICE=cpu KNN_STRATEGY=farm runs
+    the GPU path's protocol on the CPU): rank 0 puts labels, k and the other ranks' query rows
+    into the MPI-3 shared window and renders the dataset's rows into its render plane (int32, or
+    fp64 for 9-decimal data); every rank rebuilds the dataset from the plane, answers its own
+    query block and copies its report lines into the window at its offset.  The window starts at
+    1 MiB and grows collectively.  stdout == the fp64 oracle's bytes; every rank took part."""
+    rng = np.random.default_rng(np_ * 10 + decimals)
+    N, Q, A = 2100, 203, 7
+    X = rng.uniform(-20, 20, (N, A))
+    Qx = rng.uniform(-20, 20, (Q, A))
+    k = rng.integers(1, 61, Q).astype(np.int32)
+    labels = rng.integers(0, 5, N).astype(np.int32)
+    txt = _text_with_decimals(dmlp.KNNInput(labels, X, k, Qx), decimals)
+    path = tmp_path / "w.in"
+    path.write_text(txt)
+    inp = dmlp.parse_input(txt)
+    _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    exe = _ref_dropin(tmp_path) if build.reference_harness() is not None else _dropin(tmp_path)
+    env = {"KNN_DEVICE": "cpu", "KNN_STRATEGY": "farm", "KNN_WINDOW_MB": "1", "KNN_TRACE": "1"}
+    e = dict(os.environ, **env)
+    import shlex
+    cmd = [MPIEXEC, "-n", str(np_), "sh", "-c", f"exec {shlex.quote(exe)} < {shlex.quote(str(path))}"]
+    r = subprocess.run(cmd, stdin=subprocess.DEVNULL, capture_output=True, timeout=180, env=e)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout == dmlp.format_report(cs)
+    err = r.stderr.decode()
+    for rank in range(np_):  # the window protocol ran on every rank (not the serial fallback)
+        assert f"[dmlp-trace] rank {rank} window " in err, err[-2000:]

@@ -214,3 +214,110 @@ def test_bench_self_launch_rehearsal(np_):
     assert res["collective_check"]["ok"]
     assert len(res["per_rank"]) == np_
     assert all(c > 0 for c in res["collective_check"]["calls_per_rank"])
+
+
+# ---------------------------------------------------------------- wider worlds: P = 4 (2x2) and 8 (4x2)
+@pytest.mark.parametrize("strategy", ["farm", "grid2d", "shard_reduce", "shard_gather", "ring"])
+@pytest.mark.parametrize("np_", [4, 8])
+def test_native_front_end_wide(case, strategy, np_):
+    """knn_engine at the world sizes the target node runs: P = 4 makes
+    grid2d a 2 x 2 grid and P = 8 a 4 x 2 grid (column split, column merge, row-0 gather with
+    C > 1); 8 ranks share the one GPU over the host-staged plane.  == oracle bytes, every send
+    matched by a receive."""
+    path, expect = case
+    env = {"KNN_POOL_MB": "128", "KNN_HOST_POOL_MB": "32", "DMLP_HOST_THREADS": "2"}
+    assert _native(path, np_, strategy, env_extra=env) == expect
+
+
+@pytest.mark.parametrize("np_", [4, 8])
+def test_native_shared_farm_wide(case_x1, np_):
+    """knn_engine KNN_INGRESS=shm at P = 4 / 8: every rank's native step, the dataset's image and
+    rows rendered once for the node through the render plane (1/P per rank), == oracle bytes;
+    with the plane off (KNN_PLANE=0: every rank renders everything) the same bytes."""
+    (path, expect), (bad_path, bad_expect) = case_x1
+    env = {"KNN_INGRESS": "shm", "KNN_TRACE": "1", "KNN_POOL_MB": "128", "KNN_HOST_POOL_MB": "32",
+           "DMLP_HOST_THREADS": "2"}
+    out, err = _native(path, np_, "farm", env_extra=env, want_err=True)
+    assert out == expect
+    for r in range(np_):
+        assert f"rank {r} step ".encode() in err, err.decode()[-2000:]
+    assert _native(bad_path, np_, "farm", env_extra=env) == bad_expect
+    assert _native(path, np_, "farm", env_extra=dict(env, KNN_PLANE="0")) == expect
+
+
+@pytest.mark.parametrize("np_", [4])
+@pytest.mark.parametrize("strategy", ["farm", "grid2d"])
+def test_python_front_end_wide(case, case_x1, strategy, np_):
+    path, expect = case
+    env = {"DMLP_HOST_THREADS": "2"}
+    assert _python(path, np_, strategy, env) == expect
+    if strategy == "farm":  # the node-shared farm with the render plane at P = 4
+        (p1, e1), _ = case_x1
+        assert _python(p1, np_, "farm", dict(env, KNN_INGRESS="shm")) == e1
+
+
+# ---------------------------------------------------------------- the engine.h drop-in at P > 1
+@pytest.fixture(scope="module")
+def dropin_exe(tmp_path_factory):
+    from distributed_machine_learning_project_amd import build
+    d = tmp_path_factory.mktemp("dropin")
+    ref_common = build.reference_harness()
+    try:
+        if ref_common is not None:
+            return str(build.build_dropin(str(ref_common), str(d / "engine")))
+        return str(build.build_dropin(os.path.join(ROOT, "tests", "native", "mini_harness.cpp"),
+                                      str(d / "engine"),
+                                      extra_flags=['-DDMLP_COMMON_HEADER="contract_types.h"']))
+    except RuntimeError as e:
+        pytest.skip(f"drop-in build unavailable: {e}")
+
+
+@pytest.fixture(scope="module")
+def case_dec9(tmp_path_factory):
+    """9-decimal attributes: no lossless int32 rows, so the render plane ships fp64 rows."""
+    import numpy as np
+    d = tmp_path_factory.mktemp("dec9")
+    rng = np.random.default_rng(5)
+    N, Q, A = 3000, 301, 16
+    X, Qx = rng.uniform(0, 1000, (N, A)), rng.uniform(0, 1000, (Q, A))
+    k = rng.integers(1, 33, Q).astype(np.int32)
+    labels = rng.integers(0, 5, N).astype(np.int32)
+    lines = [f"{N} {Q} {A}"]
+    lines += [f"{int(l)} " + " ".join("%.9f" % v for v in row) for l, row in zip(labels, X)]
+    lines += [f"Q {int(kk)} " + " ".join("%.9f" % v for v in row) for kk, row in zip(k, Qx)]
+    txt = "\n".join(lines) + "\n"
+    p = d / "dec9.in"
+    p.write_text(txt)
+    inp = dmlp.parse_input(txt)
+    _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
+    return str(p), ref.report_lines(cs).encode()
+
+
+def _dropin_run(exe, path, np_, env_extra=None):
+    import shlex
+    env = dict(os.environ, KNN_DATA_PLANE="host", KNN_TRACE="1", KNN_POOL_MB="128",
+               KNN_HOST_POOL_MB="32", KNN_WINDOW_MB="8", DMLP_HOST_THREADS="2")
+    env.update(env_extra or {})
+    cmd = [MPIEXEC, "-n", str(np_), "sh", "-c", f"exec {shlex.quote(exe)} < {shlex.quote(path)}"]
+    r = subprocess.run(cmd, stdin=subprocess.DEVNULL, capture_output=True, env=env, timeout=180,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return r.stdout, r.stderr.decode()
+
+
+@pytest.mark.parametrize("np_", [2, 3, 4])
+def test_dropin_node_window_gpu(dropin_exe, case, case_x1, case_dec9, np_):
+    """The reference's own common.cpp + the drop-in at P > 1 (run_bench.sh config 4's
+    `mpirun ./engine < input`): the node window joined in the MPI_Init hook, rank 0's labels / k /
+    query rows in it, rank 0's native step rendering the dataset into the render plane from the
+    harness's vectors, EVERY rank's native step on its own block ([dmlp-step] rank r), report
+    lines through the window.  Inputs: k 1-40 (two screen classes), k 1-32 with an out-of-range
+    point (the device-image path), 9-decimal data (fp64 rows through the plane); the 8 MiB
+    window grows on first use.  stdout == the fp64 oracle's bytes."""
+    (p1, e1), (p2, e2) = case_x1
+    for path, expect in (case, (p1, e1), (p2, e2), case_dec9):
+        out, err = _dropin_run(dropin_exe, path, np_)
+        assert out == expect, err[-2000:]
+        for r in range(np_):
+            assert f"[dmlp-step] rank {r} path" in err, err[-2000:]
+        assert "[dmlp-trace] rank 0 window" in err

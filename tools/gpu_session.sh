@@ -22,6 +22,8 @@
 #   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
+#   plane      node render plane rehearsal: bench.py --gpus 3 / 8 on the one GPU, plane on / off
+#   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 set -u
 TAG=${1:?tag}
 shift
@@ -140,6 +142,25 @@ for task in "$@"; do
     hostprof)
       step hostprof 300 python tools/host_profile.py --steps 100
       DMLP_PIPE_DEBUG=1 step pipedebug 120 python bench.py --steps 5 --warmup 2 --no-busbw ;;
+    plane)  # node render plane: P = 3 / 8 ranks sharing the one GPU (host-staged plane), --verify,
+            # plane on / off: per-rank ms, the cgroup's CPU time in the timed region
+      for P in 3 8; do
+        Qp=$([ $P = 3 ] && echo 65536 || echo 16384)
+        for pl in 1 0; do
+          DMLP_DATA_PLANE=host KNN_PLANE=$pl step plane_p${P}_$pl 400 python bench.py --gpus $P \
+              --steps 10 --warmup 2 --min-warmup-s 1 --q-per-gpu $Qp --verify --no-busbw
+        done
+      done ;;
+    dropin_p)  # the drop-in at P = 2 / 3 through the node window on the one GPU (host-staged plane)
+      python -m distributed_machine_learning_project_amd.build --dropin \
+          distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
+      python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
+          --max 1000 --minK 16 --maxK 16 --num_labels 10 --output /tmp/dropin_bench.in > /dev/null
+      for P in 2 3; do
+        KNN_DATA_PLANE=host KNN_TRACE=1 step dropin_p$P 120 /opt/conda/bin/mpiexec -n $P sh -c \
+            "exec /tmp/eng_dropin < /tmp/dropin_bench.in > /tmp/dropin_p$P.out"
+        md5sum /tmp/dropin_p$P.out
+      done ;;
     *)
       echo "unknown task $task"; exit 2 ;;
   esac
