@@ -229,6 +229,7 @@ def main(argv=None):
                                 "early_start_calls": steps_native["early"],
                                 "early_waits": steps_native["early_waits"],
                                 "early_timeouts": steps_native["early_timeouts"],
+                                "early_query_block_waits": steps_native["early_qwaits"],
                                 "escalated_queries": steps_native["escalated"],
                                 "device_path_calls": steps_native["device_path"]}
     if thr0 and thr1:

@@ -37,6 +37,8 @@ _SIGS = {
     "dmlp_cpu_gather_rows": (None, [vp, i64, i32, vp]),
     "dmlp_cpu_rows_i32": (i32, [vp, i64, vp]),
     "dmlp_rows_from_i32": (i32, [vp, i64, vp, vp]),
+    "dmlp_render_rows": (i32, [i32, i32, vp, vp, i64, i64, i64, vp, vp, i32, vp, vp, vp, vp, vp, vp,
+                               vp, vp]),
     "dmlp_host_ops_h2d_tiles": (i32, [vp, i64, i64, i64, vp, i64, i32, vp, i32, vp, vp, vp, vp, vp,
                                       vp, vp, vp, vp, vp, i32, vp]),
     "dmlp_screen_kmax": (i32, [i32]),

@@ -59,10 +59,18 @@ def _run(cmd):
     return r
 
 
+# what the last build() did (written to _build/build_info.json and returned by build_info()):
+# the driver's "build mode" — sources compiled vs objects reused, and whether the library and
+# knn_engine were relinked — instead of a silent up-to-date check
+_INFO = {"compiled": [], "reused": [], "lib_relinked": False, "engine_relinked": False}
+
+
 def _compile(src: Path, force: bool) -> Path:
     obj = BUILD / (src.name + ".o")
     if not force and not _stale(obj, [src] + _headers()):
+        _INFO["reused"].append(src.name)
         return obj
+    _INFO["compiled"].append(src.name)
     if src.suffix == ".hip":
         # MFMA results in VGPRs: the epilogue reads every accumulator with VALU, and AGPR
         # results cost a v_accvgpr_read per value plus copies of the C-init operand
@@ -87,6 +95,7 @@ def build_lib(force: bool = False, jobs: int | None = None) -> Path:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
               "-pthread"])
         os.replace(tmp, LIB)
+        _INFO["lib_relinked"] = True
     return LIB
 
 
@@ -124,6 +133,7 @@ def build_engine(force: bool = False) -> Path | None:
     _run(["g++", *objs, "-o", str(ENGINE), f"-L{PKG}", "-ldmlp", "-Wl,-rpath,$ORIGIN",
           str(link), "-Wl,-rpath,$ORIGIN/mpi_runtime", f"-L{ROCM}/lib", "-lrccl", "-lamdhip64",
           f"-Wl,-rpath,{ROCM}/lib", "-pthread"])
+    _INFO["engine_relinked"] = True
     return ENGINE
 
 
@@ -207,11 +217,37 @@ def stage_reference_harness() -> Path | None:
 def build(force: bool = False, engine: bool = True) -> Path:
     if shutil.which(HIPCC) is None and not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
+    import time
+    t0 = time.time()
+    for key in ("compiled", "reused"):
+        _INFO[key] = []
+    _INFO["lib_relinked"] = _INFO["engine_relinked"] = False
     lib = build_lib(force)
     if engine:
         build_engine(force)
     stage_reference_harness()
+    _write_info(time.time() - t0)
     return lib
+
+
+def _write_info(seconds: float):
+    import hashlib
+    import json
+    info = dict(_INFO, arch=ARCH, seconds=round(seconds, 2),
+                mode="rebuilt" if _INFO["compiled"] or _INFO["lib_relinked"] else "up-to-date",
+                lib_sha256_16=hashlib.sha256(LIB.read_bytes()).hexdigest()[:16] if LIB.exists()
+                else None)
+    BUILD.mkdir(exist_ok=True)
+    (BUILD / "build_info.json").write_text(json.dumps(info, indent=1) + "\n")
+    print(f"[dmlp.build] {info['mode']}: {len(info['compiled'])} sources compiled, "
+          f"{len(info['reused'])} objects reused, libdmlp.so relinked: {info['lib_relinked']}, "
+          f"knn_engine relinked: {info['engine_relinked']} ({info['seconds']} s, {ARCH}, "
+          f"libdmlp {info['lib_sha256_16']})", file=sys.stderr)
+
+
+def build_info() -> dict:
+    """What the last build() in this process did (see _write_info)."""
+    return dict(_INFO)
 
 
 def main(argv=None):

@@ -81,6 +81,17 @@ void dmlp_cpu_gather_rows(const double* const* rows, int64_t nrows, int A, doubl
 // passed, 1 = ship fp64), and the device reconstruction of the fp64 rows.
 int dmlp_cpu_rows_i32(const double* src, int64_t n, int32_t* dst);
 int dmlp_rows_from_i32(const int* src, int64_t n, double* dst, void* stream);
+// The single-term screen's fp16 operands rendered on the device from rows that landed (prep.hip
+// k_render; bit for bit the host render of host_prep.cpp): src32 int32 m (x = m / 1e6, also
+// written to dst64 as the fp64 rows) or src64 fp64, rows [r0, r0 + n) of the whole array.  mode 0:
+// dataset (n, r0 multiples of 64; rows >= nvalid pad) -> tile image img, xinit xq, point-major
+// copy xrow (nullable), rounded-up max norm -> atomicMax(*nmax); mode 1: queries -> qhi img
+// [row][KT 32], qn xq.  |x - mu| out of the fp16 range sets *bad (nullable).  done / rdy
+// (nullable, *done zeroed by the caller): the last workgroup publishes *rdy = 1.
+int dmlp_render_rows(int KT, int A, const int* src32, const double* src64, int64_t r0, int64_t n,
+                     int64_t nvalid, const double* mu, double* dst64, int mode, void* img,
+                     float* xq, void* xrow, unsigned* nmax, unsigned* bad, unsigned* done,
+                     unsigned* rdy, void* stream);
 int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* stream);
 int dmlp_cpu_prep_data_tiles(const double* X, int64_t N, int A, const double* mu, int KT,
                              int64_t t0, int64_t t1, uint16_t* xhi, float* xinit, float* nmax);
@@ -240,6 +251,15 @@ int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit, i
                          const int* qk, int nq, int kmax, const unsigned* bad, const unsigned* rdy,
                          int rdy_tiles, int rdy_n, const unsigned* xnm_sl, int* cand_ids,
                          int* cand_cnt, float* cand_h, unsigned* estats, void* stream);
+// ... and the query operands in flight too (query-block early start): qrdy[b] != 0 once queries
+// [b qrdy_q, (b + 1) qrdy_q) landed (qrdy_q a multiple of 128; the list qidx must be the identity);
+// each wave waits for its own block only, counted into estats[3].
+int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
+                          int64_t n_points, const void* qhi, const float* qn, const int* qidx,
+                          const int* qk, int nq, int kmax, const unsigned* bad,
+                          const unsigned* rdy, int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
+                          int* cand_ids, int* cand_cnt, float* cand_h, unsigned* estats,
+                          const unsigned* qrdy, int qrdy_q, void* stream);
 
 // ---------------------------------------------------------------- node render plane (plane.cpp)
 // P ranks of a node stepping against ONE dataset render it once: slice i of the dataset (image
@@ -328,6 +348,7 @@ typedef struct dmlp_step_args {
   int early;                  // 1: the screen started before the dataset image landed
   int n_escalated;            // queries redone after a screen overflow
   int early_waits, early_grows, early_timeouts;
+  int early_qwaits;           // screen waves that waited for their query block (query-block start)
 } dmlp_step_args;
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
@@ -336,10 +357,12 @@ void dmlp_step_early(int on);          // 1 on, 0 off, < 0: DMLP_FAST_EARLY (def
 void dmlp_step_early_delay(int us);    // host sleep before each image slice (< 0: env)
 int dmlp_step_events(int on);          // hipEvent step timeline on / off
 int dmlp_step_timeline(double* ms, const char** names, int cap);
-// Tuning / A-B switches of the pipeline ("num_cus", "screen", "x1k", "host_ops"; pipeline.hip
-// Tuning): returns the previous value (-1: unknown key).  What the last call did (6 slots): [0]
+// Tuning / A-B switches of the pipeline ("num_cus", "screen", "x1k", "host_ops",
+// "device_render", "qb_blocks"; pipeline.hip
+// Tuning): returns the previous value (-1: unknown key).  What the last call did (7 slots): [0]
 // exact-path queries, [1] escalated queries, [2] path, [3] early start, [4] exact-path queries on
-// the fp64 MFMA screen, [5] of those handed to the fused VALU kernel (overflow).
+// the fp64 MFMA screen, [5] of those handed to the fused VALU kernel (overflow), [6] the fp16
+// screen operands were rendered on the device (prep.hip k_render).
 int dmlp_pipeline_set(const char* key, int value);
 void dmlp_pipeline_stats(int64_t* out);
 

@@ -594,11 +594,12 @@ class KnnCore {
     last_step_ = a;
     trace.mark("step");
     if (trace.on) {
-      int64_t st[6];
+      int64_t st[8];
       dmlp_pipeline_stats(st);
       std::fprintf(stderr, "[dmlp-step] rank %d path %d early %d escalated %d exact %lld "
-                   "early_waits %d early_timeouts %d\n", rt_.rank, a.path, a.early,
-                   a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts);
+                   "early_waits %d early_timeouts %d early_qwaits %d\n", rt_.rank, a.path,
+                   a.early, a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts,
+                   a.early_qwaits);
       // KNN_TRACE: the step's own hipEvent timeline (ms from step entry)
       double ms[16];
       const char* nm[16];

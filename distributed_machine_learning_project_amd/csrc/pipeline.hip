@@ -182,6 +182,28 @@ int early_qchunks() {
   static const int q = std::min(16, std::max(1, env_int("DMLP_FAST_QCHUNKS", 4)));
   return q;
 }
+// Device render (profiles/r9*): the screen's fp16 operands are rendered on the GPU (prep.hip
+// k_render) from the rows that cross PCIe for the exact re-rank anyway (lossless int32): the host
+// only packs int32 rows.  DMLP_DEVICE_RENDER=0: the host render (host_prep.cpp) as before.
+bool dr_on();  // (Tuning::device_render below)
+// Register room for the render kernels (k_render: 42 VGPRs) beside an early-start screen:
+// KT 1 / k <= 16 takes 2 x 211 VGPRs of 512, k > 16 312 at one wave per SIMD, KT 2 / k > 16 341,
+// KT 4 / k <= 16 404 — but KT 2 / k <= 16 takes 2 x 244 (hipcc -Rpass-analysis=kernel-resource-usage),
+// so there the render runs before the screen (no early start).
+bool dr_early_ok(int KT, int kmax) {
+  return KT == 1 || (KT == 2 && kmax > 16) || (KT == 4 && kmax <= 16);
+}
+// Query-block early start: the query operands cross in DMLP_QB_BLOCKS blocks after the first
+// DMLP_QB_LEAD dataset image slices, each block with a ready word, and every screen wave waits
+// only for its own block.  Off by default: with the host render, 16 blocks measured 2.63-2.69 vs
+// 2.17-2.19 ms/step (profiles/r9d_qb_ab.txt: each block's small copies and ready word are blit
+// kernels queued behind the spinning screen; the operands landed at 0.93 instead of 0.35 ms)
+constexpr int kMaxQBlocks = 64;
+int qb_blocks();  // (Tuning::qb_blocks below)
+int qb_lead() {
+  static const int v = std::max(0, env_int("DMLP_QB_LEAD", 1));
+  return v;
+}
 // test knob: the host sleeps this long before each dataset image slice of an early-start call,
 // so the screen provably waits mid-scan (tests/test_engine_gpu.py)
 int g_early_delay_us = -1;
@@ -215,6 +237,8 @@ struct Tuning {
   int screen = 0;
   int x1k = 1;
   int host_ops = 1;
+  int device_render = 1;
+  int qb_blocks = 0;
 };
 Tuning make_tuning() {
   Tuning t;
@@ -226,15 +250,20 @@ Tuning make_tuning() {
   // host operands when the render pool has at least 2 threads (Step::run: with 1 the device path
   // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
   // 3.74: profiles/r7h_host_budget.md)
+  if (env_off("DMLP_DEVICE_RENDER")) t.device_render = 0;
+  t.qb_blocks = env_int("DMLP_QB_BLOCKS", 0);
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
 }
 Tuning g_tune = make_tuning();
+bool dr_on() { return g_tune.device_render != 0; }
+int qb_blocks() { return std::min(kMaxQBlocks, std::max(0, g_tune.qb_blocks)); }
 // what the last call did (dmlp_pipeline_stats)
 struct Stats {
   int64_t n_exact = 0, n_escalated = 0, path = 0, early = 0;
   int64_t n_exact_f64 = 0, n_exact_f64_redo = 0;  // exact-path queries on the fp64 MFMA screen
+  int64_t device_render = 0;  // the screen operands were rendered on the device
 };
 Stats g_stats;
 
@@ -324,6 +353,9 @@ struct Ctx {
   hipEvent_t ev_done = nullptr;
   DBuf<short> dx_hi, dq_hi;
   DBuf<short> dx_row;  // the fp16 image point-major (dmlp_x1_rowmajor) for the pair refine
+  DBuf<double> d_mu;   // device render: the centre
+  DBuf<unsigned> dr_words;  // device render: [0, 8) slice done counters, [8, 72) query-block
+                            // done counters, [72] out-of-range flag
   DBuf<float> dx_in, dq_n;
   DBuf<unsigned> dwords;  // [0] xnmax, [1] bad, [2, 2+S) ready words, [2+S, 2+2S) slice norms,
                           // [2+2S, 2+2S+4) early-start stats
@@ -354,13 +386,16 @@ Ctx& ctx() {
 // The step's small results in one word block: [0] report length, [1] overflowed queries,
 // [2..4] early-start waits / eps growths / timeouts.
 __global__ void k_pack_small(const int64_t* __restrict__ len, const int* __restrict__ ovf,
-                             const unsigned* __restrict__ estats, int64_t* __restrict__ out) {
+                             const unsigned* __restrict__ estats, const unsigned* __restrict__ rbad,
+                             int64_t* __restrict__ out) {
   if (threadIdx.x == 0) {
     out[0] = len ? *len : 0;
     out[1] = *ovf;
     out[2] = estats ? estats[0] : 0;
     out[3] = estats ? estats[1] : 0;
     out[4] = estats ? estats[2] : 0;
+    out[5] = estats ? estats[3] : 0;
+    out[6] = rbad ? *rbad : 0;
   }
 }
 
@@ -404,6 +439,8 @@ struct HostOps {
   int rdy_tiles = 1, rdy_n = 0;
   const unsigned* xnm_sl = nullptr;
   unsigned* estats = nullptr;
+  const unsigned* qrdy = nullptr;  // query-block ready words (null: the query operands landed)
+  int qrdy_q = 128;                // queries per block
   const void* xrow = nullptr;  // xhi point-major (set once its copy kernel is queued), or none
 };
 
@@ -519,8 +556,9 @@ struct Local {
       if (hx && hx->rdy) {
         // the caller sized the early start for this all-queries pass with one slice
         if (S != 1 || idx) throw Fail{-7};
-        CKL(dmlp_screen_x1_early(KT, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd + 1, hx->rdy,
-                                 hx->rdy_tiles, hx->rdy_n, hx->xnm_sl, ci, cc, ch, hx->estats,
+        CKL(dmlp_screen_x1_early2(KT, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd + 1, hx->rdy,
+                                  hx->rdy_tiles, hx->rdy_n, hx->xnm_sl, ci, cc, ch, hx->estats,
+                                  hx->qrdy, hx->qrdy_q,
                                  st));
       } else {
         CKL(dmlp_screen_x1(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1, S, ci,
@@ -933,7 +971,7 @@ struct Step {
     a->path = 0;
     a->early = 0;
     a->n_escalated = 0;
-    a->early_waits = a->early_grows = a->early_timeouts = 0;
+    a->early_waits = a->early_grows = a->early_timeouts = a->early_qwaits = 0;
     w.marks_valid = false;
     w.marks_rec = 0;
     w.text_len = 0;  // dmlp_step_emit copies only what THIS call rendered
@@ -983,7 +1021,9 @@ struct Step {
     const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
                           g_tune.screen == 0 &&
                           (g_tune.host_ops >= 2 ||
-                           (g_tune.host_ops == 1 && (pl || dmlp_host_threads() >= 2)));
+                           (g_tune.host_ops == 1 && (pl || dr_on() || dmlp_host_threads() >= 2)));
+    // device render (the default): the GPU renders the screen operands from the landed rows
+    const bool dr = x1_front && dr_on();
     if (Q == 0) {
       a->report_len = 0;
       w.text_len = 0;
@@ -1001,7 +1041,7 @@ struct Step {
         }
         int64_t t0 = 0, t1 = 0;
         const int ns = dmlp_plane_slice(N, A, 0, &t0, &t1);
-        for (int what = x1_front ? 1 : 2; what <= 2; ++what)
+        for (int what = x1_front && !dr ? 1 : 2; what <= 2; ++what)
           for (int i = pl->rank; i < ns; i += pl->renderers)
             if (dmlp_plane_render(pl, a->X, a->Xr, N, A, mu, what, i) < 0) throw Fail{-9};
       }
@@ -1014,15 +1054,135 @@ struct Step {
     // 404 VGPR+AGPR at 1 wave/SIMD, of 512); KT 8 / k <= 32 takes all 512 (and spills), so its
     // copies could only start once the screen timed out (hipcc -Rpass-analysis=kernel-resource-usage).
     const bool early = x1_front && all_a && early_on() && KT <= 4 && nt >= 2 && nt <= 4096 &&
-                       x1_slices((int)Q, KT, kmax, nt) == 1;
+                       x1_slices((int)Q, KT, kmax, nt) == 1 && (!dr || dr_early_ok(KT, kmax));
     const int NS = early ? (int)std::min<int64_t>(kEarlySlices, nt) : 0;
     const int rt = early ? (int)((nt + NS - 1) / NS) : 1;  // image tiles per early slice
-    unsigned* words = w.dwords.get(2 + 2 * kEarlySlices + 4);
+    // query-block early start: NQB blocks of qbq queries (a multiple of 128, the widest wave's
+    // columns) rendered and copied behind the screen launch, each with its own ready word
+    int qbq = 0, NQB = 0;
+    if (early && qb_blocks() > 0) {
+      qbq = (int)(((Q + qb_blocks() - 1) / qb_blocks() + 127) / 128 * 128);
+      NQB = (int)((Q + qbq - 1) / qbq);
+      if (NQB < 2 || NQB > kMaxQBlocks) qbq = NQB = 0;
+    }
+    unsigned* words = w.dwords.get(2 + 2 * kEarlySlices + 4 + kMaxQBlocks);
     unsigned* rdy = words + 2;
     unsigned* xnm_sl = words + 2 + kEarlySlices;
     unsigned* estats = words + 2 + 2 * kEarlySlices;
+    unsigned* qrdy = words + 2 + 2 * kEarlySlices + 4;
     HostOps hx;
     bool use_hx = false, early_bad = false;
+    // ---- device render: the rows (lossless int32, fp64 where a block is not 6-decimal) cross
+    // PCIe on the side stream in dataset slices and query blocks, each followed by its render
+    // kernel (prep.hip k_render: the fp64 rows for the re-rank, the fp16 image / query fragments,
+    // the norms; under the early start its last workgroup publishes the slice's / block's ready
+    // word).  Order: the first DMLP_QB_LEAD dataset slices, the query blocks, the rest of the
+    // dataset (the plane: this rank's query blocks, then the node's slices from the segment).
+    auto dr_issue = [&]() {
+      const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
+      int* h32 = w.s_i32.get(at + nqa);
+      int* d32 = w.d_i32.get(at + nqa);
+      unsigned* drw = w.dr_words.p;
+      unsigned* rbad = drw + 72;
+      const double* mud = w.d_mu.p;
+      short* xhi_d = (short*)const_cast<void*>(hx.xhi);
+      float* xin_d = const_cast<float*>(hx.xin);
+      const int ns = (int)std::min<int64_t>(kEarlySlices, nt);
+      const int64_t rts = (nt + ns - 1) / ns;
+      unsigned* one = w.sx_nm.get(2 + kEarlySlices);
+      one[0] = 1u;
+      const int dly = early ? early_delay_us() : 0;
+      if (a->labels && N) {
+        int* lh = w.s_lab.get(N);
+        std::memcpy(lh, a->labels, N * sizeof(int));
+        CK(hipMemcpyAsync(lab_d, lh, N * sizeof(int), hipMemcpyHostToDevice, w.side));
+      }
+      auto render_x = [&](int i, const int* s32, const double* s64) {
+        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
+        if (t1 <= t0) {  // an empty slice: its ready word all the same
+          if (early) CK(hipMemcpyAsync(rdy + i, one, 4, hipMemcpyHostToDevice, w.side));
+          return;
+        }
+        CKL(dmlp_render_rows(KT, A, s32, s64, t0 * 64, (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
+                             const_cast<void*>(hx.xrow), early ? xnm_sl + i : words, rbad, drw + i,
+                             early ? rdy + i : nullptr, w.side));
+      };
+      // rows [r0, r1) of X (or Qx) -> int32 staging at h32 + off + r0 A, else fp64; returns the
+      // render's source (device int32 base or the device fp64 rows)
+      auto ship = [&](const double* src, const double* const* tab, int64_t r0, int64_t r1,
+                      int64_t off, double* dst64, const int** s32, const double** s64) {
+        const int64_t n = (r1 - r0) * A;
+        *s32 = nullptr;
+        *s64 = nullptr;
+        if (n <= 0) return;
+        if (rows_i32_on() &&
+            (tab ? dmlp_cpu_rows_i32_rows(tab + r0, r1 - r0, A, h32 + off + r0 * A)
+                 : dmlp_cpu_rows_i32(src + r0 * A, n, h32 + off + r0 * A)) == 0) {
+          CK(hipMemcpyAsync(d32 + off + r0 * A, h32 + off + r0 * A, n * 4, hipMemcpyHostToDevice,
+                            w.side));
+          *s32 = d32 + off;
+          return;
+        }
+        const double* from = src ? src + r0 * A : nullptr;
+        if (tab) {
+          double* h = w.s_f64.get(at + nqa) + off + r0 * A;
+          dmlp_cpu_gather_rows(tab + r0, r1 - r0, A, h);
+          from = h;
+        }
+        CK(hipMemcpyAsync(dst64 + r0 * A, from, n * 8, hipMemcpyHostToDevice, w.side));
+        *s64 = dst64;
+      };
+      auto xslice = [&](int i) {
+        if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
+        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
+        const int* s32;
+        const double* s64;
+        ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+        render_x(i, s32, s64 ? s64 : s32 ? nullptr : Xd);
+      };
+      const int nqb = NQB ? NQB : 1;
+      const int64_t qstep = NQB ? qbq : Q;
+      auto qblock = [&](int b) {
+        const int64_t q0 = (int64_t)b * qstep, q1 = std::min<int64_t>(Q, q0 + qstep);
+        const int* s32;
+        const double* s64;
+        ship(a->Qx, a->Qr, q0, q1, at, Qd, &s32, &s64);
+        CKL(dmlp_render_rows(KT, A, s32, s64, q0, q1 - q0, Q, mud, Qd, 1, w.dq_hi.p, w.dq_n.p, nullptr,
+                             nullptr, rbad, drw + 8 + b, NQB ? qrdy + b : nullptr, w.side));
+      };
+      if (pl) {
+        void *r32 = nullptr, *r64 = nullptr;
+        CKL(dmlp_plane_regions(pl, N, A, nullptr, nullptr, &r32, &r64));
+        plane_slices(2, [&](int i, int bits, float) {
+          if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
+          const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
+          const int64_t r0 = std::min(N, t0 * 64), r1 = std::min(N, t1 * 64), n = (r1 - r0) * A;
+          if (n > 0 && (bits & 2)) {  // fp64: from the segment, or from the node-shared X
+            const double* src = r64 ? (const double*)r64 + r0 * A : a->X ? a->X + r0 * A : nullptr;
+            if (!src) throw Fail{-10};
+            CK(hipMemcpyAsync(Xd + r0 * A, src, n * 8, hipMemcpyHostToDevice, w.side));
+            render_x(i, nullptr, Xd);
+          } else {
+            if (n > 0)
+              CK(hipMemcpyAsync(d32 + r0 * A, (const int*)r32 + r0 * A, n * 4,
+                                hipMemcpyHostToDevice, w.side));
+            render_x(i, d32, nullptr);
+          }
+        }, [&]() {
+          for (int b = 0; b < nqb; ++b) qblock(b);
+          CK(mark(M_OPS, w.side));
+        });
+      } else {
+        const int lead = early && NQB ? std::min(qb_lead(), ns) : 0;
+        for (int i = 0; i < lead; ++i) xslice(i);
+        for (int b = 0; b < nqb; ++b) qblock(b);
+        CK(mark(M_OPS, w.side));
+        for (int i = lead; i < ns; ++i) xslice(i);
+      }
+      CK(mark(M_DATA, w.side));
+      CK(hipEventRecord(w.ev_rows, w.side));
+      CK(mark(M_ROWS, w.side));
+    };
     // ---- front: the host renders the single-term screen's fp16 operands
     if (x1_front) {
       uint16_t* xhi_h = w.sx_hi.get(nt * 64 * W);
@@ -1054,7 +1214,27 @@ struct Step {
                                              chunks, w.side);
       };
       int rc;
-      if (early) {
+      if (dr) {
+        // the centre on the device; every ready word, counter and norm word cleared; the rows
+        // and the render follow the screen's launch (early start) or precede it
+        double* mud = w.d_mu.get(A);
+        CK(hipMemcpyAsync(mud, mu, A * sizeof(double), hipMemcpyHostToDevice, w.side));
+        CK(hipMemsetAsync(w.dr_words.get(80), 0, 80 * sizeof(unsigned), w.side));
+        CK(hipMemsetAsync(words, 0, (2 + 2 * kEarlySlices + 4 + kMaxQBlocks) * sizeof(unsigned),
+                          w.side));
+        if (KT <= 2 && rowmajor_on()) hx.xrow = w.dx_row.get(nt * 64 * W);
+        hx.xhi = xhi;
+        hx.xin = xin;
+        if (!early) dr_issue();
+        rc = 0;
+      } else if (early && NQB) {
+        // the ready words cleared; the query operands follow the screen's launch block by block
+        // (issue_rows), each wave waits for its own block
+        CK(hipMemsetAsync(rdy, 0, NS * sizeof(unsigned), w.side));
+        CK(hipMemsetAsync(estats, 0, 4 * sizeof(unsigned), w.side));
+        CK(hipMemsetAsync(qrdy, 0, NQB * sizeof(unsigned), w.side));
+        rc = 0;
+      } else if (early) {
         // query operands first (the whole front of the step), the ready words cleared
         CK(hipMemsetAsync(rdy, 0, (NS + 0) * sizeof(unsigned), w.side));
         CK(hipMemsetAsync(estats, 0, 4 * sizeof(unsigned), w.side));
@@ -1077,7 +1257,7 @@ struct Step {
       if (rc & 4) throw Fail{-(int)hipErrorUnknown};
       if (rc == 0) {
         CK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), w.side));  // bad = 0: host-checked
-        CK(mark(M_OPS, w.side));
+        if (!NQB && !dr) CK(mark(M_OPS, w.side));
         CK(hipEventRecord(w.ev_ops, w.side));
         CK(hipStreamWaitEvent(st, w.ev_ops, 0));
         hx.xhi = xhi;
@@ -1091,6 +1271,10 @@ struct Step {
           hx.rdy_n = NS;
           hx.xnm_sl = xnm_sl;
           hx.estats = estats;
+          if (NQB) {
+            hx.qrdy = qrdy;
+            hx.qrdy_q = qbq;
+          }
         }
         use_hx = true;
         a->early = early ? 1 : 0;
@@ -1111,6 +1295,10 @@ struct Step {
           // (host operands: called right after the first screen launch, so this mark completes
           // when it does; the device path calls it before its image is built: no mark)
           if (with_hx) CK(mark(M_SCREEN, st));
+          if (dr) {  // device render: the rows and their render (already queued without the early start)
+            if (with_hx && early) dr_issue();
+            return;
+          }
           if (with_hx && hx.rdy) {
             // the dataset image behind the queries, slice by slice, each followed by its ready
             // word (the running screen waits on it); every word is written even when a slice is
@@ -1118,8 +1306,34 @@ struct Step {
             unsigned* one = w.sx_nm.get(2 + kEarlySlices);  // (slot 0 is free in early mode)
             one[0] = 1u;
             const int dly = early_delay_us();
+            // query block b: rendered, copied, then its ready word (written even when out of the
+            // fp16 range — the call then falls back to the device image path — so the screen drains)
+            auto qblocks = [&]() {
+              const int64_t W = (int64_t)KT * 32;
+              for (int b = 0; b < NQB; ++b) {
+                const int64_t q0 = (int64_t)b * qbq, q1 = std::min<int64_t>(Q, q0 + qbq);
+                uint16_t* qh_h = w.sq_hi.p + q0 * W;
+                float* qn_h = w.sq_n.p + q0;
+                const int bad = a->Qr ? dmlp_cpu_prep_queries_rows(a->Qr + q0, q1 - q0, A, w.s_mu.p,
+                                                                   KT, qh_h, qn_h)
+                                      : dmlp_cpu_prep_queries(a->Qx + q0 * A, q1 - q0, A, w.s_mu.p,
+                                                              KT, qh_h, qn_h);
+                if (bad) early_bad = true;
+                CK(hipMemcpyAsync((short*)const_cast<void*>(hx.qhi) + q0 * W, qh_h,
+                                  (q1 - q0) * W * 2, hipMemcpyHostToDevice, w.side));
+                CK(hipMemcpyAsync(const_cast<float*>(hx.qn) + q0, qn_h, (q1 - q0) * 4,
+                                  hipMemcpyHostToDevice, w.side));
+                CK(hipMemcpyAsync(qrdy + b, one, sizeof(unsigned), hipMemcpyHostToDevice, w.side));
+              }
+              CK(mark(M_OPS, w.side));
+            };
+            // the first DMLP_QB_LEAD image slices, the query blocks, the rest of the image (the
+            // plane: the query blocks, then the node's slices)
+            const int lead = NQB ? (pl ? 0 : std::min(qb_lead(), NS)) : -1;
+            if (lead == 0) qblocks();
             if (pl && plane_image(hx.xhi, hx.xin, rdy, xnm_sl, nullptr)) early_bad = true;
             for (int i = 0; i < NS && !pl; ++i) {
+              if (i == lead && i > 0) qblocks();
               if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
               const int64_t t0 = (int64_t)i * rt, t1 = std::min<int64_t>(nt, t0 + rt);
               const int r2 = h2d_tiles_data(t0, t1, i);
@@ -1127,6 +1341,7 @@ struct Step {
               if (r2) early_bad = true;
               CK(hipMemcpyAsync(rdy + i, one, sizeof(unsigned), hipMemcpyHostToDevice, w.side));
             }
+            if (!pl && lead >= NS) qblocks();
             CK(mark(M_DATA, w.side));
           }
           if (with_hx && KT <= 2 && rowmajor_on()) {
@@ -1158,6 +1373,7 @@ struct Step {
     // copy: each separate small D2H cost a copy command's latency on the step's tail.
     int64_t* small = w.small64_h.get(8);
     int64_t* small_d = w.small64_d.get(8);
+    unsigned* dr_bad = dr ? w.dr_words.p + 72 : nullptr;  // device render: a value out of range
     auto render = [&]() {
       const int64_t* len_src = nullptr;
       if (want_report) {
@@ -1168,7 +1384,7 @@ struct Step {
         len_src = off + Q;
       }
       hipLaunchKernelGGL(k_pack_small, dim3(1), dim3(64), 0, st, len_src, Lp->ovf,
-                         a->early ? estats : nullptr, small_d);
+                         a->early ? estats : nullptr, dr_bad, small_d);
       CK(hipGetLastError());
       CK(hipMemcpyAsync(small, small_d, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
       if (want_report && a->report_mode == 1)
@@ -1182,10 +1398,24 @@ struct Step {
     spin_wait(w.ev_done);
     CK(hipStreamSynchronize(w.side));
     w.marks_valid = w.marks_on;
+    if (dr_bad && small[6]) {
+      // device render: some fp64 value lies outside the fp16 screen's range, so the screen ran on
+      // an unusable image — the whole call again on the device image path over the fp64 rows,
+      // which are complete on the device
+      a->early = 0;
+      use_hx = false;
+      dr_bad = nullptr;
+      w.marks_valid = false;
+      Lp = run_local(false, false);
+      render();
+      CK(hipEventRecord(w.ev_done, st));
+      spin_wait(w.ev_done);
+    }
     if (a->early) {
       a->early_waits = (int)small[2];
       a->early_grows = (int)small[3];
       a->early_timeouts = (int)small[4];
+      a->early_qwaits = (int)small[5];
       if (small[4] && g_early != 0) {
         std::fprintf(stderr, "[dmlp] early start: %d screen wave(s) timed out waiting for the "
                      "dataset image (overflowed queries were escalated); early start is off for "
@@ -1209,6 +1439,7 @@ struct Step {
     g_stats.n_escalated = Lp->n_escalated;
     g_stats.path = a->path;
     g_stats.early = a->early;
+    g_stats.device_render = dr && use_hx ? 1 : 0;
     return 0;
   }
 
@@ -1356,6 +1587,7 @@ extern "C" int dmlp_knn_local(const double* X, int64_t N, int A, const double* Q
     g_stats.n_escalated = L.n_escalated;
     g_stats.path = 2;
     g_stats.early = 0;
+    g_stats.device_render = 0;
     return 0;
   } catch (const Fail& f) {
     return drain_and_fail(wp, st, f.code);
@@ -1437,12 +1669,15 @@ extern "C" int dmlp_step_timeline(double* ms, const char** names, int cap) {
   }
 }
 
-// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops".  Returns the previous
+// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render",
+// "qb_blocks".  Returns the previous
 // value, or -1 for an unknown key.
 extern "C" int dmlp_pipeline_set(const char* key, int value) {
   const std::string k = key ? key : "";
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
-           : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops : nullptr;
+           : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
+           : k == "device_render" ? &g_tune.device_render
+           : k == "qb_blocks" ? &g_tune.qb_blocks : nullptr;
   if (!f) return -1;
   const int old = *f;
   *f = value;
@@ -1459,4 +1694,5 @@ extern "C" void dmlp_pipeline_stats(int64_t* out) {
   out[3] = g_stats.early;
   out[4] = g_stats.n_exact_f64;
   out[5] = g_stats.n_exact_f64_redo;
+  out[6] = g_stats.device_render;
 }

@@ -467,3 +467,134 @@ extern "C" int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* s
                                       (hipStream_t)stream);
   return e == hipSuccess ? 0 : -(int)e;
 }
+
+// ---------------------------------------------------------------- device render (dmlp_step)
+// The single-term screen's fp16 operands rendered ON THE DEVICE from the rows that crossed PCIe
+// for the exact re-rank anyway: lossless int32 m (x = m / 1e6, written out here as the fp64 rows
+// the re-rank reads) or fp64.  The host then only packs int32 rows: no host render of the fp16
+// image and query fragments, and 15 MB less over PCIe at the bench shape.  The arithmetic is
+// host_prep.cpp's, bit for bit: c = x - mu in fp64, hi = fp16(fp32(c)) (round to nearest even,
+// subnormals kept), |c|^2 as four fp64 partial sums s[a & 3] (each product and sum rounded) taken
+// (s0 + s2) + (s1 + s3) and rounded to fp32.
+//   mode 0 (dataset rows [r0, r0 + n), n padded to whole 64-point tiles; rows >= nvalid are
+//          padding): the tile image (prep.hip's hi-only layout), xinit = -|c|^2 / 2 (-inf for
+//          padding), the point-major copy xrow (the pair refine's member loads; may be null), and
+//          the rounded-up max |c|^2 of these rows into *nmax (atomicMax of non-negative fp32 bits).
+//   mode 1 (query rows): qhi [row][KT 32] and qn = |c|^2.
+// A value with |c| >= 65504 (fp64 rows only: int32 rows are below 2^31 / 1e6 in magnitude) sets
+// *bad.  done / rdy (nullable): the last workgroup to finish publishes *rdy = 1 with a release
+// store — the early-start screen's ready word (screen_x1.hip k_screen_x1 rdy / qrdy).
+// 64 VGPRs (8 waves per SIMD): the kernel has to find wave slots beside an early-start screen.
+namespace {
+template <int KT, bool I32>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render(
+    const int* __restrict__ src32, const double* __restrict__ src64, int64_t r0, int64_t n,
+    int64_t nvalid, int A, const double* __restrict__ mu, double* __restrict__ dst64, int mode,
+    uint4* __restrict__ img, float* __restrict__ xq, uint4* __restrict__ xrow,
+    unsigned* __restrict__ nmax, unsigned* __restrict__ bad, unsigned* __restrict__ done,
+    unsigned* __restrict__ rdy) {
+  constexpr int W = KT * 32;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = r0 + i;
+  const bool live = i < n;
+  const bool valid = live && p < nvalid;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  bool ok = true;
+  const int64_t t = p >> 6;
+  const int pl = (int)(p & 63), rt = pl >> 4, r = pl & 15;
+  for (int a0 = 0; a0 < W && live; a0 += 8) {
+    unsigned hw[4];
+#pragma unroll
+    for (int j2 = 0; j2 < 4; ++j2) {
+      unsigned short h2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int a = a0 + 2 * j2 + e;
+        double c = 0.0;
+        if (valid && a < A) {
+          double x;
+          if (I32) {
+            x = (double)src32[p * A + a] / 1.0e6;  // IEEE division: the exact input double
+            dst64[p * A + a] = x;
+          } else {
+            x = src64[p * A + a];
+          }
+          c = __dsub_rn(x, mu[a]);
+          if (!(fabs(c) < 65504.0)) {
+            ok = false;
+            c = 0.0;
+          }
+          s[a & 3] = __dadd_rn(s[a & 3], __dmul_rn(c, c));
+        }
+        h2[e] = __builtin_bit_cast(unsigned short, (_Float16)(float)c);
+      }
+      hw[j2] = (unsigned)h2[0] | ((unsigned)h2[1] << 16);
+    }
+    const uint4 v = {hw[0], hw[1], hw[2], hw[3]};
+    if (mode == 0) {
+      const int kt = a0 >> 5, kg = (a0 >> 3) & 3;
+      img[((t * 4 + rt) * KT + kt) * 64 + kg * 16 + r] = v;
+      if (xrow) xrow[p * (W / 8) + (a0 >> 3)] = v;
+    } else {
+      img[p * (W / 8) + (a0 >> 3)] = v;
+    }
+  }
+  const float ssf = (float)__dadd_rn(__dadd_rn(s[0], s[2]), __dadd_rn(s[1], s[3]));
+  if (live) {
+    if (mode == 0) xq[p] = valid ? -0.5f * ssf : -INFINITY;
+    else xq[p] = ssf;
+  }
+  if (mode == 0 && nmax) {
+    float up = valid ? __fadd_rn(__fmul_rn(ssf, 1.0f + 1.0e-6f), 1.0e-30f) : 0.0f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) up = fmaxf(up, __shfl_xor(up, o));
+    if ((threadIdx.x & 63) == 0 && up > 0.0f) atomicMax(nmax, __float_as_uint(up));
+  }
+  if (!ok && bad) atomicOr(bad, 1u);
+  if (done) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __threadfence();  // this workgroup's stores (and its atomics) before its count
+      const unsigned prev = atomicAdd(done, 1u);
+      if (prev == gridDim.x - 1 && rdy) {
+        __threadfence();
+        __hip_atomic_store(rdy, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int dmlp_render_rows(int KT, int A, const int* src32, const double* src64, int64_t r0,
+                                int64_t n, int64_t nvalid, const double* mu, double* dst64,
+                                int mode, void* img, float* xq, void* xrow, unsigned* nmax,
+                                unsigned* bad, unsigned* done, unsigned* rdy, void* stream) {
+  if (n <= 0) {
+    return 0;
+  }
+  if ((!src32 && !src64) || (src32 && !dst64) || A < 1 || A > KT * 32 || !img || !xq ||
+      (mode != 0 && mode != 1) || (mode == 0 && ((r0 & 63) || (n & 63))))
+    return -1;
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+#define DMLP_RENDER(KTV)                                                                       \
+  do {                                                                                         \
+    if (src32)                                                                                 \
+      hipLaunchKernelGGL((k_render<KTV, true>), grid, block, 0, st, src32, nullptr, r0, n, nvalid, \
+                         A, mu, dst64, mode, (uint4*)img, xq, (uint4*)xrow, nmax, bad, done, rdy); \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_render<KTV, false>), grid, block, 0, st, nullptr, src64, r0, n,     \
+                         nvalid, A, mu, dst64, mode, (uint4*)img, xq, (uint4*)xrow, nmax, bad,  \
+                         done, rdy);                                                           \
+  } while (0)
+  if (KT == 1) DMLP_RENDER(1);
+  else if (KT == 2) DMLP_RENDER(2);
+  else if (KT == 4) DMLP_RENDER(4);
+  else if (KT == 8) DMLP_RENDER(8);
+  else return -1;
+#undef DMLP_RENDER
+  DMLP_LAUNCH_CHECK();
+  return 0;
+}
+

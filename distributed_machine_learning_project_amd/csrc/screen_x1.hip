@@ -101,7 +101,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     int n_qblocks, int hl, int* __restrict__ cand_ids, int* __restrict__ cand_cnt,
     float* __restrict__ cand_h, const float* __restrict__ hseed, int ccap,
     const unsigned* __restrict__ rdy, int rdy_tiles, int rdy_n,
-    const unsigned* __restrict__ xnm_sl, unsigned* __restrict__ estats, long long rdy_to) {
+    const unsigned* __restrict__ xnm_sl, unsigned* __restrict__ estats, long long rdy_to,
+    const unsigned* __restrict__ qrdy, int qrdy_q) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   // COLLECT (large k, second pass): the threshold is fixed at the query's seed hseed[p] (a
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
@@ -158,25 +159,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // estats[0..2] at the end (the pipeline reports them).
   int have = 0;          // slices known landed (wave-uniform)
   bool rdy_fail = false;
-  unsigned n_wait = 0, n_grow = 0, n_to = 0;
-  auto rdy_probe = [&](int i) -> bool {
-    unsigned* const f = const_cast<unsigned*>(rdy + i);
+  unsigned n_wait = 0, n_grow = 0, n_to = 0, n_qwait = 0;
+  auto word_probe = [&](const unsigned* w) -> bool {
+    unsigned* const f = const_cast<unsigned*>(w);
     return __builtin_amdgcn_readfirstlane(
                __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
   };
-  auto wait_slice = [&](int i) -> bool {
-    if (rdy_probe(i)) return true;
-    ++n_wait;
+  auto rdy_probe = [&](int i) -> bool { return word_probe(rdy + i); };
+  auto wait_word = [&](const unsigned* w, unsigned& waits) -> bool {
+    if (word_probe(w)) return true;
+    ++waits;
     const long long t0 = wall_clock64();
     for (;;) {
       __builtin_amdgcn_s_sleep(2);
-      if (rdy_probe(i)) return true;
+      if (word_probe(w)) return true;
       if (wall_clock64() - t0 > rdy_to) {
         ++n_to;
         return false;
       }
     }
   };
+  auto wait_slice = [&](int i) -> bool { return wait_word(rdy + i, n_wait); };
   // m folded with the max norms of slices [lo, hi] (system-scope loads: ~1-2 us each, so the
   // words of slices already seen are not read again)
   auto fold_xnm = [&](float m, int lo, int hi) {
@@ -194,6 +197,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   auto widen = [&](int need) { return need < rdy_n - 1 && rdy_probe(rdy_n - 1) ? rdy_n - 1 : need; };
   float xnmax;
   if (rdy) {
+    // QUERY-BLOCK EARLY START (qrdy): the query operands cross PCIe in blocks of qrdy_q queries
+    // (a multiple of the wave's columns), each with its own ready word: this wave waits only for
+    // its own block before the prologue reads its queries' fragments and norms
+    if (qrdy) rdy_fail |= !wait_word(qrdy + pbase / qrdy_q, n_qwait);
     // tiles 0..2: the prologue and step 0's loads
     const int need = widen(min(2 / rdy_tiles, rdy_n - 1));
     for (int i = 0; i <= need && !rdy_fail; ++i) rdy_fail |= !wait_slice(i);
@@ -613,10 +620,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   }
   // final threshold over everything buffered, then the candidate ids
   compact(true);
-  if (rdy && estats && lane == 0 && (n_wait | n_grow | n_to)) {
+  if (rdy && estats && lane == 0 && (n_wait | n_grow | n_to | n_qwait)) {
     atomicAdd(estats + 0, n_wait);
     atomicAdd(estats + 1, n_grow);
     atomicAdd(estats + 2, n_to);
+    atomicAdd(estats + 3, n_qwait);
   }
 }
 
@@ -637,7 +645,8 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
               int* cand_ids, int* cand_cnt, float* cand_h, hipStream_t stream,
               const float* hseed = nullptr, int ccap = 0, const unsigned* rdy = nullptr,
               int rdy_tiles = 1, int rdy_n = 0, const unsigned* xnm_sl = nullptr,
-              unsigned* estats = nullptr, long long rdy_to = 0) {
+              unsigned* estats = nullptr, long long rdy_to = 0,
+              const unsigned* qrdy = nullptr, int qrdy_q = 1) {
   using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
   const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
   const int tps = (int)((n_tiles + S - 1) / S);
@@ -648,7 +657,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap, rdy, rdy_tiles,     \
-                     rdy_n, xnm_sl, estats, rdy_to)
+                     rdy_n, xnm_sl, estats, rdy_to, qrdy, qrdy_q)
   if (hseed) {  // the COLLECT pass (SUB = 16, CT = 4, fp16 only: see dmlp_screen_x1_collect)
     if constexpr (SUB == 16 && CTV == 4 && F16) DMLP_X1_LAUNCH(16);
     else return -3;
@@ -847,6 +856,17 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
 // (fast_step.hip's early start): one data slice per workgroup (S = 1), rdy[i] != 0 once image
 // tiles [i rdy_tiles, (i + 1) rdy_tiles) and their max norm xnm_sl[i] (fp32 bits) landed.  The
 // result is the one dmlp_screen_x1(KT, 1, ...) gives with S = 1 once every slice landed.
+// ... with the query operands in flight too (qrdy != null): qrdy[b] != 0 once queries
+// [b qrdy_q, (b + 1) qrdy_q) have their fragments and norms on the device (qrdy_q a multiple of
+// 128, a wave's columns); the waits for them are counted into estats[3].
+extern "C" int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const float* xinit,
+                                     int64_t n_tiles, int64_t n_points, const void* qhi,
+                                     const float* qn, const int* qidx, const int* qk, int nq,
+                                     int kmax, const unsigned* bad, const unsigned* rdy,
+                                     int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
+                                     int* cand_ids, int* cand_cnt, float* cand_h,
+                                     unsigned* estats, const unsigned* qrdy, int qrdy_q,
+                                     void* stream);
 extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit,
                                     int64_t n_tiles, int64_t n_points, const void* qhi,
                                     const float* qn, const int* qidx, const int* qk, int nq,
@@ -854,10 +874,24 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
                                     int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
                                     int* cand_ids, int* cand_cnt, float* cand_h,
                                     unsigned* estats, void* stream) {
+  return dmlp_screen_x1_early2(KT, A, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, kmax,
+                               bad, rdy, rdy_tiles, rdy_n, xnm_sl, cand_ids, cand_cnt, cand_h,
+                               estats, nullptr, 128, stream);
+}
+extern "C" int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const float* xinit,
+                                     int64_t n_tiles, int64_t n_points, const void* qhi,
+                                     const float* qn, const int* qidx, const int* qk, int nq,
+                                     int kmax, const unsigned* bad, const unsigned* rdy,
+                                     int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
+                                     int* cand_ids, int* cand_cnt, float* cand_h,
+                                     unsigned* estats, const unsigned* qrdy, int qrdy_q,
+                                     void* stream) {
   if (nq <= 0) return 0;
   if (n_tiles < 1 || n_tiles > 4096 || n_points > n_tiles * 64 || !rdy || !xnm_sl ||
       rdy_tiles < 1 || rdy_n < 1 || (int64_t)rdy_tiles * rdy_n < n_tiles)
     return -1;
+  // (qrdy: the list must be every query in order, qidx[p] == p — the all-queries pass)
+  if (qrdy && (qrdy_q < 128 || qrdy_q % 128 != 0)) return -1;
   if (kmax > 64 || !x1_kt_ok(KT) || A > KT * 32) return -3;
   float r1, r2, r3;
   dmlp_screen_x1_bound2(A, 1, &r1, &r2, &r3);
@@ -877,7 +911,7 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
   return launch_x1<KTV, SUBV, 4, 2, CTV, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, \
                                                qk, nq, bad, bad, r1, r2, r3, 1, cand_ids,      \
                                                cand_cnt, cand_h, st, nullptr, 0, rdy, rdy_tiles, \
-                                               rdy_n, xnm_sl, estats, rdy_to)
+                                               rdy_n, xnm_sl, estats, rdy_to, qrdy, qrdy_q)
   if (KT == 1) {
     if (sub == 32) DMLP_X1E(1, 32, 4);
     if (ct == 8) DMLP_X1E(1, 16, 8);

@@ -152,12 +152,12 @@ def pipeline_options(**kw):
 
 def pipeline_stats():
     """What the last native call did: {"n_exact", "n_escalated", "path", "early", "n_exact_f64",
-    "n_exact_f64_redo"} (the last two: exact-path queries on the fp64 MFMA screen, and those of
-    them that overflowed to the fused VALU kernel)."""
-    out = (C.c_int64 * 6)()
+    "n_exact_f64_redo", "device_render"} (exact-path queries on the fp64 MFMA screen, and those of
+    them that overflowed to the fused VALU kernel; whether the GPU rendered the screen operands)."""
+    out = (C.c_int64 * 8)()
     _lib.lib().dmlp_pipeline_stats(out)
     return {"n_exact": out[0], "n_escalated": out[1], "path": out[2], "early": out[3],
-            "n_exact_f64": out[4], "n_exact_f64_redo": out[5]}
+            "n_exact_f64": out[4], "n_exact_f64_redo": out[5], "device_render": out[6]}
 
 
 # ---------------------------------------------------------------- rows on the device
@@ -247,7 +247,8 @@ class StepArgs(C.Structure):
                 ("stream", C.c_void_p), ("plane", C.c_void_p), ("report_len", C.c_int64),
                 ("path", C.c_int),
                 ("early", C.c_int), ("n_escalated", C.c_int), ("early_waits", C.c_int),
-                ("early_grows", C.c_int), ("early_timeouts", C.c_int)]
+                ("early_grows", C.c_int), ("early_timeouts", C.c_int),
+                ("early_qwaits", C.c_int)]
 
 
 class Plane(C.Structure):
@@ -271,12 +272,13 @@ class StepResult:
     early_waits: int = 0
     early_grows: int = 0
     early_timeouts: int = 0
+    early_qwaits: int = 0
 
 
 # calls the native step served and its early-start counters (bench.py reports them for the timed
 # region; tests check that the early start ran)
 STEP_STATS = {"calls": 0, "early": 0, "early_waits": 0, "early_grows": 0, "early_timeouts": 0,
-              "escalated": 0, "device_path": 0}
+              "early_qwaits": 0, "escalated": 0, "device_path": 0}
 _IO = {"h2d": 0, "d2h": 0}  # host <-> device bytes the steps issued (bench.py diagnostics)
 
 
@@ -353,6 +355,7 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     STEP_STATS["early_waits"] += a.early_waits
     STEP_STATS["early_grows"] += a.early_grows
     STEP_STATS["early_timeouts"] += a.early_timeouts
+    STEP_STATS["early_qwaits"] += a.early_qwaits
     STEP_STATS["escalated"] += a.n_escalated
     STEP_STATS["device_path"] += 1 if a.path == 2 else 0
     kt = screen_kt(A)
@@ -363,7 +366,8 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     if _EVENTS[0]:
         _read_timeline()
     return StepResult(lab, cs, od, oi, int(a.report_len), a.path, a.early, a.n_escalated,
-                      int(st["n_exact"]), a.early_waits, a.early_grows, a.early_timeouts)
+                      int(st["n_exact"]), a.early_waits, a.early_grows, a.early_timeouts,
+                      a.early_qwaits)
 
 
 def step_emit(dst, nbytes: int):

@@ -98,21 +98,29 @@ def _early_inputs(n, A, kmax, Q, seed):
     return out
 
 
+@pytest.mark.parametrize("render", ["device", "host"])
 @pytest.mark.parametrize("n,A,kmax", [(2000, 32, 16), (5000, 32, 32), (3000, 64, 64),
-                                        (3000, 128, 32), (3000, 256, 32)])
-def test_native_step_early_start(gpu, n, A, kmax):
+                                        (3000, 64, 16), (3000, 128, 32), (3000, 256, 32)])
+def test_native_step_early_start(gpu, n, A, kmax, render):
     """Early start: the screen starts on the query operands while the dataset image crosses
     PCIe in slices with ready words.  The host sleeps 400 us before each image slice
     (dmlp_step_early_delay), so the screen provably waits mid-scan; the device counters then show
     waits > 0, eps growths > 0 (the far point sits in the last slice) and no timeout.  Two
     different inputs of equal shape alternate A, B, A, B (early on), then once with the early
-    start off; every report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
+    start off.  The query operands cross in blocks behind the screen's launch (query-block early
+    start): each wave waits for its own block, counted apart; every report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
     variant (one wave per SIMD, 404 of 512 registers).  A = 256 (KT = 8, all 512 registers): the
     step refuses the early start there — its image copies (blit kernels) would find no free wave
     slot beside the spinning screen — and the results stay exact.  One screen slice needs a full
-    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4)."""
+    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4).  render: the screen
+    operands rendered on the GPU from the landed int32 rows (the default; its render kernels run
+    beside the spinning screen and publish the ready words — except at A = 64 / k <= 16, whose
+    screen leaves no registers for them: rendered first, no early start) or on the host."""
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
+    old_dr = L.dmlp_pipeline_set(b"device_render", 1 if render == "device" else 0)
+    old_qb = L.dmlp_pipeline_set(b"qb_blocks", 16)  # the query-block early start on
+    no_early = render == "device" and A == 64 and kmax <= 16
     Q = 131072 + 64 * 3 if A <= 64 else 65536 + 64
     cases = _early_inputs(n, A, kmax, Q, seed=n + A + kmax)
     dsts = []
@@ -129,16 +137,22 @@ def test_native_step_early_start(gpu, n, A, kmax):
             assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
-            assert r.early == (early if A <= 128 else 0)
+            assert r.early == (early if A <= 128 and not no_early else 0)
+            assert K.pipeline_stats()["device_render"] == (1 if render == "device" else 0)
             if A <= 64:
                 assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
-            if r.early:
+            if r.early:  # (the queries in 16 blocks: DMLP_QB_BLOCKS)
                 assert r.early_timeouts == 0
                 assert r.early_waits > 0, "the screen never waited for a slice"
+                # query-block early start: the query blocks cross after the first (delayed) image
+                # slice, so waves waited for their own block
+                assert r.early_qwaits > 0, "no wave waited for its query block"
                 assert r.early_grows > 0, "no column's eps grew with a later slice"
     finally:
         L.dmlp_step_early(-1)
         L.dmlp_step_early_delay(-1)
+        L.dmlp_pipeline_set(b"device_render", old_dr)
+        L.dmlp_pipeline_set(b"qb_blocks", old_qb)
 
 
 def test_debug_listing(gpu, workload):
@@ -168,9 +182,10 @@ print("POLICY", _lib.lib().dmlp_host_threads(), r.path, int(ok))
 def test_step_policy_host_budget_and_shared_device(gpu, monkeypatch):
     """The step's automatic choices (profiles/r7h_host_budget.md): (1) ranks sharing one GPU
     (DMLP_DEVICE_RANKS > 1, set by Comm.init / knn_engine) run without the early start, which
-    made P = 3 on one MI355X 2.8x slower; DMLP_FAST_EARLY=1 still forces it.  (2) A render pool
-    of one thread takes the device-image path (measured faster there); DMLP_HOST_OPS=1 forces the
-    host operands.  Results == the oracle's either way."""
+    made P = 3 on one MI355X 2.8x slower; DMLP_FAST_EARLY=1 still forces it.  (2) With the host
+    render (DMLP_DEVICE_RENDER=0) a render pool of one thread takes the device-image path
+    (measured faster there); DMLP_HOST_OPS=1 forces the host operands.  Results == the oracle's
+    either way."""
     import os
     import subprocess
     import sys
@@ -194,11 +209,16 @@ def test_step_policy_host_budget_and_shared_device(gpu, monkeypatch):
         monkeypatch.delenv("DMLP_FAST_EARLY", raising=False)
         L.dmlp_step_early(-1)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for env, want_path in (({"DMLP_HOST_THREADS": "1"}, 2),
-                           ({"DMLP_HOST_THREADS": "1", "DMLP_HOST_OPS": "1"}, 0),
-                           ({"DMLP_HOST_THREADS": "2"}, 0)):
+    # (3) with the device render (the default) the host only packs int32 rows: a one-thread pool
+    # keeps the single-term fp16 operands (path 0) as well
+    for env, want_path in (({"DMLP_HOST_THREADS": "1", "DMLP_DEVICE_RENDER": "0"}, 2),
+                           ({"DMLP_HOST_THREADS": "1", "DMLP_HOST_OPS": "1",
+                             "DMLP_DEVICE_RENDER": "0"}, 0),
+                           ({"DMLP_HOST_THREADS": "2", "DMLP_DEVICE_RENDER": "0"}, 0),
+                           ({"DMLP_HOST_THREADS": "1"}, 0)):
         e = dict(os.environ, **env)
         e.pop("DMLP_HOST_OPS", None) if "DMLP_HOST_OPS" not in env else None
+        e.pop("DMLP_DEVICE_RENDER", None) if "DMLP_DEVICE_RENDER" not in env else None
         out = subprocess.run([sys.executable, "-c", _POLICY_CHILD], cwd=root, env=e,
                              capture_output=True, text=True, timeout=100)
         line = [x for x in out.stdout.splitlines() if x.startswith("POLICY")]

@@ -649,3 +649,92 @@ def test_step_mixed_k_one_pass(torch_cuda, A):
     assert bytes(dst[:r.report_len]) == dmlp.format_report(cs_ref)
     np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
     assert r.path == 0 and r.n_escalated >= 1
+
+
+@pytest.mark.parametrize("N,Q,A", [(6000, 700, 32), (1000, 300, 40), (130, 65, 7), (4097, 129, 64)])
+def test_device_render_matches_host_render(torch_cuda, N, Q, A):
+    """dmlp_render_rows (prep.hip k_render): the screen's fp16 operands rendered on the device
+    from the lossless int32 rows (or fp64 rows) are bit for bit host_prep.cpp's render — tile
+    image, xinit, point-major copy, max norm, query fragments and norms — and the int32 path
+    writes back the exact fp64 rows.  Two dataset slices and two query blocks, each publishing its
+    ready word from its last workgroup."""
+    import ctypes as C
+    torch = torch_cuda
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    inp = dmlp.generate(N, Q, A, 0.0, 1000.0, 1, 8, 5, seed=N + A)
+    kt = 1 if A <= 32 else 2 if A <= 64 else 4 if A <= 128 else 8
+    W = kt * 32
+    nt = (N + 63) // 64
+    mu = np.zeros(A)
+    L.dmlp_cpu_center(inp.X.ctypes.data, N, A, mu.ctypes.data)
+    img_h = np.zeros(nt * 64 * W, np.uint16)
+    xin_h = np.zeros(nt * 64, np.float32)
+    nmax_h = C.c_uint()
+    assert L.dmlp_cpu_prep_data(inp.X.ctypes.data, N, A, mu.ctypes.data, kt, img_h.ctypes.data,
+                                xin_h.ctypes.data, C.byref(nmax_h)) == 0
+    qhi_h = np.zeros(Q * W, np.uint16)
+    qn_h = np.zeros(Q, np.float32)
+    assert L.dmlp_cpu_prep_queries(inp.Qx.ctypes.data, Q, A, mu.ctypes.data, kt,
+                                   qhi_h.ctypes.data, qn_h.ctypes.data) == 0
+    x32 = np.zeros(N * A, np.int32)
+    q32 = np.zeros(Q * A, np.int32)
+    assert L.dmlp_cpu_rows_i32(inp.X.ctypes.data, N * A, x32.ctypes.data) == 0
+    assert L.dmlp_cpu_rows_i32(inp.Qx.ctypes.data, Q * A, q32.ctypes.data) == 0
+    dev = torch.device("cuda")
+    p = lambda t: t.data_ptr()
+    mu_d = torch.from_numpy(mu).to(dev)
+    for src in ("i32", "f64"):
+        img = torch.zeros(nt * 64 * W, dtype=torch.int16, device=dev)
+        xin = torch.zeros(nt * 64, dtype=torch.float32, device=dev)
+        xrow = torch.zeros(nt * 64 * W, dtype=torch.int16, device=dev)
+        words = torch.zeros(16, dtype=torch.int32, device=dev)  # nmax, bad, done[4], rdy[4]
+        Xd = torch.zeros(N * A, dtype=torch.float64, device=dev)
+        qhi = torch.zeros(Q * W, dtype=torch.int16, device=dev)
+        qn = torch.zeros(Q, dtype=torch.float32, device=dev)
+        Qd = torch.zeros(Q * A, dtype=torch.float64, device=dev)
+        xs = torch.from_numpy(x32).to(dev) if src == "i32" else torch.from_numpy(inp.X.ravel()).to(dev)
+        qs = torch.from_numpy(q32).to(dev) if src == "i32" else torch.from_numpy(inp.Qx.ravel()).to(dev)
+        w0 = p(words)
+        half_t = nt // 2
+        for j, (t0, t1) in enumerate(((0, half_t), (half_t, nt))):
+            args = (p(xs), None) if src == "i32" else (None, p(xs))
+            assert L.dmlp_render_rows(kt, A, *args, t0 * 64, (t1 - t0) * 64, N, p(mu_d), p(Xd), 0,
+                                      p(img), p(xin), p(xrow), w0, w0 + 4, w0 + 8 + 4 * j,
+                                      w0 + 24 + 4 * j, None) == 0
+        hq = Q // 2
+        for j, (q0, q1) in enumerate(((0, hq), (hq, Q))):
+            args = (p(qs), None) if src == "i32" else (None, p(qs))
+            assert L.dmlp_render_rows(kt, A, *args, q0, q1 - q0, Q, p(mu_d), p(Qd), 1, p(qhi),
+                                      p(qn), None, None, w0 + 4, w0 + 16 + 4 * j, w0 + 32 + 4 * j,
+                                      None) == 0
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(img.cpu().numpy().view(np.uint16), img_h)
+        np.testing.assert_array_equal(xin.cpu().numpy(), xin_h)
+        # the point-major copy: each point's W fp16 values in attribute order
+        ref_row = np.zeros((nt * 64, W), np.uint16)
+        t = np.arange(nt * 64)
+        for a0 in range(0, W, 8):
+            kt_, kg = a0 // 32, (a0 // 8) % 4
+            idx = (((t >> 6) * 4 + ((t & 63) >> 4)) * kt + kt_) * 64 + kg * 16 + (t & 15)
+            ref_row[:, a0:a0 + 8] = img_h.reshape(-1, 8)[idx]
+        np.testing.assert_array_equal(xrow.cpu().numpy().view(np.uint16).reshape(-1, W), ref_row)
+        np.testing.assert_array_equal(qhi.cpu().numpy().view(np.uint16), qhi_h)
+        np.testing.assert_array_equal(qn.cpu().numpy(), qn_h)
+        w = words.cpu().numpy().view(np.uint32)
+        assert w[0] == nmax_h.value and w[1] == 0
+        assert list(w[6:8]) == [1, 1] and list(w[8:10]) == [1, 1]  # every ready word published
+        if src == "i32":
+            np.testing.assert_array_equal(Xd.cpu().numpy(), inp.X.ravel())
+            np.testing.assert_array_equal(Qd.cpu().numpy(), inp.Qx.ravel())
+    # an fp64 value outside the fp16 range flags *bad
+    X2 = inp.X.copy()
+    X2[N // 2, 0] = 1.0e6
+    xs = torch.from_numpy(X2.ravel()).to(dev)
+    words = torch.zeros(4, dtype=torch.int32, device=dev)
+    img = torch.zeros(nt * 64 * W, dtype=torch.int16, device=dev)
+    xin = torch.zeros(nt * 64, dtype=torch.float32, device=dev)
+    assert L.dmlp_render_rows(kt, A, None, p(xs), 0, nt * 64, N, p(mu_d), None, 0, p(img), p(xin),
+                              None, p(words), p(words) + 4, None, None, None) == 0
+    torch.cuda.synchronize()
+    assert int(words[1]) == 1

@@ -22,7 +22,11 @@
 #   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
+#   qb         query-block early start A/B (DMLP_QB_BLOCKS / DMLP_QB_LEAD), step timelines
+#   dr         device render A/B (DMLP_DEVICE_RENDER, DMLP_QB_BLOCKS), step timelines
 #   plane      node render plane rehearsal: bench.py --gpus 3 / 8 on the one GPU, plane on / off
+#   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
+#   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 set -u
 TAG=${1:?tag}
@@ -142,6 +146,14 @@ for task in "$@"; do
     hostprof)
       step hostprof 300 python tools/host_profile.py --steps 100
       DMLP_PIPE_DEBUG=1 step pipedebug 120 python bench.py --steps 5 --warmup 2 --no-busbw ;;
+    qb)  # query-block early start: off / 16 blocks (lead 1, 2) / 8 blocks, interleaved
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step qb_ab 900 bash tools/kernel_ab.sh qb0:DMLP_QB_BLOCKS=0 \
+          qb16:DMLP_QB_BLOCKS=16 qb16l2:DMLP_QB_BLOCKS=16,DMLP_QB_LEAD=2 qb8:DMLP_QB_BLOCKS=8
+      python3 tools/ab_timeline.py gpurun_out/ab ;;
+    dr)  # device render of the screen operands: host render / device render, +/- query blocks
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step dr_ab 900 bash tools/kernel_ab.sh hr:DMLP_DEVICE_RENDER=0 \
+          dr:DMLP_DEVICE_RENDER=1 drqb16:DMLP_QB_BLOCKS=16 drqb4:DMLP_QB_BLOCKS=4,DMLP_QB_LEAD=2
+      python3 tools/ab_timeline.py gpurun_out/ab ;;
     plane)  # node render plane: P = 3 / 8 ranks sharing the one GPU (host-staged plane), --verify,
             # plane on / off: per-rank ms, the cgroup's CPU time in the timed region
       for P in 3 8; do
@@ -151,6 +163,15 @@ for task in "$@"; do
               --steps 10 --warmup 2 --min-warmup-s 1 --q-per-gpu $Qp --verify --no-busbw
         done
       done ;;
+    rehearsal)  # host budget of an 8-GPU node: the GPU rank + 7 CPU phantom ranks, 2 threads each
+      step reh_solo2 300 python tools/host_rehearsal.py --ranks 1 --threads 2
+      step reh_solo14 300 python tools/host_rehearsal.py --ranks 1 --threads 14
+      for R in device host; do
+        for PL in 1 0; do
+          step reh_${R}_p$PL 300 python tools/host_rehearsal.py --ranks 8 --threads 2 --plane $PL --render $R
+        done
+      done
+      grep -h '^{' "$OUT"/reh_*.log ;;
     dropin_p)  # the drop-in at P = 2 / 3 through the node window on the one GPU (host-staged plane)
       python -m distributed_machine_learning_project_amd.build --dropin \
           distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
@@ -161,6 +182,18 @@ for task in "$@"; do
             "exec /tmp/eng_dropin < /tmp/dropin_bench.in > /tmp/dropin_p$P.out"
         md5sum /tmp/dropin_p$P.out
       done ;;
+    final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
+            # default and the exact path, the P = 3 host-plane rehearsal with --verify
+      step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
+          --timeout-method thread
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+      step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      step verify 300 python bench.py --steps 200 --verify
+      step exact 300 python bench.py --exact --steps 5 --warmup 1 --min-warmup-s 0 --verify
+      DMLP_DATA_PLANE=host step p3 400 python bench.py --gpus 3 --steps 30 --warmup 3 \
+          --min-warmup-s 1 --no-busbw --verify
+      grep -ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*' "$OUT"/bench_driver.log \
+          "$OUT"/verify.log "$OUT"/exact.log "$OUT"/p3.log ;;
     *)
       echo "unknown task $task"; exit 2 ;;
   esac
