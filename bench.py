@@ -230,6 +230,10 @@ def main(argv=None):
                                 "early_waits": steps_native["early_waits"],
                                 "early_timeouts": steps_native["early_timeouts"],
                                 "early_query_block_waits": steps_native["early_qwaits"],
+                                # host time per step until everything was issued (render / int32
+                                # pack, plane waits): the per-rank host budget
+                                "host_issue_ms_per_step": round(
+                                    steps_native["host_ms"] / max(1, steps_native["calls"]), 4),
                                 "escalated_queries": steps_native["escalated"],
                                 "device_path_calls": steps_native["device_path"]}
     if thr0 and thr1:
@@ -332,6 +336,11 @@ def _world_report(comm, host_plane, a):
     t = torch.ones(1, dtype=torch.float32, device=comm.device)
     dist.all_reduce(t)
     out["allreduce_check"] = int(t.item())
+    # the farm's dataset replication (parallel/strategies.py probe_replication, untimed): every
+    # GPU over its own PCIe link ("h2d") or 1/P each + an all-gather over xGMI ("xgmi")
+    out["replication_probe"] = getattr(comm, "replication", None)
+    out["replication_mode"] = (os.environ.get("KNN_DATA_INGRESS") or
+                               (getattr(comm, "replication", None) or {}).get("mode", "h2d"))
     if out["allreduce_check"] != comm.world:
         raise RuntimeError(f"all-reduce of ones gave {out['allreduce_check']} on {comm.world} ranks")
     return out
@@ -382,6 +391,8 @@ def _diagnostics(comm, eng, step, n, my_ms, steps_native=None):
     mine = {"rank": comm.rank, "device": str(comm.device), "numa_node": type(comm)._numa,
             "ms_per_step": round(my_ms, 4),
             "timed_native_step_calls": (steps_native or {}).get("calls"),
+            "host_issue_ms_per_step": round((steps_native or {}).get("host_ms", 0.0) /
+                                            max(1, (steps_native or {}).get("calls") or 1), 4),
             "host_threads": _host_threads(),
             "step_timeline_ms": {k: round(v, 4) for k, v in timeline.items()},
             "phases_ms": {k: round(v, 4) for k, v in phases.items()},
@@ -485,9 +496,15 @@ def _bench_native(a):
                     with open(met) as f:
                         mj = _json.load(f)
                     times.append(float(mj["time_ms"]))
-                    for key in ("pack_ms", "knn_ms", "emit_ms"):
+                    for key in ("pack_ms", "knn_ms", "emit_ms", "step_ms"):
                         if key in mj:
                             parts.setdefault(key, []).append(float(mj[key]))
+                    for rk in range(1, P):  # the drop-in's node window: each rank's step time
+                        rp = f"{met}.r{rk}"
+                        if os.path.exists(rp):
+                            with open(rp) as f:
+                                parts.setdefault(f"rank{rk}_step_ms", []).append(
+                                    float(_json.load(f)["step_ms"]))
                     if dropin:
                         import re as _re
                         m = _re.search(rb"Time taken: (\d+) ms", pr.stderr)

@@ -349,11 +349,20 @@ typedef struct dmlp_step_args {
   int n_escalated;            // queries redone after a screen overflow
   int early_waits, early_grows, early_timeouts;
   int early_qwaits;           // screen waves that waited for their query block (query-block start)
+  float host_ms;              // host time from entry until every copy / kernel of the call was
+                              // issued (the render / pack work and the plane's waits)
+  // (input) the dataset's rows already on THIS device as lossless int32 [N][A] (x = m / 1e6: the
+  // replica completed over xGMI by an all-gather, parallel/strategies.py "xgmi"): no dataset rows
+  // cross PCIe (the host still renders the screen image from X, or the plane does); null: none
+  const int* X32d;
 } dmlp_step_args;
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
 int dmlp_step_emit(char* dst, int64_t bytes, void* stream);
 void dmlp_step_early(int on);          // 1 on, 0 off, < 0: DMLP_FAST_EARLY (default on)
+// Right before a timed call after an idle stretch: wake the render pool, touch the staging, keep
+// the GPU busy gpu_us microseconds (clocks up).  Synchronous.
+int dmlp_step_prewarm(int gpu_us);
 void dmlp_step_early_delay(int us);    // host sleep before each image slice (< 0: env)
 int dmlp_step_events(int on);          // hipEvent step timeline on / off
 int dmlp_step_timeline(double* ms, const char** names, int cap);

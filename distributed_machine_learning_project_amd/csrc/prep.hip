@@ -484,17 +484,19 @@ extern "C" int dmlp_d2h_async(void* dst, const void* src, int64_t bytes, void* s
 // A value with |c| >= 65504 (fp64 rows only: int32 rows are below 2^31 / 1e6 in magnitude) sets
 // *bad.  done / rdy (nullable): the last workgroup to finish publishes *rdy = 1 with a release
 // store — the early-start screen's ready word (screen_x1.hip k_screen_x1 rdy / qrdy).
-// 64 VGPRs (8 waves per SIMD): the kernel has to find wave slots beside an early-start screen.
+// One-wave workgroups of <= 64 VGPRs: the kernel has to find wave slots beside an early-start
+// screen, whose one-wave workgroups fill every CU (a multi-wave workgroup found none: every
+// early wave timed out, profiles/r9e).
 namespace {
 template <int KT, bool I32>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_render(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_render(
     const int* __restrict__ src32, const double* __restrict__ src64, int64_t r0, int64_t n,
     int64_t nvalid, int A, const double* __restrict__ mu, double* __restrict__ dst64, int mode,
     uint4* __restrict__ img, float* __restrict__ xq, uint4* __restrict__ xrow,
     unsigned* __restrict__ nmax, unsigned* __restrict__ bad, unsigned* __restrict__ done,
     unsigned* __restrict__ rdy) {
   constexpr int W = KT * 32;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t p = r0 + i;
   const bool live = i < n;
   const bool valid = live && p < nvalid;
@@ -552,7 +554,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
   if (!ok && bad) atomicOr(bad, 1u);
   if (done) {
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     if (threadIdx.x == 0) {
       __threadfence();  // this workgroup's stores (and its atomics) before its count
       const unsigned prev = atomicAdd(done, 1u);
@@ -576,7 +578,7 @@ extern "C" int dmlp_render_rows(int KT, int A, const int* src32, const double* s
   if ((!src32 && !src64) || (src32 && !dst64) || A < 1 || A > KT * 32 || !img || !xq ||
       (mode != 0 && mode != 1) || (mode == 0 && ((r0 & 63) || (n & 63))))
     return -1;
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  const dim3 grid((unsigned)((n + 63) / 64)), block(64);
   hipStream_t st = (hipStream_t)stream;
 #define DMLP_RENDER(KTV)                                                                       \
   do {                                                                                         \

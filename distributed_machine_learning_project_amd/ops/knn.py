@@ -248,7 +248,7 @@ class StepArgs(C.Structure):
                 ("path", C.c_int),
                 ("early", C.c_int), ("n_escalated", C.c_int), ("early_waits", C.c_int),
                 ("early_grows", C.c_int), ("early_timeouts", C.c_int),
-                ("early_qwaits", C.c_int)]
+                ("early_qwaits", C.c_int), ("host_ms", C.c_float), ("X32d", C.c_void_p)]
 
 
 class Plane(C.Structure):
@@ -278,7 +278,7 @@ class StepResult:
 # calls the native step served and its early-start counters (bench.py reports them for the timed
 # region; tests check that the early start ran)
 STEP_STATS = {"calls": 0, "early": 0, "early_waits": 0, "early_grows": 0, "early_timeouts": 0,
-              "early_qwaits": 0, "escalated": 0, "device_path": 0}
+              "early_qwaits": 0, "escalated": 0, "device_path": 0, "host_ms": 0.0}
 _IO = {"h2d": 0, "d2h": 0}  # host <-> device bytes the steps issued (bench.py diagnostics)
 
 
@@ -291,7 +291,8 @@ def step_stats(reset: bool = False):
 
 
 def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_base=0,
-         exact=False, report=None, lists=False, kstride=None, plane=None) -> StepResult:
+         exact=False, report=None, lists=False, kstride=None, plane=None,
+         x32=None) -> StepResult:
     """One rank's whole Engine::KNN call from host arrays (dmlp_step): X_host [N, A] /
     Q_host [Q, A] fp64, labels_host [N] int32 (page-locked or registered memory for real
     overlap; a node-shared segment is), k_host [Q] int32.
@@ -302,6 +303,8 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
       k_range: (a lower bound of min k, an upper bound of max k) when known, else scanned.
       plane:  a Plane (node render plane): the dataset's image and rows are rendered once per
               node, slice by slice, by the plane's renderers into a node-shared segment.
+      x32:    the dataset's rows already on this GPU as lossless int32 [N * A] (a torch tensor:
+              the xGMI replica, parallel/strategies.py): no dataset rows cross PCIe.
     Returns once everything is complete (one host sync in the common case)."""
     torch = _torch()
     L = _lib.lib()
@@ -348,6 +351,7 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
         a.report_dst, a.report_cap = report.ctypes.data, report.nbytes
     a.stream = _stream()
     a.plane = C.cast(C.pointer(plane), C.c_void_p) if plane is not None else None
+    a.X32d = x32.data_ptr() if x32 is not None else None
     _lib.check(L.dmlp_step(C.byref(a)), "dmlp_step")
     st = pipeline_stats()
     STEP_STATS["calls"] += 1
@@ -356,11 +360,12 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     STEP_STATS["early_grows"] += a.early_grows
     STEP_STATS["early_timeouts"] += a.early_timeouts
     STEP_STATS["early_qwaits"] += a.early_qwaits
+    STEP_STATS["host_ms"] += a.host_ms
     STEP_STATS["escalated"] += a.n_escalated
     STEP_STATS["device_path"] += 1 if a.path == 2 else 0
     kt = screen_kt(A)
     _IO["h2d"] += ((N + 63) // 64 * 64 * (kt * 64 + 4) + Q * (kt * 64 + 4) if a.path == 0 else 0)
-    _IO["h2d"] += (N + Q) * A * 4 + N * 4  # (lossless int32 rows; fp64 rows would be twice)
+    _IO["h2d"] += (Q if x32 is not None else N + Q) * A * 4 + N * 4  # (lossless int32 rows)
     if a.report_mode == 1:
         _IO["d2h"] += L.dmlp_format_bound(Q)
     if _EVENTS[0]:

@@ -83,6 +83,10 @@ class Engine:
                 K.step(w.X, w.labels, (0, 3), w.Qx, k, report="device")
             K.step_stats(reset=True)
             self.comm.sync()
+            if self.comm.world > 1 and self.strategy == "farm":
+                # how the replicated dataset reaches every GPU: measured, not assumed
+                from .strategies import probe_replication
+                self.comm.replication = probe_replication(self.comm)
         self.comm.barrier()
 
     # ------------------------------------------------------------------ API

@@ -242,7 +242,9 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     torch = _torch()
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
-    mode = os.environ.get("KNN_DATA_INGRESS", "h2d") if comm.world > 1 else "h2d"
+    mode = os.environ.get("KNN_DATA_INGRESS", "auto") if comm.world > 1 else "h2d"
+    if mode == "auto":  # the replication the untimed probe measured faster (Engine._warmup)
+        mode = (getattr(comm, "replication", None) or {}).get("mode", "h2d")
     max_rows = int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)
     kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
     if max_rows and N > max_rows:
@@ -253,7 +255,11 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
             d, i, lb, cs = be.knn_streamed(inp.X, inp.labels, (lo, hi), Ql, np.array(kl_h),
                                            max_rows, kstride=kmax)
         return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
-    if mode == "h2d" and be.on_gpu:
+    if mode in ("h2d", "xgmi") and be.on_gpu:
+        x32 = None
+        if mode == "xgmi" and not debug:
+            with tr.phase("replica"):  # 1/P of the rows over PCIe, the rest over xGMI
+                x32 = _x32_replica(comm, be, inp)
         with tr.phase("step"):
             # lo / hi / kmax None (one rank, farm()): the native step scans them
             k_range = (None if kmax is None else inp.k_range_all if comm.world == 1
@@ -266,7 +272,7 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
                      and os.environ.get("KNN_PLANE", "1") != "0" else None)
             r = be.step(inp.X, inp.labels, None if lo is None else (lo, hi), inp.Qx[a:b], kl_h,
                         k_range=k_range, qid_base=a, report=rep, lists=debug, kstride=kmax,
-                        plane=plane)
+                        plane=plane, x32=x32)
         if debug:
             return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, r.dist, r.ids, r.label,
                                      r.checksum, True)
@@ -299,6 +305,76 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
         d, i, lb, cs = be.knn(X, Ql, np.array(kl_h), labels=lab, label_range=(lo, hi),
                               kstride=kmax)
     return _farm_shared_tail(comm, be, inp, tr, counts, a, kmax, d, i, lb, cs, debug)
+
+
+def _x32_replica(comm, be, inp):
+    """The dataset's rows on every GPU as lossless int32, assembled over xGMI: each rank packs
+    and copies over its own PCIe link only its 1/P shard (rows [r s, (r + 1) s), s = ceil(N / P),
+    zero-padded), and one all-gather (RCCL) completes the replica — instead of every GPU pulling
+    all N rows over its own link.  bench_4 replicates the dataset with one MPI_Bcast (@0xc199);
+    this is its xGMI form.  None (every rank agrees, one 4-byte all-reduce) when some value is
+    not a 6-decimal number: the rows then go through the render plane."""
+    torch = _torch()
+    from .. import _lib
+    from . import dist_api as dist
+    N, A = inp.X.shape
+    P, r = comm.world, comm.rank
+    s = -(-N // P)
+    r0, r1 = min(N, r * s), min(N, (r + 1) * s)
+    st = getattr(inp, "_x32_stage", None)
+    if st is None or st.numel() != s * A:
+        st = torch.zeros(s * A, dtype=torch.int32).pin_memory()
+        inp._x32_stage = st
+    h = st.numpy()
+    bad = 0
+    if r1 > r0:
+        bad = int(_lib.lib().dmlp_cpu_rows_i32(inp.X[r0:r1].ctypes.data, (r1 - r0) * A,
+                                               h.ctypes.data))
+    flag = torch.tensor([bad], dtype=torch.int32, device=be.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag.item()):
+        return None
+    shard = st.to(be.device, non_blocking=True)
+    full = torch.empty(P * s * A, dtype=torch.int32, device=be.device)
+    dist.all_gather_into_tensor(full, shard)
+    return full
+
+
+def probe_replication(comm, nbytes=32 << 20, iters=3):
+    """Untimed, at Engine construction (P > 1 on GPUs): how the replicated dataset should reach
+    every GPU.  Measures, with every rank at once, the page-locked H2D bandwidth of one GPU and
+    an all-gather of nbytes; "xgmi" (1/P over PCIe + the all-gather) when that is faster than
+    every GPU copying everything over its own link ("h2d").  Every rank takes the same decision
+    (maxima over ranks)."""
+    import time
+    torch = _torch()
+    from . import dist_api as dist
+    P = comm.world
+    n = nbytes // 4 // P * P
+    h = torch.zeros(n, dtype=torch.int32).pin_memory()
+    d = torch.empty(n, dtype=torch.int32, device=comm.device)
+    shard = torch.zeros(n // P, dtype=torch.int32, device=comm.device)
+
+    def timed(fn):
+        fn()
+        comm.sync()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        comm.sync()
+        t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64,
+                         device=comm.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_h2d = timed(lambda: d.copy_(h, non_blocking=True))
+    t_ag = timed(lambda: dist.all_gather_into_tensor(d, shard))
+    t_x = t_h2d / P + t_ag
+    return {"mode": "xgmi" if t_x < t_h2d else "h2d", "bytes": n * 4,
+            "h2d_GBps_per_gpu_concurrent": round(n * 4 / t_h2d / 1e9, 2),
+            "allgather_GBps": round(n * 4 / t_ag / 1e9, 2),
+            "est_ms_h2d": round(t_h2d * 1e3, 4), "est_ms_xgmi": round(t_x * 1e3, 4)}
 
 
 def _step_egress(comm, inp, r, qid_base):

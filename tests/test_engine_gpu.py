@@ -120,7 +120,12 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     L = _lib.lib()
     old_dr = L.dmlp_pipeline_set(b"device_render", 1 if render == "device" else 0)
     old_qb = L.dmlp_pipeline_set(b"qb_blocks", 16)  # the query-block early start on
-    no_early = render == "device" and A == 64 and kmax <= 16
+    # an early-start step renders on the host whatever the switch says (the device render's
+    # kernels get no reliable wave slots beside the spinning screen: pipeline.hip dr_early_ok)
+    dr_used = False
+    # KT 2 / k <= 16: its screen leaves no registers for the early start's copies (pipeline.hip
+    # early_room): no early start there
+    no_room = A > 32 and A <= 64 and kmax <= 16
     Q = 131072 + 64 * 3 if A <= 64 else 65536 + 64
     cases = _early_inputs(n, A, kmax, Q, seed=n + A + kmax)
     dsts = []
@@ -137,10 +142,13 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
             assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
-            assert r.early == (early if A <= 128 and not no_early else 0)
-            assert K.pipeline_stats()["device_render"] == (1 if render == "device" else 0)
+            assert r.early == (early if A <= 128 and not no_room else 0)
+            if early and A <= 128:
+                assert K.pipeline_stats()["device_render"] == (1 if dr_used else 0)
             if A <= 64:
                 assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
+            if not r.early and early and render == "device":
+                assert K.pipeline_stats()["device_render"] == 1  # (no early start: rendered first)
             if r.early:  # (the queries in 16 blocks: DMLP_QB_BLOCKS)
                 assert r.early_timeouts == 0
                 assert r.early_waits > 0, "the screen never waited for a slice"

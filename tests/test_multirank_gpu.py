@@ -176,6 +176,10 @@ def test_python_shared_step_farm(case_x1, np_):
     assert _python(path, np_, "farm", env) == expect
     assert _python(bad_path, np_, "farm", env) == bad_expect
     assert _python(path, np_, "farm", dict(env, KNN_DATA_INGRESS="allgather")) == expect
+    # the xGMI replica: each rank ships 1/P of the int32 rows, one all-gather completes them
+    # (here over the host-staged plane), the native step renders from the device replica
+    assert _python(path, np_, "farm", dict(env, KNN_DATA_INGRESS="xgmi")) == expect
+    assert _python(bad_path, np_, "farm", dict(env, KNN_DATA_INGRESS="xgmi")) == bad_expect
 
 
 @pytest.mark.parametrize("np_", [2, 3])

@@ -151,9 +151,16 @@ for task in "$@"; do
           qb16:DMLP_QB_BLOCKS=16 qb16l2:DMLP_QB_BLOCKS=16,DMLP_QB_LEAD=2 qb8:DMLP_QB_BLOCKS=8
       python3 tools/ab_timeline.py gpurun_out/ab ;;
     dr)  # device render of the screen operands: host render / device render, +/- query blocks
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step dr_ab 900 bash tools/kernel_ab.sh hr:DMLP_DEVICE_RENDER=0 \
-          dr:DMLP_DEVICE_RENDER=1 drqb16:DMLP_QB_BLOCKS=16 drqb4:DMLP_QB_BLOCKS=4,DMLP_QB_LEAD=2
-      python3 tools/ab_timeline.py gpurun_out/ab ;;
+      # (the early-start bench shape renders on the host either way: Q = 32768 per step, no early
+      # start, and the bench shape with the early start off)
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 AB_ARGS="--q-per-gpu 32768" step dr_ab 900 bash tools/kernel_ab.sh \
+          hr:DMLP_DEVICE_RENDER=0 dr:DMLP_DEVICE_RENDER=1
+      python3 tools/ab_timeline.py gpurun_out/ab > "$OUT/dr_q32k.txt"; rm -rf gpurun_out/ab
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step dr_ab2 900 bash tools/kernel_ab.sh \
+          early_hr:DMLP_DEVICE_RENDER=0 noearly_hr:DMLP_DEVICE_RENDER=0,DMLP_FAST_EARLY=0 \
+          noearly_dr:DMLP_DEVICE_RENDER=1,DMLP_FAST_EARLY=0
+      python3 tools/ab_timeline.py gpurun_out/ab > "$OUT/dr_bench.txt"
+      cat "$OUT/dr_q32k.txt" "$OUT/dr_bench.txt" ;;
     plane)  # node render plane: P = 3 / 8 ranks sharing the one GPU (host-staged plane), --verify,
             # plane on / off: per-rank ms, the cgroup's CPU time in the timed region
       for P in 3 8; do
@@ -172,15 +179,13 @@ for task in "$@"; do
         done
       done
       grep -h '^{' "$OUT"/reh_*.log ;;
-    dropin_p)  # the drop-in at P = 2 / 3 through the node window on the one GPU (host-staged plane)
-      python -m distributed_machine_learning_project_amd.build --dropin \
-          distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
-      python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
-          --max 1000 --minK 16 --maxK 16 --num_labels 10 --output /tmp/dropin_bench.in > /dev/null
+    dropin_p)  # the drop-in at P = 2 / 3 through the node window on the one GPU (host-staged plane):
+               # bench.py --harness dropin (per-rank step times), knn_engine's shm farm beside it
       for P in 2 3; do
-        KNN_DATA_PLANE=host KNN_TRACE=1 step dropin_p$P 120 /opt/conda/bin/mpiexec -n $P sh -c \
-            "exec /tmp/eng_dropin < /tmp/dropin_bench.in > /tmp/dropin_p$P.out"
-        md5sum /tmp/dropin_p$P.out
+        KNN_DATA_PLANE=host step dropin_p$P 600 python bench.py --harness dropin --gpus $P --steps 5 \
+            --warmup 1 --q-per-gpu 65536
+        KNN_DATA_PLANE=host step native_p$P 600 python bench.py --harness native --gpus $P --steps 5 \
+            --warmup 1 --q-per-gpu 65536 --ingress shm
       done ;;
     final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
             # default and the exact path, the P = 3 host-plane rehearsal with --verify

@@ -5,6 +5,7 @@
 #   gpurun -- bash tools/kernel_ab.sh A B                            # library builds, kernel trace
 #   gpurun -- bash tools/kernel_ab.sh base: ct8:DMLP_X1_CT=8          # environment switches
 #   AB_PROF=0 AB_ROUNDS=3 gpurun -- bash tools/kernel_ab.sh c1:DMLP_HOST_OPS_CHUNKS=1 c2:DMLP_HOST_OPS_CHUNKS=2
+# AB_ARGS: extra bench.py arguments (e.g. "--q-per-gpu 32768").
 # AB_PROF=1 (default): rocprofv3 --kernel-trace --stats per run (tools/ab_summary.py reads the
 # kernel medians); AB_PROF=0: plain bench.py runs (host-side settings: no tracer overhead).
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -27,7 +28,7 @@ for round in $(seq 1 "$ROUNDS"); do
     LOG=gpurun_out/ab/$NAME.$round.log
     if [ "$PROF" = 0 ]; then
       env "${ENVS[@]}" timeout -k 10 120 python bench.py --steps "$STEPS" --warmup 20 --no-busbw \
-          > "$LOG" 2>&1 || { tail -20 "$LOG"; exit 1; }
+          ${AB_ARGS:-} > "$LOG" 2>&1 || { tail -20 "$LOG"; exit 1; }
     else
       env "${ENVS[@]}" timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/ab/$NAME.$round \
           -o run --output-format csv -- python3 bench.py --steps "$STEPS" --warmup 3 --no-busbw \
