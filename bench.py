@@ -109,6 +109,12 @@ def main(argv=None):
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="untimed traced steps after the timed ones: per-rank phase times, PCIe "
                          "and collective bytes, collective-sequence check (0: skip)")
+    ap.add_argument("--contract-runs", type=int, default=3,
+                    help="one GPU: after the timed steps, this many fresh processes of the engine.h "
+                         "drop-in linked with the reference's own common.cpp at this config (the "
+                         "reference's contract: one Engine::KNN call per process, parse untimed, "
+                         "the report written to a redirected stdout) -> reference_contract in the "
+                         "JSON (0: skip)")
     ap.add_argument("--harness", default="python", choices=["python", "native", "dropin"],
                     help="native: time the reference-contract binary (knn_engine: parse untimed, "
                          "'Time taken' = KNN + report + barrier, common.cpp:121-131) at this "
@@ -260,6 +266,23 @@ def main(argv=None):
         extra["verify_ok"] = got == ref
         extra["verify_s"] = round(time.perf_counter() - t_v, 1)
 
+    if comm.is_root and world == 1 and a.contract_runs > 0 and comm.on_gpu:
+        # the same config through the reference's own contract (bench_4's binary is timed this
+        # way by run_bench.sh:114-120): fresh processes, median of their Engine::KNN clocks
+        try:
+            t_c = time.perf_counter()
+            res, src = _contract_runs(a, True, (("bench", Q),), a.contract_runs, 0)
+            b = res["bench"]
+            extra["reference_contract"] = {
+                "harness": f"engine.h drop-in + {src}, one process per run, stdout to a file",
+                "runs": b["runs"], "time_ms_median": b["time_ms_median"],
+                "time_ms_min": b["time_ms_min"],
+                "knn_ms_median": b.get("knn_ms_median"), "emit_ms_median": b.get("emit_ms_median"),
+                "harness_time_taken_ms": b.get("harness_time_taken_ms"),
+                "queries_per_s": round(Q / (b["time_ms_median"] / 1e3), 1),
+                "wall_s": round(time.perf_counter() - t_c, 1)}
+        except Exception as e:  # noqa: BLE001 — a diagnostic beside the headline, never fatal
+            extra["reference_contract"] = {"error": str(e)[-300:]}
     if comm.is_root:
         value = Q / (ms / 1e3)
         line = {
@@ -426,17 +449,26 @@ def _bench_native(a):
     KNN_METRICS sidecar carries that time with microsecond resolution ("Time taken" on stderr is
     whole milliseconds).  --steps runs per config (median reported), --warmup runs discarded.
     Rank 0's stdout is checked byte-for-byte against the Python engine's CPU oracle for Q = 1000."""
+    P = max(1, a.gpus)
+    steps = a.steps if a.steps != 200 else 5  # one process per run: 5 by default
+    res, harness_src = _contract_runs(a, a.harness == "dropin", (("bench", a.q_per_gpu * P),
+                                                                  ("q1000", 1000)), steps, a.warmup)
+    dropin = a.harness == "dropin"
+    kmin = a.k if a.kmin is None else a.kmin
+    _print_native(a, res, harness_src, dropin, P, steps, kmin)
+
+
+def _contract_runs(a, dropin, shapes, steps, warmup):
+    """Fresh processes through the reference contract at each (tag, Q) of shapes: the drop-in
+    (engine.h + the reference's common.cpp) or knn_engine.  Returns ({tag: entry}, harness)."""
     import json as _json
     import statistics
     import subprocess
     import tempfile
 
-    import numpy as np
-
     from distributed_machine_learning_project_amd import build
     from distributed_machine_learning_project_amd.utils.io import generate, to_text
 
-    dropin = a.harness == "dropin"
     harness_src = None
     if dropin:
         # engine.h + dropin_engine.cpp linked with the reference's own common.cpp (its parse,
@@ -458,16 +490,15 @@ def _bench_native(a):
     P = max(1, a.gpus)
     kmin = a.k if a.kmin is None else a.kmin
     kmax = max(kmin, a.k if a.kmax is None else a.kmax)
-    steps = a.steps if a.steps != 200 else 5  # one process per run: 5 by default
     res = {}
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
-        for tag, q in (("bench", a.q_per_gpu * P), ("q1000", 1000)):
+        for tag, q in shapes:
             inp = generate(a.n_data, q, a.attrs, 0.0, 1000.0, kmin, kmax, a.labels, seed=42)
             path = os.path.join(td, f"{tag}.in")
             with open(path, "w") as f:
                 f.write(to_text(inp))
             times, out0, harness_ms, parts = [], None, [], {}
-            for r in range(a.warmup + steps):
+            for r in range(warmup + steps):
                 met = os.path.join(td, f"{tag}_{r}.json")
                 env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy,
                            KNN_INGRESS=a.ingress)  # shm: per-GPU ingress from a shared window
@@ -490,7 +521,7 @@ def _bench_native(a):
                                                  open(errp, "rb").read())
                 if pr.returncode != 0:
                     raise RuntimeError(pr.stderr.decode()[-2000:])
-                if r >= a.warmup:
+                if r >= warmup:
                     # KNN_METRICS: the engine's own microsecond clock (the harness prints whole
                     # milliseconds; the drop-in's covers Engine::KNN, pack and report included)
                     with open(met) as f:
@@ -523,6 +554,10 @@ def _bench_native(a):
                 _, cs = K.finalize_cpu(i, inp.k, inp.labels)
                 entry["verify_ok"] = bytes(out0) == format_report(cs)
             res[tag] = entry
+    return res, harness_src
+
+
+def _print_native(a, res, harness_src, dropin, P, steps, kmin):
     ms = res["bench"]["time_ms_median"]
     Q = res["bench"]["Q"]
     value = Q / (ms / 1e3)
@@ -538,7 +573,8 @@ def _bench_native(a):
                     "native knn_engine (reference contract: Time taken = KNN + report + barrier)"),
         "data": "synthetic (generate_input.py distribution, seed 42; reference inputs absent)",
         "config": {"model": f"bench_4 exact k-NN classifier N={a.n_data} A={a.attrs} "
-                            f"k={a.k if kmin == kmax else f'{kmin}-{kmax}'} labels={a.labels}",
+                            f"k={a.k if a.kmax is None or kmin == a.kmax else f'{kmin}-{a.kmax}'} "
+                            f"labels={a.labels}",
                    "global_batch": Q, "seq_len": a.attrs,
                    "parallelism": f"{a.strategy}{P}", "num_data": a.n_data},
         "q1000": res["q1000"], "bench_runs": res["bench"],

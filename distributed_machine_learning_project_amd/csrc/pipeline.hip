@@ -247,6 +247,7 @@ struct Tuning {
   int host_ops = 1;
   int device_render = 1;
   int qb_blocks = 0;
+  int word_write = 0;
 };
 Tuning make_tuning() {
   Tuning t;
@@ -260,12 +261,21 @@ Tuning make_tuning() {
   // 3.74: profiles/r7h_host_budget.md)
   if (env_off("DMLP_DEVICE_RENDER")) t.device_render = 0;
   t.qb_blocks = env_int("DMLP_QB_BLOCKS", 0);
+  t.word_write = env_int("DMLP_WORD_WRITE", 0);
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
 }
 Tuning g_tune = make_tuning();
 bool dr_on() { return g_tune.device_render != 0; }
+// An early-start ready word (or a slice's norm word) set on the side stream behind the copies
+// it guards: a 4-byte copy from page-locked memory (which this runtime runs as a blit kernel that
+// needs a wave slot beside the spinning screen), or DMLP_WORD_WRITE=1 a stream write-value
+// packet (no kernel).
+hipError_t put_word(unsigned* dst, unsigned v, const unsigned* host_src, hipStream_t s) {
+  if (g_tune.word_write) return hipStreamWriteValue32(s, dst, v, 0);
+  return hipMemcpyAsync(dst, host_src, sizeof(unsigned), hipMemcpyHostToDevice, s);
+}
 int qb_blocks() { return std::min(kMaxQBlocks, std::max(0, g_tune.qb_blocks)); }
 // what the last call did (dmlp_pipeline_stats)
 struct Stats {
@@ -1120,7 +1130,7 @@ struct Step {
       auto render_x = [&](int i, const int* s32, const double* s64) {
         const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
         if (t1 <= t0) {  // an empty slice: its ready word all the same
-          if (early) CK(hipMemcpyAsync(rdy + i, one, 4, hipMemcpyHostToDevice, w.side));
+          if (early) CK(put_word(rdy + i, 1u, one, w.side));
           return;
         }
         CKL(dmlp_render_rows(KT, A, s32, s64, t0 * 64, (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
@@ -1347,7 +1357,7 @@ struct Step {
                                   (q1 - q0) * W * 2, hipMemcpyHostToDevice, w.side));
                 CK(hipMemcpyAsync(const_cast<float*>(hx.qn) + q0, qn_h, (q1 - q0) * 4,
                                   hipMemcpyHostToDevice, w.side));
-                CK(hipMemcpyAsync(qrdy + b, one, sizeof(unsigned), hipMemcpyHostToDevice, w.side));
+                CK(put_word(qrdy + b, 1u, one, w.side));
               }
               CK(mark(M_OPS, w.side));
             };
@@ -1363,7 +1373,7 @@ struct Step {
               const int r2 = h2d_tiles_data(t0, t1, i);
               if (r2 & 4) throw Fail{-(int)hipErrorUnknown};
               if (r2) early_bad = true;
-              CK(hipMemcpyAsync(rdy + i, one, sizeof(unsigned), hipMemcpyHostToDevice, w.side));
+              CK(put_word(rdy + i, 1u, one, w.side));
             }
             if (!pl && lead >= NS) qblocks();
             CK(mark(M_DATA, w.side));
@@ -1508,8 +1518,8 @@ struct Step {
       m = std::max(m, nm);
       if (rdy) {
         std::memcpy(nh + 2 + i, &nm, 4);
-        CK(hipMemcpyAsync(xnm_sl + i, nh + 2 + i, 4, hipMemcpyHostToDevice, w.side));
-        CK(hipMemcpyAsync(rdy + i, nh, 4, hipMemcpyHostToDevice, w.side));
+        CK(put_word(xnm_sl + i, nh[2 + i], nh + 2 + i, w.side));
+        CK(put_word(rdy + i, 1u, nh, w.side));
       }
     }, [] {});
     if (mx) *mx = bad ? INFINITY : m;
@@ -1524,12 +1534,16 @@ struct Step {
     unsigned* xnm_h = w.sx_nm.p + 2 + i;
     short* xhi = (short*)const_cast<void*>(d.hx->xhi) + t0 * 64 * d.W;
     float* xin = const_cast<float*>(d.hx->xin) + t0 * 64;
-    return a->Xr ? dmlp_host_ops_h2d_tiles_rows(a->Xr, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT,
-                                                xhi_h, xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin,
-                                                d.xnm_sl + i, w.dq_hi.p, w.dq_n.p, 1, w.side)
-                 : dmlp_host_ops_h2d_tiles(a->X, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT, xhi_h,
-                                           xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin,
-                                           d.xnm_sl + i, w.dq_hi.p, w.dq_n.p, 1, w.side);
+    unsigned* xd = g_tune.word_write ? nullptr : d.xnm_sl + i;  // (null: no 4-byte copy)
+    const int rc =
+        a->Xr ? dmlp_host_ops_h2d_tiles_rows(a->Xr, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT, xhi_h,
+                                             xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin, xd,
+                                             w.dq_hi.p, w.dq_n.p, 1, w.side)
+              : dmlp_host_ops_h2d_tiles(a->X, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT, xhi_h,
+                                        xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin, xd, w.dq_hi.p,
+                                        w.dq_n.p, 1, w.side);
+    if (!xd && !(rc & 4)) CK(put_word(d.xnm_sl + i, *xnm_h, xnm_h, w.side));
+    return rc;
   }
 };
 
@@ -1733,7 +1747,8 @@ extern "C" int dmlp_pipeline_set(const char* key, int value) {
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
            : k == "device_render" ? &g_tune.device_render
-           : k == "qb_blocks" ? &g_tune.qb_blocks : nullptr;
+           : k == "qb_blocks" ? &g_tune.qb_blocks
+           : k == "word_write" ? &g_tune.word_write : nullptr;
   if (!f) return -1;
   const int old = *f;
   *f = value;

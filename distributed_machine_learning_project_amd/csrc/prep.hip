@@ -386,7 +386,7 @@ static int host_ops_h2d_tiles(const double* X, const double* const* Xr, int64_t 
   }
   if (rc & 1) m = INFINITY;
   memcpy(xnm_h, &m, 4);
-  h2d(xnm_d, xnm_h, 4);
+  if (xnm_d) h2d(xnm_d, xnm_h, 4);  // (null: the caller writes the word itself)
   for (int c = 0; c < chunks; ++c) {
     const int64_t q0 = Q * c / chunks, q1 = Q * (c + 1) / chunks;
     if (q1 <= q0) continue;

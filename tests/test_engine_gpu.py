@@ -112,10 +112,10 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     variant (one wave per SIMD, 404 of 512 registers).  A = 256 (KT = 8, all 512 registers): the
     step refuses the early start there — its image copies (blit kernels) would find no free wave
     slot beside the spinning screen — and the results stay exact.  One screen slice needs a full
-    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4).  render: the screen
-    operands rendered on the GPU from the landed int32 rows (the default; its render kernels run
-    beside the spinning screen and publish the ready words — except at A = 64 / k <= 16, whose
-    screen leaves no registers for them: rendered first, no early start) or on the host."""
+    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4).  A = 64 / k <= 16 (KT 2,
+    2 x 244 registers) leaves no slot for the copies: no early start there.  render: the device
+    render switch on or off — an early-start step renders on the host either way
+    (pipeline.hip dr_early_ok); without the early start the switch's render runs."""
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
     old_dr = L.dmlp_pipeline_set(b"device_render", 1 if render == "device" else 0)
@@ -143,7 +143,7 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
             assert r.early == (early if A <= 128 and not no_room else 0)
-            if early and A <= 128:
+            if r.early:
                 assert K.pipeline_stats()["device_render"] == (1 if dr_used else 0)
             if A <= 64:
                 assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"

@@ -24,6 +24,7 @@
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
 #   qb         query-block early start A/B (DMLP_QB_BLOCKS / DMLP_QB_LEAD), step timelines
 #   dr         device render A/B (DMLP_DEVICE_RENDER, DMLP_QB_BLOCKS), step timelines
+#   ww         early-start ready words by stream write-value packets (DMLP_WORD_WRITE) A/B
 #   plane      node render plane rehearsal: bench.py --gpus 3 / 8 on the one GPU, plane on / off
 #   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
@@ -161,6 +162,14 @@ for task in "$@"; do
           noearly_dr:DMLP_DEVICE_RENDER=1,DMLP_FAST_EARLY=0
       python3 tools/ab_timeline.py gpurun_out/ab > "$OUT/dr_bench.txt"
       cat "$OUT/dr_q32k.txt" "$OUT/dr_bench.txt" ;;
+    ww)  # early-start ready words as stream write-value packets instead of 4-byte blit copies,
+         # with and without the query-block early start; the early-start tests under the switch
+      DMLP_WORD_WRITE=1 step ww_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
+          --timeout 120 --timeout-method thread -k "early_start or native_step"
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ww_ab 900 bash tools/kernel_ab.sh base:DMLP_WORD_WRITE=0 \
+          ww:DMLP_WORD_WRITE=1 wwqb16:DMLP_WORD_WRITE=1,DMLP_QB_BLOCKS=16 \
+          wwqb8l2:DMLP_WORD_WRITE=1,DMLP_QB_BLOCKS=8,DMLP_QB_LEAD=2
+      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/ww_ab.txt" ;;
     plane)  # node render plane: P = 3 / 8 ranks sharing the one GPU (host-staged plane), --verify,
             # plane on / off: per-rank ms, the cgroup's CPU time in the timed region
       for P in 3 8; do
