@@ -109,12 +109,13 @@ def main(argv=None):
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="untimed traced steps after the timed ones: per-rank phase times, PCIe "
                          "and collective bytes, collective-sequence check (0: skip)")
-    ap.add_argument("--contract-runs", type=int, default=3,
+    ap.add_argument("--contract-runs", type=int,
+                    default=int(os.environ.get("DMLP_BENCH_CONTRACT_RUNS", "3")),
                     help="one GPU: after the timed steps, this many fresh processes of the engine.h "
                          "drop-in linked with the reference's own common.cpp at this config (the "
                          "reference's contract: one Engine::KNN call per process, parse untimed, "
                          "the report written to a redirected stdout) -> reference_contract in the "
-                         "JSON (0: skip)")
+                         "JSON (0: skip; default DMLP_BENCH_CONTRACT_RUNS or 3)")
     ap.add_argument("--harness", default="python", choices=["python", "native", "dropin"],
                     help="native: time the reference-contract binary (knn_engine: parse untimed, "
                          "'Time taken' = KNN + report + barrier, common.cpp:121-131) at this "

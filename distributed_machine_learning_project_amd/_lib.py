@@ -86,6 +86,9 @@ _SIGS = {
     "dmlp_screen_x1_collect": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "dmlp_set_x1_mode": (None, [i32]),
     "dmlp_set_x1_ct": (None, [i32]),
+    "dmlp_set_x1_ring": (None, [i32]),
+    "dmlp_get_x1_ring": (i32, []),
+    "dmlp_x1_ring_launches": (C.c_int64, []),
     "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
                           vp, vp]),

@@ -164,6 +164,11 @@ int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cols(int KT, int kmax);
 int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
+// the LDS-ring screen (k <= 16, A <= 32, >= one 512-query workgroup per CU): 0 off, or its
+// sub-buffer depth 16 / 14 / 12 (DMLP_X1_RING); launches counts the ring kernels run so far
+void dmlp_set_x1_ring(int sub);
+int dmlp_get_x1_ring(void);
+int64_t dmlp_x1_ring_launches(void);
 int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax);  // A > 64: one wave per SIMD
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);

@@ -1740,10 +1740,15 @@ extern "C" int dmlp_step_timeline(double* ms, const char** names, int cap) {
 }
 
 // Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render",
-// "qb_blocks".  Returns the previous
+// "qb_blocks", "word_write", "x1_ring".  Returns the previous
 // value, or -1 for an unknown key.
 extern "C" int dmlp_pipeline_set(const char* key, int value) {
   const std::string k = key ? key : "";
+  if (k == "x1_ring") {  // the LDS-ring screen (screen_x1.hip): 0 off, 16 / 14 / 12
+    const int old = dmlp_get_x1_ring();
+    dmlp_set_x1_ring(value);
+    return old;
+  }
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
            : k == "device_render" ? &g_tune.device_render

@@ -51,22 +51,37 @@ int x1_mode() {
 }
 __device__ unsigned long long g_x1_dbg[8];
 
-template <int KT, int SUB, int DEPTH, int CHECK, int CTV>
+// RING = 0: one wave per workgroup, each wave streams its slice's fragments from L2 into a
+// register ring.  RING = R > 0: W = 8 waves per workgroup (one CU: 2 per SIMD), each with its own
+// 64 query columns, share an R-tile LDS ring of the slice's fragments and C operands, filled by
+// LDS-DMA (buffer_load ... lds): every tile crosses L2 -> CU once per workgroup instead of once
+// per wave (the texture path ran ~90 % busy on per-wave loads: VERDICT r4, r5q/r7j profiles).
+// The waves are not lock-stepped by barriers: each tile's 5 pieces (4 x 1 KiB of fragments + the
+// 256-byte C operand) are issued by 5 of the 8 waves in rotation, a per-slot ready counter
+// releases the tile and a per-slot done counter lets the slot be refilled, so one wave's
+// compaction delays the others only once it falls RING - L tiles behind.
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int RING = 0>
 struct X1Cfg {
+  static constexpr int W = RING ? 8 : 1;        // waves per workgroup
   static constexpr int CT = CTV;                // MFMA column tiles per wave (4 or 8)
-  static constexpr int NCOL = 16 * CT;          // queries per wave (= workgroup)
-  // column pitch in entries: 4 interleaved sub-buffers + 4 pad slots; 68 = 4 (mod 64) puts the
-  // 64 lanes of an append (16 columns x 4 sub-buffers, same fill) on 64 distinct banks
+  static constexpr int NCOL = 16 * CT;          // queries per wave
+  // column pitch in entries: 4 interleaved sub-buffers + 4 pad slots (which hold the 4
+  // sub-buffer counts during a compaction); CP = 4 (mod 8) puts the 64 lanes of an append (16
+  // columns x 4 sub-buffers, same fill) on 64 distinct banks
   static constexpr int CP = 4 * SUB + 4;
   // the fill check runs every CHECK steps, so a sub-buffer is compacted once it holds more than
   // SUB - CHECK entries (CHECK more appends always fit) and keeps at most SUB - CHECK of them
   static constexpr int CAPE = 4 * (SUB - CHECK);  // group entries a column may keep
-  static constexpr int IDCAP = 4 * (SUB - 1);  // group-id stride per (query, slice), any CHECK
+  // group-id stride per (query, slice): the k class's (x1_sub: 16 or 32), any CHECK / ring SUB
+  static constexpr int IDCAP = 4 * ((SUB <= 16 ? 16 : 32) - 1);
   static constexpr int SBUF = NCOL * CP * 4;
-  // + a 512-byte ring of two 4-step windows of the rows' -|x'|^2/2 (the MFMA C operand): the
-  // ring loads read it with ds_read_b128 instead of a 16-byte-per-lane buffer load per step
-  static constexpr int XRING = 512;
-  static constexpr int LDS = SBUF + NCOL * 4 * 4 + NCOL * 4 * 4 + XRING;
+  // per wave without a ring: a 512-byte ring of two 4-step windows of the rows' -|x'|^2/2 (the
+  // MFMA C operand), read with ds_read_b128 instead of a 16-byte-per-lane buffer load per step
+  static constexpr int XRING = RING ? 0 : 512;
+  static constexpr int TILEB = 4096 * KT;       // fragment bytes of a 64-point tile (hi only)
+  static constexpr int RINGB = RING * (TILEB + 256);
+  static constexpr int FLAGB = (2 * RING + 4) * 4;  // ready[R], done[R], fail
+  static constexpr int LDS = W * SBUF + (RING ? RINGB + FLAGB : XRING);
   static constexpr int D = DEPTH;               // register-ring depth (steps in flight)
 };
 
@@ -92,8 +107,8 @@ __device__ __forceinline__ unsigned unord32(unsigned o) {
   return o ^ ((o >> 31) ? 0x80000000u : 0xffffffffu);
 }
 
-template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE, bool F16>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32 || KT >= 4) ? 1 : 2))) void k_screen_x1(
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, int MODE, bool F16, int RING = 0>
+__global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu((CTV == 8 || SUB == 32 || KT >= 4) ? 1 : 2))) void k_screen_x1(
     const u32x4* __restrict__ xfrag, const f32x4* __restrict__ xinit4, int n_tiles, int n_points,
     const bf16x8* __restrict__ qhi, const float* __restrict__ qn, const int* __restrict__ qidx,
     const int* __restrict__ qk, int nq, const unsigned* __restrict__ xnmax_bits,
@@ -103,27 +118,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const unsigned* __restrict__ rdy, int rdy_tiles, int rdy_n,
     const unsigned* __restrict__ xnm_sl, unsigned* __restrict__ estats, long long rdy_to,
     const unsigned* __restrict__ qrdy, int qrdy_q) {
-  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV, RING>;
   // COLLECT (large k, second pass): the threshold is fixed at the query's seed hseed[p] (a
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
   // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
   constexpr bool COLLECT = (MODE & 16) != 0;
+  static_assert(!(COLLECT && RING), "the COLLECT pass runs without the ring");
   constexpr int CT = C::CT;
   constexpr int D = C::D;
   constexpr int NH = C::NCOL / 64;  // columns per lane in the lane-owns-column phases
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned* const sbuf = (unsigned*)smem;                    // [col][CP] interleaved entries
-  int* const lcnt = (int*)(smem + C::SBUF);                  // [col][m] counts
-  float* const lh = (float*)(lcnt + C::NCOL * 4);            // [col] threshold
-  int* const lk = (int*)(lh + C::NCOL);                      // [col] k
-  float* const leps = (float*)(lk + C::NCOL);                // [col] eps
-  int* const lflag = (int*)(leps + C::NCOL);                 // [col] 1 = overflowed
+  const int wv = RING ? (int)(threadIdx.x >> 6) : 0;        // wave of the workgroup
+  unsigned* const sbuf = (unsigned*)(smem + wv * C::SBUF);   // [col][CP] interleaved entries
+  const unsigned sb0 = (unsigned)(wv * C::SBUF);             // its LDS byte offset
 
   const int lane = threadIdx.x & 63;
   const int c = lane & 15;
   const int kg = lane >> 4;
 
-  // ---- block -> (query block, slice); XCD-aware when S % 8 == 0 (slice s stays on one XCD's L2)
+  // ---- block -> (query block, slice); XCD-aware when S % 8 == 0 (slice s stays on one XCD's L2).
+  // A ring workgroup's query block is W consecutive waves' columns.
   const int b = blockIdx.x;
   int qb, s;
   if ((S & 7) == 0) {
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   if (t1 > n_tiles) t1 = n_tiles;
   const int nt = t1 > t0 ? t1 - t0 : 0;
   const int nsteps = nt * 4;
-  const int pbase = qb * C::NCOL;
+  const int pbase = (qb * C::W + wv) * C::NCOL;
 
   if (*bad) {
     for (int col = lane; col < C::NCOL; col += 64)
@@ -156,7 +170,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // overflowed (the pipeline escalates them).  The ready word is written by a host-initiated copy:
   // it is polled with relaxed system-scope loads and followed by a system-scope acquire fence
   // before any image load.  Per wave: waits that had to spin, eps growths and timeouts go to
-  // estats[0..2] at the end (the pipeline reports them).
+  // estats[0..2] at the end (the pipeline reports them).  With the LDS ring the wave that issues
+  // a tile's pieces does the slice waits; every wave grows its eps as its scan reaches a slice.
   int have = 0;          // slices known landed (wave-uniform)
   bool rdy_fail = false;
   unsigned n_wait = 0, n_grow = 0, n_to = 0, n_qwait = 0;
@@ -195,8 +210,136 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   // of probing slice by slice — each probe is a system-scope round trip on the wave's critical
   // path (the per-slice probes cost the screen ~0.075 ms: profiles/r7n_refine_ab.txt, r7s)
   auto widen = [&](int need) { return need < rdy_n - 1 && rdy_probe(rdy_n - 1) ? rdy_n - 1 : need; };
+
+  // slice-local buffer resources: step j's fragments sit at j * KT * hl KiB (hi at +0, lo — when
+  // the image carries it (hl = 2) — at +1 KiB per kt) and its -|x|^2/2 at j * 64 B, so the ring
+  // loads need no address arithmetic beyond one scalar offset; prefetches past the slice read
+  // zeros instead of faulting
+  const int ks = hl * 1024;          // bytes between kt fragments of a step
+  const int frags = 4 * KT * hl;     // 1 KiB fragments per 64-point tile
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(xfrag + (int64_t)t0 * (frags * 64)), (short)0, nt * frags * 64 * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
+
+  // ---- the LDS ring (RING > 0): [R][TILEB] fragments | [R][256] C operands | ready[R] |
+  // done[R] | fail | next.  ready[t % R] counts the published tiles of the slot (tile t is in
+  // once it reaches t / R + 1); done[t % R] counts the waves that have read tile t out (slot t
+  // may take tile t + R once it reaches 8 (t / R + 1)); next is the first tile nobody claimed.
+  // A tile is claimed (compare-and-swap on next) by the first wave whose scan comes within L
+  // tiles of it: that wave issues all its pieces (4 KT LDS-DMA fragments + the C operand) and
+  // publishes it once its vmcnt drained — at its next tile, or before a compaction.  Every wait
+  // is bounded (RTO); a timed-out wait sets fail and the workgroup's queries report overflow.
+  constexpr int L = 3;
+  constexpr long long RTO = 20000000;  // 200 ms of the 100 MHz wall clock: a bug, not a wait
+  constexpr unsigned ringA = (unsigned)(C::W * C::SBUF);
+  constexpr unsigned ringN = ringA + (unsigned)(RING * C::TILEB);
+  unsigned* const rready = (unsigned*)(smem + ringN + RING * 256);
+  unsigned* const rdone = rready + RING;
+  unsigned* const rfail = rdone + RING;
+  unsigned* const rnext = rfail + 1;
+  typedef __attribute__((address_space(3))) void* lds_vp;
+  auto lds_wait = [&](unsigned* f, unsigned want) -> bool {
+    auto ld = [&]() {
+      return (unsigned)__builtin_amdgcn_readfirstlane(
+          (int)__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    if (ld() >= want) return true;
+    const long long ts = wall_clock64();
+    for (;;) {
+      __builtin_amdgcn_s_sleep(1);
+      if (ld() >= want) return true;
+      if (wall_clock64() - ts > RTO) {
+        ++n_to;
+        return false;
+      }
+    }
+  };
+  auto ring_fail = [&]() {
+    __hip_atomic_store(rfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  int have_p = 0;  // slices this wave saw landed as a producer
+  // claim tile t (t == next): true if this wave now owns its pieces
+  auto claim = [&](int t) -> bool {
+    if ((unsigned)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+            rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != (unsigned)t)
+      return false;
+    int got = 0;
+    if (lane == 0) {
+      unsigned e = (unsigned)t;
+      got = __hip_atomic_compare_exchange_strong(rnext, &e, (unsigned)t + 1u, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return __builtin_amdgcn_readlane(got, 0) != 0;
+  };
+  // issue tile t's pieces into slot t % R (the claimer only)
+  auto produce = [&](int t) {
+    if (rdy && have_p < rdy_n) {
+      const int si = min(t / rdy_tiles, rdy_n - 1);
+      if (si >= have_p) {
+        const int need = widen(si);
+        bool ok = true;
+        if (need == si)
+          for (int i = have_p; i <= si && ok; ++i) ok &= wait_slice(i);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the host's DMA wrote them
+        have_p = ok ? need + 1 : rdy_n;
+        if (!ok) ring_fail();
+      }
+    }
+    const int slot = t % RING;
+    if (t >= RING && !lds_wait(rdone + slot, 8u * (unsigned)(t / RING))) ring_fail();
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xr, (lds_vp)(smem + ringA + slot * C::TILEB + (p * KT + kt) * 1024), 16,
+            lane * 16 + kt * ks, (t * 4 + p) * (KT * ks), 0, 0);
+    if (lane < 16)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ir, (lds_vp)(smem + ringN + slot * 256), 16,
+                                               lane * 16, t * 256, 0, 0);
+  };
+  auto publish = [&](int t) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces landed
+    if (lane == 0)
+      __hip_atomic_fetch_add(rready + t % RING, 1u, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto done_read = [&](int t) {  // this wave's reads of tile t are issued: retire, then count
+    if (lane == 0)
+      __hip_atomic_fetch_add(rdone + t % RING, 1u, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  int pend = -1;  // the tile this wave issued and has not published yet
+
   float xnmax;
-  if (rdy) {
+  if constexpr (RING > 0) {
+    if (nsteps > 0) {
+      if ((int)threadIdx.x < 2 * RING + 2) rready[threadIdx.x] = 0u;  // ready, done, fail, next
+      __syncthreads();
+      unsigned own = 0;
+      for (int t = 0; t < L && t < nt; ++t)
+        if (claim(t)) {
+          produce(t);
+          own |= 1u << t;
+        }
+      if (own) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        for (int t = 0; t < L && t < nt; ++t)
+          if ((own >> t) & 1u) publish(t);
+      }
+    }
+    // (a wave past the last query has no block to wait for)
+    if (rdy && qrdy && pbase < nq) rdy_fail |= !wait_word(qrdy + pbase / qrdy_q, n_qwait);
+    if (nsteps > 0 && !lds_wait(rready, 1u)) ring_fail();
+    if (rdy) {  // slice 0 (at least) landed: a producer waited for it
+      const int need = widen(0);
+      xnmax = fold_xnm(0.0f, 0, need);
+      have = need + 1;
+    } else {
+      xnmax = __uint_as_float(*xnmax_bits);
+    }
+  } else if (rdy) {
     // QUERY-BLOCK EARLY START (qrdy): the query operands cross PCIe in blocks of qrdy_q queries
     // (a multiple of the wave's columns), each with its own ready word: this wave waits only for
     // its own block before the prologue reads its queries' fragments and norms
@@ -210,6 +353,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   } else {
     xnmax = __uint_as_float(*xnmax_bits);
   }
+  auto eps_of = [&](float qv, float xm) {
+    return r1 * sqrtf(qv) * sqrtf(xm) + r2 * xm + r3 * (sqrtf(qv) + sqrtf(xm)) + r3 * 0x1p-15f;
+  };
 
   bf16x8 bh[CT][KT];
   float h[CT];
@@ -228,51 +374,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const float sd = COLLECT && valid ? hseed[p] : -FLT_MAX;
     const bool sbad = COLLECT && sd == INFINITY;
     h[ct] = valid && !sbad ? (COLLECT ? fmaxf(sd, -FLT_MAX) : -FLT_MAX) : INFINITY;
-    addr[ct] = (unsigned)(((ct * 16 + c) * C::CP + kg) * 4);
+    addr[ct] = sb0 + (unsigned)(((ct * 16 + c) * C::CP + kg) * 4);
     lim[ct] = addr[ct] + (SUB - CHECK) * 16;
-    if (lane < 16) {
-      const int col = ct * 16 + c;
-      lh[col] = h[ct];
-      lk[col] = valid ? qk[q] : 0;
-      leps[col] = valid ? r1 * sqrtf(qn[q]) * sqrtf(xnmax) + r2 * xnmax +
-                              r3 * (sqrtf(qn[q]) + sqrtf(xnmax)) + r3 * 0x1p-15f
-                        : 0.0f;
-      lflag[col] = sbad ? 1 : 0;
-    }
   }
-  // slice-local buffer resources: step j's fragments sit at j * KT * hl KiB (hi at +0, lo — when
-  // the image carries it (hl = 2) — at +1 KiB per kt) and its -|x|^2/2 at j * 64 B, so the ring
-  // loads need no address arithmetic beyond one scalar offset; prefetches past the slice read
-  // zeros instead of faulting
-  const int ks = hl * 1024;          // bytes between kt fragments of a step
-  const int frags = 4 * KT * hl;     // 1 KiB fragments per 64-point tile
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(xfrag + (int64_t)t0 * (frags * 64)), (short)0, nt * frags * 64 * 16, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(xinit4 + (int64_t)t0 * 16), (short)0, nt * 16 * 16, 0x00020000);
+  // per column in the lane-owns-column layout (lane j: column j + 64 hb): threshold, k, eps and
+  // overflow flag, kept in registers; h[ct] above is the threshold in the MFMA layout (lane
+  // c + 16 kg: column 16 ct + c), refreshed from oh by a lane shuffle
+  float oh[NH], oe[NH];
+  int okk[NH], ofl[NH];
+#pragma unroll
+  for (int hb = 0; hb < NH; ++hb) {
+    const int p = pbase + lane + 64 * hb;
+    const bool valid = p < nq;
+    const int q = valid ? qidx[p] : 0;
+    const float sd = COLLECT && valid ? hseed[p] : -FLT_MAX;
+    const bool sbad = COLLECT && sd == INFINITY;
+    oh[hb] = valid && !sbad ? (COLLECT ? fmaxf(sd, -FLT_MAX) : -FLT_MAX) : INFINITY;
+    okk[hb] = valid ? qk[q] : 0;
+    oe[hb] = valid ? eps_of(qn[q], xnmax) : 0.0f;
+    ofl[hb] = sbad ? 1 : 0;
+  }
+  // h[ct] of the MFMA layout from the owners' oh
+  auto pull_h = [&]() {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) h[ct] = __shfl(oh[ct >> 2], (ct & 3) * 16 + c);
+  };
 
   // ---- batched compaction: lane j owns column j.  FINAL: write the column's candidate ids.
   // A column's entries are interleaved: slot s holds entry s >> 2 of sub-buffer s & 3, so the
   // lane reads its column as 16-byte vectors and re-deals the survivors by writing them back at
-  // consecutive slots (slot s -> sub-buffer s & 3 again, i.e. round-robin).
+  // consecutive slots (slot s -> sub-buffer s & 3 again, i.e. round-robin).  The 4 sub-buffer
+  // counts travel through the column's pad slots 4 SUB .. 4 SUB + 3.
   int nout[NH];  // COLLECT: group entries this lane's column has flushed so far
 #pragma unroll
   for (int hb = 0; hb < NH; ++hb) nout[hb] = 0;
   auto compact = [&](const bool final_pass) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) lcnt[(ct * 16 + c) * 4 + kg] = (int)(addr[ct] - (lim[ct] - (SUB - CHECK) * 16)) >> 4;
+    for (int ct = 0; ct < CT; ++ct)
+      sbuf[(ct * 16 + c) * C::CP + 4 * SUB + kg] =
+          (addr[ct] - (lim[ct] - (SUB - CHECK) * 16)) >> 4;
     dmlp::wave_sync();
 #pragma unroll 1
     for (int hb = 0; hb < NH; ++hb) {
     const int j = lane + 64 * hb;
     unsigned* const colbuf = sbuf + j * C::CP;
-    const int4 n4 = *(const int4*)(lcnt + j * 4);
+    const int4 n4 = *(const int4*)(colbuf + 4 * SUB);
     const int nm[4] = {n4.x, n4.y, n4.z, n4.w};
     if constexpr (COLLECT) {
       // flush: every buffered entry (appended at a group max >= the fixed seed) goes to the
       // column's global list as (ordered 16-bit key << 16 | slice-relative group index)
       const int pc = pbase + j;
-      bool ov = lflag[j] != 0;
+      bool ov = ofl[hb] != 0;
       int no = nout[hb];
       int* const out = cand_ids + ((int64_t)pc * S + s) * ccap;
       if (pc < nq && !ov) {
@@ -291,19 +443,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       }
       nout[hb] = no;
       if (!final_pass) {
-        *(int4*)(lcnt + j * 4) = int4{0, 0, 0, 0};
-        if (ov) { lh[j] = INFINITY; lflag[j] = 1; }  // stop appending: the query overflowed
+        *(int4*)(colbuf + 4 * SUB) = int4{0, 0, 0, 0};
+        if (ov) { oh[hb] = INFINITY; ofl[hb] = 1; }  // stop appending: the query overflowed
       } else if (pc < nq) {
         cand_cnt[(int64_t)pc * S + s] = ov ? -1 : no;
-        cand_h[2 * ((int64_t)pc * S + s)] = lh[j];
-        cand_h[2 * ((int64_t)pc * S + s) + 1] = leps[j];
+        cand_h[2 * ((int64_t)pc * S + s)] = oh[hb];
+        cand_h[2 * ((int64_t)pc * S + s) + 1] = oe[hb];
       }
       continue;
     }
-    const int kc = lk[j];
-    const float epc = leps[j];
-    const int flag = lflag[j];
-    float hc = lh[j];
+    const int kc = okk[hb];
+    const float epc = oe[hb];
+    const int flag = ofl[hb];
+    float hc = oh[hb];
     // entries -> ordered keys in place (0 = empty slot)
     unsigned e[4 * SUB];
     // every buffered key is >= key(hc): appended at h = hc or kept at the last compaction
@@ -368,8 +520,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
 #pragma unroll
       for (int i = 0; i < 4 * SUB; ++i) {
         const bool keep = e[i] >= kh;
-        // every lane stores; a dropped entry lands in the column's pad slot (never read)
-        colbuf[keep ? pos : 4 * SUB] = unord32(e[i]);
+        // every lane stores; a dropped entry lands in the next free slot (overwritten by the
+        // next kept one, or past the new count: never read)
+        colbuf[pos] = unord32(e[i]);
         pos += keep ? 1 : 0;
       }
       const bool ovf = flag || pos > C::CAPE;
@@ -378,9 +531,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
       nn.y = ovf ? 0 : (pos + 2) >> 2;
       nn.z = ovf ? 0 : (pos + 1) >> 2;
       nn.w = ovf ? 0 : pos >> 2;
-      *(int4*)(lcnt + j * 4) = nn;
-      lh[j] = ovf ? INFINITY : hc;
-      lflag[j] = ovf ? 1 : 0;
+      *(int4*)(colbuf + 4 * SUB) = nn;
+      oh[hb] = ovf ? INFINITY : hc;
+      ofl[hb] = ovf ? 1 : 0;
     } else {
       // kept entries out as (ordered 16-bit key << 16 | slice-relative group index): the refine
       // takes the k-th largest key over ALL slices of the query (a global threshold, as tight as
@@ -405,9 +558,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     if (!final_pass) {
       dmlp::wave_sync();
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * lcnt[(ct * 16 + c) * 4 + kg];
-        h[ct] = (MODE & 128) ? INFINITY : lh[ct * 16 + c];
+      for (int ct = 0; ct < CT; ++ct)
+        addr[ct] = lim[ct] - (SUB - CHECK) * 16 + 16 * sbuf[(ct * 16 + c) * C::CP + 4 * SUB + kg];
+      pull_h();
+      if (MODE & 128) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) h[ct] = INFINITY;
       }
       // resolve these LDS loads here, not at the next use: otherwise the waitcnt pass sees them
       // pending after the conditional call and drains lgkmcnt at every following step
@@ -437,6 +593,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
   do {                                                                                          \
     DMLP_LOADA(J, R);                                                                           \
     DMLP_LOADX(J, R);                                                                           \
+  } while (0)
+  // ring: step R of the tile in LDS slot SL
+#define DMLP_RLOAD(SL, R)                                                                       \
+  do {                                                                                          \
+    _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
+      A[R][kt] = *(__attribute__((address_space(3))) const bf16x8*)(size_t)(                    \
+          ringA + (SL) * C::TILEB + ((R) * KT + kt) * 1024 + lane * 16);                        \
+    Xi[R] = *(__attribute__((address_space(3))) const f32x4*)(size_t)(                          \
+        ringN + (SL) * 256 + (R) * 64 + kg * 16);                                               \
   } while (0)
 #define DMLP_MFMA(R, AB)                                                                        \
   do {                                                                                          \
@@ -494,43 +659,105 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     }                                                                                           \
   } while (0)
   // one compaction call site per CHECK steps (each inlined copy is ~8 KiB of code: one per
-  // step of the unrolled ring would not stay in the instruction cache)
+  // step of the unrolled ring would not stay in the instruction cache).  Ring: a tile this wave
+  // issued is published before the (long) compaction, so the other waves never wait on it.
 #define DMLP_CHECK()                                                                            \
   do {                                                                                          \
-    if (trig) compact(false);                                                                   \
+    if (trig) {                                                                                 \
+      if (RING && pend >= 0) {                                                                  \
+        publish(pend);                                                                          \
+        pend = -1;                                                                              \
+      }                                                                                         \
+      compact(false);                                                                           \
+    }                                                                                           \
     trig = 0;                                                                                   \
   } while (0)
 
-  // EARLY START: a new slice's max norm raises the eps of every column (see above)
-  auto eps_of = [&](float qv, float xm) {
-    return r1 * sqrtf(qv) * sqrtf(xm) + r2 * xm + r3 * (sqrtf(qv) + sqrtf(xm)) + r3 * 0x1p-15f;
-  };
+  // EARLY START: a new slice's max norm raises the eps of every column (see above); the owners
+  // update oe / oh, the MFMA layout takes the new thresholds by the shuffle
   auto grow = [&](float xm) {
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int col = ct * 16 + c;
-      const int p = pbase + col;
+    for (int hb = 0; hb < NH; ++hb) {
+      const int p = pbase + lane + 64 * hb;
       if (p < nq) {
-        const float e_old = leps[col];
         const float e_new = eps_of(qn[qidx[p]], xm);
-        if (h[ct] > -FLT_MAX && h[ct] < INFINITY) h[ct] -= 2.0f * (e_new - e_old);
-        dmlp::wave_sync();  // every lane has read e_old before lane c rewrites it
-        if (lane < 16) {
-          leps[col] = e_new;
-          lh[col] = h[ct];
-        }
+        if (oh[hb] > -FLT_MAX && oh[hb] < INFINITY) oh[hb] -= 2.0f * (e_new - oe[hb]);
+        oe[hb] = e_new;
       }
     }
-    dmlp::wave_sync();
+    if (MODE & 128) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const float hn = __shfl(oh[ct >> 2], (ct & 3) * 16 + c);
+        h[ct] = h[ct] == INFINITY ? h[ct] : hn;
+      }
+    } else {
+      pull_h();
+    }
   };
-  if (rdy && rdy_fail) {  // the data never arrived: report overflow, stop appending
-    for (int col = lane; col < C::NCOL; col += 64) lflag[col] = 1;
+  auto fail_all = [&]() {  // the data never arrived: report overflow, stop appending
+#pragma unroll
+    for (int hb = 0; hb < NH; ++hb) {
+      ofl[hb] = 1;
+      oh[hb] = INFINITY;
+    }
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) h[ct] = INFINITY;
+  };
+  if (rdy && rdy_fail) {
+    fail_all();
     have = rdy_n;
-    dmlp::wave_sync();
   }
   unsigned long long trig = 0;  // wave-uniform: some lane's sub-buffer passed its limit
+  if constexpr (RING > 0) {
+    if (nsteps > 0) {
+      // tile 0 into the register ring, then per tile i: publish / claim + issue tile i + L,
+      // wait for tile i + 1, and run tile i's 4 steps while reading tile i + 1 out of LDS
+      _Pragma("unroll") for (int r = 0; r < 4; ++r) DMLP_RLOAD(0, r);
+      done_read(0);
+      for (int i = 0; i < nt; ++i) {
+        if (pend >= 0) {
+          publish(pend);
+          pend = -1;
+        }
+        if (i + L < nt && claim(i + L)) {
+          produce(i + L);
+          pend = i + L;
+        }
+        const int sl1 = (i + 1) % RING;
+        if (i + 1 < nt) {
+          if (!lds_wait(rready + sl1, (unsigned)((i + 1) / RING + 1))) ring_fail();
+          if (rdy && have < rdy_n) {  // eps over tile i + 1's slice before any of it is judged
+            const int si = min((i + 1) / rdy_tiles, rdy_n - 1);
+            if (si >= have) {
+              const int need = widen(si);
+              const float xm = fold_xnm(xnmax, have, need);
+              have = need + 1;
+              if (xm > xnmax) {
+                grow(xm);
+                xnmax = xm;
+                ++n_grow;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = i * 4 + r;
+          DMLP_MFMA(r, r & 1);
+          DMLP_RLOAD(sl1, r);  // (past the last tile: a stale slot, never used)
+          if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
+          if (r % CHECK == CHECK - 1) DMLP_CHECK();
+        }
+        if (i + 1 < nt) done_read(i + 1);
+      }
+      DMLP_EPILOGUE(1, nsteps - 1);
+      // a failed wait anywhere in the workgroup: every wave's queries report overflow
+      if (__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+              rfail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)))
+        fail_all();
+    }
+  } else {
   // The C-operand ring: window w (steps 4w .. 4w + 3, 64 floats) sits in LDS slot w & 1; lane L
   // moves float L of a window (one dword per lane, 4 steps ahead of its first read).  16 lanes
   // read each 16-byte row group (an LDS broadcast), so the per-step norm traffic leaves the
@@ -575,11 +802,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
               ++n_grow;
             }
           } else {
-            for (int col = lane; col < C::NCOL; col += 64) lflag[col] = 1;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) h[ct] = INFINITY;
+            fail_all();
             have = rdy_n;
-            dmlp::wave_sync();
           }
         }
       }
@@ -608,9 +832,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CTV == 8 ||
     const int jl = ((nsteps + D - 1) / D) * D - 1;
     DMLP_EPILOGUE(jl & 1, jl);
   }
+  }
 #undef DMLP_LOAD
 #undef DMLP_LOADA
 #undef DMLP_LOADX
+#undef DMLP_RLOAD
 #undef DMLP_MFMA
 #undef DMLP_EPILOGUE
 #undef DMLP_CHECK
@@ -638,7 +864,36 @@ int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
 int g_x1_ct = 4;
 int x1_ct(int kmax) { return x1_sub(kmax) == 16 ? g_x1_ct : 4; }
 
-template <int KT, int SUB, int DEPTH, int CHECK, int CTV, bool F16>
+// the LDS-ring variants (RING > 0): DMLP_X1_RING = 0 (off) or the sub-buffer depth of the ring
+// kernel — 16 (5-tile ring), 14 (9 tiles) or 12 (13 tiles): a shallower candidate buffer leaves
+// more LDS to the ring, i.e. more slack between the fastest and the slowest wave, at the price
+// of more frequent compactions (and 40 / 48 instead of 56 kept group entries per column)
+int g_x1_ring = -1;
+int64_t g_x1_ring_launches = 0;
+int x1_ring() {
+  if (g_x1_ring < 0) {
+    const char* e = getenv("DMLP_X1_RING");
+    const int v = e ? atoi(e) : 0;
+    g_x1_ring = (v == 16 || v == 14 || v == 12) ? v : 0;
+  }
+  return g_x1_ring;
+}
+int x1_num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+// the ring kernel fills the chip only with a workgroup (8 x 64 queries of a slice) per CU
+bool x1_ring_fits(int nq, int S) {
+  return x1_ring() && (int64_t)((nq + 511) / 512) * S >= x1_num_cus();
+}
+
+template <int KT, int SUB, int DEPTH, int CHECK, int CTV, bool F16, int RING = 0>
 int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, int64_t n_points,
               const void* qhi, const float* qn, const int* qidx, const int* qk, int nq,
               const unsigned* xnmax, const unsigned* bad, float r1, float r2, float r3, int S,
@@ -647,20 +902,33 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
               int rdy_tiles = 1, int rdy_n = 0, const unsigned* xnm_sl = nullptr,
               unsigned* estats = nullptr, long long rdy_to = 0,
               const unsigned* qrdy = nullptr, int qrdy_q = 1) {
-  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV>;
-  const int n_qblocks = (nq + C::NCOL - 1) / C::NCOL;
+  using C = X1Cfg<KT, SUB, DEPTH, CHECK, CTV, RING>;
+  const int n_qblocks = ((nq + C::NCOL - 1) / C::NCOL + C::W - 1) / C::W;  // workgroups per slice
   const int tps = (int)((n_tiles + S - 1) / S);
   const int64_t grid = (int64_t)n_qblocks * S;
   if (grid <= 0) return 0;
+  if constexpr (C::LDS > 65536) {  // past the default dynamic-LDS limit: raise it once
+    static const hipError_t la = hipFuncSetAttribute(
+        (const void*)k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, 0, F16, RING>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    static const hipError_t lb = hipFuncSetAttribute(
+        (const void*)k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, 8, F16, RING>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (la != hipSuccess || lb != hipSuccess) return -(int)(la != hipSuccess ? la : lb);
+  }
 #define DMLP_X1_LAUNCH(M)                                                                      \
-  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M, F16>), dim3((unsigned)grid), dim3(64), C::LDS, stream, \
+  hipLaunchKernelGGL((k_screen_x1<KT, SUB, DEPTH, CHECK, CTV, M, F16, RING>), dim3((unsigned)grid), dim3(C::W * 64), C::LDS, stream, \
                      (const u32x4*)xfrag, (const f32x4*)xinit, (int)n_tiles, (int)n_points,     \
                      (const bf16x8*)qhi, qn, qidx, qk, nq, xnmax, bad, r1, r2, r3, S, tps,      \
                      n_qblocks, hl, cand_ids, cand_cnt, cand_h, hseed, ccap, rdy, rdy_tiles,     \
                      rdy_n, xnm_sl, estats, rdy_to, qrdy, qrdy_q)
   if (hseed) {  // the COLLECT pass (SUB = 16, CT = 4, fp16 only: see dmlp_screen_x1_collect)
-    if constexpr (SUB == 16 && CTV == 4 && F16) DMLP_X1_LAUNCH(16);
+    if constexpr (SUB == 16 && CTV == 4 && F16 && RING == 0) DMLP_X1_LAUNCH(16);
     else return -3;
+  } else if constexpr (RING > 0) {
+    ++g_x1_ring_launches;
+    if (x1_mode() == 8) DMLP_X1_LAUNCH(8);  // event counters
+    else DMLP_X1_LAUNCH(0);
   } else if constexpr (KT <= 2) {
     // ablation modes only for the A <= 64 variants (each mode is a full kernel instantiation)
     switch (x1_mode()) {
@@ -738,6 +1006,10 @@ extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles 
 extern "C" void dmlp_set_x1_mode(int mode) { g_x1_mode = mode; }
 // column tiles per wave of the k <= 16 variants (4 or 8; A/B)
 extern "C" void dmlp_set_x1_ct(int ct) { g_x1_ct = ct == 4 ? 4 : 8; }
+// the LDS-ring screen for k <= 16, A <= 32 (0 off; 16 / 14 / 12: its sub-buffer depth)
+extern "C" void dmlp_set_x1_ring(int sub) { g_x1_ring = (sub == 16 || sub == 14 || sub == 12) ? sub : 0; }
+extern "C" int dmlp_get_x1_ring(void) { return x1_ring(); }
+extern "C" int64_t dmlp_x1_ring_launches(void) { return g_x1_ring_launches; }
 extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_dbg), sizeof(g_x1_dbg));
   if (e != hipSuccess) return -(int)e;
@@ -831,6 +1103,11 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
   do {                                                                                         \
     if (KT == 1) {                                                                             \
       if (sub == 32) return launch_x1<1, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                      \
+      if (ct == 4 && x1_ring_fits(nq, S)) {                                                    \
+        if (x1_ring() == 16) return launch_x1<1, 16, 4, 2, 4, F16, 5>(DMLP_X1_ARGS);           \
+        if (x1_ring() == 14) return launch_x1<1, 14, 4, 2, 4, F16, 9>(DMLP_X1_ARGS);           \
+        return launch_x1<1, 12, 4, 2, 4, F16, 13>(DMLP_X1_ARGS);                               \
+      }                                                                                        \
       return ct == 8 ? launch_x1<1, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                            \
                      : launch_x1<1, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                           \
     }                                                                                          \
@@ -907,14 +1184,19 @@ extern "C" int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const flo
     const double ms = e ? atof(e) : 50.0;
     return (long long)(ms * khz);
   }();
-#define DMLP_X1E(KTV, SUBV, CTV)                                                                \
-  return launch_x1<KTV, SUBV, 4, 2, CTV, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, \
+#define DMLP_X1E(KTV, SUBV, CTV, ...)                                                           \
+  return launch_x1<KTV, SUBV, 4, 2, CTV, true, ##__VA_ARGS__>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, \
                                                qk, nq, bad, bad, r1, r2, r3, 1, cand_ids,      \
                                                cand_cnt, cand_h, st, nullptr, 0, rdy, rdy_tiles, \
                                                rdy_n, xnm_sl, estats, rdy_to, qrdy, qrdy_q)
   if (KT == 1) {
     if (sub == 32) DMLP_X1E(1, 32, 4);
     if (ct == 8) DMLP_X1E(1, 16, 8);
+    if (x1_ring_fits(nq, 1)) {
+      if (x1_ring() == 16) DMLP_X1E(1, 16, 4, 5);
+      if (x1_ring() == 14) DMLP_X1E(1, 14, 4, 9);
+      DMLP_X1E(1, 12, 4, 13);
+    }
     DMLP_X1E(1, 16, 4);
   }
   if (KT == 2) {

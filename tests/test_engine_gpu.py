@@ -163,6 +163,46 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
         L.dmlp_pipeline_set(b"qb_blocks", old_qb)
 
 
+@pytest.mark.parametrize("sub", [16, 14, 12])
+def test_screen_lds_ring(gpu, sub):
+    """The LDS-ring screen (screen_x1.hip RING > 0: 8 waves per workgroup share each fragment
+    tile through an LDS ring filled by LDS-DMA, ready / done counters instead of barriers) at
+    each of its sub-buffer depths: early-start steps (image slices delayed 400 us, query blocks
+    behind the launch) and plain steps, two inputs of one shape alternated through the reused
+    ring slots (94 tiles through 5 / 9 / 13 slots); every report, label and checksum == its
+    oracle's, no escalation, no timed-out wait, and the ring kernel is what ran."""
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    old_ring = L.dmlp_pipeline_set(b"x1_ring", sub)
+    old_qb = L.dmlp_pipeline_set(b"qb_blocks", 16)
+    Q = 131072 + 64 * 3  # 257 workgroups of 512 queries: one per CU and then some
+    cases = _early_inputs(6000, 32, 16, Q, seed=300 + sub)
+    import torch
+    dsts = [torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy() for _ in cases]
+    n0 = L.dmlp_x1_ring_launches()
+    try:
+        L.dmlp_step_early_delay(400)
+        for rnd, early in enumerate((1, 1, 0, 0)):
+            L.dmlp_step_early(early)
+            inp, lab_ref, cs, expect = cases[rnd % 2]
+            dst = dsts[rnd % 2]
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
+            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
+            assert r.early == early
+            assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
+            if r.early:
+                assert r.early_timeouts == 0
+                assert r.early_waits > 0 and r.early_grows > 0
+        assert L.dmlp_x1_ring_launches() == n0 + 4
+    finally:
+        L.dmlp_step_early(-1)
+        L.dmlp_step_early_delay(-1)
+        L.dmlp_pipeline_set(b"x1_ring", old_ring)
+        L.dmlp_pipeline_set(b"qb_blocks", old_qb)
+
+
 def test_debug_listing(gpu, workload):
     inp, _, d, i = workload
     eng = _engine("ring", debug=True)

@@ -29,6 +29,7 @@
 #   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
+#   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
 set -u
 TAG=${1:?tag}
 shift
@@ -36,6 +37,9 @@ cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# bench.py's reference-contract runs (fresh drop-in processes after the timed steps) only where a
+# task wants the driver's line: bench, bench3, final
+export DMLP_BENCH_CONTRACT_RUNS=0
 step() {  # name seconds cmd...  (stdout+stderr to $OUT/name.log)
   local name=$1 secs=$2
   shift 2
@@ -54,9 +58,9 @@ for task in "$@"; do
       step ktests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
           --timeout-method thread -k "${KTESTS:?KTESTS}" ;;
     bench)
-      step bench 300 python bench.py ;;
+      DMLP_BENCH_CONTRACT_RUNS=3 step bench 300 python bench.py ;;
     bench3)  # three headline runs in a row (run-to-run spread: timed_step_ms, cgroup throttling)
-      for r in 1 2 3; do step bench_$r 300 python bench.py; done ;;
+      for r in 1 2 3; do DMLP_BENCH_CONTRACT_RUNS=3 step bench_$r 300 python bench.py; done ;;
     verify)
       step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
     exact)
@@ -196,12 +200,22 @@ for task in "$@"; do
         KNN_DATA_PLANE=host step native_p$P 600 python bench.py --harness native --gpus $P --steps 5 \
             --warmup 1 --q-per-gpu 65536 --ingress shm
       done ;;
+    ring)  # the LDS-ring screen (DMLP_X1_RING): its GPU tests, then off / 16 / 14 / 12 under the
+           # kernel tracer (screen medians) and as plain bench runs (ms/step)
+      step ring_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 180 \
+          --timeout-method thread -k "lds_ring"
+      AB_ROUNDS=2 AB_STEPS=30 step ring_prof 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
+          r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
+      python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/ring_kernels.txt"; rm -rf gpurun_out/ab
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ring_ab 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
+          r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
+      grep -h '"ms_per_step"' "$OUT"/ring_ab.log | tee "$OUT/ring_ms.txt" ;;
     final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
             # default and the exact path, the P = 3 host-plane rehearsal with --verify
       step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
           --timeout-method thread
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-      step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      DMLP_BENCH_CONTRACT_RUNS=3 step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
       step verify 300 python bench.py --steps 200 --verify
       step exact 300 python bench.py --exact --steps 5 --warmup 1 --min-warmup-s 0 --verify
       DMLP_DATA_PLANE=host step p3 400 python bench.py --gpus 3 --steps 30 --warmup 3 \

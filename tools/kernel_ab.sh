@@ -10,6 +10,7 @@
 # kernel medians); AB_PROF=0: plain bench.py runs (host-side settings: no tracer overhead).
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
+export DMLP_BENCH_CONTRACT_RUNS=0  # no reference-contract processes after the timed steps
 PROF=${AB_PROF:-1}
 ROUNDS=${AB_ROUNDS:-2}
 STEPS=${AB_STEPS:-30}
