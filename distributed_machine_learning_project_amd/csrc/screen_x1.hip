@@ -232,38 +232,44 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   // is bounded (RTO); a timed-out wait sets fail and the workgroup's queries report overflow.
   constexpr int L = 3;
   constexpr long long RTO = 20000000;  // 200 ms of the 100 MHz wall clock: a bug, not a wait
+  // The counters are plain LDS words with relaxed atomics: one wave's LDS operations execute in
+  // issue order, so a counter read that returned before a wave's ring reads were issued orders
+  // them (and a done increment issued after a wave's reads lands after them); a wavefront fence
+  // keeps the compiler from moving the reads across.  An LDS-DMA piece is in LDS once the
+  // issuing wave's vmcnt drained, before it publishes.
   constexpr unsigned ringA = (unsigned)(C::W * C::SBUF);
   constexpr unsigned ringN = ringA + (unsigned)(RING * C::TILEB);
-  unsigned* const rready = (unsigned*)(smem + ringN + RING * 256);
-  unsigned* const rdone = rready + RING;
-  unsigned* const rfail = rdone + RING;
-  unsigned* const rnext = rfail + 1;
+  typedef __attribute__((address_space(3))) unsigned lds_u32;
+  lds_u32* const rready = (lds_u32*)(size_t)(ringN + RING * 256);
+  lds_u32* const rdone = rready + RING;
+  lds_u32* const rfail = rdone + RING;
+  lds_u32* const rnext = rfail + 1;
   typedef __attribute__((address_space(3))) void* lds_vp;
-  auto lds_wait = [&](unsigned* f, unsigned want) -> bool {
-    auto ld = [&]() {
-      return (unsigned)__builtin_amdgcn_readfirstlane(
-          (int)__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-    };
-    if (ld() >= want) return true;
+  auto lds_ld = [&](lds_u32* f) {
+    return (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  };
+  // spin until *f >= want (v: the value already read)
+  auto lds_wait_v = [&](lds_u32* f, unsigned want, unsigned v) -> bool {
+    if (v >= want) return true;
     const long long ts = wall_clock64();
     for (;;) {
       __builtin_amdgcn_s_sleep(1);
-      if (ld() >= want) return true;
+      if (lds_ld(f) >= want) return true;
       if (wall_clock64() - ts > RTO) {
         ++n_to;
         return false;
       }
     }
   };
+  auto lds_wait = [&](lds_u32* f, unsigned want) { return lds_wait_v(f, want, lds_ld(f)); };
   auto ring_fail = [&]() {
     __hip_atomic_store(rfail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   int have_p = 0;  // slices this wave saw landed as a producer
-  // claim tile t (t == next): true if this wave now owns its pieces
-  auto claim = [&](int t) -> bool {
-    if ((unsigned)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
-            rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != (unsigned)t)
-      return false;
+  // claim tile t given nx, a read of next: true if this wave now owns its pieces
+  auto claim_v = [&](int t, unsigned nx) -> bool {
+    if (nx != (unsigned)t) return false;
     int got = 0;
     if (lane == 0) {
       unsigned e = (unsigned)t;
@@ -272,6 +278,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
     }
     return __builtin_amdgcn_readlane(got, 0) != 0;
   };
+  auto claim = [&](int t) { return claim_v(t, lds_ld(rnext)); };
   // issue tile t's pieces into slot t % R (the claimer only)
   auto produce = [&](int t) {
     if (rdy && have_p < rdy_n) {
@@ -302,12 +309,13 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   auto publish = [&](int t) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces landed
     if (lane == 0)
-      __hip_atomic_fetch_add(rready + t % RING, 1u, __ATOMIC_RELEASE,
+      __hip_atomic_fetch_add(rready + t % RING, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  auto done_read = [&](int t) {  // this wave's reads of tile t are issued: retire, then count
+  auto done_read = [&](int t) {  // this wave's reads of tile t are issued (LDS order retires them)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (lane == 0)
-      __hip_atomic_fetch_add(rdone + t % RING, 1u, __ATOMIC_RELEASE,
+      __hip_atomic_fetch_add(rdone + t % RING, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   int pend = -1;  // the tile this wave issued and has not published yet
@@ -332,6 +340,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
     // (a wave past the last query has no block to wait for)
     if (rdy && qrdy && pbase < nq) rdy_fail |= !wait_word(qrdy + pbase / qrdy_q, n_qwait);
     if (nsteps > 0 && !lds_wait(rready, 1u)) ring_fail();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (rdy) {  // slice 0 (at least) landed: a producer waited for it
       const int need = widen(0);
       xnmax = fold_xnm(0.0f, 0, need);
@@ -713,38 +722,48 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
     if (nsteps > 0) {
       // tile 0 into the register ring, then per tile i: publish / claim + issue tile i + L,
       // wait for tile i + 1, and run tile i's 4 steps while reading tile i + 1 out of LDS
-      _Pragma("unroll") for (int r = 0; r < 4; ++r) DMLP_RLOAD(0, r);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) DMLP_RLOAD(0, r);
       done_read(0);
       for (int i = 0; i < nt; ++i) {
         if (pend >= 0) {
           publish(pend);
           pend = -1;
         }
-        if (i + L < nt && claim(i + L)) {
-          produce(i + L);
-          pend = i + L;
-        }
         const int sl1 = (i + 1) % RING;
-        if (i + 1 < nt) {
-          if (!lds_wait(rready + sl1, (unsigned)((i + 1) / RING + 1))) ring_fail();
-          if (rdy && have < rdy_n) {  // eps over tile i + 1's slice before any of it is judged
-            const int si = min((i + 1) / rdy_tiles, rdy_n - 1);
-            if (si >= have) {
-              const int need = widen(si);
-              const float xm = fold_xnm(xnmax, have, need);
-              have = need + 1;
-              if (xm > xnmax) {
-                grow(xm);
-                xnmax = xm;
-                ++n_grow;
-              }
-            }
-          }
-        }
+        // both counter reads issue before step 0's MFMAs and are consumed after them
+        const unsigned nx = __hip_atomic_load(rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned rd = __hip_atomic_load(rready + sl1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int j = i * 4 + r;
           DMLP_MFMA(r, r & 1);
+          if (r == 0) {
+            if (i + L < nt && claim_v(i + L, (unsigned)__builtin_amdgcn_readfirstlane((int)nx))) {
+              produce(i + L);
+              pend = i + L;
+            }
+            if (i + 1 < nt) {
+              if (!lds_wait_v(rready + sl1, (unsigned)((i + 1) / RING + 1),
+                              (unsigned)__builtin_amdgcn_readfirstlane((int)rd)))
+                ring_fail();
+              if (rdy && have < rdy_n) {  // eps over tile i + 1's slice before any of it is judged
+                const int si = min((i + 1) / rdy_tiles, rdy_n - 1);
+                if (si >= have) {
+                  const int need = widen(si);
+                  const float xm = fold_xnm(xnmax, have, need);
+                  have = need + 1;
+                  if (xm > xnmax) {
+                    grow(xm);
+                    xnmax = xm;
+                    ++n_grow;
+                  }
+                }
+              }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
           DMLP_RLOAD(sl1, r);  // (past the last tile: a stale slot, never used)
           if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
           if (r % CHECK == CHECK - 1) DMLP_CHECK();
@@ -753,9 +772,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
       }
       DMLP_EPILOGUE(1, nsteps - 1);
       // a failed wait anywhere in the workgroup: every wave's queries report overflow
-      if (__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
-              rfail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)))
-        fail_all();
+      if (lds_ld(rfail)) fail_all();
     }
   } else {
   // The C-operand ring: window w (steps 4w .. 4w + 3, 64 floats) sits in LDS slot w & 1; lane L

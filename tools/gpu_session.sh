@@ -30,6 +30,7 @@
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 #   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
+#   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
 TAG=${1:?tag}
 shift
@@ -210,6 +211,18 @@ for task in "$@"; do
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ring_ab 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
           r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
       grep -h '"ms_per_step"' "$OUT"/ring_ab.log | tee "$OUT/ring_ms.txt" ;;
+    ringpmc)  # counters of the screen without / with the LDS ring (RINGS, default "0 12")
+      for R in ${RINGS:-0 12}; do
+        n=0
+        for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM" \
+                 "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"; do
+          n=$((n + 1))
+          DMLP_X1_RING=$R step ringpmc${R}_$n 120 rocprofv3 --kernel-trace --pmc $C -d "$OUT/ringpmc${R}_$n" \
+              -o run --output-format csv -- python3 tools/quick_gpu_bench.py --q 131072 --iters 2 --check 0
+        done
+      done
+      python3 tools/pmc_summary.py "$OUT" > "$OUT/ringpmc_summary.txt"; cat "$OUT/ringpmc_summary.txt" ;;
     final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
             # default and the exact path, the P = 3 host-plane rehearsal with --verify
       step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \

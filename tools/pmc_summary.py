@@ -13,9 +13,11 @@ import sys
 def family(name):
     m = re.search(r"(k_[a-z0-9_]+)", name)
     fam = m.group(1) if m else name[:40]
-    t = re.search(r"k_screen_x1ILi(\d+)ELi(\d+)ELi4ELi2ELi(\d+)ELi(\d+)", name)
+    t = re.search(r"k_screen_x1ILi(\d+)ELi(\d+)ELi4ELi2ELi(\d+)ELi(\d+)ELb\dELi(\d+)E", name) or \
+        re.search(r"k_screen_x1ILi(\d+)ELi(\d+)ELi4ELi2ELi(\d+)ELi(\d+)()", name)
     if t:
-        fam += f"<KT{t.group(1)},SUB{t.group(2)},CT{t.group(3)},MODE{t.group(4)}>"
+        ring = f",RING{t.group(5)}" if t.group(5) else ""
+        fam += f"<KT{t.group(1)},SUB{t.group(2)},CT{t.group(3)},MODE{t.group(4)}{ring}>"
     t = re.search(r"k_refine<(\d+), (\d+), (true|false)>", name) or re.search(r"k_refine_pairILi(\d+)", name)
     if t:
         fam += "<" + ",".join(t.groups()) + ">"
