@@ -38,7 +38,8 @@ namespace {
 // wrong results, timing only), 8 event counters (g_x1_dbg), 32 / 64 fragment loads on every 2nd /
 // 4th step only (the others reuse stale ring registers: wrong results, timing only — what a
 // shared data ring would save on the texture path), 128 no hit after the first compaction (the
-// threshold jumps to +inf: the step cost of a perfectly seeded threshold; profiles/r6c).  MODE 16
+// threshold jumps to +inf: the step cost of a perfectly seeded threshold; profiles/r6c), 256
+// per-lane exec-masked appends, 512 per-column-tile uniform append branches.  MODE 16
 // is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = -1;  // -1: DMLP_X1_MODE (read once; default 0)
@@ -231,6 +232,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   // publishes it once its vmcnt drained — at its next tile, or before a compaction.  Every wait
   // is bounded (RTO); a timed-out wait sets fail and the workgroup's queries report overflow.
   constexpr int L = 3;
+  constexpr int RS = RING > 0 ? RING : 1;  // (the per-wave variant never runs the ring code)
   constexpr long long RTO = 20000000;  // 200 ms of the 100 MHz wall clock: a bug, not a wait
   // The counters are plain LDS words with relaxed atomics: one wave's LDS operations execute in
   // issue order, so a counter read that returned before a wave's ring reads were issued orders
@@ -293,8 +295,8 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
         if (!ok) ring_fail();
       }
     }
-    const int slot = t % RING;
-    if (t >= RING && !lds_wait(rdone + slot, 8u * (unsigned)(t / RING))) ring_fail();
+    const int slot = t % RS;
+    if (t >= RING && !lds_wait(rdone + slot, 8u * (unsigned)(t / RS))) ring_fail();
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
@@ -309,13 +311,13 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   auto publish = [&](int t) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces landed
     if (lane == 0)
-      __hip_atomic_fetch_add(rready + t % RING, 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(rready + t % RS, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   auto done_read = [&](int t) {  // this wave's reads of tile t are issued (LDS order retires them)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (lane == 0)
-      __hip_atomic_fetch_add(rdone + t % RING, 1u, __ATOMIC_RELAXED,
+      __hip_atomic_fetch_add(rdone + t % RS, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   int pend = -1;  // the tile this wave issued and has not published yet
@@ -643,7 +645,18 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
       }                                                                                         \
       unsigned gl_ = (unsigned)((J) * 4 + kg);                                                  \
       asm volatile("" : "+v"(gl_)); /* one VGPR: each key is a single v_and_or / v_bfi */       \
-      if (MODE & 256) {                                                                         \
+      if (MODE & 512) {                                                                         \
+        /* per column tile, a wave-uniform branch on its own hit mask: a taken step pays the   \
+           append VALU only for the tiles some lane hit (~2 lane-keys of 256 per taken step) */ \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                     \
+          if (__ballot(hit_[ct])) {                                                             \
+            *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                   \
+                (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                  \
+            addr[ct] += hit_[ct] ? 16u : 0u;                                                    \
+            trig |= __ballot(addr[ct] > lim[ct]);                                               \
+          }                                                                                     \
+        }                                                                                       \
+      } else if (MODE & 256) {                                                                  \
         /* per tile, only the lanes that hit (exec-masked) store and advance: ~1/64 of the     \
            lane-tiles of a taken step hit (215 appends per query over 6250 steps), so the      \
            branch-free form spent most of its VALU on misses */                                 \
@@ -730,7 +743,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
           publish(pend);
           pend = -1;
         }
-        const int sl1 = (i + 1) % RING;
+        const int sl1 = (i + 1) % RS;
         // both counter reads issue before step 0's MFMAs and are consumed after them
         const unsigned nx = __hip_atomic_load(rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned rd = __hip_atomic_load(rready + sl1, __ATOMIC_RELAXED,
@@ -745,7 +758,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
               pend = i + L;
             }
             if (i + 1 < nt) {
-              if (!lds_wait_v(rready + sl1, (unsigned)((i + 1) / RING + 1),
+              if (!lds_wait_v(rready + sl1, (unsigned)((i + 1) / RS + 1),
                               (unsigned)__builtin_amdgcn_readfirstlane((int)rd)))
                 ring_fail();
               if (rdy && have < rdy_n) {  // eps over tile i + 1's slice before any of it is judged
@@ -958,6 +971,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 64: DMLP_X1_LAUNCH(64); break;
       case 128: DMLP_X1_LAUNCH(128); break;
       case 256: DMLP_X1_LAUNCH(256); break;
+      case 512: DMLP_X1_LAUNCH(512); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }
