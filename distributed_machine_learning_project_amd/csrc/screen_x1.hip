@@ -39,7 +39,8 @@ namespace {
 // 4th step only (the others reuse stale ring registers: wrong results, timing only — what a
 // shared data ring would save on the texture path), 128 no hit after the first compaction (the
 // threshold jumps to +inf: the step cost of a perfectly seeded threshold; profiles/r6c), 256
-// per-lane exec-masked appends, 512 per-column-tile uniform append branches.  MODE 16
+// per-lane exec-masked appends, 512 per-column-tile uniform append branches, 1024 the fill test
+// at every taken step (the r9 form) instead of at the check points.  MODE 16
 // is not an ablation: the
 // COLLECT pass of the large-k pipeline (dmlp_screen_x1_collect)
 int g_x1_mode = -1;  // -1: DMLP_X1_MODE (read once; default 0)
@@ -624,22 +625,23 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   } while (0)
 #define DMLP_EPILOGUE(AB, J)                                                                    \
   do {                                                                                          \
+    /* per column tile: the 4-row group max, and the wave's hit mask straight from the        \
+       compare (an SGPR pair: the uniform branches below test it with one s_cmp) */            \
     float m_[CT];                                                                               \
-    bool hit_[CT];                                                                              \
-    bool any_ = false;                                                                          \
+    unsigned long long hm_[CT];                                                                 \
+    unsigned long long any_ = 0;                                                                \
     _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
       m_[ct] = fmaxf(fmaxf(acc[AB][ct][0], acc[AB][ct][1]), fmaxf(acc[AB][ct][2], acc[AB][ct][3])); \
-      hit_[ct] = m_[ct] >= h[ct];                                                               \
-      any_ |= hit_[ct];                                                                         \
+      hm_[ct] = __builtin_amdgcn_ballot_w64(m_[ct] >= h[ct]);                                   \
+      any_ |= hm_[ct];                                                                          \
     }                                                                                           \
     if (MODE & 8) {                                                                             \
       if (lane == 0) atomicAdd(&g_x1_dbg[0], 1ull);                                             \
     }                                                                                           \
-    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && __ballot(any_)) {                        \
+    if (!(MODE & 1) && (C::D == 4 || (J) < nsteps) && any_) {                                   \
       if (MODE & 8) {                                                                           \
         int np_ = 0;                                                                            \
-        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += hit_[ct] ? 1 : 0;              \
-        for (int o_ = 32; o_ > 0; o_ >>= 1) np_ += __shfl_xor(np_, o_);                         \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) np_ += __popcll(hm_[ct]);             \
         if (lane == 0) { atomicAdd(&g_x1_dbg[1], 1ull);                                         \
                          atomicAdd(&g_x1_dbg[2], (unsigned long long)np_); }                    \
       }                                                                                         \
@@ -649,24 +651,20 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
         /* per column tile, a wave-uniform branch on its own hit mask: a taken step pays the   \
            append VALU only for the tiles some lane hit (~2 lane-keys of 256 per taken step) */ \
         _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                     \
-          if (__ballot(hit_[ct])) {                                                             \
+          if (hm_[ct]) {                                                                        \
             *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                   \
                 (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                  \
-            addr[ct] += hit_[ct] ? 16u : 0u;                                                    \
-            trig |= __ballot(addr[ct] > lim[ct]);                                               \
+            addr[ct] += m_[ct] >= h[ct] ? 16u : 0u;                                             \
           }                                                                                     \
         }                                                                                       \
       } else if (MODE & 256) {                                                                  \
-        /* per tile, only the lanes that hit (exec-masked) store and advance: ~1/64 of the     \
-           lane-tiles of a taken step hit (215 appends per query over 6250 steps), so the      \
-           branch-free form spent most of its VALU on misses */                                 \
+        /* per tile, only the lanes that hit (exec-masked) store and advance */                 \
         _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                     \
-          if (hit_[ct]) {                                                                       \
+          if (m_[ct] >= h[ct]) {                                                                \
             *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                   \
                 (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                  \
             addr[ct] += 16u;                                                                    \
           }                                                                                     \
-          trig |= __ballot(addr[ct] > lim[ct]);                                                 \
         }                                                                                       \
       } else {                                                                                  \
       /* branch-free: every lane writes its entry to the next free slot and advances only on  \
@@ -674,8 +672,8 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                       \
         *(__attribute__((address_space(3))) unsigned*)(size_t)addr[ct] =                       \
             (__float_as_uint(m_[ct]) & 0xffff0000u) | gl_;                                      \
-        addr[ct] += hit_[ct] ? 16u : 0u;                                                        \
-        trig |= __ballot(addr[ct] > lim[ct]);                                                   \
+        addr[ct] += m_[ct] >= h[ct] ? 16u : 0u;                                                 \
+        if (MODE & 1024) trig_acc |= __builtin_amdgcn_ballot_w64(addr[ct] > lim[ct]);           \
       }                                                                                         \
       }                                                                                         \
     }                                                                                           \
@@ -685,6 +683,16 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
   // issued is published before the (long) compaction, so the other waves never wait on it.
 #define DMLP_CHECK()                                                                            \
   do {                                                                                          \
+    /* the fill test at the check point itself (addresses only grow between checks): one    \
+       compare per column tile every CHECK steps instead of one per tile per taken step */   \
+    unsigned long long trig = 0;                                                                \
+    if (MODE & 1024) {                                                                          \
+      trig = trig_acc;                                                                          \
+      trig_acc = 0;                                                                             \
+    } else {                                                                                    \
+      _Pragma("unroll") for (int ct = 0; ct < CT; ++ct)                                         \
+        trig |= __builtin_amdgcn_ballot_w64(addr[ct] > lim[ct]);                                \
+    }                                                                                           \
     if (trig) {                                                                                 \
       if (RING && pend >= 0) {                                                                  \
         publish(pend);                                                                          \
@@ -692,7 +700,6 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
       }                                                                                         \
       compact(false);                                                                           \
     }                                                                                           \
-    trig = 0;                                                                                   \
   } while (0)
 
   // EARLY START: a new slice's max norm raises the eps of every column (see above); the owners
@@ -730,7 +737,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
     fail_all();
     have = rdy_n;
   }
-  unsigned long long trig = 0;  // wave-uniform: some lane's sub-buffer passed its limit
+  unsigned long long trig_acc = 0;  // MODE 1024 (ablation): the fill test per taken step
   if constexpr (RING > 0) {
     if (nsteps > 0) {
       // tile 0 into the register ring, then per tile i: publish / claim + issue tile i + L,
@@ -972,6 +979,7 @@ int launch_x1(int hl, const void* xfrag, const float* xinit, int64_t n_tiles, in
       case 128: DMLP_X1_LAUNCH(128); break;
       case 256: DMLP_X1_LAUNCH(256); break;
       case 512: DMLP_X1_LAUNCH(512); break;
+      case 1024: DMLP_X1_LAUNCH(1024); break;
 
       default: DMLP_X1_LAUNCH(0); break;
     }

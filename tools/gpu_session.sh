@@ -30,7 +30,7 @@
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 #   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
-#   x1mode     a screen MODE (e.g. MODE=512) vs production: tests under it, kernel medians, ms/step
+#   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
 TAG=${1:?tag}
@@ -212,15 +212,15 @@ for task in "$@"; do
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ring_ab 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
           r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
       grep -h '"ms_per_step"' "$OUT"/ring_ab.log | tee "$OUT/ring_ms.txt" ;;
-    x1mode)  # a screen mode against the production one (MODE, e.g. 512): correctness under it (the
-             # screen / step tests), kernel medians, plain ms/step
-      DMLP_X1_MODE=${MODE:?MODE} step x1mode_tests 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
+    x1mode)  # screen modes against the production one (MODES, e.g. "1024 512"): the screen / step
+             # tests on the production mode, kernel medians, plain ms/step
+      step x1mode_tests 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
           --timeout 180 --timeout-method thread -k "screen or x1 or native_step or early_start or single_term"
-      AB_ROUNDS=2 AB_STEPS=30 step x1mode_prof 600 bash tools/kernel_ab.sh m0:DMLP_X1_MODE=0 \
-          m$MODE:DMLP_X1_MODE=$MODE
+      V=(m0:DMLP_X1_MODE=0)
+      for M in ${MODES:?MODES}; do V+=(m$M:DMLP_X1_MODE=$M); done
+      AB_ROUNDS=2 AB_STEPS=30 step x1mode_prof 600 bash tools/kernel_ab.sh "${V[@]}"
       python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/x1mode_kernels.txt"; rm -rf gpurun_out/ab
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step x1mode_ab 600 bash tools/kernel_ab.sh m0:DMLP_X1_MODE=0 \
-          m$MODE:DMLP_X1_MODE=$MODE ;;
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step x1mode_ab 600 bash tools/kernel_ab.sh "${V[@]}" ;;
     ringpmc)  # counters of the screen without / with the LDS ring (RINGS, default "0 12")
       for R in ${RINGS:-0 12}; do
         n=0
