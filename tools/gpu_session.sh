@@ -122,7 +122,7 @@ for task in "$@"; do
     harness)
       step harness 600 python bench.py --harness native ;;
     dropin)
-      step dropin 600 python bench.py --harness dropin --steps 5 --warmup 1
+      step dropin 600 python bench.py --harness dropin --steps 20 --warmup 1
       python -m distributed_machine_learning_project_amd.build --dropin \
           distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
       python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
