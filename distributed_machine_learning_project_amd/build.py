@@ -87,6 +87,11 @@ def build_lib(force: bool = False, jobs: int | None = None) -> Path:
     BUILD.mkdir(exist_ok=True)
     hip, cpp = _sources()
     srcs = hip + cpp
+    if not force and not _stale(LIB, srcs + _headers()):
+        # the library is newer than every source and header: up to date even where its objects
+        # did not travel (a GPU box gets the tree without _build/) — no 2-minute recompile there
+        _INFO["reused"].extend(s.name for s in srcs)
+        return LIB
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
@@ -162,6 +167,15 @@ def build_dropin(common_cpp: str, out: str | None = None, debug: bool = False,
     # default output in this package's build directory (never written into the harness's tree)
     BUILD.mkdir(exist_ok=True)
     out = Path(out or (BUILD / ("engine.debug" if debug else "engine"))).resolve()
+    # up to date: same flags (a stamp beside the binary) and newer than its inputs
+    stamp = out.with_name(out.name + ".flags")
+    key = repr((str(common_cpp), debug, list(extra_flags), inplace))
+    deps = [common_cpp, CSRC / "dropin_engine.cpp", PKG / "include" / "engine.h", LIB] + _headers()
+    hdr0 = common_cpp.parent / "common.h"
+    if hdr0.exists():
+        deps.append(hdr0)
+    if (stamp.exists() and stamp.read_text() == key and not _stale(out, deps)):
+        return out
     with tempfile.TemporaryDirectory(dir=BUILD, prefix="dropin_") as td:
         stage = Path(td)
         if inplace:
@@ -180,6 +194,7 @@ def build_dropin(common_cpp: str, out: str | None = None, debug: bool = False,
             flags += ["-g", "-DDEBUG"]
         _run(["g++", *flags, str(src), str(CSRC / "dropin_engine.cpp"), "-o", str(out),
               *_engine_link_flags()])
+    stamp.write_text(key)
     return out
 
 

@@ -188,10 +188,8 @@ for task in "$@"; do
     rehearsal)  # host budget of an 8-GPU node: the GPU rank + 7 CPU phantom ranks, 2 threads each
       step reh_solo2 300 python tools/host_rehearsal.py --ranks 1 --threads 2
       step reh_solo14 300 python tools/host_rehearsal.py --ranks 1 --threads 14
-      for R in device host; do
-        for PL in 1 0; do
-          step reh_${R}_p$PL 300 python tools/host_rehearsal.py --ranks 8 --threads 2 --plane $PL --render $R
-        done
+      for PL in 1 0; do
+        step reh_p$PL 300 python tools/host_rehearsal.py --ranks 8 --threads 2 --plane $PL
       done
       grep -h '^{' "$OUT"/reh_*.log ;;
     dropin_p)  # the drop-in at P = 2 / 3 through the node window on the one GPU (host-staged plane):

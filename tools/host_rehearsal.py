@@ -7,8 +7,8 @@ do on a real node: the node render plane's protocol (their share of the dataset'
 centre's handshake, the waits for every other slice) and their own query block's host work.
 Every rank gets DMLP_HOST_THREADS threads (16 CPUs / 8 ranks = 2 on a node granting 16 per
 GPU).  The GPU rank's ms/step against its solo run (same threads, no phantoms) is the contention
-the host budget costs; --plane 0 makes every rank render the whole dataset (no plane),
---render host the host fp16 render instead of the device render.
+the host budget costs; --plane 0 makes every rank render the whole dataset (no plane);
+--render sets the GPU rank's DMLP_DEVICE_RENDER (an early-start step renders on the host anyway).
 
     python tools/host_rehearsal.py --ranks 8 --threads 2 --plane 1 --render device --steps 100
 """
@@ -50,28 +50,27 @@ def _phantom(path, rank, world, qblk, steps, plane_on, render, threads, ready):
     Xp = inp.X.ctypes.data
     ready.put(rank)
     for _ in range(steps):
+        # an early-start step's host work (the bench shape always starts early, and an early step
+        # renders its screen operands on the host whatever DMLP_DEVICE_RENDER says: pipeline.hip
+        # dr_early_ok): the centre, this rank's query operands, the image and the int32 rows
         pl = inp.plane(rank, world) if plane_on else None
-        if render == "host" or not plane_on:
-            if pl is not None:
-                assert L.dmlp_plane_get_mu(C.byref(pl), A, mu.ctypes.data) == 0
-            else:
-                L.dmlp_cpu_center(Xp, N, A, mu.ctypes.data)
-        if render == "host":  # this rank's query operands on the host
-            L.dmlp_cpu_prep_queries(inp.Qx[q0:q1].ctypes.data, q1 - q0, A, mu.ctypes.data, kt,
-                                    qhi.ctypes.data, qn.ctypes.data)
         if pl is not None:
-            whats = (1, 2) if render == "host" else (2,)
-            for what in whats:
+            assert L.dmlp_plane_get_mu(C.byref(pl), A, mu.ctypes.data) == 0
+        else:
+            L.dmlp_cpu_center(Xp, N, A, mu.ctypes.data)
+        L.dmlp_cpu_prep_queries(inp.Qx[q0:q1].ctypes.data, q1 - q0, A, mu.ctypes.data, kt,
+                                qhi.ctypes.data, qn.ctypes.data)
+        if pl is not None:  # this rank's share of the node's slices, then every other slice
+            for what in (1, 2):
                 for i in range(rank, ns, world):
                     L.dmlp_plane_render(C.byref(pl), Xp, None, N, A, mu.ctypes.data, what, i)
         else:  # the whole dataset, this rank alone
-            if render == "host":
-                L.dmlp_cpu_prep_data_tiles(Xp, N, A, mu.ctypes.data, kt, 0, nt, img.ctypes.data,
-                                           xin.ctypes.data, C.byref(nm))
+            L.dmlp_cpu_prep_data_tiles(Xp, N, A, mu.ctypes.data, kt, 0, nt, img.ctypes.data,
+                                       xin.ctypes.data, C.byref(nm))
             L.dmlp_cpu_rows_i32(Xp, N * A, x32.ctypes.data)
         L.dmlp_cpu_rows_i32(inp.Qx[q0:q1].ctypes.data, (q1 - q0) * A, h32.ctypes.data)
         if pl is not None:
-            for what in ((1, 2) if render == "host" else (2,)):
+            for what in (1, 2):
                 for i in range(ns):
                     assert L.dmlp_plane_wait(C.byref(pl), what, i, None, None) == 0
         inp.barrier(world)  # the egress barrier of every front end
