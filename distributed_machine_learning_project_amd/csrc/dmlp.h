@@ -364,6 +364,8 @@ typedef struct dmlp_step_args {
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
 int dmlp_step_emit(char* dst, int64_t bytes, void* stream);
+// The last dmlp_step's report text as it sits on the device (report_mode 2) and its length.
+int dmlp_step_text(const char** dev, int64_t* len);
 void dmlp_step_early(int on);          // 1 on, 0 off, < 0: DMLP_FAST_EARLY (default on)
 // Right before a timed call after an idle stretch: wake the render pool, touch the staging, keep
 // the GPU busy gpu_us microseconds (clocks up).  Synchronous.

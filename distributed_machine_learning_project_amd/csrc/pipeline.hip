@@ -1667,6 +1667,19 @@ extern "C" int dmlp_step_emit(char* dst, int64_t bytes, void* stream) {
   }
 }
 
+// The last dmlp_step's report text on the device (report_mode 2) and its length: a caller that
+// streams it out in pieces (the drop-in's chunked egress to stdout) copies the pieces itself.
+extern "C" int dmlp_step_text(const char** dev, int64_t* len) {
+  try {
+    Ctx& w = ctx();
+    *dev = w.d_text.p;
+    *len = w.text_len;
+    return 0;
+  } catch (const Fail& f) {
+    return f.code;
+  }
+}
+
 // Right before a timed call after a long idle stretch (the reference harness parses its input
 // for seconds, then constructs the Engine, untimed, and starts its clock: common.cpp:119-124):
 // wake the render pool (its workers then spin into the call instead of sleeping on a futex),

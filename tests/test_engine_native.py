@@ -148,9 +148,17 @@ def test_dropin_engine_h_debug_cpu(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("strategy", ["farm", "shard_reduce"])
 def test_dropin_engine_h_gpu(tmp_path, strategy):
+    """One rank on the MI355X: stdout == the oracle's bytes.  The farm's report streams to
+    stdout in pieces as their copies land (KnnCore::emit_chunks): 4 (default), 7 (uneven
+    pieces) and 1 (the whole text after the step)."""
     path, inp, res, lab, cs = _case(tmp_path, N=5000, Q=400, A=12, kmax=150)
-    out = _run_dropin(_dropin(tmp_path), path, {"KNN_STRATEGY": strategy})
+    exe = _dropin(tmp_path)
+    out = _run_dropin(exe, path, {"KNN_STRATEGY": strategy})
     assert out == dmlp.format_report(cs)
+    if strategy == "farm":
+        for chunks in ("7", "1"):
+            out = _run_dropin(exe, path, {"KNN_STRATEGY": strategy, "KNN_EMIT_CHUNKS": chunks})
+            assert out == dmlp.format_report(cs), chunks
 
 
 # ---------------------------------------------------------------- the reference's own harness
