@@ -245,7 +245,7 @@ struct Tuning {
   int screen = 0;
   int x1k = 1;
   int host_ops = 1;
-  int device_render = 1;
+  int device_render = 0;  // DMLP_DEVICE_RENDER=1: r9r measured it slower (profiles/r9r_device_render_ab.txt)
   int qb_blocks = 0;
   int word_write = 0;
 };
@@ -259,7 +259,7 @@ Tuning make_tuning() {
   // host operands when the render pool has at least 2 threads (Step::run: with 1 the device path
   // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
   // 3.74: profiles/r7h_host_budget.md)
-  if (env_off("DMLP_DEVICE_RENDER")) t.device_render = 0;
+  t.device_render = env_int("DMLP_DEVICE_RENDER", 0) != 0 ? 1 : 0;
   t.qb_blocks = env_int("DMLP_QB_BLOCKS", 0);
   t.word_write = env_int("DMLP_WORD_WRITE", 0);
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;

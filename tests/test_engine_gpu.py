@@ -257,13 +257,15 @@ def test_step_policy_host_budget_and_shared_device(gpu, monkeypatch):
         monkeypatch.delenv("DMLP_FAST_EARLY", raising=False)
         L.dmlp_step_early(-1)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    # (3) with the device render (the default) the host only packs int32 rows: a one-thread pool
-    # keeps the single-term fp16 operands (path 0) as well
+    # (3) with the device render (DMLP_DEVICE_RENDER=1) the host only packs int32 rows: a
+    # one-thread pool keeps the single-term fp16 operands (path 0) as well; the default is the host
+    # render (the device render measured slower: profiles/r9r_device_render_ab.txt)
     for env, want_path in (({"DMLP_HOST_THREADS": "1", "DMLP_DEVICE_RENDER": "0"}, 2),
                            ({"DMLP_HOST_THREADS": "1", "DMLP_HOST_OPS": "1",
                              "DMLP_DEVICE_RENDER": "0"}, 0),
                            ({"DMLP_HOST_THREADS": "2", "DMLP_DEVICE_RENDER": "0"}, 0),
-                           ({"DMLP_HOST_THREADS": "1"}, 0)):
+                           ({"DMLP_HOST_THREADS": "1"}, 2),
+                           ({"DMLP_HOST_THREADS": "1", "DMLP_DEVICE_RENDER": "1"}, 0)):
         e = dict(os.environ, **env)
         e.pop("DMLP_HOST_OPS", None) if "DMLP_HOST_OPS" not in env else None
         e.pop("DMLP_DEVICE_RENDER", None) if "DMLP_DEVICE_RENDER" not in env else None
