@@ -45,6 +45,21 @@ def _headers():
     return sorted(CSRC.glob("*.h"))
 
 
+def _included(srcs):
+    """The csrc headers these sources include, transitively (#include "x.h"): a library object
+    does not go stale when only an engine-side header (engine_core.h, ...) changes."""
+    import re
+    seen, todo = set(), list(srcs)
+    while todo:
+        f = todo.pop()
+        for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read_text(errors="replace"), re.M):
+            h = CSRC / name
+            if h.exists() and h not in seen:
+                seen.add(h)
+                todo.append(h)
+    return sorted(seen)
+
+
 def _stale(target: Path, deps) -> bool:
     if not target.exists():
         return True
@@ -67,7 +82,7 @@ _INFO = {"compiled": [], "reused": [], "lib_relinked": False, "engine_relinked":
 
 def _compile(src: Path, force: bool) -> Path:
     obj = BUILD / (src.name + ".o")
-    if not force and not _stale(obj, [src] + _headers()):
+    if not force and not _stale(obj, [src] + _included([src])):
         _INFO["reused"].append(src.name)
         return obj
     _INFO["compiled"].append(src.name)
@@ -87,7 +102,7 @@ def build_lib(force: bool = False, jobs: int | None = None) -> Path:
     BUILD.mkdir(exist_ok=True)
     hip, cpp = _sources()
     srcs = hip + cpp
-    if not force and not _stale(LIB, srcs + _headers()):
+    if not force and not _stale(LIB, srcs + _included(srcs)):
         # the library is newer than every source and header: up to date even where its objects
         # did not travel (a GPU box gets the tree without _build/) — no 2-minute recompile there
         _INFO["reused"].extend(s.name for s in srcs)

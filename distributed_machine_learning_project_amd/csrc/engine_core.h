@@ -245,12 +245,18 @@ class KnnCore {
     if (in->Q > (1 << 30)) return false;
     wake_d2h();
     N_ = in->N; Q_ = in->Q; A_ = in->A;
-    lo_ = 0; hi_ = 1;
-    if (N_) {
-      lo_ = *std::min_element(in->labels.begin(), in->labels.end());
-      hi_ = *std::max_element(in->labels.begin(), in->labels.end()) + 1;
+    // the label range and the largest k: scanned by the step on its render pool (hi <= lo, kmax
+    // 0), not here on one thread — except for the lists mode, which sizes its outputs by kmax
+    lo_ = 0; hi_ = 0;
+    kmax_ = 0;
+    if (debug_) {
+      lo_ = 0; hi_ = 1;
+      if (N_) {
+        lo_ = *std::min_element(in->labels.begin(), in->labels.end());
+        hi_ = *std::max_element(in->labels.begin(), in->labels.end()) + 1;
+      }
+      kmax_ = Q_ ? std::max(1, *std::max_element(in->k.begin(), in->k.end())) : 1;
     }
-    kmax_ = Q_ ? std::max(1, *std::max_element(in->k.begin(), in->k.end())) : 1;
     const int chunks = getenv("KNN_EMIT_CHUNKS") ? std::atoi(getenv("KNN_EMIT_CHUNKS")) : 4;
     if (sink && !debug_ && chunks > 1 && rt_.gpu) {
       const dmlp_step_args a = step_host(nullptr, Xr, in->labels.data(), nullptr, Qr,
