@@ -63,6 +63,26 @@ def _layout(N, Q, A):
     return off, o
 
 
+def _roomy_dir(directory: str, need: int) -> str:
+    """directory when its filesystem has room for need bytes, else the first of $TMPDIR / /tmp /
+    /var/tmp that has (a small /dev/shm — a container's 64 MiB default — would otherwise end in
+    SIGBUS when the segment's pages are first written); the file-backed mapping is shared and
+    page-locked the same way."""
+    import tempfile
+
+    def room(d):
+        try:
+            st = os.statvfs(d)
+        except OSError:
+            return 0
+        return st.f_bavail * st.f_frsize
+
+    for d in (directory, os.environ.get("TMPDIR") or "", tempfile.gettempdir(), "/tmp", "/var/tmp"):
+        if d and os.path.isdir(d) and os.access(d, os.W_OK) and room(d) >= need + (64 << 20):
+            return d
+    return directory
+
+
 class SharedInput(KNNInput):
     """KNNInput whose arrays are views of a node-shared mapping (same on every rank)."""
     shared = True
@@ -105,6 +125,7 @@ class SharedInput(KNNInput):
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
         off, total = _layout(N, Q, A)
+        directory = _roomy_dir(directory, total)
         path = os.path.join(directory, f"dmlp_input_{os.getpid()}_{uuid.uuid4().hex[:8]}")
         mm = np.memmap(path, np.uint8, "w+", shape=(total,))
         if query_nodes:
