@@ -31,6 +31,7 @@
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 #   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
 #   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
+#   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
 TAG=${1:?tag}
@@ -219,6 +220,11 @@ for task in "$@"; do
       AB_ROUNDS=2 AB_STEPS=30 step x1mode_prof 600 bash tools/kernel_ab.sh "${V[@]}"
       python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/x1mode_kernels.txt"; rm -rf gpurun_out/ab
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step x1mode_ab 600 bash tools/kernel_ab.sh "${V[@]}" ;;
+    prewarm)  # the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000 (GPU busy before the call)
+      for US in 0 300 2000 5000; do
+        KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
+      done
+      grep -ho '"knn_ms_median": [0-9.]*' "$OUT"/prewarm_*.log ;;
     ringpmc)  # counters of the screen without / with the LDS ring (RINGS, default "0 12")
       for R in ${RINGS:-0 12}; do
         n=0
