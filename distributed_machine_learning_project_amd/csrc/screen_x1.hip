@@ -1030,7 +1030,7 @@ extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
 }
 // group ids per (query, slice) (refine expands each to its 4 members)
 extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
-// resident workgroups (= waves) per CU: LDS-bound at 19.5 KiB (SUB 16, 4 tiles) / 36.3 KiB
+// resident workgroups (= waves) per CU: LDS-bound at 17.5 KiB (SUB 16, 4 tiles) / 33.5 KiB
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {
   return x1_sub(kmax) == 16 ? (x1_ct(kmax) == 8 ? 4 : 8) : 4;
