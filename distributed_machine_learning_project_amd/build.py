@@ -77,7 +77,8 @@ def _run(cmd):
 # what the last build() did (written to _build/build_info.json and returned by build_info()):
 # the driver's "build mode" — sources compiled vs objects reused, and whether the library and
 # knn_engine were relinked — instead of a silent up-to-date check
-_INFO = {"compiled": [], "reused": [], "lib_relinked": False, "engine_relinked": False}
+_INFO = {"compiled": [], "reused": [], "lib_relinked": False, "engine_relinked": False,
+         "lib_matches_sources": False, "source_hash_16": None}
 
 
 def _compile(src: Path, force: bool) -> Path:
@@ -98,15 +99,37 @@ def _compile(src: Path, force: bool) -> Path:
     return obj
 
 
+SRCHASH = LIB.with_name(LIB.name + ".srchash")  # travels with the library (untracked, like it)
+
+
+def _source_hash(srcs) -> str:
+    """sha256 over what the library is built from: every source and included header (name and
+    bytes), the compile flags and the target — the library's identity, whatever the mtimes."""
+    import hashlib
+    h = hashlib.sha256(repr((ARCH, COMMON, sorted(PER_FILE.items()))).encode())
+    for f in sorted(set(srcs) | set(_included(srcs))):
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()
+
+
 def build_lib(force: bool = False, jobs: int | None = None) -> Path:
     BUILD.mkdir(exist_ok=True)
     hip, cpp = _sources()
     srcs = hip + cpp
-    if not force and not _stale(LIB, srcs + _included(srcs)):
-        # the library is newer than every source and header: up to date even where its objects
-        # did not travel (a GPU box gets the tree without _build/) — no 2-minute recompile there
+    want = _source_hash(srcs)
+    _INFO["source_hash_16"] = want[:16]
+    force = force or os.environ.get("DMLP_BUILD_FORCE", "") == "1"
+    if (not force and LIB.exists() and SRCHASH.exists() and SRCHASH.read_text().strip() == want):
+        # the library was linked from exactly these sources, flags and target: up to date even
+        # where its objects did not travel (a GPU box gets the tree without _build/) or the
+        # mtimes moved (a checkout) — no recompile there
         _INFO["reused"].extend(s.name for s in srcs)
+        _INFO["lib_matches_sources"] = True
         return LIB
+    # a library of unknown or other sources: rebuild it from scratch (an object's mtime cannot
+    # tell which sources it came from), unless only the record is missing and the mtimes agree
+    if LIB.exists() and SRCHASH.exists():
+        force = True
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
@@ -116,6 +139,8 @@ def build_lib(force: bool = False, jobs: int | None = None) -> Path:
               "-pthread"])
         os.replace(tmp, LIB)
         _INFO["lib_relinked"] = True
+    SRCHASH.write_text(want + "\n")
+    _INFO["lib_matches_sources"] = True
     return LIB
 
 
@@ -252,6 +277,7 @@ def build(force: bool = False, engine: bool = True) -> Path:
     for key in ("compiled", "reused"):
         _INFO[key] = []
     _INFO["lib_relinked"] = _INFO["engine_relinked"] = False
+    _INFO["lib_matches_sources"] = False
     lib = build_lib(force)
     if engine:
         build_engine(force)
