@@ -245,9 +245,10 @@ void pack(const std::vector<DataPoint>& dataset, const std::vector<Query>& queri
 
 // Labels, k and tables of row pointers into the harness's own attribute vectors (no row copy):
 // the single-GPU fast path reads the rows in place (KnnCore::KNN_rows).
+// identity (optional): set to whether every query's id is its index (the report's own ids)
 void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>& queries, int A,
                 dmlp_rt::Input& in, std::vector<const double*>& xr,
-                std::vector<const double*>& qr) {
+                std::vector<const double*>& qr, bool* identity = nullptr) {
   in.N = (int64_t)dataset.size();
   in.Q = (int64_t)queries.size();
   in.A = A;
@@ -257,9 +258,10 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
   qr.resize(in.Q);
   // on the render pool (warm workers, no thread start per call)
   const int64_t rows = in.N + in.Q;
-  std::atomic<bool> bad{false};
+  std::atomic<bool> bad{false}, renumbered{false};
   auto work = [&](int t, int nt) {
     const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
+    bool other_ids = false;
     for (int64_t r = a; r < b; ++r) {
       if (r < in.N) {
         const DataPoint& d = dataset[r];
@@ -271,12 +273,15 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
         if ((int)q.attrs.size() != A) bad = true;
         in.k[r - in.N] = q.k;
         qr[r - in.N] = q.attrs.data();
+        other_ids |= q.id != (int)(r - in.N);
       }
     }
+    if (other_ids) renumbered = true;
   };
   using Work = decltype(work);
   dmlp_host_pool_run([](void* c, int t, int nt) { (*(Work*)c)(t, nt); }, &work);
   if (bad) throw std::runtime_error("data point or query with wrong attribute count");
+  if (identity) *identity = !renumbered;
 }
 
 void cout_sink(void*, const char* bytes, size_t n) { std::cout.write(bytes, (std::streamsize)n); }
@@ -490,11 +495,11 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     // under the write of the previous piece), else whole, below, with the ids rewritten
     std::swap(in.labels, s->labels);
     std::swap(in.k, s->k);
-    index_rows(dataset, queries, p.num_attrs, in, s->xr, s->qr);
+    bool identity = false;
+    index_rows(dataset, queries, p.num_attrs, in, s->xr, s->qr, &identity);
+    identity = identity && !kListsMode;
     s->core->trace.mark("index");
     t1 = std::chrono::steady_clock::now();
-    bool identity = !kListsMode;
-    for (size_t i = 0; i < queries.size() && identity; ++i) identity = queries[i].id == (int)i;
     done = s->core->KNN_rows(&in, s->xr.data(), s->qr.data(), &out,
                              identity ? &cout_sink : nullptr, nullptr);
     emitted = done && identity && out.text_len > 0 && out.text.size() >= out.text_len &&
