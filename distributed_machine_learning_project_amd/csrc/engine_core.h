@@ -181,6 +181,8 @@ class KnnCore {
   hipStream_t wake_st_ = nullptr;
   HostBuf<char> wake_h_;
   static constexpr int kMaxChunks = 16;
+  double last_emit_ms = 0.0;  // the last KNN_rows' streamed report (0: none streamed)
+
   hipEvent_t emit_ev_[kMaxChunks] = {};
   // the device text of the last step -> out->text in `chunks` copies; sink gets each piece once
   // its copy completed (the host spins on the piece's event), in order
@@ -241,6 +243,7 @@ class KnnCore {
   // them to the harness's stdout: the report's D2H runs under the write instead of before it)
   bool KNN_rows(Input* in, const double* const* Xr, const double* const* Qr, Output* out,
                 Sink sink = nullptr, void* sink_ctx = nullptr) {
+    last_emit_ms = 0.0;
     if (rt_.world != 1 || strategy_ != "farm" || dynamic_ || !fast_ || !in) return false;
     if (in->Q > (1 << 30)) return false;
     wake_d2h();
@@ -262,7 +265,10 @@ class KnnCore {
       const dmlp_step_args a = step_host(nullptr, Xr, in->labels.data(), nullptr, Qr,
                                          in->k.data(), Q_, 0, 2, out);
       trace.mark("report");
+      const auto e0 = std::chrono::steady_clock::now();
       emit_chunks(a.report_len, std::min(chunks, kMaxChunks), out, sink, sink_ctx);
+      last_emit_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e0)
+                         .count();
       trace.mark("emit_chunks");
       return true;
     }
