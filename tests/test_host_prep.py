@@ -233,3 +233,24 @@ def test_host_i32_range_matches_numpy(n):
         assert (lo.value, hi.value) == (0, -1)
     else:
         assert (lo.value, hi.value) == (int(a.min()), int(a.max()))
+
+
+def test_build_records_source_identity(tmp_path):
+    """build() (what __graft_entry__.build runs) records what it did, and the library's identity is
+    the hash of its sources: the srchash beside libdmlp.so matches a fresh hash of the tree, and
+    build_info says whether anything was compiled."""
+    import json
+    from distributed_machine_learning_project_amd import build
+    build.build(engine=False)
+    info = build.build_info()
+    assert info["lib_matches_sources"] is True
+    srcs = sum(build._sources(), [])
+    want = build._source_hash(srcs)
+    assert build.SRCHASH.read_text().strip() == want
+    assert info["source_hash_16"] == want[:16]
+    rec = json.loads((build.BUILD / "build_info.json").read_text())
+    assert rec["mode"] in ("up-to-date", "rebuilt") and rec["arch"] == "gfx950"
+    # the headers a library object depends on are the ones its sources include, not every csrc
+    # header (engine_core.h changes relink knn_engine only)
+    names = {h.name for h in build._included(srcs)}
+    assert "dmlp.h" in names and "engine_core.h" not in names
