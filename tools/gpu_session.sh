@@ -31,6 +31,7 @@
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 #   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
 #   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
+#   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -220,6 +221,13 @@ for task in "$@"; do
       AB_ROUNDS=2 AB_STEPS=30 step x1mode_prof 600 bash tools/kernel_ab.sh "${V[@]}"
       python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/x1mode_kernels.txt"; rm -rf gpurun_out/ab
       AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step x1mode_ab 600 bash tools/kernel_ab.sh "${V[@]}" ;;
+    qbsmall)  # the query-block early start with few blocks and write-value words, blocks first / after
+              # the first image slice, against the default
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step qbsmall_ab 900 bash tools/kernel_ab.sh base:DMLP_QB_BLOCKS=0 \
+          qb2l0:DMLP_QB_BLOCKS=2,DMLP_QB_LEAD=0,DMLP_WORD_WRITE=1 \
+          qb4l0:DMLP_QB_BLOCKS=4,DMLP_QB_LEAD=0,DMLP_WORD_WRITE=1 \
+          qb2l1:DMLP_QB_BLOCKS=2,DMLP_QB_LEAD=1,DMLP_WORD_WRITE=1
+      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/qbsmall_ab.txt" ;;
     prewarm)  # the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000 (GPU busy before the call)
       for US in 0 300 2000 5000; do
         KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
