@@ -220,6 +220,24 @@ def test_bench_self_launch_rehearsal(np_):
     assert all(c > 0 for c in res["collective_check"]["calls_per_rank"])
 
 
+def test_bench_driver_path_eight_ranks():
+    """The driver's N = 8 command line in miniature: bench.py --gpus 8 (its default node-shared
+    ingress, the node render plane with 8 renderers, the native step on every rank) on the one
+    GPU over the host-staged plane, small Q, --verify of the whole report against the fp64
+    oracle; the JSON reports 8 ranks and every rank's row."""
+    import json
+    env = dict(os.environ, DMLP_DATA_PLANE="host", OMP_NUM_THREADS="2", DMLP_HOST_THREADS="2",
+               DMLP_BENCH_CONTRACT_RUNS="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "3",
+           "--warmup", "1", "--min-warmup-s", "0", "--n-data", "20000", "--q-per-gpu", "2048",
+           "--verify", "--no-busbw"]
+    r = subprocess.run(cmd, capture_output=True, env=env, timeout=400, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert res["n_gpus"] == 8 and res["verify_ok"]
+    assert len(res["per_rank"]) == 8
+
+
 # ---------------------------------------------------------------- wider worlds: P = 4 (2x2) and 8 (4x2)
 @pytest.mark.parametrize("strategy", ["farm", "grid2d", "shard_reduce", "shard_gather", "ring"])
 @pytest.mark.parametrize("np_", [4, 8])
