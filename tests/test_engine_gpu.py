@@ -203,6 +203,34 @@ def test_screen_lds_ring(gpu, sub):
         L.dmlp_pipeline_set(b"qb_blocks", old_qb)
 
 
+@pytest.mark.parametrize("sub", [14, 12])
+def test_screen_lds_ring_slices(gpu, sub):
+    """The LDS-ring screen over many data slices (a small query set against a large dataset: the
+    step splits the scan into S slices to fill the chip, S % 8 == 0 maps a slice to one XCD) and
+    with k varying per query: report, labels and checksums == the oracle's, no escalation, and
+    the ring kernel ran."""
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    old_ring = L.dmlp_pipeline_set(b"x1_ring", sub)
+    inp = dmlp.generate(60000, 8192 + 64, 32, 0.0, 1000.0, 1, 16, 8, seed=400 + sub)
+    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    import torch
+    dst = torch.empty(48 * len(inp.k) + 64, dtype=torch.uint8).pin_memory().numpy()
+    n0 = L.dmlp_x1_ring_launches()
+    try:
+        L.dmlp_step_early(0)
+        for _ in range(2):
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert bytes(dst[:r.report_len]) == dmlp.format_report(cs)
+            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+            assert r.n_escalated == 0
+        assert L.dmlp_x1_ring_launches() >= n0 + 2
+    finally:
+        L.dmlp_step_early(-1)
+        L.dmlp_pipeline_set(b"x1_ring", old_ring)
+
+
 def test_debug_listing(gpu, workload):
     inp, _, d, i = workload
     eng = _engine("ring", debug=True)
