@@ -169,6 +169,7 @@ int dmlp_screen_x1_waves_per_cu(int kmax);
 void dmlp_set_x1_ring(int sub);
 int dmlp_get_x1_ring(void);
 int64_t dmlp_x1_ring_launches(void);
+int dmlp_set_x1_ring_force(int on);  // the ring on any grid size (tests); returns the previous
 int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax);  // A > 64: one wave per SIMD
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);

@@ -1762,6 +1762,7 @@ extern "C" int dmlp_pipeline_set(const char* key, int value) {
     dmlp_set_x1_ring(value);
     return old;
   }
+  if (k == "x1_ring_force") return dmlp_set_x1_ring_force(value);  // ... on any grid (tests)
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
            : k == "device_render" ? &g_tune.device_render

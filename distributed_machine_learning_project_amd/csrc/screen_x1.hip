@@ -925,9 +925,11 @@ int x1_num_cus() {
   }();
   return n;
 }
-// the ring kernel fills the chip only with a workgroup (8 x 64 queries of a slice) per CU
+// the ring kernel fills the chip only with a workgroup (8 x 64 queries of a slice) per CU (tests
+// force it onto smaller grids: g_x1_ring_force)
+int g_x1_ring_force = 0;
 bool x1_ring_fits(int nq, int S) {
-  return x1_ring() && (int64_t)((nq + 511) / 512) * S >= x1_num_cus();
+  return x1_ring() && (g_x1_ring_force || (int64_t)((nq + 511) / 512) * S >= x1_num_cus());
 }
 
 template <int KT, int SUB, int DEPTH, int CHECK, int CTV, bool F16, int RING = 0>
@@ -1048,6 +1050,12 @@ extern "C" void dmlp_set_x1_ct(int ct) { g_x1_ct = ct == 4 ? 4 : 8; }
 // the LDS-ring screen for k <= 16, A <= 32 (0 off; 16 / 14 / 12: its sub-buffer depth)
 extern "C" void dmlp_set_x1_ring(int sub) { g_x1_ring = (sub == 16 || sub == 14 || sub == 12) ? sub : 0; }
 extern "C" int dmlp_get_x1_ring(void) { return x1_ring(); }
+// 1: the ring kernel whenever it is on, whatever the grid (tests); returns the previous value
+extern "C" int dmlp_set_x1_ring_force(int on) {
+  const int old = g_x1_ring_force;
+  g_x1_ring_force = on ? 1 : 0;
+  return old;
+}
 extern "C" int64_t dmlp_x1_ring_launches(void) { return g_x1_ring_launches; }
 extern "C" int dmlp_x1_debug_counters(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x1_dbg), sizeof(g_x1_dbg));

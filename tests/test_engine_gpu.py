@@ -212,6 +212,7 @@ def test_screen_lds_ring_slices(gpu, sub):
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
     old_ring = L.dmlp_pipeline_set(b"x1_ring", sub)
+    old_force = L.dmlp_pipeline_set(b"x1_ring_force", 1)  # (a grid smaller than one WG per CU)
     inp = dmlp.generate(60000, 8192 + 64, 32, 0.0, 1000.0, 1, 16, 8, seed=400 + sub)
     d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
     lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
@@ -229,6 +230,7 @@ def test_screen_lds_ring_slices(gpu, sub):
     finally:
         L.dmlp_step_early(-1)
         L.dmlp_pipeline_set(b"x1_ring", old_ring)
+        L.dmlp_pipeline_set(b"x1_ring_force", old_force)
 
 
 def test_debug_listing(gpu, workload):
