@@ -81,9 +81,21 @@ _INFO = {"compiled": [], "reused": [], "lib_relinked": False, "engine_relinked":
          "lib_matches_sources": False, "source_hash_16": None}
 
 
+def _obj_hash(src: Path) -> str:
+    import hashlib
+    h = hashlib.sha256(repr((ARCH, COMMON, PER_FILE.get(src.name, []))).encode())
+    for f in [src] + _included([src]):
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()
+
+
 def _compile(src: Path, force: bool) -> Path:
+    # an object is current when the hash of its source, included headers and flags recorded
+    # beside it matches (content, not mtimes: a checkout of older sources recompiles)
     obj = BUILD / (src.name + ".o")
-    if not force and not _stale(obj, [src] + _included([src])):
+    stamp = obj.with_name(obj.name + ".srchash")
+    want = _obj_hash(src)
+    if not force and obj.exists() and stamp.exists() and stamp.read_text().strip() == want:
         _INFO["reused"].append(src.name)
         return obj
     _INFO["compiled"].append(src.name)
@@ -96,6 +108,7 @@ def _compile(src: Path, force: bool) -> Path:
         # host-only code: plain g++ without -march (no FMA contraction, SSE2 like the reference)
         cmd = ["g++", *COMMON, f"-I{CSRC}", "-pthread", "-c", str(src), "-o", str(obj)]
     _run(cmd)
+    stamp.write_text(want + "\n")
     return obj
 
 
@@ -126,14 +139,11 @@ def build_lib(force: bool = False, jobs: int | None = None) -> Path:
         _INFO["reused"].extend(s.name for s in srcs)
         _INFO["lib_matches_sources"] = True
         return LIB
-    # a library of unknown or other sources: rebuild it from scratch (an object's mtime cannot
-    # tell which sources it came from), unless only the record is missing and the mtimes agree
-    if LIB.exists() and SRCHASH.exists():
-        force = True
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or _stale(LIB, objs):
+    if force or _INFO["compiled"] or _stale(LIB, objs) or not SRCHASH.exists() or \
+            SRCHASH.read_text().strip() != want:
         tmp = LIB.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp),
               "-pthread"])
