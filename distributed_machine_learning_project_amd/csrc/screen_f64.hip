@@ -357,7 +357,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SUB == 16 ? 
   compact(true);
 }
 
-int f64_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
+// sub-buffer depth: 16 (two waves per SIMD) for k <= 16 up to A = 32; A in (32, 64] keeps its
+// 12 / 16 query fragments per column tile in registers only at one wave per SIMD (512 registers:
+// the two-wave form spills 184 / 340 bytes per lane), so it always takes the 32-deep form
+int f64_sub(int kmax, int NM) { return kmax <= 16 && NM <= 8 ? 16 : 32; }
 
 template <int NM, int SUB>
 int launch_f64(const double2* frag, const double* xi, int64_t n_tiles, const double* Qx, int A,
@@ -376,7 +379,7 @@ int launch_f64(const double2* frag, const double* xi, int64_t n_tiles, const dou
   return 0;
 }
 
-int f64_nm(int A) { return A <= 8 ? 2 : A <= 16 ? 4 : A <= 32 ? 8 : 0; }
+int f64_nm(int A) { return A <= 8 ? 2 : A <= 16 ? 4 : A <= 32 ? 8 : A <= 48 ? 12 : A <= 64 ? 16 : 0; }
 
 // Slices so that the grid fills 2 waves per SIMD (1024 SIMDs) with at most 4096 tiles (2^16
 // groups) per slice and at most 256 slices (the refine's prefix array).
@@ -404,7 +407,7 @@ F64Ws f64_ws(char* base, int64_t N, int A, int nq, int kmax) {
   const int NM = f64_nm(A);
   const int64_t n_tiles = (N + 63) / 64;
   const int S = f64_slices(nq, n_tiles);
-  const int idcap = 4 * (f64_sub(kmax) - 1);
+  const int idcap = 4 * (f64_sub(kmax, NM) - 1);
   auto al = [](int64_t x) { return (x + 255) & ~int64_t(255); };
   F64Ws w{};
   int64_t o = 0;
@@ -422,7 +425,7 @@ F64Ws f64_ws(char* base, int64_t N, int A, int nq, int kmax) {
 
 // Layout probe (tests): scores of queries Qx[0..16) against points [0, 16) computed exactly as
 // k_screen_f64 does (image, C operand, f64 MFMA chain, result rows g + 4r -> point 4g + r),
-// written out[query * 16 + point].  NM = A padded / 4 (<= 8).
+// written out[query * 16 + point].  NM = A padded / 4 (<= 16).
 __global__ void k_f64_probe(const double2* __restrict__ frag, const double* __restrict__ xi,
                             const double* __restrict__ Qx, int A, const double* __restrict__ mu,
                             int NM, double* __restrict__ out) {
@@ -470,7 +473,7 @@ extern "C" void dmlp_exact_f64_layout(int64_t N, int A, int nq, int kmax, int64_
   const int S = f64_slices(nq, n_tiles);
   out[0] = S;
   out[1] = (n_tiles + S - 1) / S;
-  out[2] = 4 * (f64_sub(kmax) - 1);
+  out[2] = 4 * (f64_sub(kmax, f64_nm(A)) - 1);
   out[3] = (int64_t)(size_t)w.cand_ids;
   out[4] = (int64_t)(size_t)w.cand_cnt;
   out[5] = (int64_t)(size_t)w.cand_h;
@@ -487,7 +490,7 @@ extern "C" int dmlp_refine_groups_exact(int cap, const int* cand_ids, const int*
                                         void* stream);
 
 // Largest A / k the fp64 screen serves (A: the query fragments live in registers).
-extern "C" int dmlp_exact_f64_amax(void) { return 32; }
+extern "C" int dmlp_exact_f64_amax(void) { return 64; }
 extern "C" int dmlp_exact_f64_kmax(void) { return 64; }
 
 extern "C" int64_t dmlp_exact_f64_bytes(int64_t N, int A, int nq, int kmax) {
@@ -495,7 +498,7 @@ extern "C" int64_t dmlp_exact_f64_bytes(int64_t N, int A, int nq, int kmax) {
   return f64_ws(nullptr, N, A, nq, kmax).bytes;
 }
 
-// Exact top-k of queries qidx[0..nq) (k <= 64, A <= 32): out_*[q * kstride + j], j < k, sorted by
+// Exact top-k of queries qidx[0..nq) (k <= 64, A <= 64): out_*[q * kstride + j], j < k, sorted by
 // (dist asc, id desc), bit-identical to dmlp_exact_topk.  A query whose candidates overflow gets
 // status[q] = 1 and nothing written (the caller runs dmlp_exact_topk on it); *ovf_count (device)
 // is ADDED the number of them.  ws: dmlp_exact_f64_bytes(N, A, nq, kmax) bytes.
@@ -522,7 +525,7 @@ extern "C" int dmlp_exact_f64(const double* X, int64_t N, int A, const double* Q
   hipLaunchKernelGGL(k_f64_norms, dim3((unsigned)((n_tiles * 64 + 255) / 256)), dim3(256), 0, st,
                      X, N, A, w.mu, n_tiles * 64, w.xi, w.xnmax);
   DMLP_LAUNCH_CHECK();
-  const int sub = f64_sub(kmax);
+  const int sub = f64_sub(kmax, NM);
 #define DMLP_F64(NMV)                                                                          \
   rc = sub == 16 ? launch_f64<NMV, 16>(w.frag, w.xi, n_tiles, Qx, A, w.mu, qidx, qk, nq, w.xnmax, S, \
                                        w.cand_ids, w.cand_cnt, w.cand_h, st)                  \
@@ -530,7 +533,13 @@ extern "C" int dmlp_exact_f64(const double* X, int64_t N, int A, const double* Q
                                        w.cand_ids, w.cand_cnt, w.cand_h, st)
   if (NM == 2) DMLP_F64(2);
   else if (NM == 4) DMLP_F64(4);
-  else DMLP_F64(8);
+  else if (NM == 8) DMLP_F64(8);
+  else if (NM == 12)
+    rc = launch_f64<12, 32>(w.frag, w.xi, n_tiles, Qx, A, w.mu, qidx, qk, nq, w.xnmax, S,
+                            w.cand_ids, w.cand_cnt, w.cand_h, st);
+  else
+    rc = launch_f64<16, 32>(w.frag, w.xi, n_tiles, Qx, A, w.mu, qidx, qk, nq, w.xnmax, S,
+                            w.cand_ids, w.cand_cnt, w.cand_h, st);
 #undef DMLP_F64
   if (rc) return rc;
   if (getenv("DMLP_EXACT_F64_SCREEN_ONLY")) return 0;  // debugging: the candidates stay in ws

@@ -159,7 +159,7 @@ def test_fused_exact_kernel(torch_cuda, N, Q, A, kmin, kmax, lo, hi, monkeypatch
     assert K.pipeline_stats()["n_exact_f64"] == 0
 
 
-@pytest.mark.parametrize("A", [32, 7, 1])
+@pytest.mark.parametrize("A", [32, 7, 1, 48, 64])
 def test_exact_f64_mfma_layout(torch_cuda, A):
     """The fp64 screen's operand / result maps (v_mfma_f64_16x16x4_f64, screen_f64.hip) on exact
     integer data: 16 queries x the first 16 points, every score q'.x' - |x'|^2/2 exact."""
@@ -190,6 +190,9 @@ def test_exact_f64_mfma_layout(torch_cuda, A):
     (9000, 64, 16, 16, 16, 1e6, 1e6 + 1),   # offset data: centring keeps the keys tight
     (700, 33, 3, 1, 40, 0, 2),              # heavy exact ties: overflow -> VALU kernel
     (1000, 20, 1, 1, 64, 0, 10),            # A = 1
+    (6000, 150, 48, 1, 16, 0, 1000),        # A in (32, 64]: 12 fragments, one wave per SIMD
+    (5000, 90, 64, 8, 64, -50, 50),         # A = 64, mixed k up to 64
+    (3000, 70, 37, 1, 32, 0, 1000),         # odd A padded to 40 -> 12 fragments
 ])
 def test_exact_f64_screen(torch_cuda, N, Q, A, kmin, kmax, lo, hi):
     """The exact path's fp64 MFMA screen (screen_f64.hip) + exact group re-rank == the CPU path
