@@ -32,6 +32,7 @@
 #   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
 #   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
 #   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
+#   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -228,6 +229,14 @@ for task in "$@"; do
           qb4l0:DMLP_QB_BLOCKS=4,DMLP_QB_LEAD=0,DMLP_WORD_WRITE=1 \
           qb2l1:DMLP_QB_BLOCKS=2,DMLP_QB_LEAD=1,DMLP_WORD_WRITE=1
       python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/qbsmall_ab.txt" ;;
+    exact64)  # the exact path at A = 48 / 64 on the fp64 MFMA screen vs the VALU kernel, --verify
+      for A in 48 64; do
+        step exact_a${A}_f64 300 python bench.py --exact --attrs $A --steps 3 --warmup 1 \
+            --min-warmup-s 0 --verify --no-busbw
+        DMLP_EXACT_F64=0 step exact_a${A}_valu 300 python bench.py --exact --attrs $A --steps 3 \
+            --warmup 1 --min-warmup-s 0 --verify --no-busbw
+      done
+      grep -ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*' "$OUT"/exact_a*.log ;;
     prewarm)  # the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000 (GPU busy before the call)
       for US in 0 300 2000 5000; do
         KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
