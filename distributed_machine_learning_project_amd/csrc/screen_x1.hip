@@ -751,8 +751,8 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
           pend = -1;
         }
         const int sl1 = (i + 1) % RS;
-        // both counter reads issue before step 0's MFMAs and are consumed two steps later; tile
-        // i + 1's reads go out at steps 2 and 3 (into the ring registers steps 0 .. 3 freed)
+        // both counter reads issue before step 0's MFMAs and are consumed after them (consuming
+        // them two steps later, with tile i + 1's reads at steps 2 and 3, measured slower: r9x)
         const unsigned nx = __hip_atomic_load(rnext, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned rd = __hip_atomic_load(rready + sl1, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
         for (int r = 0; r < 4; ++r) {
           const int j = i * 4 + r;
           DMLP_MFMA(r, r & 1);
-          if (r == 2) {
+          if (r == 0) {
             if (i + L < nt && claim_v(i + L, (unsigned)__builtin_amdgcn_readfirstlane((int)nx))) {
               produce(i + L);
               pend = i + L;
@@ -784,12 +784,8 @@ __global__ __launch_bounds__(RING ? 512 : 64) __attribute__((amdgpu_waves_per_eu
               }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            DMLP_RLOAD(sl1, 0);  // (past the last tile: a stale slot, never used)
-            DMLP_RLOAD(sl1, 1);
-          } else if (r == 3) {
-            DMLP_RLOAD(sl1, 2);
-            DMLP_RLOAD(sl1, 3);
           }
+          DMLP_RLOAD(sl1, r);  // (past the last tile: a stale slot, never used)
           if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
           if (r % CHECK == CHECK - 1) DMLP_CHECK();
         }
@@ -907,10 +903,10 @@ int g_x1_ct = 4;
 int x1_ct(int kmax) { return x1_sub(kmax) == 16 ? g_x1_ct : 4; }
 
 // the LDS-ring variants (RING > 0): DMLP_X1_RING = 0 (off) or the sub-buffer depth of the ring
-// kernel — 16 (5-tile ring) or 14 / 12 (8 tiles: a power of two, a mask per slot index): a
-// shallower candidate buffer leaves LDS to the ring, i.e. slack between the fastest and the
-// slowest wave, at the price of more frequent compactions (and 40 / 48 instead of 56 kept group
-// entries per column)
+// kernel — 16 (5-tile ring), 14 (9 tiles) or 12 (13 tiles): a shallower candidate buffer leaves
+// more LDS to the ring, i.e. more slack between the fastest and the slowest wave, at the price
+// of more frequent compactions (and 40 / 48 instead of 56 kept group entries per column; 8-tile
+// rings, a mask per slot index, measured slower: r9x)
 int g_x1_ring = -1;
 int64_t g_x1_ring_launches = 0;
 int x1_ring() {
@@ -1158,8 +1154,8 @@ extern "C" int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const fl
       if (sub == 32) return launch_x1<1, 32, 4, 2, 4, F16>(DMLP_X1_ARGS);                      \
       if (ct == 4 && x1_ring_fits(nq, S)) {                                                    \
         if (x1_ring() == 16) return launch_x1<1, 16, 4, 2, 4, F16, 5>(DMLP_X1_ARGS);           \
-        if (x1_ring() == 14) return launch_x1<1, 14, 4, 2, 4, F16, 8>(DMLP_X1_ARGS);           \
-        return launch_x1<1, 12, 4, 2, 4, F16, 8>(DMLP_X1_ARGS);                                \
+        if (x1_ring() == 14) return launch_x1<1, 14, 4, 2, 4, F16, 9>(DMLP_X1_ARGS);           \
+        return launch_x1<1, 12, 4, 2, 4, F16, 13>(DMLP_X1_ARGS);                               \
       }                                                                                        \
       return ct == 8 ? launch_x1<1, 16, 4, 2, 8, F16>(DMLP_X1_ARGS)                            \
                      : launch_x1<1, 16, 4, 2, 4, F16>(DMLP_X1_ARGS);                           \
@@ -1247,8 +1243,8 @@ extern "C" int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const flo
     if (ct == 8) DMLP_X1E(1, 16, 8);
     if (x1_ring_fits(nq, 1)) {
       if (x1_ring() == 16) DMLP_X1E(1, 16, 4, 5);
-      if (x1_ring() == 14) DMLP_X1E(1, 14, 4, 8);
-      DMLP_X1E(1, 12, 4, 8);
+      if (x1_ring() == 14) DMLP_X1E(1, 14, 4, 9);
+      DMLP_X1E(1, 12, 4, 13);
     }
     DMLP_X1E(1, 16, 4);
   }
