@@ -178,3 +178,32 @@ def test_plane_wait_times_out(tmp_path):
     assert L.dmlp_plane_wait(C.byref(pl), 1, 0, None, None) == -4
     assert time.monotonic() - t < 1
     assert L.dmlp_plane_bytes(N, 300, 0) == -1  # beyond the screen's 256 attributes: no plane
+
+
+def test_shared_segment_falls_back_from_a_small_dev_shm(tmp_path, monkeypatch):
+    """utils/shm.py: a segment that does not fit the requested directory (a container's 64 MiB
+    /dev/shm) goes to the first roomy candidate ($TMPDIR here) instead of dying of SIGBUS when its
+    pages are first written; a segment that fits stays where it was asked."""
+    import os
+    from distributed_machine_learning_project_amd.utils import shm
+    small = tmp_path / "small"
+    small.mkdir()
+    roomy = tmp_path / "roomy"
+    roomy.mkdir()
+    real = os.statvfs
+
+    class _St:
+        def __init__(self, free):
+            self.f_bavail, self.f_frsize = free, 1
+
+    def fake(d):
+        if str(d) == str(small):
+            return _St(1 << 20)  # 1 MiB free
+        if str(d) == str(roomy):
+            return _St(1 << 40)
+        return real(d)
+
+    monkeypatch.setattr(shm.os, "statvfs", fake)
+    monkeypatch.setenv("TMPDIR", str(roomy))
+    assert shm._roomy_dir(str(small), 512 << 20) == str(roomy)
+    assert shm._roomy_dir(str(roomy), 512 << 20) == str(roomy)
