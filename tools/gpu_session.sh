@@ -33,6 +33,7 @@
 #   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
 #   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
+#   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -237,6 +238,16 @@ for task in "$@"; do
             --warmup 1 --min-warmup-s 0 --verify --no-busbw
       done
       grep -ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*' "$OUT"/exact_a*.log ;;
+    modes)  # the replicated dataset's two ingress modes at P = 3 / 4 on the one GPU (host plane),
+            # --verify, collective bytes per step in the JSON
+      for P in 3 4; do
+        for M in h2d xgmi; do
+          DMLP_DATA_PLANE=host KNN_DATA_INGRESS=$M step modes_p${P}_$M 400 python bench.py --gpus $P \
+              --steps 10 --warmup 2 --min-warmup-s 1 --q-per-gpu 32768 --verify --no-busbw
+        done
+      done
+      grep -ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*\|"collective_bytes_per_step": {[^}]*}' \
+          "$OUT"/modes_*.log ;;
     prewarm)  # the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000 (GPU busy before the call)
       for US in 0 300 2000 5000; do
         KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
