@@ -363,8 +363,11 @@ def _world_report(comm, host_plane, a):
     # the farm's dataset replication (parallel/strategies.py probe_replication, untimed): every
     # GPU over its own PCIe link ("h2d") or 1/P each + an all-gather over xGMI ("xgmi")
     out["replication_probe"] = getattr(comm, "replication", None)
-    out["replication_mode"] = (os.environ.get("KNN_DATA_INGRESS") or
-                               (getattr(comm, "replication", None) or {}).get("mode", "h2d"))
+    from distributed_machine_learning_project_amd.parallel.strategies import replication_mode
+    ingress = os.environ.get("KNN_DATA_INGRESS", "auto")
+    out["replication_mode"] = (ingress if ingress != "auto" else
+                               replication_mode(getattr(comm, "replication", None),
+                                                a.n_data * a.attrs * 4))
     if out["allreduce_check"] != comm.world:
         raise RuntimeError(f"all-reduce of ones gave {out['allreduce_check']} on {comm.world} ranks")
     return out

@@ -243,8 +243,8 @@ def _farm_shared(comm, be, inp, tr, N, Q, A, lo, hi, kmax, debug):
     counts, displs = block_partition(Q, comm.world)
     a, b = displs[comm.rank], displs[comm.rank] + counts[comm.rank]
     mode = os.environ.get("KNN_DATA_INGRESS", "auto") if comm.world > 1 else "h2d"
-    if mode == "auto":  # the replication the untimed probe measured faster (Engine._warmup)
-        mode = (getattr(comm, "replication", None) or {}).get("mode", "h2d")
+    if mode == "auto":  # from the untimed probe's measurements (Engine._warmup), for this N x A
+        mode = replication_mode(getattr(comm, "replication", None), N * A * 4)
     max_rows = int(os.environ.get("KNN_MAX_DEVICE_ROWS", "0") or 0)
     kl_h = inp.k[a:b]  # a view of the node-shared segment (never written here)
     if max_rows and N > max_rows:
@@ -340,12 +340,31 @@ def _x32_replica(comm, be, inp):
     return full
 
 
+# In "h2d" mode the dataset's int32 rows cross each GPU's own link BEHIND the screen (only the
+# re-rank waits for them); in "xgmi" mode 1/P of them cross and an all-gather completes them
+# BEFORE the step (plus one small all-reduce + host sync on the pack's range check).  So xgmi pays
+# only when the rows could not hide behind the screen: their concurrent H2D takes longer than
+# about the screen's own time.
+_ROWS_HIDE_S = 1.0e-3
+
+
+def replication_mode(probe, row_bytes: int) -> str:
+    """"xgmi" when every GPU copying row_bytes over its own link (at the bandwidth the probe saw
+    with all ranks copying at once) would outlast what the screen hides and the all-gather is
+    faster than that copy; else "h2d".  No probe: "h2d"."""
+    if not probe or not probe.get("h2d_GBps_per_gpu_concurrent"):
+        return "h2d"
+    t_h2d = row_bytes / (probe["h2d_GBps_per_gpu_concurrent"] * 1e9)
+    ag = probe.get("allgather_GBps") or 0.0
+    t_x = (t_h2d / max(1, probe.get("world", 1))) + (row_bytes / (ag * 1e9) if ag else float("inf"))
+    return "xgmi" if t_h2d > _ROWS_HIDE_S and t_x < t_h2d else "h2d"
+
+
 def probe_replication(comm, nbytes=32 << 20, iters=3):
     """Untimed, at Engine construction (P > 1 on GPUs): how the replicated dataset should reach
     every GPU.  Measures, with every rank at once, the page-locked H2D bandwidth of one GPU and
-    an all-gather of nbytes; "xgmi" (1/P over PCIe + the all-gather) when that is faster than
-    every GPU copying everything over its own link ("h2d").  Every rank takes the same decision
-    (maxima over ranks)."""
+    an all-gather of nbytes (maxima over ranks: every rank sees the same numbers and takes the
+    same decision); replication_mode turns them into the choice for a call's dataset."""
     import time
     torch = _torch()
     from . import dist_api as dist
@@ -371,10 +390,14 @@ def probe_replication(comm, nbytes=32 << 20, iters=3):
     t_h2d = timed(lambda: d.copy_(h, non_blocking=True))
     t_ag = timed(lambda: dist.all_gather_into_tensor(d, shard))
     t_x = t_h2d / P + t_ag
-    return {"mode": "xgmi" if t_x < t_h2d else "h2d", "bytes": n * 4,
-            "h2d_GBps_per_gpu_concurrent": round(n * 4 / t_h2d / 1e9, 2),
-            "allgather_GBps": round(n * 4 / t_ag / 1e9, 2),
-            "est_ms_h2d": round(t_h2d * 1e3, 4), "est_ms_xgmi": round(t_x * 1e3, 4)}
+    out = {"bytes": n * 4, "world": P,
+           "h2d_GBps_per_gpu_concurrent": round(n * 4 / t_h2d / 1e9, 2),
+           "allgather_GBps": round(n * 4 / t_ag / 1e9, 2),
+           "est_ms_h2d": round(t_h2d * 1e3, 4), "est_ms_xgmi": round(t_x * 1e3, 4)}
+    # the choice for the bench_4 dataset (1e5 x 32 int32 rows); each call decides for its own
+    # N x A (replication_mode)
+    out["mode"] = replication_mode(out, 100_000 * 32 * 4)
+    return out
 
 
 def _step_egress(comm, inp, r, qid_base):

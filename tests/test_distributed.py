@@ -331,3 +331,18 @@ def test_collective_log_recv_any_source():
     for p in ps:
         p.join(timeout=60)
     assert out[0][0] is True, out[0][1]
+
+
+def test_replication_mode_rule():
+    """The farm's dataset replication (parallel/strategies.py replication_mode): the rows cross
+    each GPU's own link behind the screen unless that concurrent copy would outlast what the
+    screen hides (~1 ms) and the all-gather route is faster; no probe: h2d."""
+    from distributed_machine_learning_project_amd.parallel.strategies import replication_mode
+    rows = 100_000 * 32 * 4  # bench_4's int32 rows, 12.8 MB
+    fast = {"world": 8, "h2d_GBps_per_gpu_concurrent": 50.0, "allgather_GBps": 300.0}
+    slow = {"world": 8, "h2d_GBps_per_gpu_concurrent": 5.0, "allgather_GBps": 300.0}
+    assert replication_mode(fast, rows) == "h2d"          # 0.26 ms: hidden behind the screen
+    assert replication_mode(slow, rows) == "xgmi"         # 2.6 ms of rows vs 0.3 + 0.04 ms
+    assert replication_mode(dict(slow, allgather_GBps=1.0), rows) == "h2d"  # a slower gather
+    assert replication_mode(None, rows) == "h2d"
+    assert replication_mode(fast, 10 * rows) == "xgmi"    # 2.6 ms of rows again
