@@ -182,9 +182,10 @@ int early_qchunks() {
   static const int q = std::min(16, std::max(1, env_int("DMLP_FAST_QCHUNKS", 4)));
   return q;
 }
-// Device render (profiles/r9*): the screen's fp16 operands are rendered on the GPU (prep.hip
+// Device render (DMLP_DEVICE_RENDER=1): the screen's fp16 operands rendered on the GPU (prep.hip
 // k_render) from the rows that cross PCIe for the exact re-rank anyway (lossless int32): the host
-// only packs int32 rows.  DMLP_DEVICE_RENDER=0: the host render (host_prep.cpp) as before.
+// only packs int32 rows.  Off by default: the operands then wait for the int32 rows, and it
+// measured slower than the host render (host_prep.cpp) at every size (profiles/r9r).
 bool dr_on();  // (Tuning::device_render below)
 // The render kernels (k_render: one-wave workgroups, 40 VGPRs, no LDS) would have to run beside
 // an early-start screen that fills the GPU and spins on their ready words.  Measured
@@ -197,9 +198,9 @@ bool dr_on();  // (Tuning::device_render below)
 bool dr_early_ok(int, int) { return false; }
 // The early start's copies (small ones run as blit kernels) need a wave slot beside the spinning
 // screen: the screen variant must leave registers free (of 512 per SIMD lane; hipcc
-// -Rpass-analysis=kernel-resource-usage): KT 1 k <= 16 2 x 211 (80 free), KT 1 k > 16 312,
-// KT 2 k > 16 341, KT 4 310 / 404 — but KT 2 k <= 16 takes 2 x 244 (16 free: every wave timed
-// out, profiles/r9h) and KT 8 up to all 512.
+// -Rpass-analysis=kernel-resource-usage): KT 1 k <= 16 2 x 208 (96 free), KT 1 k > 16 320,
+// KT 2 k > 16 350, KT 4 322 / 415 — but KT 2 k <= 16 takes 2 x 241 (16 free after the allocation
+// granule: every wave timed out, profiles/r9h) and KT 8 up to all 512.
 bool early_room(int KT, int kmax) { return KT == 1 || (KT == 2 && kmax > 16) || KT == 4; }
 // Query-block early start: the query operands cross in DMLP_QB_BLOCKS blocks after the first
 // DMLP_QB_LEAD dataset image slices, each block with a ready word, and every screen wave waits
