@@ -34,7 +34,6 @@
 #   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
-#   qchunks    early-start query render slices 2 / 4 / 8 (DMLP_FAST_QCHUNKS)
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -249,10 +248,6 @@ for task in "$@"; do
       done
       grep -ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*\|"collective_bytes_per_step": {[^}]*}' \
           "$OUT"/modes_*.log ;;
-    qchunks)  # the early start's query-operand render/copy slices (DMLP_FAST_QCHUNKS) 2 / 4 / 8
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step qchunks_ab 900 bash tools/kernel_ab.sh q4:DMLP_FAST_QCHUNKS=4 \
-          q2:DMLP_FAST_QCHUNKS=2 q8:DMLP_FAST_QCHUNKS=8
-      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/qchunks_ab.txt" ;;
     prewarm)  # the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000 (GPU busy before the call)
       for US in 0 300 2000 5000; do
         KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
