@@ -249,6 +249,7 @@ struct Tuning {
   int device_render = 0;  // DMLP_DEVICE_RENDER=1: r9r measured it slower (profiles/r9r_device_render_ab.txt)
   int qb_blocks = 0;
   int word_write = 0;
+  int report_chunks = 0;  // DMLP_REPORT_CHUNKS: the report's tail in query chunks (Step::run)
 };
 Tuning make_tuning() {
   Tuning t;
@@ -263,6 +264,7 @@ Tuning make_tuning() {
   t.device_render = env_int("DMLP_DEVICE_RENDER", 0) != 0 ? 1 : 0;
   t.qb_blocks = env_int("DMLP_QB_BLOCKS", 0);
   t.word_write = env_int("DMLP_WORD_WRITE", 0);
+  t.report_chunks = env_int("DMLP_REPORT_CHUNKS", 0);
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
@@ -340,6 +342,8 @@ const char* const kMarkNames[M_N] = {"enter", "operands_landed", "data_landed", 
                                      "screen_done", "knn_done", "format_done",
                                      "report_d2h_done"};
 
+constexpr int kMaxTail = 8;  // report tail chunks at most
+
 struct Ctx {
   int dev = -1;
   hipStream_t side = nullptr;  // host->device copies of dmlp_step
@@ -385,6 +389,12 @@ struct Ctx {
   DBuf<int64_t> d_off;
   DBuf<char> d_text;
   int64_t text_len = 0;  // the last dmlp_step's report bytes on the device (dmlp_step_emit)
+  // the chunked report tail (Step::run, report_chunks): per chunk a format-done event on `st`, its
+  // end offset's copy on `side` (+ event), the text copies on their own stream
+  hipStream_t tail = nullptr;
+  hipEvent_t ev_tf[kMaxTail] = {}, ev_ts[kMaxTail] = {}, ev_tail = nullptr;
+  DBuf<int64_t> d_off_t;
+  HBuf<int64_t> tail_end_h;
 };
 
 Ctx& ctx() {
@@ -398,6 +408,12 @@ Ctx& ctx() {
     CK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
+    CK(hipStreamCreateWithFlags(&w.tail, hipStreamNonBlocking));
+    for (int i = 0; i < kMaxTail; ++i) {
+      CK(hipEventCreateWithFlags(&w.ev_tf[i], hipEventDisableTiming));
+      CK(hipEventCreateWithFlags(&w.ev_ts[i], hipEventDisableTiming));
+    }
+    CK(hipEventCreateWithFlags(&w.ev_tail, hipEventDisableTiming));
   }
   return w;
 }
@@ -495,6 +511,10 @@ struct Local {
   const HostOps* hx = nullptr;
   hipEvent_t rows = nullptr;
   std::function<void()> issue_rows;
+  // the chunked report tail: the all-queries single-slice pass re-ranks in `chunks` query ranges
+  // and calls on_chunk(q0, q1) behind each (the step formats that range and starts its copy)
+  std::function<void(int64_t, int64_t)> on_chunk;
+  int chunks = 1;
   // state
   int* kk = nullptr;
   int* kd = nullptr;
@@ -591,6 +611,19 @@ struct Local {
                            cc, ch, st));
       }
       wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
+      if (on_chunk && chunks > 1 && !idx && S == 1) {
+        // query ranges of whole pair-refine workgroups (8 queries); q = qidx[p] = q0 + p
+        const int64_t span = ((nq + chunks - 1) / chunks + 7) / 8 * 8;
+        for (int64_t q0 = 0; q0 < nq; q0 += span) {
+          const int n = (int)std::min<int64_t>(span, nq - q0);
+          CKL(dmlp_refine_groups_rm(cap, ci + q0 * cap, cc + q0, ch + 2 * q0, S, X, A, Qx, xf,
+                                    hx ? hx->xrow : nullptr, xi, qh, KT, hl, N, qi + q0, kd, n,
+                                    out_d, out_i, kstride, fin ? labels : nullptr, lo, hi, lab, cs,
+                                    stat, ovf, kcls, st));
+          on_chunk(q0, q0 + n);
+        }
+        return;
+      }
       CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
                                 qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
                                 fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls, st));
@@ -1316,6 +1349,34 @@ struct Step {
       }
       // (rc != 0: data or queries outside the fp16 screen's range -> the device image path)
     }
+    // ---- the chunked report tail (report_chunks > 1, report_mode 1): the re-rank runs in query
+    // ranges; behind each range its lines are formatted at their absolute offsets (each range's
+    // base is the previous range's end, on the device) and that end crosses to the host, which
+    // then starts the range's text copy on the tail stream — the report's D2H runs under the next
+    // range's re-rank instead of after the whole re-rank
+    const int RC = std::min(g_tune.report_chunks, kMaxTail);
+    const bool tail_on = want_report && a->report_mode == 1 && RC > 1 && Q >= 1024 * (int64_t)RC;
+    char* text = want_report ? w.d_text.get((size_t)dmlp_format_bound((int)Q)) : nullptr;
+    int64_t* toff = tail_on ? w.d_off_t.get((size_t)dmlp_format_scratch((int)Q) + 4 * kMaxTail)
+                            : nullptr;
+    int64_t* tend = tail_on ? w.tail_end_h.get(kMaxTail) : nullptr;
+    int ntail = 0;
+    int64_t tsoff = 0;
+    const int64_t* tprev = nullptr;  // the last formatted range's absolute end (device)
+    auto on_chunk = [&](int64_t q0, int64_t q1) {
+      const int c = ntail;
+      if (c >= kMaxTail) throw Fail{-11};
+      const int n = (int)(q1 - q0);
+      int64_t* lo = toff + tsoff;
+      tsoff += dmlp_format_scratch(n);
+      CKL(dmlp_format_report_at(ocs + q0, n, (int)(a->qid_base + q0), lo, text, tprev, st));
+      tprev = lo + n;
+      CK(hipEventRecord(w.ev_tf[c], st));
+      CK(hipStreamWaitEvent(w.side, w.ev_tf[c], 0));
+      CK(hipMemcpyAsync(tend + c, lo + n, sizeof(int64_t), hipMemcpyDeviceToHost, w.side));
+      CK(hipEventRecord(w.ev_ts[c], w.side));
+      ntail = c + 1;
+    };
     // ---- dispatch: screens on `st`, the rows behind the first of them on the side stream
     auto run_local = [&](bool with_hx, bool rows_pending) {
       std::unique_ptr<Local> Lp(new Local(w));
@@ -1325,6 +1386,10 @@ struct Step {
       L.lab = olab; L.cs = ocs; L.exact = a->exact != 0; L.st = st;
       L.hx = with_hx ? &hx : nullptr;
       L.rows = w.ev_rows;
+      if (rows_pending && tail_on) {
+        L.on_chunk = on_chunk;
+        L.chunks = RC;
+      }
       if (rows_pending) {
         L.issue_rows = [&]() {
           // (host operands: called right after the first screen launch, so this mark completes
@@ -1401,6 +1466,7 @@ struct Step {
       CK(hipStreamSynchronize(st));
       a->early = 0;
       use_hx = false;
+      ntail = 0;  // (any ranges formatted behind the abandoned screen are rendered again whole)
       Lp = run_local(false, false);
     }
     // ---- the report behind the re-rank, then the one host sync.  The small results (report
@@ -1411,9 +1477,11 @@ struct Step {
     unsigned* dr_bad = dr ? w.dr_words.p + 72 : nullptr;  // device render: a value out of range
     auto render = [&]() {
       const int64_t* len_src = nullptr;
-      if (want_report) {
+      if (want_report && ntail > 0) {  // formatted range by range behind the re-rank
+        CK(mark(M_FORMAT, st));
+        len_src = tprev;
+      } else if (want_report) {
         int64_t* off = w.d_off.get((size_t)dmlp_format_scratch((int)Q));
-        char* text = w.d_text.get((size_t)dmlp_format_bound((int)Q));
         CKL(dmlp_format_report(ocs, (int)Q, (int)a->qid_base, off, text, st));
         CK(mark(M_FORMAT, st));
         len_src = off + Q;
@@ -1422,7 +1490,7 @@ struct Step {
                          a->early ? estats : nullptr, dr_bad, small_d);
       CK(hipGetLastError());
       CK(hipMemcpyAsync(small, small_d, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      if (want_report && a->report_mode == 1)
+      if (want_report && a->report_mode == 1 && ntail == 0)
         CK(hipMemcpyAsync(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q),
                           hipMemcpyDeviceToHost, st));
     };
@@ -1430,6 +1498,23 @@ struct Step {
                      .count();
     CK(mark(M_REFINE, st));
     render();
+    if (ntail > 0) {
+      // each range's text once its end offset has landed: [previous end, this end)
+      int64_t s0 = 0;
+      const int64_t bound = dmlp_format_bound((int)Q);
+      for (int c = 0; c < ntail; ++c) {
+        spin_wait(w.ev_ts[c]);
+        const int64_t e = tend[c];
+        if (e < s0 || e > bound) throw Fail{-11};
+        if (e > s0)
+          CK(hipMemcpyAsync(a->report_dst + s0, text + s0, (size_t)(e - s0), hipMemcpyDeviceToHost,
+                            w.tail));
+        s0 = e;
+      }
+      CK(hipEventRecord(w.ev_tail, w.tail));
+      CK(hipStreamWaitEvent(st, w.ev_tail, 0));
+      ntail = 0;  // a later render (escalation, device-render redo) formats and copies it whole
+    }
     CK(mark(M_D2H, st));
     CK(hipEventRecord(w.ev_done, st));
     spin_wait(w.ev_done);
@@ -1754,7 +1839,7 @@ extern "C" int dmlp_step_timeline(double* ms, const char** names, int cap) {
 }
 
 // Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render",
-// "qb_blocks", "word_write", "x1_ring".  Returns the previous
+// "qb_blocks", "word_write", "report_chunks", "x1_ring".  Returns the previous
 // value, or -1 for an unknown key.
 extern "C" int dmlp_pipeline_set(const char* key, int value) {
   const std::string k = key ? key : "";
@@ -1768,7 +1853,8 @@ extern "C" int dmlp_pipeline_set(const char* key, int value) {
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
            : k == "device_render" ? &g_tune.device_render
            : k == "qb_blocks" ? &g_tune.qb_blocks
-           : k == "word_write" ? &g_tune.word_write : nullptr;
+           : k == "word_write" ? &g_tune.word_write
+           : k == "report_chunks" ? &g_tune.report_chunks : nullptr;
   if (!f) return -1;
   const int old = *f;
   *f = value;

@@ -163,6 +163,47 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
         L.dmlp_pipeline_set(b"qb_blocks", old_qb)
 
 
+@pytest.mark.parametrize("chunks", [2, 3, 8])
+def test_report_chunked_tail(gpu, chunks):
+    """The chunked report tail (pipeline.hip Step::run, report_chunks): the re-rank runs in query
+    ranges, each range's lines are formatted at their absolute offsets behind it and its text is
+    copied while the next range re-ranks.  Early-start and plain steps on two alternated inputs,
+    then an input whose 120 copies of one point overflow the refine of the queries sitting on it
+    (those escalate and the whole report is rendered again): every report byte == the oracle's,
+    into a destination pre-filled with 0xAA each call (a range never copied would show)."""
+    from distributed_machine_learning_project_amd import _lib
+    import torch
+    L = _lib.lib()
+    old = L.dmlp_pipeline_set(b"report_chunks", chunks)
+    Q = 131072 + 64 * 3
+    cases = _early_inputs(2000, 32, 16, Q, seed=500 + chunks)
+    dup = dmlp.generate(2000, Q, 32, 0.0, 1000.0, 1, 16, 8, seed=600 + chunks)
+    dup.X[1:121] = dup.X[0]
+    dup.Qx[[7, Q // 2, Q - 3]] = dup.X[0]
+    d, i = K.knn_cpu(dup.X, dup.Qx, dup.k)
+    lab_d, cs_d = K.finalize_cpu(i, dup.k, dup.labels)
+    cases.append((dup, lab_d, cs_d, dmlp.format_report(cs_d)))
+    dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
+    try:
+        for rnd, (ci, early) in enumerate(((0, 1), (1, 1), (0, 0), (1, 0), (2, 1), (2, 0))):
+            L.dmlp_step_early(early)
+            inp, lab_ref, cs, expect = cases[ci]
+            dst[:] = 0xAA
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert r.report_len == len(expect), f"round {rnd}"
+            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
+            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
+            assert r.early == early
+            if ci == 2:
+                assert r.n_escalated > 0, "the duplicated point overflowed no refine"
+            else:
+                assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
+    finally:
+        L.dmlp_step_early(-1)
+        L.dmlp_pipeline_set(b"report_chunks", old)
+
+
 @pytest.mark.parametrize("sub", [16, 14, 12])
 def test_screen_lds_ring(gpu, sub):
     """The LDS-ring screen (screen_x1.hip RING > 0: 8 waves per workgroup share each fragment

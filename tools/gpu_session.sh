@@ -34,6 +34,7 @@
 #   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
+#   tail       the chunked report tail: tests, --verify, A/B DMLP_REPORT_CHUNKS 0 / 2 / 4 / 8
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -85,6 +86,13 @@ for task in "$@"; do
     qchunks)  # early start: query render slices 2 / 4 / 6 (DMLP_FAST_QCHUNKS), interleaved
       AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step qchunks_ab 900 bash tools/kernel_ab.sh \
           q2:DMLP_FAST_QCHUNKS=2 q4:DMLP_FAST_QCHUNKS=4 q6:DMLP_FAST_QCHUNKS=6 ;;
+    tail)  # the chunked report tail (DMLP_REPORT_CHUNKS): GPU tests, --verify, A/B off / 2 / 4 / 8
+      step tail_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+          --timeout-method thread -k "report_chunked or native_step"
+      DMLP_REPORT_CHUNKS=4 step tail_verify 300 python bench.py --steps 50 --warmup 2 --verify
+      AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step tail_ab 900 bash tools/kernel_ab.sh \
+          c0:DMLP_REPORT_CHUNKS=0 c2:DMLP_REPORT_CHUNKS=2 c4:DMLP_REPORT_CHUNKS=4 c8:DMLP_REPORT_CHUNKS=8
+      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/tail_ab_timeline.txt" ;;
     warm)  # the headline bench after a 3 s warm-up instead of 0.6 s (box-to-box host variance)
       step bench_warm3 300 python bench.py --min-warmup-s 3 ;;
     prof)
