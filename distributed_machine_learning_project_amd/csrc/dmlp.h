@@ -361,6 +361,14 @@ typedef struct dmlp_step_args {
   // replica completed over xGMI by an all-gather, parallel/strategies.py "xgmi"): no dataset rows
   // cross PCIe (the host still renders the screen image from X, or the plane does); null: none
   const int* X32d;
+  // (input, optional, report_mode 1 with the chunked report tail) the report handed over in
+  // pieces as their copies land, in order, while later query ranges still re-rank: sink(ctx,
+  // bytes, n) is called on this thread for report_dst[0, report_sunk) before dmlp_step returns;
+  // the caller hands over [report_sunk, report_len) itself.  A piece is handed over only once no
+  // query up to its range can still be redone (no overflow counted so far).
+  void (*report_sink)(void* ctx, const char* bytes, int64_t n);
+  void* report_sink_ctx;
+  int64_t report_sunk;        // (result) bytes already given to report_sink
 } dmlp_step_args;
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.

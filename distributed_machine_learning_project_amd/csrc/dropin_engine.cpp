@@ -502,8 +502,8 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     t1 = std::chrono::steady_clock::now();
     done = s->core->KNN_rows(&in, s->xr.data(), s->qr.data(), &out,
                              identity ? &cout_sink : nullptr, nullptr);
-    emitted = done && identity && out.text_len > 0 && out.text.size() >= out.text_len &&
-              s->core->last_step_.report_mode == 2;
+    // (streamed: in pieces behind the step, or from inside it — KNN_REPORT_TAIL)
+    emitted = done && identity && s->core->last_emit_ms > 0.0;
   }
   if (!done) {
     if (root) pack(dataset, queries, p.num_attrs, in);
@@ -561,6 +561,8 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
         << ", \"lists_mode\": " << (kListsMode ? "true" : "false")
         << ", \"rows_in_place\": " << (done ? "true" : "false")
         << ", \"node_window\": " << (win_text ? "true" : "false")
+        << ", \"report_tail\": " << s->core->report_tail_
+        << ", \"report_bytes_in_step\": " << s->core->tail_sunk_
         << ", \"step_ms\": " << s->step_ms << "}\n";
     }
   }

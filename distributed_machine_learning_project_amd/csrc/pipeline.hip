@@ -392,9 +392,10 @@ struct Ctx {
   // the chunked report tail (Step::run, report_chunks): per chunk a format-done event on `st`, its
   // end offset's copy on `side` (+ event), the text copies on their own stream
   hipStream_t tail = nullptr;
-  hipEvent_t ev_tf[kMaxTail] = {}, ev_ts[kMaxTail] = {}, ev_tail = nullptr;
+  hipEvent_t ev_tf[kMaxTail] = {}, ev_ts[kMaxTail] = {}, ev_tc[kMaxTail] = {}, ev_tail = nullptr;
   DBuf<int64_t> d_off_t;
   HBuf<int64_t> tail_end_h;
+  HBuf<int> tail_ovf_h;  // the overflow counter behind each range (report_sink: final or not)
 };
 
 Ctx& ctx() {
@@ -412,6 +413,7 @@ Ctx& ctx() {
     for (int i = 0; i < kMaxTail; ++i) {
       CK(hipEventCreateWithFlags(&w.ev_tf[i], hipEventDisableTiming));
       CK(hipEventCreateWithFlags(&w.ev_ts[i], hipEventDisableTiming));
+      CK(hipEventCreateWithFlags(&w.ev_tc[i], hipEventDisableTiming));
     }
     CK(hipEventCreateWithFlags(&w.ev_tail, hipEventDisableTiming));
   }
@@ -1040,6 +1042,7 @@ struct Step {
     w.marks_valid = false;
     w.marks_rec = 0;
     w.text_len = 0;  // dmlp_step_emit copies only what THIS call rendered
+    a->report_sunk = 0;
     if (Q < 0 || N < 0 || A < 1 || Q > (1 << 30)) return -1;
     const dmlp_plane* pl = a->plane;
     if (pl && (!pl->base || pl->rank < 0 || pl->renderers < 1 || pl->gen <= 0 ||
@@ -1360,6 +1363,7 @@ struct Step {
     int64_t* toff = tail_on ? w.d_off_t.get((size_t)dmlp_format_scratch((int)Q) + 4 * kMaxTail)
                             : nullptr;
     int64_t* tend = tail_on ? w.tail_end_h.get(kMaxTail) : nullptr;
+    int* tovf = tail_on ? w.tail_ovf_h.get(kMaxTail) : nullptr;
     int ntail = 0;
     int64_t tsoff = 0;
     const int64_t* tprev = nullptr;  // the last formatted range's absolute end (device)
@@ -1374,6 +1378,10 @@ struct Step {
       CK(hipEventRecord(w.ev_tf[c], st));
       CK(hipStreamWaitEvent(w.side, w.ev_tf[c], 0));
       CK(hipMemcpyAsync(tend + c, lo + n, sizeof(int64_t), hipMemcpyDeviceToHost, w.side));
+      // the overflow count so far (read no earlier than this range's re-rank: later ranges' and
+      // the screen's overflows only make it larger) — 0: no query up to here is redone
+      if (a->report_sink)
+        CK(hipMemcpyAsync(tovf + c, w.ovf.p, sizeof(int), hipMemcpyDeviceToHost, w.side));
       CK(hipEventRecord(w.ev_ts[c], w.side));
       ntail = c + 1;
     };
@@ -1500,8 +1508,20 @@ struct Step {
     render();
     if (ntail > 0) {
       // each range's text once its end offset has landed: [previous end, this end)
+      // With a report_sink, range c-1's bytes go to the sink (once their copy landed) while range
+      // c+1 still re-ranks, up to the first range behind which an overflow was counted (those
+      // queries are redone and the report rendered again below; the bytes before stay the same)
       int64_t s0 = 0;
       const int64_t bound = dmlp_format_bound((int)Q);
+      bool sink_ok = a->report_sink != nullptr && !dr;
+      int64_t ready = 0;  // the copied bytes the sink may take: [a->report_sunk, ready)
+      int ready_c = -1;   // the range whose copy ends at `ready`
+      auto hand_over = [&]() {
+        if (ready_c < 0 || ready <= a->report_sunk) return;
+        spin_wait(w.ev_tc[ready_c]);
+        a->report_sink(a->report_sink_ctx, a->report_dst + a->report_sunk, ready - a->report_sunk);
+        a->report_sunk = ready;
+      };
       for (int c = 0; c < ntail; ++c) {
         spin_wait(w.ev_ts[c]);
         const int64_t e = tend[c];
@@ -1509,8 +1529,16 @@ struct Step {
         if (e > s0)
           CK(hipMemcpyAsync(a->report_dst + s0, text + s0, (size_t)(e - s0), hipMemcpyDeviceToHost,
                             w.tail));
+        CK(hipEventRecord(w.ev_tc[c], w.tail));
         s0 = e;
+        sink_ok = sink_ok && tovf[c] == 0;
+        hand_over();  // the previous range, under this one's copy and the next one's re-rank
+        if (sink_ok) {
+          ready = e;
+          ready_c = c;
+        }
       }
+      hand_over();
       CK(hipEventRecord(w.ev_tail, w.tail));
       CK(hipStreamWaitEvent(st, w.ev_tail, 0));
       ntail = 0;  // a later render (escalation, device-render redo) formats and copies it whole

@@ -248,7 +248,9 @@ class StepArgs(C.Structure):
                 ("path", C.c_int),
                 ("early", C.c_int), ("n_escalated", C.c_int), ("early_waits", C.c_int),
                 ("early_grows", C.c_int), ("early_timeouts", C.c_int),
-                ("early_qwaits", C.c_int), ("host_ms", C.c_float), ("X32d", C.c_void_p)]
+                ("early_qwaits", C.c_int), ("host_ms", C.c_float), ("X32d", C.c_void_p),
+                ("report_sink", C.c_void_p), ("report_sink_ctx", C.c_void_p),
+                ("report_sunk", C.c_int64)]
 
 
 class Plane(C.Structure):
@@ -273,6 +275,10 @@ class StepResult:
     early_grows: int = 0
     early_timeouts: int = 0
     early_qwaits: int = 0
+    report_sunk: int = 0   # report bytes handed to `sink` inside the step (the chunked tail)
+
+
+_SINK_T = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int64)
 
 
 # calls the native step served and its early-start counters (bench.py reports them for the timed
@@ -292,7 +298,7 @@ def step_stats(reset: bool = False):
 
 def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_base=0,
          exact=False, report=None, lists=False, kstride=None, plane=None,
-         x32=None) -> StepResult:
+         x32=None, sink=None) -> StepResult:
     """One rank's whole Engine::KNN call from host arrays (dmlp_step): X_host [N, A] /
     Q_host [Q, A] fp64, labels_host [N] int32 (page-locked or registered memory for real
     overlap; a node-shared segment is), k_host [Q] int32.
@@ -305,6 +311,9 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
               node, slice by slice, by the plane's renderers into a node-shared segment.
       x32:    the dataset's rows already on this GPU as lossless int32 [N * A] (a torch tensor:
               the xGMI replica, parallel/strategies.py): no dataset rows cross PCIe.
+      sink:   with a report array and the chunked report tail (report_chunks > 1): sink(bytes) is
+              called inside the step with the report's leading pieces as their copies land;
+              StepResult.report_sunk counts them, the rest is only in `report`.
     Returns once everything is complete (one host sync in the common case)."""
     torch = _torch()
     L = _lib.lib()
@@ -352,7 +361,12 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     a.stream = _stream()
     a.plane = C.cast(C.pointer(plane), C.c_void_p) if plane is not None else None
     a.X32d = x32.data_ptr() if x32 is not None else None
+    cb = None
+    if sink is not None:
+        cb = _SINK_T(lambda _ctx, b, n: sink(C.string_at(b, n)))
+        a.report_sink = C.cast(cb, C.c_void_p)
     _lib.check(L.dmlp_step(C.byref(a)), "dmlp_step")
+    del cb
     st = pipeline_stats()
     STEP_STATS["calls"] += 1
     STEP_STATS["early"] += a.early
@@ -372,7 +386,7 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
         _read_timeline()
     return StepResult(lab, cs, od, oi, int(a.report_len), a.path, a.early, a.n_escalated,
                       int(st["n_exact"]), a.early_waits, a.early_grows, a.early_timeouts,
-                      a.early_qwaits)
+                      a.early_qwaits, int(a.report_sunk))
 
 
 def step_emit(dst, nbytes: int):

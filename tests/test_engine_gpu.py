@@ -170,7 +170,9 @@ def test_report_chunked_tail(gpu, chunks):
     copied while the next range re-ranks.  Early-start and plain steps on two alternated inputs,
     then an input whose 120 copies of one point overflow the refine of the queries sitting on it
     (those escalate and the whole report is rendered again): every report byte == the oracle's,
-    into a destination pre-filled with 0xAA each call (a range never copied would show)."""
+    into a destination pre-filled with 0xAA each call (a range never copied would show).  Every
+    other call passes a report_sink: it must see exactly the report's leading bytes — all of them
+    when nothing escalated, none when a query of the first range overflowed."""
     from distributed_machine_learning_project_amd import _lib
     import torch
     L = _lib.lib()
@@ -185,20 +187,28 @@ def test_report_chunked_tail(gpu, chunks):
     cases.append((dup, lab_d, cs_d, dmlp.format_report(cs_d)))
     dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
     try:
-        for rnd, (ci, early) in enumerate(((0, 1), (1, 1), (0, 0), (1, 0), (2, 1), (2, 0))):
+        for rnd, (ci, early) in enumerate(((0, 1), (1, 1), (0, 0), (1, 0), (2, 1), (2, 0), (2, 1),
+                                           (1, 0), (0, 1))):
             L.dmlp_step_early(early)
             inp, lab_ref, cs, expect = cases[ci]
             dst[:] = 0xAA
-            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            pieces = []
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst,
+                       sink=pieces.append if rnd % 2 == 0 else None)
             assert r.report_len == len(expect), f"round {rnd}"
             assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
             assert r.early == early
+            # the sink (report_sink): the report's leading bytes, in order, during the step
+            assert b"".join(pieces) == expect[:r.report_sunk], f"round {rnd}"
             if ci == 2:
                 assert r.n_escalated > 0, "the duplicated point overflowed no refine"
+                assert r.report_sunk == 0, "a range behind an overflow went to the sink"
             else:
                 assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
+                if rnd % 2 == 0:
+                    assert r.report_sunk == r.report_len and len(pieces) >= 2, f"round {rnd}"
     finally:
         L.dmlp_step_early(-1)
         L.dmlp_pipeline_set(b"report_chunks", old)

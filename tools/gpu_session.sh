@@ -35,6 +35,7 @@
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
 #   tail       the chunked report tail: tests, --verify, A/B DMLP_REPORT_CHUNKS 0 / 2 / 4 / 8
+#   sinktail   the drop-in report written from inside the step (KNN_REPORT_TAIL 0 / 2 / 4), contract A/B
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
@@ -93,6 +94,28 @@ for task in "$@"; do
       AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step tail_ab 900 bash tools/kernel_ab.sh \
           c0:DMLP_REPORT_CHUNKS=0 c2:DMLP_REPORT_CHUNKS=2 c4:DMLP_REPORT_CHUNKS=4 c8:DMLP_REPORT_CHUNKS=8
       python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/tail_ab_timeline.txt" ;;
+    sinktail)  # the one-rank drop-in's report written from inside the step (KNN_REPORT_TAIL): GPU
+               # tests, the contract at 0 / 2 / 4 interleaved, stdout bytes equal at Q = 131072
+      step sink_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
+          --timeout-method thread -k "report_chunked or native_step or dropin"
+      for R in 1 2; do
+        for T in 0 2 4; do
+          KNN_REPORT_TAIL=$T step contract_t${T}_$R 600 python bench.py --harness dropin --steps 10 \
+              --warmup 1
+        done
+      done
+      python -m distributed_machine_learning_project_amd.build --dropin \
+          distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
+      python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
+          --max 1000 --minK 16 --maxK 16 --num_labels 10 --output /tmp/dropin_bench.in > /dev/null
+      for T in 0 2 4; do
+        KNN_REPORT_TAIL=$T KNN_TRACE=1 timeout -k 10 120 /tmp/eng_dropin < /tmp/dropin_bench.in \
+            > /tmp/dropin_t$T.out 2> "$OUT/dropin_trace_t$T.txt" || exit 1
+      done
+      cmp /tmp/dropin_t0.out /tmp/dropin_t2.out && cmp /tmp/dropin_t0.out /tmp/dropin_t4.out && \
+          echo "report bytes equal at KNN_REPORT_TAIL 0 / 2 / 4" | tee "$OUT/sink_cmp.txt" || exit 1
+      grep -ho '"time_ms_median": [0-9.]*\|"knn_ms_median": [0-9.]*\|"emit_ms_median": [0-9.]*' \
+          "$OUT"/contract_t*.log | tee "$OUT/contract_medians.txt" ;;
     warm)  # the headline bench after a 3 s warm-up instead of 0.6 s (box-to-box host variance)
       step bench_warm3 300 python bench.py --min-warmup-s 3 ;;
     prof)
