@@ -327,7 +327,7 @@ def _dropin_run(exe, path, np_, env_extra=None):
     return r.stdout, r.stderr.decode()
 
 
-@pytest.mark.parametrize("np_", [2, 3, 4])
+@pytest.mark.parametrize("np_", [2, 3, 4, 8])
 def test_dropin_node_window_gpu(dropin_exe, case, case_x1, case_dec9, np_):
     """The reference's own common.cpp + the drop-in at P > 1 (run_bench.sh config 4's
     `mpirun ./engine < input`): the node window joined in the MPI_Init hook, rank 0's labels / k /
@@ -335,7 +335,8 @@ def test_dropin_node_window_gpu(dropin_exe, case, case_x1, case_dec9, np_):
     harness's vectors, EVERY rank's native step on its own block ([dmlp-step] rank r), report
     lines through the window.  Inputs: k 1-40 (two screen classes), k 1-32 with an out-of-range
     point (the device-image path), 9-decimal data (fp64 rows through the plane); the 8 MiB
-    window grows on first use.  stdout == the fp64 oracle's bytes."""
+    window grows on first use; P = 8 is the target node's world size (eight ranks on the one
+    GPU here).  stdout == the fp64 oracle's bytes."""
     (p1, e1), (p2, e2) = case_x1
     for path, expect in (case, (p1, e1), (p2, e2), case_dec9):
         out, err = _dropin_run(dropin_exe, path, np_)
