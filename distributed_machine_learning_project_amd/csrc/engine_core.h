@@ -270,18 +270,26 @@ class KnnCore {
       // the chunked report tail (pipeline.hip): the re-rank in report_tail_ query ranges, each
       // range's text copied behind it and handed to the sink while later ranges still re-rank;
       // the step returns what it could not hand over yet (a range behind an overflow, or none)
-      (void)dmlp_pipeline_set("report_chunks", report_tail_);
       struct Fwd {
         Sink sink;
         void* ctx;
       } fwd{sink, sink_ctx};
-      const dmlp_step_args a = step_host(
-          nullptr, Xr, in->labels.data(), nullptr, Qr, in->k.data(), Q_, 0, 1, out, nullptr,
-          [](void* c, const char* b, int64_t n) {
-            Fwd* f = (Fwd*)c;
-            f->sink(f->ctx, b, (size_t)n);
-          },
-          &fwd);
+      // (the library's tuning is process-wide: this call's value, then the previous one again)
+      const int prev = dmlp_pipeline_set("report_chunks", report_tail_);
+      dmlp_step_args a;
+      try {
+        a = step_host(nullptr, Xr, in->labels.data(), nullptr, Qr, in->k.data(), Q_, 0, 1, out,
+                      nullptr,
+                      [](void* c, const char* b, int64_t n) {
+                        Fwd* f = (Fwd*)c;
+                        f->sink(f->ctx, b, (size_t)n);
+                      },
+                      &fwd);
+      } catch (...) {
+        (void)dmlp_pipeline_set("report_chunks", prev);
+        throw;
+      }
+      (void)dmlp_pipeline_set("report_chunks", prev);
       trace.mark("report");
       const auto e1 = std::chrono::steady_clock::now();
       out->text_len = (size_t)std::max<int64_t>(a.report_len, 0);
