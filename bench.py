@@ -251,7 +251,11 @@ def main(argv=None):
     if a.diag_steps > 0:
         extra.update(_diagnostics(comm, eng, step, a.diag_steps, my_ms, steps_native))
     if world > 1 and comm.backend == "nccl" and not a.no_busbw:
-        extra["allreduce_busbw_GBps"] = round(_allreduce_busbw(comm), 1)
+        # a diagnostic beside the headline: a failure records itself instead of losing the line
+        try:
+            extra["allreduce_busbw_GBps"] = round(_allreduce_busbw(comm), 1)
+        except Exception as e:  # noqa: BLE001
+            extra["allreduce_busbw_GBps"] = {"error": f"{type(e).__name__}: {e}"[-300:]}
     if a.verify and comm.is_root:
         import hashlib
         from distributed_machine_learning_project_amd.ops import knn as K

@@ -83,10 +83,12 @@ class Engine:
                 K.step(w.X, w.labels, (0, 3), w.Qx, k, report="device")
             K.step_stats(reset=True)
             self.comm.sync()
-            if self.comm.world > 1 and self.strategy == "farm":
-                # how the replicated dataset reaches every GPU: measured, not assumed
-                from .strategies import probe_replication
-                self.comm.replication = probe_replication(self.comm)
+        if self.comm.world > 1 and self.strategy == "farm" and (
+                self.comm.on_gpu or os.environ.get("DMLP_PROBE_FAIL")):
+            # how the replicated dataset reaches every GPU: measured, not assumed — and a probe
+            # that fails on any rank only costs its own record ({"error": ...}, mode "h2d")
+            from .strategies import probe_replication_safe
+            self.comm.replication = probe_replication_safe(self.comm)
         self.comm.barrier()
 
     # ------------------------------------------------------------------ API

@@ -24,6 +24,8 @@ results (exact fp64 distances, (dist asc, id desc) order, vote tie -> larger lab
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from .comm import block_partition, dims_create
@@ -398,6 +400,33 @@ def probe_replication(comm, nbytes=32 << 20, iters=3):
     # N x A (replication_mode)
     out["mode"] = replication_mode(out, 100_000 * 32 * 4)
     return out
+
+
+def probe_replication_safe(comm):
+    """probe_replication that cannot take the run down with it (the first real 8-GPU run has no
+    second chance): a failure on any rank — DMLP_PROBE_FAIL=<rank>|all injects one before the
+    probe's first collective — is agreed on by one MAX all-reduce, and every rank then records
+    {"error": ..., "mode": "h2d"} (the replication that needs no collective).  A failure inside
+    the probe's collectives is bounded by the process group's timeout (KNN_TIMEOUT_S)."""
+    torch = _torch()
+    from . import dist_api as dist
+    err = None
+    inj = os.environ.get("DMLP_PROBE_FAIL", "")
+    try:
+        if inj and (inj == "all" or str(comm.rank) in inj.split(",")):
+            raise RuntimeError(f"injected probe failure on rank {comm.rank} (DMLP_PROBE_FAIL)")
+        if not comm.on_gpu:
+            raise RuntimeError("replication probe needs GPUs")
+    except Exception as e:  # noqa: BLE001 — recorded, never fatal
+        err = f"{type(e).__name__}: {e}"
+    flag = torch.tensor([1 if err else 0], dtype=torch.int32, device=comm.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag.item()):
+        return {"error": err or "probe failed on another rank", "mode": "h2d", "world": comm.world}
+    try:
+        return probe_replication(comm)
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"[-300:], "mode": "h2d", "world": comm.world}
 
 
 def _step_egress(comm, inp, r, qid_base):

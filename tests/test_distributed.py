@@ -273,6 +273,23 @@ def test_bench_launches_its_ranks(ingress):
     assert isinstance(res["warmup_curve_ms"], list)
 
 
+@pytest.mark.parametrize("inject", ["1", "all"])
+def test_bench_survives_replication_probe_failure(inject):
+    """the replication probe run at Engine construction (P > 1) must not cost
+    the headline line when it fails — on one rank before its first collective, or on every rank —
+    at np 3: every rank agrees on the failure, takes the "h2d" replication, and rank 0's JSON
+    carries the probe's error beside a valid, verified headline."""
+    import json
+    r = _bench(["--gpus", "3", "--steps", "2", "--warmup", "1", "--min-warmup-s", "0",
+                "--n-data", "1500", "--q-per-gpu", "200", "--verify", "--diag-steps", "0"],
+               {"DMLP_DATA_PLANE": "host", "DMLP_PROBE_FAIL": inject})
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert res["n_gpus"] == 3 and res["verify_ok"] and res["value"] > 0
+    assert "error" in res["replication_probe"] and res["replication_probe"]["mode"] == "h2d"
+    assert res["replication_mode"] == "h2d"
+
+
 def test_collective_log_compare():
     """The collective-sequence comparison (parallel/dist_api.py compare_logs) flags a rank that
     enters a different collective, a different size, a missing call and an unmatched send."""

@@ -296,6 +296,26 @@ for task in "$@"; do
         done
       done
       python3 tools/pmc_summary.py "$OUT" > "$OUT/ringpmc_summary.txt"; cat "$OUT/ringpmc_summary.txt" ;;
+    blits)  # which copies / memsets the runtime runs as kernels (tests/native/copy_kind_probe.cpp,
+            # built to tools/bin), then every runtime kernel and SDMA copy of 4 bench steps
+      step copykind 120 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/ck" -o run \
+          --output-format csv -- tools/bin/copy_kind_probe
+      python3 tools/copy_kind.py probe "$OUT/ck" > "$OUT/copy_kind.txt"; cat "$OUT/copy_kind.txt"
+      step blits 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/bl" -o run \
+          --output-format csv -- tools/bin/step_driver --steps 6 --warmup 30 --timeline
+      python3 tools/copy_kind.py step "$OUT/bl" > "$OUT/step_copies.txt"; tail -80 "$OUT/step_copies.txt" ;;
+    lnr)  # large-N steps (native step driver): host render vs device render (DMLP_DEVICE_RENDER) at
+          # the verdict's shapes, alternating, with the step timeline and host issue per step
+      for SH in "1000000 32 10" "1000000 128 6" "10000000 32 4"; do
+        set -- $SH
+        for R in 1 2; do
+          for DR in 0 1; do
+            DMLP_DEVICE_RENDER=$DR step lnr_n$1_a$2_dr${DR}_$R 300 tools/bin/step_driver --n $1 \
+                --a $2 --q 16384 --steps $3 --warmup 2 --timeline
+          done
+        done
+      done
+      grep -h '^{' "$OUT"/lnr_*.log | tee "$OUT/lnr_summary.txt" ;;
     final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
             # default and the exact path, the P = 3 host-plane rehearsal with --verify
       step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
