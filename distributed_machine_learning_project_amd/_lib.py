@@ -69,7 +69,9 @@ _SIGS = {
     "dmlp_screen_x1": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp, i32,
                              vp, vp, vp, vp]),
     "dmlp_screen_x1_early": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp,
-                                   i32, i32, vp, vp, vp, vp, vp, vp]),
+                                   i32, i32, vp, vp, vp, vp, vp]),
+    "dmlp_screen_x1_part": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp,
+                                  i32, i32, i32, vp, vp, vp, vp]),
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),
     "dmlp_refine_groups2": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, i32, vp]),
     "dmlp_x1_seed": (i32, [vp, vp, i32, i32, vp, vp]),
@@ -84,12 +86,6 @@ _SIGS = {
     "dmlp_pipeline_set": (i32, [C.c_char_p, i32]),
     "dmlp_pipeline_stats": (None, [vp]),
     "dmlp_screen_x1_collect": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
-    "dmlp_set_x1_mode": (None, [i32]),
-    "dmlp_set_x1_ct": (None, [i32]),
-    "dmlp_set_x1_ring": (None, [i32]),
-    "dmlp_get_x1_ring": (i32, []),
-    "dmlp_x1_ring_launches": (C.c_int64, []),
-    "dmlp_x1_debug_counters": (i32, [vp, i32]),
     "dmlp_screen": (i32, [i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp, f32, i32, vp,
                           vp, vp]),
     "dmlp_screen_hl": (i32, [i32, i32, i32, i32, vp, vp, i64, vp, vp, vp, vp, vp, i32, vp, vp,
@@ -122,6 +118,7 @@ _SIGS = {
     "dmlp_cpu_merge": (i32, [vp, vp, i32, i64, i32, vp, i64, vp, vp, i32]),
     "dmlp_kdtree_knn": (i32, [vp, i64, i32, vp, i64, vp, i32, vp, vp]),
     "dmlp_cpu_format_report": (i64, [vp, i64, i64, vp]),
+    "dmlp_cpu_write_input": (i32, [C.c_char_p, vp, vp, i64, vp, vp, i64, i32]),
     "dmlp_cpu_i32_range": (None, [vp, i64, i32p, i32p]),
     "dmlp_host_i32_range": (None, [vp, i64, i32p, i32p]),
     "dmlp_atomic_fetch_add_i64": (i64, [vp, i64]),

@@ -20,6 +20,7 @@
 #include <numeric>
 #include <thread>
 #include <unordered_map>
+#include <string>
 #include <vector>
 
 namespace {
@@ -426,3 +427,60 @@ extern "C" int64_t dmlp_atomic_fetch_add_i64(int64_t* p, int64_t v) {
   return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST);
 }
 extern "C" void dmlp_atomic_store_i64(int64_t* p, int64_t v) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }
+
+// The input file of the reference's format (generate_input.py:6-23: "<N> <Q> <A>", then
+// "<label> <a_0> ... <a_{A-1}>" per point and "Q <k> <a_0> ..." per query, attributes "%.6f") for
+// arrays in memory — bench.py's reference-contract runs write hundreds of MB of it, formatted on
+// the render pool in row ranges and written in order.  0, or -1 when the file cannot be written.
+extern "C" int dmlp_cpu_write_input(const char* path, const int* labels, const double* X,
+                                    int64_t N, const int* k, const double* Qx, int64_t Q, int A) {
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  std::fprintf(f, "%lld %lld %d\n", (long long)N, (long long)Q, A);
+  const int64_t rows = N + Q, block = 1 << 14;
+  int rc = 0;
+  std::vector<std::string> part;
+  for (int64_t b0 = 0; b0 < rows && rc == 0; b0 += block * 64) {
+    const int64_t b1 = std::min(rows, b0 + block * 64);
+    const int64_t nb = (b1 - b0 + block - 1) / block;
+    part.assign(nb, std::string());
+    struct Job {
+      std::vector<std::string>* part;
+      int64_t b0, b1, block, N;
+      int A;
+      const int *labels, *k;
+      const double *X, *Qx;
+    } j{&part, b0, b1, block, N, A, labels, k, X, Qx};
+    dmlp_host_pool_run([](void* c, int t, int nt) {
+      Job& J = *(Job*)c;
+      char buf[64];
+      for (int64_t p = t; p < (int64_t)J.part->size(); p += nt) {
+        std::string& s = (*J.part)[p];
+        s.reserve((size_t)J.block * (J.A * 12 + 16));
+        const int64_t r0 = J.b0 + p * J.block, r1 = std::min(J.b1, r0 + J.block);
+        for (int64_t r = r0; r < r1; ++r) {
+          const bool q = r >= J.N;
+          const double* row = q ? J.Qx + (r - J.N) * J.A : J.X + r * J.A;
+          int n = q ? std::snprintf(buf, sizeof buf, "Q %d", J.k[r - J.N])
+                    : std::snprintf(buf, sizeof buf, "%d", J.labels[r]);
+          s.append(buf, (size_t)n);
+          for (int a = 0; a < J.A; ++a) {
+            n = std::snprintf(buf, sizeof buf, " %.6f", row[a]);
+            if (n >= (int)sizeof buf) {  // (a huge value: its own buffer)
+              std::vector<char> big((size_t)n + 1);
+              std::snprintf(big.data(), big.size(), " %.6f", row[a]);
+              s.append(big.data(), (size_t)n);
+            } else {
+              s.append(buf, (size_t)n);
+            }
+          }
+          s.push_back('\n');
+        }
+      }
+    }, &j);
+    for (const std::string& s : part)
+      if (std::fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
+  }
+  if (std::fclose(f) != 0) rc = -1;
+  return rc;
+}

@@ -164,12 +164,6 @@ int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cols(int KT, int kmax);
 int dmlp_screen_x1_cap(int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
-// the LDS-ring screen (k <= 16, A <= 32, >= one 512-query workgroup per CU): 0 off, or its
-// sub-buffer depth 16 / 14 / 12 (DMLP_X1_RING); launches counts the ring kernels run so far
-void dmlp_set_x1_ring(int sub);
-int dmlp_get_x1_ring(void);
-int64_t dmlp_x1_ring_launches(void);
-int dmlp_set_x1_ring_force(int on);  // the ring on any grid size (tests); returns the previous
 int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax);  // A > 64: one wave per SIMD
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);
 void dmlp_screen_x1_bound(int A, float* r1, float* r2);
@@ -185,10 +179,12 @@ int dmlp_screen_x1(int KT, int hl, int A, const void* xfrag, const float* xinit,
                    const int* qk, int nq, int kmax, const unsigned* xnmax_bits,
                    const unsigned* bad, int S, int* cand_ids, int* cand_cnt, float* cand_h,
                    void* stream);
-void dmlp_set_x1_mode(int mode);
-
-void dmlp_set_x1_ct(int ct);
-int dmlp_x1_debug_counters(unsigned long long* out, int reset);
+// ... slices [s_first, s_first + S_l) of it only (the candidate lists laid out for all S)
+int dmlp_screen_x1_part(int KT, int hl, int A, const void* xfrag, const float* xinit,
+                        int64_t n_tiles, int64_t n_points, const void* qhi, const float* qn,
+                        const int* qidx, const int* qk, int nq, int kmax,
+                        const unsigned* xnmax_bits, const unsigned* bad, int S, int s_first,
+                        int S_l, int* cand_ids, int* cand_cnt, float* cand_h, void* stream);
 // Profiling / tuning switches (process-wide): ablation mode, 4-row group appends on/off,
 // sub-buffer depth (8 / 16, 0 = automatic).
 void dmlp_set_stream_mode(int mode);
@@ -247,25 +243,17 @@ int dmlp_screen_x1_collect(int KT, int A, const void* xfrag, const float* xinit,
                            const float* hseed, int ccap, int S, int* cand_ids, int* cand_cnt,
                            float* cand_h, void* stream);
 // The single-term screen (fp16 host image, S = 1) started while the image is still crossing
-// PCIe: rdy[i] != 0 once tiles [i rdy_tiles, (i + 1) rdy_tiles) and their max norm xnm_sl[i]
-// landed; the screen waits per slice (bounded by DMLP_EARLY_TIMEOUT_MS of wall clock, default 50:
-// a timed-out wave reports its queries overflowed) and grows each column's eps with the slices
-// it has seen.  estats (nullable, device, zeroed by the caller): [0] waits that had to spin,
-// [1] eps growths, [2] timeouts, summed over the waves.
+// PCIe: rdy[i] != 0 once tiles [i rdy_tiles, (i + 1) rdy_tiles) landed, its value the slice's max
+// norm (fp32 bits; a norm of 0 is published as 1); the screen waits per slice (bounded by
+// DMLP_EARLY_TIMEOUT_MS of wall clock, default 50: a timed-out wave reports its queries
+// overflowed) and grows each column's eps with the slices it has seen.  estats (nullable,
+// device, zeroed by the caller): [0] waits that had to spin, [1] eps growths, [2] timeouts,
+// summed over the waves.
 int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
                          int64_t n_points, const void* qhi, const float* qn, const int* qidx,
                          const int* qk, int nq, int kmax, const unsigned* bad, const unsigned* rdy,
-                         int rdy_tiles, int rdy_n, const unsigned* xnm_sl, int* cand_ids,
-                         int* cand_cnt, float* cand_h, unsigned* estats, void* stream);
-// ... and the query operands in flight too (query-block early start): qrdy[b] != 0 once queries
-// [b qrdy_q, (b + 1) qrdy_q) landed (qrdy_q a multiple of 128; the list qidx must be the identity);
-// each wave waits for its own block only, counted into estats[3].
-int dmlp_screen_x1_early2(int KT, int A, const void* xfrag, const float* xinit, int64_t n_tiles,
-                          int64_t n_points, const void* qhi, const float* qn, const int* qidx,
-                          const int* qk, int nq, int kmax, const unsigned* bad,
-                          const unsigned* rdy, int rdy_tiles, int rdy_n, const unsigned* xnm_sl,
-                          int* cand_ids, int* cand_cnt, float* cand_h, unsigned* estats,
-                          const unsigned* qrdy, int qrdy_q, void* stream);
+                         int rdy_tiles, int rdy_n, int* cand_ids, int* cand_cnt, float* cand_h,
+                         unsigned* estats, void* stream);
 
 // ---------------------------------------------------------------- node render plane (plane.cpp)
 // P ranks of a node stepping against ONE dataset render it once: slice i of the dataset (image
@@ -354,21 +342,12 @@ typedef struct dmlp_step_args {
   int early;                  // 1: the screen started before the dataset image landed
   int n_escalated;            // queries redone after a screen overflow
   int early_waits, early_grows, early_timeouts;
-  int early_qwaits;           // screen waves that waited for their query block (query-block start)
   float host_ms;              // host time from entry until every copy / kernel of the call was
                               // issued (the render / pack work and the plane's waits)
   // (input) the dataset's rows already on THIS device as lossless int32 [N][A] (x = m / 1e6: the
   // replica completed over xGMI by an all-gather, parallel/strategies.py "xgmi"): no dataset rows
   // cross PCIe (the host still renders the screen image from X, or the plane does); null: none
   const int* X32d;
-  // (input, optional, report_mode 1 with the chunked report tail) the report handed over in
-  // pieces as their copies land, in order, while later query ranges still re-rank: sink(ctx,
-  // bytes, n) is called on this thread for report_dst[0, report_sunk) before dmlp_step returns;
-  // the caller hands over [report_sunk, report_len) itself.  A piece is handed over only once no
-  // query up to its range can still be redone (no overflow counted so far).
-  void (*report_sink)(void* ctx, const char* bytes, int64_t n);
-  void* report_sink_ctx;
-  int64_t report_sunk;        // (result) bytes already given to report_sink
 } dmlp_step_args;
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
@@ -383,7 +362,7 @@ void dmlp_step_early_delay(int us);    // host sleep before each image slice (< 
 int dmlp_step_events(int on);          // hipEvent step timeline on / off
 int dmlp_step_timeline(double* ms, const char** names, int cap);
 // Tuning / A-B switches of the pipeline ("num_cus", "screen", "x1k", "host_ops",
-// "device_render", "qb_blocks"; pipeline.hip
+// "device_render"; pipeline.hip
 // Tuning): returns the previous value (-1: unknown key).  What the last call did (7 slots): [0]
 // exact-path queries, [1] escalated queries, [2] path, [3] early start, [4] exact-path queries on
 // the fp64 MFMA screen, [5] of those handed to the fused VALU kernel (overflow), [6] the fp16
@@ -477,6 +456,11 @@ int64_t dmlp_parse_body(const char* buf, int64_t len, int64_t body_off, int64_t 
 // Page-lock / unlock an existing host range (node-shared input segments).  0 or a hipError_t.
 int dmlp_host_register(void* p, int64_t bytes);
 int dmlp_host_unregister(void* p);
+
+// The reference's input file (generate_input.py's format, "%.6f" attributes) from arrays,
+// formatted on the render pool.  0 or -1.
+int dmlp_cpu_write_input(const char* path, const int* labels, const double* X, int64_t N,
+                         const int* k, const double* Qx, int64_t Q, int A);
 
 const char* dmlp_version(void);
 int dmlp_device_count(void);

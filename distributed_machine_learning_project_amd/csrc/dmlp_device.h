@@ -13,6 +13,16 @@ typedef __attribute__((ext_vector_type(2))) int i32x2;
 
 namespace dmlp {
 
+// Host <-> device copy through the SDMA engines whatever its size.  This runtime runs a
+// hipMemcpyAsync below ~32 KiB (and every device-to-device copy) as a blit KERNEL
+// (__amd_rocclr_copyBuffer): a wave slot beside the step's spinning screen and an engine switch
+// in the stream.  The "no compute units" kind takes the DMA path for page-locked host memory as
+// well (profiles/r10a_copy_kind.txt: a 4-byte H2D / D2H as one SDMA copy).  Both host pointers
+// must be page-locked (hipHostMalloc / hipHostRegister) or device memory.
+inline hipError_t dma_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDeviceNoCU, s);
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 // Compiler + wave-level ordering point for LDS traffic of one wave (ds ops of a wave execute

@@ -182,11 +182,6 @@ class KnnCore {
   HostBuf<char> wake_h_;
   static constexpr int kMaxChunks = 16;
   double last_emit_ms = 0.0;  // the last KNN_rows' streamed report (0: none streamed)
-  // KNN_REPORT_TAIL=n > 1: the one-rank drop-in streams its report from inside the step (the
-  // re-rank in n query ranges, each range written while the next ones re-rank) instead of in
-  // KNN_EMIT_CHUNKS pieces after it; tail_sunk_: the bytes the last such call wrote in the step
-  int report_tail_ = getenv("KNN_REPORT_TAIL") ? std::atoi(getenv("KNN_REPORT_TAIL")) : 0;
-  int64_t tail_sunk_ = 0;
 
   hipEvent_t emit_ev_[kMaxChunks] = {};
   // the device text of the last step -> out->text in `chunks` copies; sink gets each piece once
@@ -266,42 +261,6 @@ class KnnCore {
       kmax_ = Q_ ? std::max(1, *std::max_element(in->k.begin(), in->k.end())) : 1;
     }
     const int chunks = getenv("KNN_EMIT_CHUNKS") ? std::atoi(getenv("KNN_EMIT_CHUNKS")) : 4;
-    if (sink && !debug_ && report_tail_ > 1 && rt_.gpu) {
-      // the chunked report tail (pipeline.hip): the re-rank in report_tail_ query ranges, each
-      // range's text copied behind it and handed to the sink while later ranges still re-rank;
-      // the step returns what it could not hand over yet (a range behind an overflow, or none)
-      struct Fwd {
-        Sink sink;
-        void* ctx;
-      } fwd{sink, sink_ctx};
-      // (the library's tuning is process-wide: this call's value, then the previous one again)
-      const int prev = dmlp_pipeline_set("report_chunks", report_tail_);
-      dmlp_step_args a;
-      try {
-        a = step_host(nullptr, Xr, in->labels.data(), nullptr, Qr, in->k.data(), Q_, 0, 1, out,
-                      nullptr,
-                      [](void* c, const char* b, int64_t n) {
-                        Fwd* f = (Fwd*)c;
-                        f->sink(f->ctx, b, (size_t)n);
-                      },
-                      &fwd);
-      } catch (...) {
-        (void)dmlp_pipeline_set("report_chunks", prev);
-        throw;
-      }
-      (void)dmlp_pipeline_set("report_chunks", prev);
-      trace.mark("report");
-      const auto e1 = std::chrono::steady_clock::now();
-      out->text_len = (size_t)std::max<int64_t>(a.report_len, 0);
-      if (a.report_len > a.report_sunk)
-        sink(sink_ctx, out->text.data() + a.report_sunk, (size_t)(a.report_len - a.report_sunk));
-      // (the emit time: the rest's write; the sunk pieces' writes overlap the step's re-rank)
-      last_emit_ms = std::max(1e-3, std::chrono::duration<double, std::milli>(
-                                        std::chrono::steady_clock::now() - e1).count());
-      tail_sunk_ = a.report_sunk;
-      trace.mark("emit_tail");
-      return true;
-    }
     if (sink && !debug_ && chunks > 1 && rt_.gpu) {
       const dmlp_step_args a = step_host(nullptr, Xr, in->labels.data(), nullptr, Qr,
                                          in->k.data(), Q_, 0, 2, out);
@@ -661,13 +620,9 @@ class KnnCore {
   dmlp_step_args step_host(const double* X, const double* const* Xr, const int* labels,
                            const double* Qx, const double* const* Qr, const int* k, int64_t nq,
                            int64_t qid_base, int report_mode, Output* out,
-                           const dmlp_plane* plane = nullptr,
-                           void (*report_sink)(void*, const char*, int64_t) = nullptr,
-                           void* report_sink_ctx = nullptr) {
+                           const dmlp_plane* plane = nullptr) {
     dmlp_step_args a{};
     a.plane = plane;
-    a.report_sink = report_sink;
-    a.report_sink_ctx = report_sink_ctx;
     a.X = X; a.Xr = Xr; a.N = N_; a.A = A_;
     a.labels = labels; a.label_lo = lo_; a.label_hi = hi_;
     a.Qx = Qx; a.Qr = Qr; a.k = k; a.Q = nq;
@@ -700,9 +655,8 @@ class KnnCore {
       int64_t st[8];
       dmlp_pipeline_stats(st);
       std::fprintf(stderr, "[dmlp-step] rank %d path %d early %d escalated %d exact %lld "
-                   "early_waits %d early_timeouts %d early_qwaits %d\n", rt_.rank, a.path,
-                   a.early, a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts,
-                   a.early_qwaits);
+                   "early_waits %d early_timeouts %d\n", rt_.rank, a.path, a.early,
+                   a.n_escalated, (long long)st[0], a.early_waits, a.early_timeouts);
       // KNN_TRACE: the step's own hipEvent timeline (ms from step entry)
       double ms[16];
       const char* nm[16];

@@ -53,6 +53,7 @@
 #include <vector>
 
 #include "dmlp.h"
+#include "dmlp_device.h"
 
 namespace {
 
@@ -202,17 +203,6 @@ bool dr_early_ok(int, int) { return false; }
 // KT 2 k > 16 350, KT 4 322 / 415 — but KT 2 k <= 16 takes 2 x 241 (16 free after the allocation
 // granule: every wave timed out, profiles/r9h) and KT 8 up to all 512.
 bool early_room(int KT, int kmax) { return KT == 1 || (KT == 2 && kmax > 16) || KT == 4; }
-// Query-block early start: the query operands cross in DMLP_QB_BLOCKS blocks after the first
-// DMLP_QB_LEAD dataset image slices, each block with a ready word, and every screen wave waits
-// only for its own block.  Off by default: with the host render, 16 blocks measured 2.63-2.69 vs
-// 2.17-2.19 ms/step (profiles/r9d_qb_ab.txt: each block's small copies and ready word are blit
-// kernels queued behind the spinning screen; the operands landed at 0.93 instead of 0.35 ms)
-constexpr int kMaxQBlocks = 64;
-int qb_blocks();  // (Tuning::qb_blocks below)
-int qb_lead() {
-  static const int v = std::max(0, env_int("DMLP_QB_LEAD", 1));
-  return v;
-}
 // test knob: the host sleeps this long before each dataset image slice of an early-start call,
 // so the screen provably waits mid-scan (tests/test_engine_gpu.py)
 int g_early_delay_us = -1;
@@ -247,9 +237,6 @@ struct Tuning {
   int x1k = 1;
   int host_ops = 1;
   int device_render = 0;  // DMLP_DEVICE_RENDER=1: r9r measured it slower (profiles/r9r_device_render_ab.txt)
-  int qb_blocks = 0;
-  int word_write = 0;
-  int report_chunks = 0;  // DMLP_REPORT_CHUNKS: the report's tail in query chunks (Step::run)
 };
 Tuning make_tuning() {
   Tuning t;
@@ -262,24 +249,37 @@ Tuning make_tuning() {
   // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
   // 3.74: profiles/r7h_host_budget.md)
   t.device_render = env_int("DMLP_DEVICE_RENDER", 0) != 0 ? 1 : 0;
-  t.qb_blocks = env_int("DMLP_QB_BLOCKS", 0);
-  t.word_write = env_int("DMLP_WORD_WRITE", 0);
-  t.report_chunks = env_int("DMLP_REPORT_CHUNKS", 0);
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
 }
 Tuning g_tune = make_tuning();
 bool dr_on() { return g_tune.device_render != 0; }
-// An early-start ready word (or a slice's norm word) set on the side stream behind the copies
-// it guards: a 4-byte copy from page-locked memory (which this runtime runs as a blit kernel that
-// needs a wave slot beside the spinning screen), or DMLP_WORD_WRITE=1 a stream write-value
-// packet (no kernel).
-hipError_t put_word(unsigned* dst, unsigned v, const unsigned* host_src, hipStream_t s) {
-  if (g_tune.word_write) return hipStreamWriteValue32(s, dst, v, 0);
-  return hipMemcpyAsync(dst, host_src, sizeof(unsigned), hipMemcpyHostToDevice, s);
+// Every small host <-> device copy of the step goes through the SDMA engines (dmlp::dma_copy: a
+// copy below ~32 KiB would otherwise be a blit kernel, a memset a fill kernel) — its words are
+// cleared by a DMA copy from this page-locked block of zeros.
+constexpr int kZeroBytes = 4096;
+const void* zero_block() {
+  static void* z = [] {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, kZeroBytes, hipHostMallocDefault) != hipSuccess) return (void*)nullptr;
+    std::memset(p, 0, kZeroBytes);
+    return p;
+  }();
+  return z;
 }
-int qb_blocks() { return std::min(kMaxQBlocks, std::max(0, g_tune.qb_blocks)); }
+hipError_t dma_zero(void* dst, size_t bytes, hipStream_t s) {
+  const void* z = zero_block();
+  if (!z || bytes > (size_t)kZeroBytes) return hipMemsetAsync(dst, 0, bytes, s);
+  return dmlp::dma_copy(dst, z, bytes, s);
+}
+// an early-start slice's ready word: its max norm's fp32 bits, never 0 (0 = not landed): a
+// norm of 0 is published as the smallest denormal (a valid upper bound)
+unsigned ready_bits(float nm) {
+  unsigned b = 0;
+  std::memcpy(&b, &nm, 4);
+  return b ? b : 1u;
+}
 // what the last call did (dmlp_pipeline_stats)
 struct Stats {
   int64_t n_exact = 0, n_escalated = 0, path = 0, early = 0;
@@ -342,8 +342,6 @@ const char* const kMarkNames[M_N] = {"enter", "operands_landed", "data_landed", 
                                      "screen_done", "knn_done", "format_done",
                                      "report_d2h_done"};
 
-constexpr int kMaxTail = 8;  // report tail chunks at most
-
 struct Ctx {
   int dev = -1;
   hipStream_t side = nullptr;  // host->device copies of dmlp_step
@@ -380,8 +378,7 @@ struct Ctx {
   DBuf<unsigned> dr_words;  // device render: [0, 8) slice done counters, [8, 72) query-block
                             // done counters, [72] out-of-range flag
   DBuf<float> dx_in, dq_n;
-  DBuf<unsigned> dwords;  // [0] xnmax, [1] bad, [2, 2+S) ready words, [2+S, 2+2S) slice norms,
-                          // [2+2S, 2+2S+4) early-start stats
+  DBuf<unsigned> dwords;  // the step's words (kW_*): cleared by one DMA copy per call
   DBuf<int> d_i32, d_lab, d_lb;
   DBuf<double> d_X, d_Q, d_od;
   DBuf<int> d_oi;
@@ -389,14 +386,13 @@ struct Ctx {
   DBuf<int64_t> d_off;
   DBuf<char> d_text;
   int64_t text_len = 0;  // the last dmlp_step's report bytes on the device (dmlp_step_emit)
-  // the chunked report tail (Step::run, report_chunks): per chunk a format-done event on `st`, its
-  // end offset's copy on `side` (+ event), the text copies on their own stream
-  hipStream_t tail = nullptr;
-  hipEvent_t ev_tf[kMaxTail] = {}, ev_ts[kMaxTail] = {}, ev_tc[kMaxTail] = {}, ev_tail = nullptr;
-  DBuf<int64_t> d_off_t;
-  HBuf<int64_t> tail_end_h;
-  HBuf<int> tail_ovf_h;  // the overflow counter behind each range (report_sink: final or not)
 };
+
+// dmlp_step's device words (Ctx::dwords): [kW_XNMAX] the image's max norm, [kW_BAD] out of range,
+// [kW_RDY, + kEarlySlices) the early start's ready words (norm bits), [kW_EST, + 4) early-start
+// counters, [kW_OVF] the overflow counter.  All zeroed per call (one DMA copy).
+constexpr int kW_XNMAX = 0, kW_BAD = 1, kW_RDY = 2, kW_EST = kW_RDY + kEarlySlices,
+              kW_OVF = kW_EST + 4, kW_N = kW_OVF + 1;
 
 Ctx& ctx() {
   static Ctx c[16];
@@ -409,13 +405,6 @@ Ctx& ctx() {
     CK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
-    CK(hipStreamCreateWithFlags(&w.tail, hipStreamNonBlocking));
-    for (int i = 0; i < kMaxTail; ++i) {
-      CK(hipEventCreateWithFlags(&w.ev_tf[i], hipEventDisableTiming));
-      CK(hipEventCreateWithFlags(&w.ev_ts[i], hipEventDisableTiming));
-      CK(hipEventCreateWithFlags(&w.ev_tc[i], hipEventDisableTiming));
-    }
-    CK(hipEventCreateWithFlags(&w.ev_tail, hipEventDisableTiming));
   }
   return w;
 }
@@ -464,7 +453,7 @@ int* identity(Ctx& w, int64_t n, hipStream_t st) {  // device 0, 1, ..., n-1 (gr
   if (w.ident_len < n) {
     int* h = w.ident_h.get(m);
     for (int64_t i = 0; i < m; ++i) h[i] = (int)i;
-    CK(hipMemcpyAsync(p, h, m * sizeof(int), hipMemcpyHostToDevice, st));
+    CK(dmlp::dma_copy(p, h, m * sizeof(int), st));
     w.ident_len = m;
   }
   return p;
@@ -479,12 +468,9 @@ struct HostOps {
   unsigned* words = nullptr;  // [0] xnmax bits, [1] bad (0)
   const void* qhi = nullptr;
   const float* qn = nullptr;
-  const unsigned* rdy = nullptr;
+  const unsigned* rdy = nullptr;  // ready words, one per slice (the slice's norm bits)
   int rdy_tiles = 1, rdy_n = 0;
-  const unsigned* xnm_sl = nullptr;
   unsigned* estats = nullptr;
-  const unsigned* qrdy = nullptr;  // query-block ready words (null: the query operands landed)
-  int qrdy_q = 128;                // queries per block
   const void* xrow = nullptr;  // xhi point-major (set once its copy kernel is queued), or none
 };
 
@@ -513,10 +499,14 @@ struct Local {
   const HostOps* hx = nullptr;
   hipEvent_t rows = nullptr;
   std::function<void()> issue_rows;
-  // the chunked report tail: the all-queries single-slice pass re-ranks in `chunks` query ranges
-  // and calls on_chunk(q0, q1) behind each (the step formats that range and starts its copy)
-  std::function<void(int64_t, int64_t)> on_chunk;
-  int chunks = 1;
+  // (dmlp_step) k already clamped to N and on the device (kd_pre), every k in [1, 64] and <= N
+  // (all_a_pre), the overflow counter zeroed on the device (ovf_pre): no host pass over the
+  // queries and no copy or memset on `st` between the operands' event and the screen
+  const int* kk_pre = nullptr;
+  int* kd_pre = nullptr;
+  int* ovf_pre = nullptr;
+  bool all_a_pre = false;
+  int kmax_pre = 0;
   // state
   int* kk = nullptr;
   int* kd = nullptr;
@@ -580,12 +570,13 @@ struct Local {
       qi = qbuf.get(nq);
       int* h = hbuf.get((size_t)nq);
       std::memcpy(h, idx->data(), nq * sizeof(int));
-      CK(hipMemcpyAsync(qi, h, nq * sizeof(int), hipMemcpyHostToDevice, st));
+      CK(dmlp::dma_copy(qi, h, nq * sizeof(int), st));
     } else {
       qi = identity(w, Q, st);
     }
     int kcls = 1;
     if (idx) for (int q : *idx) kcls = std::max(kcls, kk[q]);
+    else if (kmax_pre > 0) kcls = kmax_pre;
     else for (int64_t q = 0; q < Q; ++q) kcls = std::max(kcls, kk[q]);
     const int64_t nt = (N + 63) / 64;
     const bool fin = labels != nullptr;
@@ -604,28 +595,13 @@ struct Local {
       if (hx && hx->rdy) {
         // the caller sized the early start for this all-queries pass with one slice
         if (S != 1 || idx) throw Fail{-7};
-        CKL(dmlp_screen_x1_early2(KT, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd + 1, hx->rdy,
-                                  hx->rdy_tiles, hx->rdy_n, hx->xnm_sl, ci, cc, ch, hx->estats,
-                                  hx->qrdy, hx->qrdy_q,
-                                 st));
+        CKL(dmlp_screen_x1_early(KT, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd + 1, hx->rdy,
+                                 hx->rdy_tiles, hx->rdy_n, ci, cc, ch, hx->estats, st));
       } else {
         CKL(dmlp_screen_x1(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1, S, ci,
                            cc, ch, st));
       }
       wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
-      if (on_chunk && chunks > 1 && !idx && S == 1) {
-        // query ranges of whole pair-refine workgroups (8 queries); q = qidx[p] = q0 + p
-        const int64_t span = ((nq + chunks - 1) / chunks + 7) / 8 * 8;
-        for (int64_t q0 = 0; q0 < nq; q0 += span) {
-          const int n = (int)std::min<int64_t>(span, nq - q0);
-          CKL(dmlp_refine_groups_rm(cap, ci + q0 * cap, cc + q0, ch + 2 * q0, S, X, A, Qx, xf,
-                                    hx ? hx->xrow : nullptr, xi, qh, KT, hl, N, qi + q0, kd, n,
-                                    out_d, out_i, kstride, fin ? labels : nullptr, lo, hi, lab, cs,
-                                    stat, ovf, kcls, st));
-          on_chunk(q0, q0 + n);
-        }
-        return;
-      }
       CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
                                 qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
                                 fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls, st));
@@ -642,7 +618,7 @@ struct Local {
       int kmax1 = 1;
       for (int q : *idx) kmax1 = std::max(kmax1, kp[q]);
       int* kpd = w.kp_d.get(Q);
-      CK(hipMemcpyAsync(kpd, kp, Q * sizeof(int), hipMemcpyHostToDevice, st));
+      CK(dmlp::dma_copy(kpd, kp, Q * sizeof(int), st));
       const int cap1 = dmlp_screen_x1_cap(kmax1);
       int* i1 = w.k1_ids.get((size_t)nq * S1 * cap1);
       int* c1 = w.k1_cnt.get((size_t)nq * S1);
@@ -714,7 +690,7 @@ struct Local {
       std::memcpy(h + base, v->data(), v->size() * sizeof(int));
       base += v->size();
     }
-    CK(hipMemcpyAsync(qi, h, fq.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    CK(dmlp::dma_copy(qi, h, fq.size() * sizeof(int), st));
     base = 0;
     if (!fused.empty()) {
       // A <= 32, 1 <= k <= 64: the fp64 MFMA screen + exact group re-rank (screen_f64.hip); its
@@ -730,14 +706,14 @@ struct Local {
         int* fst = w.f64_stat.get(Q);
         int* fov = w.f64_ovf.get(1);
         int* oh = w.f64_h.get(1);
-        CK(hipMemsetAsync(fov, 0, sizeof(int), st));
+        CK(dma_zero(fov, sizeof(int), st));
         CKL(dmlp_exact_f64(X, N, A, Qx, qi, kd, (int)fused.size(), kfmax, out_d, out_i, kstride,
                            fst, fov, fws, wb, st));
-        CK(hipMemcpyAsync(oh, fov, sizeof(int), hipMemcpyDeviceToHost, st));
+        CK(dmlp::dma_copy(oh, fov, sizeof(int), st));
         CK(hipStreamSynchronize(st));
         if (*oh > 0) {
           int* sh = w.f64_st_h.get(Q);
-          CK(hipMemcpyAsync(sh, fst, Q * sizeof(int), hipMemcpyDeviceToHost, st));
+          CK(dmlp::dma_copy(sh, fst, Q * sizeof(int), st));
           CK(hipStreamSynchronize(st));
           for (int q : fused)
             if (sh[q]) redo.push_back(q);
@@ -752,7 +728,7 @@ struct Local {
           int* q2 = w.qidx_f2.get(redo.size());
           int* h2 = w.lf2_h.get(redo.size());
           std::memcpy(h2, redo.data(), redo.size() * sizeof(int));
-          CK(hipMemcpyAsync(q2, h2, redo.size() * sizeof(int), hipMemcpyHostToDevice, st));
+          CK(dmlp::dma_copy(q2, h2, redo.size() * sizeof(int), st));
           ql = q2;
           n = (int)redo.size();
           km = 0;
@@ -792,11 +768,11 @@ struct Local {
     int* kf = w.kfull.get(Q);
     int* kh = w.kfull_h.get(Q);
     std::memcpy(kh, k_host, Q * sizeof(int));
-    CK(hipMemcpyAsync(kf, kh, Q * sizeof(int), hipMemcpyHostToDevice, st));
+    CK(dmlp::dma_copy(kf, kh, Q * sizeof(int), st));
     int* qi = w.qidx_r.get(r.size());
     int* h = w.lr_h.get(r.size());
     std::memcpy(h, r.data(), r.size() * sizeof(int));
-    CK(hipMemcpyAsync(qi, h, r.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    CK(dmlp::dma_copy(qi, h, r.size() * sizeof(int), st));
     CKL(dmlp_finalize(out_d, out_i, kstride, kf, qi, (int)r.size(), labels, lo, hi, lab, cs, st));
   }
 
@@ -804,15 +780,21 @@ struct Local {
     g_stats.n_exact_f64 = g_stats.n_exact_f64_redo = 0;
     if (Q == 0) return;
     KT = dmlp_screen_kt(A);
-    kk = w.kk_h.get(Q);
     lds_ok = KT <= 8 && !exact;
     x1_ok = dmlp_screen_x1_qw(KT) > 0 && !exact;
     const bool screen = (lds_ok || x1_ok) && N > 0;
     all_a = screen && x1_ok;
     const int ka = dmlp_screen_x1_kmax();  // the single-term one-pass class: k <= 64
-    for (int64_t q = 0; q < Q; ++q) {
-      kk[q] = (int)std::min<int64_t>(k_host[q], N);
-      all_a = all_a && k_host[q] >= 1 && k_host[q] <= ka && k_host[q] <= N;
+    if (kd_pre) {
+      // (the step's bounds: every k in [1, 64] and <= N, so kk == k; on the device already)
+      kk = const_cast<int*>(kk_pre);
+      all_a = all_a && all_a_pre;
+    } else {
+      kk = w.kk_h.get(Q);
+      for (int64_t q = 0; q < Q; ++q) {
+        kk[q] = (int)std::min<int64_t>(k_host[q], N);
+        all_a = all_a && k_host[q] >= 1 && k_host[q] <= ka && k_host[q] <= N;
+      }
     }
     // the first screen of class a: the single-term one (k <= 64), or on the device image the
     // 3-term streaming screen (k <= 32; the A/B switch "screen") or LDS screen
@@ -833,11 +815,19 @@ struct Local {
       else f.push_back((int)q);
       if (k_host[q] > N) rest.push_back((int)q);
     }
-    kd = w.kdev.get(Q);
-    CK(hipMemcpyAsync(kd, kk, Q * sizeof(int), hipMemcpyHostToDevice, st));
+    if (kd_pre) {
+      kd = kd_pre;
+    } else {
+      kd = w.kdev.get(Q);
+      CK(dmlp::dma_copy(kd, kk, Q * sizeof(int), st));
+    }
     stat = w.status.get(Q);
-    ovf = w.ovf.get(1);
-    CK(hipMemsetAsync(ovf, 0, sizeof(int), st));
+    if (ovf_pre) {
+      ovf = ovf_pre;
+    } else {
+      ovf = w.ovf.get(1);
+      CK(dma_zero(ovf, sizeof(int), st));
+    }
     if (hx && hx->rdy && !all_a) throw Fail{-8};  // early start sized for one all-queries pass
     // every refine writes its queries' padding and status itself; the fill is only needed for
     // rows no refine covers (exact path, k < 1)
@@ -887,7 +877,7 @@ struct Local {
     // a 3-term screen's own overflow goes to the exact path (escalated twice: no third screen)
     const int redone = (int)(esc.size() + esc_bc.size() + fq.size());
     if (!esc.empty() || !esc_bc.empty()) {
-      CK(hipMemsetAsync(ovf, 0, sizeof(int), st));
+      CK(dma_zero(ovf, sizeof(int), st));
       for (int q : esc) CK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
       for (int q : esc_bc) CK(hipMemsetAsync(stat + q, 0, sizeof(int), st));
       const HostOps* keep = hx;
@@ -897,7 +887,7 @@ struct Local {
       hx = keep;
       int n2 = 0;
       int* h = w.small_h.get(4);
-      CK(hipMemcpyAsync(h, ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+      CK(dmlp::dma_copy(h, ovf, sizeof(int), st));
       CK(hipStreamSynchronize(st));
       n2 = h[0];
       if (n2) {
@@ -937,7 +927,7 @@ struct Step {
     if (a->labels && N) {
       int* lh = w.s_lab.get(N);
       std::memcpy(lh, a->labels, N * sizeof(int));
-      CK(hipMemcpyAsync(lab_d, lh, N * sizeof(int), hipMemcpyHostToDevice, w.side));
+      CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
     }
     const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
     auto rows = [&](const double* src, const double* const* tab, int64_t nr, double* dst,
@@ -949,7 +939,7 @@ struct Step {
         if ((tab ? dmlp_cpu_rows_i32_rows(tab, nr, (int)A, h32) : dmlp_cpu_rows_i32(src, n, h32)) ==
             0) {
           int* d32 = w.d_i32.get(at + nqa) + off;
-          CK(hipMemcpyAsync(d32, h32, n * 4, hipMemcpyHostToDevice, w.side));
+          CK(dmlp::dma_copy(d32, h32, n * 4, w.side));
           CKL(dmlp_rows_from_i32(d32, n, dst, w.side));
           return;
         }
@@ -982,7 +972,7 @@ struct Step {
           CK(hipMemcpyAsync(Xd + r0 * A, src, n * 8, hipMemcpyHostToDevice, w.side));
         } else {
           int* d32 = w.d_i32.get(at + nqa) + r0 * A;
-          CK(hipMemcpyAsync(d32, (const int*)r32 + r0 * A, n * 4, hipMemcpyHostToDevice, w.side));
+          CK(dmlp::dma_copy(d32, (const int*)r32 + r0 * A, n * 4, w.side));
           CKL(dmlp_rows_from_i32(d32, n, Xd + r0 * A, w.side));
         }
       }, [&]() { rows(a->Qx, a->Qr, Q, Qd, at); });
@@ -1038,11 +1028,10 @@ struct Step {
     a->path = 0;
     a->early = 0;
     a->n_escalated = 0;
-    a->early_waits = a->early_grows = a->early_timeouts = a->early_qwaits = 0;
+    a->early_waits = a->early_grows = a->early_timeouts = 0;
     w.marks_valid = false;
     w.marks_rec = 0;
     w.text_len = 0;  // dmlp_step_emit copies only what THIS call rendered
-    a->report_sunk = 0;
     if (Q < 0 || N < 0 || A < 1 || Q > (1 << 30)) return -1;
     const dmlp_plane* pl = a->plane;
     if (pl && (!pl->base || pl->rank < 0 || pl->renderers < 1 || pl->gen <= 0 ||
@@ -1090,8 +1079,10 @@ struct Step {
                           g_tune.screen == 0 &&
                           (g_tune.host_ops >= 2 ||
                            (g_tune.host_ops == 1 && (pl || dr_on() || dmlp_host_threads() >= 2)));
-    // device render (the default): the GPU renders the screen operands from the landed rows
-    bool dr = x1_front && dr_on();
+    // device render (opt-in, DMLP_DEVICE_RENDER=1): the GPU renders the screen operands from the
+    // landed rows.  With a plane every rank must render the same slice kinds, so a plane step
+    // always renders on the host (a device-render rank never renders its image slices)
+    bool dr = x1_front && dr_on() && !pl;
     if (Q == 0) {
       a->report_len = 0;
       w.text_len = 0;
@@ -1107,11 +1098,7 @@ struct Step {
             throw Fail{-9};
           }
         }
-        int64_t t0 = 0, t1 = 0;
-        const int ns = dmlp_plane_slice(N, A, 0, &t0, &t1);
-        for (int what = x1_front && !dr ? 1 : 2; what <= (a->X32d ? 1 : 2); ++what)
-          for (int i = pl->rank; i < ns; i += pl->renderers)
-            if (dmlp_plane_render(pl, a->X, a->Xr, N, A, mu, what, i) < 0) throw Fail{-9};
+        render_plane_share(mu, x1_front ? 1 : 2, a->X32d ? 1 : 2);
       }
       return 0;
     }
@@ -1124,27 +1111,31 @@ struct Step {
     if (early && !dr_early_ok(KT, kmax)) dr = false;
     const int NS = early ? (int)std::min<int64_t>(kEarlySlices, nt) : 0;
     const int rt = early ? (int)((nt + NS - 1) / NS) : 1;  // image tiles per early slice
-    // query-block early start: NQB blocks of qbq queries (a multiple of 128, the widest wave's
-    // columns) rendered and copied behind the screen launch, each with its own ready word
-    int qbq = 0, NQB = 0;
-    if (early && qb_blocks() > 0) {
-      qbq = (int)(((Q + qb_blocks() - 1) / qb_blocks() + 127) / 128 * 128);
-      NQB = (int)((Q + qbq - 1) / qbq);
-      if (NQB < 2 || NQB > kMaxQBlocks) qbq = NQB = 0;
-    }
-    unsigned* words = w.dwords.get(2 + 2 * kEarlySlices + 4 + kMaxQBlocks);
-    unsigned* rdy = words + 2;
-    unsigned* xnm_sl = words + 2 + kEarlySlices;
-    unsigned* estats = words + 2 + 2 * kEarlySlices;
-    unsigned* qrdy = words + 2 + 2 * kEarlySlices + 4;
+    unsigned* words = w.dwords.get(kW_N);
+    unsigned* rdy = words + kW_RDY;
+    unsigned* estats = words + kW_EST;
     HostOps hx;
     bool use_hx = false, early_bad = false;
+    // ---- the step's words (norm, bad, ready words, counters, overflow) zeroed by one DMA copy, and
+    // on the all-class-a path k on the device — both on the side stream ahead of the operands,
+    // so nothing sits on `st` between the operands' event and the screen
+    CK(dma_zero(words, kW_N * sizeof(unsigned), w.side));
+    int* kd_pre = nullptr;
+    if (x1_front && all_a) {
+      int* kh = w.kk_h.get(Q);
+      struct Cp { int* dst; const int* src; int64_t n; } cp{kh, a->k, Q};
+      dmlp_host_pool_run([](void* c, int t, int nt_) {
+        const Cp& p = *(const Cp*)c;
+        const int64_t lo = p.n * t / nt_, hi = p.n * (t + 1) / nt_;
+        if (hi > lo) std::memcpy(p.dst + lo, p.src + lo, (hi - lo) * sizeof(int));
+      }, &cp);
+      kd_pre = w.kdev.get(Q);
+      CK(dmlp::dma_copy(kd_pre, kh, Q * sizeof(int), w.side));
+    }
     // ---- device render: the rows (lossless int32, fp64 where a block is not 6-decimal) cross
-    // PCIe on the side stream in dataset slices and query blocks, each followed by its render
-    // kernel (prep.hip k_render: the fp64 rows for the re-rank, the fp16 image / query fragments,
-    // the norms; under the early start its last workgroup publishes the slice's / block's ready
-    // word).  Order: the first DMLP_QB_LEAD dataset slices, the query blocks, the rest of the
-    // dataset (the plane: this rank's query blocks, then the node's slices from the segment).
+    // PCIe on the side stream, the query block first, then the dataset in slices, each followed
+    // by its render kernel (prep.hip k_render: the fp64 rows for the re-rank, the fp16 image /
+    // query fragments, the norms)
     auto dr_issue = [&]() {
       const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
       int* h32 = w.s_i32.get(at + nqa);
@@ -1156,24 +1147,11 @@ struct Step {
       float* xin_d = const_cast<float*>(hx.xin);
       const int ns = (int)std::min<int64_t>(kEarlySlices, nt);
       const int64_t rts = (nt + ns - 1) / ns;
-      unsigned* one = w.sx_nm.get(2 + kEarlySlices);
-      one[0] = 1u;
-      const int dly = early ? early_delay_us() : 0;
       if (a->labels && N) {
         int* lh = w.s_lab.get(N);
         std::memcpy(lh, a->labels, N * sizeof(int));
-        CK(hipMemcpyAsync(lab_d, lh, N * sizeof(int), hipMemcpyHostToDevice, w.side));
+        CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
       }
-      auto render_x = [&](int i, const int* s32, const double* s64) {
-        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
-        if (t1 <= t0) {  // an empty slice: its ready word all the same
-          if (early) CK(put_word(rdy + i, 1u, one, w.side));
-          return;
-        }
-        CKL(dmlp_render_rows(KT, A, s32, s64, t0 * 64, (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
-                             const_cast<void*>(hx.xrow), early ? xnm_sl + i : words, rbad, drw + i,
-                             early ? rdy + i : nullptr, w.side));
-      };
       // rows [r0, r1) of X (or Qx) -> int32 staging at h32 + off + r0 A, else fp64; returns the
       // render's source (device int32 base or the device fp64 rows)
       auto ship = [&](const double* src, const double* const* tab, int64_t r0, int64_t r1,
@@ -1185,8 +1163,7 @@ struct Step {
         if (rows_i32_on() &&
             (tab ? dmlp_cpu_rows_i32_rows(tab + r0, r1 - r0, A, h32 + off + r0 * A)
                  : dmlp_cpu_rows_i32(src + r0 * A, n, h32 + off + r0 * A)) == 0) {
-          CK(hipMemcpyAsync(d32 + off + r0 * A, h32 + off + r0 * A, n * 4, hipMemcpyHostToDevice,
-                            w.side));
+          CK(dmlp::dma_copy(d32 + off + r0 * A, h32 + off + r0 * A, n * 4, w.side));
           *s32 = d32 + off;
           return;
         }
@@ -1199,56 +1176,23 @@ struct Step {
         CK(hipMemcpyAsync(dst64 + r0 * A, from, n * 8, hipMemcpyHostToDevice, w.side));
         *s64 = dst64;
       };
-      auto xslice = [&](int i) {
-        if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
-        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
-        if (a->X32d) {  // the xGMI replica: rendered straight from the device
-          render_x(i, a->X32d, nullptr);
-          return;
-        }
+      {  // the queries
         const int* s32;
         const double* s64;
-        ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
-        render_x(i, s32, s64 ? s64 : s32 ? nullptr : Xd);
-      };
-      const int nqb = NQB ? NQB : 1;
-      const int64_t qstep = NQB ? qbq : Q;
-      auto qblock = [&](int b) {
-        const int64_t q0 = (int64_t)b * qstep, q1 = std::min<int64_t>(Q, q0 + qstep);
-        const int* s32;
-        const double* s64;
-        ship(a->Qx, a->Qr, q0, q1, at, Qd, &s32, &s64);
-        CKL(dmlp_render_rows(KT, A, s32, s64, q0, q1 - q0, Q, mud, Qd, 1, w.dq_hi.p, w.dq_n.p, nullptr,
-                             nullptr, rbad, drw + 8 + b, NQB ? qrdy + b : nullptr, w.side));
-      };
-      if (pl && !a->X32d) {
-        void *r32 = nullptr, *r64 = nullptr;
-        CKL(dmlp_plane_regions(pl, N, A, nullptr, nullptr, &r32, &r64));
-        plane_slices(2, [&](int i, int bits, float) {
-          if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
-          const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
-          const int64_t r0 = std::min(N, t0 * 64), r1 = std::min(N, t1 * 64), n = (r1 - r0) * A;
-          if (n > 0 && (bits & 2)) {  // fp64: from the segment, or from the node-shared X
-            const double* src = r64 ? (const double*)r64 + r0 * A : a->X ? a->X + r0 * A : nullptr;
-            if (!src) throw Fail{-10};
-            CK(hipMemcpyAsync(Xd + r0 * A, src, n * 8, hipMemcpyHostToDevice, w.side));
-            render_x(i, nullptr, Xd);
-          } else {
-            if (n > 0)
-              CK(hipMemcpyAsync(d32 + r0 * A, (const int*)r32 + r0 * A, n * 4,
-                                hipMemcpyHostToDevice, w.side));
-            render_x(i, d32, nullptr);
-          }
-        }, [&]() {
-          for (int b = 0; b < nqb; ++b) qblock(b);
-          CK(mark(M_OPS, w.side));
-        });
-      } else {
-        const int lead = early && NQB ? std::min(qb_lead(), ns) : 0;
-        for (int i = 0; i < lead; ++i) xslice(i);
-        for (int b = 0; b < nqb; ++b) qblock(b);
+        ship(a->Qx, a->Qr, 0, Q, at, Qd, &s32, &s64);
+        CKL(dmlp_render_rows(KT, A, s32, s64, 0, Q, Q, mud, Qd, 1, w.dq_hi.p, w.dq_n.p, nullptr,
+                             nullptr, rbad, drw + 8, nullptr, w.side));
         CK(mark(M_OPS, w.side));
-        for (int i = lead; i < ns; ++i) xslice(i);
+      }
+      for (int i = 0; i < ns; ++i) {  // the dataset, slice by slice
+        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
+        if (t1 <= t0) continue;
+        const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
+        const double* s64 = nullptr;
+        if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+        CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64, (t1 - t0) * 64,
+                             N, mud, Xd, 0, xhi_d, xin_d, const_cast<void*>(hx.xrow), words + kW_XNMAX,
+                             rbad, drw + i, nullptr, w.side));
       }
       CK(mark(M_DATA, w.side));
       CK(hipEventRecord(w.ev_rows, w.side));
@@ -1286,49 +1230,44 @@ struct Step {
       };
       int rc;
       if (dr) {
-        // the centre on the device; every ready word, counter and norm word cleared; the rows
-        // and the render follow the screen's launch (early start) or precede it
+        // the centre on the device; the render counters cleared; the rows and the render precede
+        // the screen (device render never starts early)
         double* mud = w.d_mu.get(A);
-        CK(hipMemcpyAsync(mud, mu, A * sizeof(double), hipMemcpyHostToDevice, w.side));
-        CK(hipMemsetAsync(w.dr_words.get(80), 0, 80 * sizeof(unsigned), w.side));
-        CK(hipMemsetAsync(words, 0, (2 + 2 * kEarlySlices + 4 + kMaxQBlocks) * sizeof(unsigned),
-                          w.side));
+        CK(dmlp::dma_copy(mud, mu, A * sizeof(double), w.side));
+        CK(dma_zero(w.dr_words.get(80), 80 * sizeof(unsigned), w.side));
         if (KT <= 2 && rowmajor_on()) hx.xrow = w.dx_row.get(nt * 64 * W);
         hx.xhi = xhi;
         hx.xin = xin;
-        if (!early) dr_issue();
-        rc = 0;
-      } else if (early && NQB) {
-        // the ready words cleared; the query operands follow the screen's launch block by block
-        // (issue_rows), each wave waits for its own block
-        CK(hipMemsetAsync(rdy, 0, NS * sizeof(unsigned), w.side));
-        CK(hipMemsetAsync(estats, 0, 4 * sizeof(unsigned), w.side));
-        CK(hipMemsetAsync(qrdy, 0, NQB * sizeof(unsigned), w.side));
+        dr_issue();
         rc = 0;
       } else if (early) {
-        // query operands first (the whole front of the step), the ready words cleared
-        CK(hipMemsetAsync(rdy, 0, (NS + 0) * sizeof(unsigned), w.side));
-        CK(hipMemsetAsync(estats, 0, 4 * sizeof(unsigned), w.side));
-        rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, words + 1, qhi, qn,
+        // query operands first (the whole front of the step); the image follows the screen's launch
+        rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, nullptr, qhi, qn,
                        early_qchunks());
       } else if (pl) {
         // this rank's query operands, then the dataset image from the node render plane; the
-        // image's max norm (+inf when a slice is outside the fp16 range) into words[0]
-        rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, words + 1, qhi, qn,
+        // image's max norm (+inf when a slice is outside the fp16 range) into words[XNMAX]
+        rc = h2d_tiles(nt, nt, a->Qx, a->Qr, Q, xnm_h + 1, xhi, xin, nullptr, qhi, qn,
                        host_slices());
         float mx = 0.0f;
-        if (plane_image(xhi, xin, nullptr, nullptr, &mx)) rc |= 1;
+        if (plane_image(xhi, xin, nullptr, &mx)) rc |= 1;
         std::memcpy(xnm_h, &mx, 4);
-        CK(hipMemcpyAsync(words, xnm_h, 4, hipMemcpyHostToDevice, w.side));
+        CK(dmlp::dma_copy(words + kW_XNMAX, xnm_h, 4, w.side));
         CK(mark(M_DATA, w.side));
       } else {
-        rc = h2d_tiles(0, nt, a->Qx, a->Qr, Q, xnm_h, xhi, xin, words, qhi, qn, host_slices());
+        rc = h2d_tiles(0, nt, a->Qx, a->Qr, Q, xnm_h, xhi, xin, words + kW_XNMAX, qhi, qn,
+                       host_slices());
         CK(mark(M_DATA, w.side));
       }
       if (rc & 4) throw Fail{-(int)hipErrorUnknown};
+      if (rc != 0 && pl && early) {
+        // this rank falls back to the device image path (its queries are outside the fp16
+        // range), but its share of the plane's image slices is still owed to the other ranks
+        // (its row slices follow in issue_rows_now as usual)
+        render_plane_share(mu, 1, 1);
+      }
       if (rc == 0) {
-        CK(hipMemsetAsync(words + 1, 0, sizeof(unsigned), w.side));  // bad = 0: host-checked
-        if (!NQB && !dr) CK(mark(M_OPS, w.side));
+        if (!dr) CK(mark(M_OPS, w.side));
         CK(hipEventRecord(w.ev_ops, w.side));
         CK(hipStreamWaitEvent(st, w.ev_ops, 0));
         hx.xhi = xhi;
@@ -1340,51 +1279,14 @@ struct Step {
           hx.rdy = rdy;
           hx.rdy_tiles = rt;
           hx.rdy_n = NS;
-          hx.xnm_sl = xnm_sl;
           hx.estats = estats;
-          if (NQB) {
-            hx.qrdy = qrdy;
-            hx.qrdy_q = qbq;
-          }
         }
         use_hx = true;
         a->early = early ? 1 : 0;
       }
       // (rc != 0: data or queries outside the fp16 screen's range -> the device image path)
     }
-    // ---- the chunked report tail (report_chunks > 1, report_mode 1): the re-rank runs in query
-    // ranges; behind each range its lines are formatted at their absolute offsets (each range's
-    // base is the previous range's end, on the device) and that end crosses to the host, which
-    // then starts the range's text copy on the tail stream — the report's D2H runs under the next
-    // range's re-rank instead of after the whole re-rank
-    const int RC = std::min(g_tune.report_chunks, kMaxTail);
-    const bool tail_on = want_report && a->report_mode == 1 && RC > 1 && Q >= 1024 * (int64_t)RC;
     char* text = want_report ? w.d_text.get((size_t)dmlp_format_bound((int)Q)) : nullptr;
-    int64_t* toff = tail_on ? w.d_off_t.get((size_t)dmlp_format_scratch((int)Q) + 4 * kMaxTail)
-                            : nullptr;
-    int64_t* tend = tail_on ? w.tail_end_h.get(kMaxTail) : nullptr;
-    int* tovf = tail_on ? w.tail_ovf_h.get(kMaxTail) : nullptr;
-    int ntail = 0;
-    int64_t tsoff = 0;
-    const int64_t* tprev = nullptr;  // the last formatted range's absolute end (device)
-    auto on_chunk = [&](int64_t q0, int64_t q1) {
-      const int c = ntail;
-      if (c >= kMaxTail) throw Fail{-11};
-      const int n = (int)(q1 - q0);
-      int64_t* lo = toff + tsoff;
-      tsoff += dmlp_format_scratch(n);
-      CKL(dmlp_format_report_at(ocs + q0, n, (int)(a->qid_base + q0), lo, text, tprev, st));
-      tprev = lo + n;
-      CK(hipEventRecord(w.ev_tf[c], st));
-      CK(hipStreamWaitEvent(w.side, w.ev_tf[c], 0));
-      CK(hipMemcpyAsync(tend + c, lo + n, sizeof(int64_t), hipMemcpyDeviceToHost, w.side));
-      // the overflow count so far (read no earlier than this range's re-rank: later ranges' and
-      // the screen's overflows only make it larger) — 0: no query up to here is redone
-      if (a->report_sink)
-        CK(hipMemcpyAsync(tovf + c, w.ovf.p, sizeof(int), hipMemcpyDeviceToHost, w.side));
-      CK(hipEventRecord(w.ev_ts[c], w.side));
-      ntail = c + 1;
-    };
     // ---- dispatch: screens on `st`, the rows behind the first of them on the side stream
     auto run_local = [&](bool with_hx, bool rows_pending) {
       std::unique_ptr<Local> Lp(new Local(w));
@@ -1394,62 +1296,36 @@ struct Step {
       L.lab = olab; L.cs = ocs; L.exact = a->exact != 0; L.st = st;
       L.hx = with_hx ? &hx : nullptr;
       L.rows = w.ev_rows;
-      if (rows_pending && tail_on) {
-        L.on_chunk = on_chunk;
-        L.chunks = RC;
+      if (with_hx && kd_pre) {
+        // (the words' zero copy and k's copy precede the operands' event on the side stream)
+        L.kd_pre = kd_pre;
+        L.kk_pre = w.kk_h.p;
+        L.all_a_pre = true;
+        L.kmax_pre = kmax;
+        L.ovf_pre = (int*)(words + kW_OVF);
       }
       if (rows_pending) {
         L.issue_rows = [&]() {
           // (host operands: called right after the first screen launch, so this mark completes
           // when it does; the device path calls it before its image is built: no mark)
           if (with_hx) CK(mark(M_SCREEN, st));
-          if (dr) {  // device render: the rows and their render (already queued without the early start)
-            if (with_hx && early) dr_issue();
-            return;
-          }
+          if (dr) return;  // device render: the rows and their render are queued already
           if (with_hx && hx.rdy) {
             // the dataset image behind the queries, slice by slice, each followed by its ready
-            // word (the running screen waits on it); every word is written even when a slice is
-            // outside the fp16 range, so the screen always drains
-            unsigned* one = w.sx_nm.get(2 + kEarlySlices);  // (slot 0 is free in early mode)
-            one[0] = 1u;
+            // word (the slice's norm bits: the running screen waits on it); every word is
+            // written even when a slice is outside the fp16 range, so the screen always drains
             const int dly = early_delay_us();
-            // query block b: rendered, copied, then its ready word (written even when out of the
-            // fp16 range — the call then falls back to the device image path — so the screen drains)
-            auto qblocks = [&]() {
-              const int64_t W = (int64_t)KT * 32;
-              for (int b = 0; b < NQB; ++b) {
-                const int64_t q0 = (int64_t)b * qbq, q1 = std::min<int64_t>(Q, q0 + qbq);
-                uint16_t* qh_h = w.sq_hi.p + q0 * W;
-                float* qn_h = w.sq_n.p + q0;
-                const int bad = a->Qr ? dmlp_cpu_prep_queries_rows(a->Qr + q0, q1 - q0, A, w.s_mu.p,
-                                                                   KT, qh_h, qn_h)
-                                      : dmlp_cpu_prep_queries(a->Qx + q0 * A, q1 - q0, A, w.s_mu.p,
-                                                              KT, qh_h, qn_h);
-                if (bad) early_bad = true;
-                CK(hipMemcpyAsync((short*)const_cast<void*>(hx.qhi) + q0 * W, qh_h,
-                                  (q1 - q0) * W * 2, hipMemcpyHostToDevice, w.side));
-                CK(hipMemcpyAsync(const_cast<float*>(hx.qn) + q0, qn_h, (q1 - q0) * 4,
-                                  hipMemcpyHostToDevice, w.side));
-                CK(put_word(qrdy + b, 1u, one, w.side));
+            if (pl) {
+              if (plane_image(hx.xhi, hx.xin, rdy, nullptr)) early_bad = true;
+            } else {
+              for (int i = 0; i < NS; ++i) {
+                if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
+                const int64_t t0 = (int64_t)i * rt, t1 = std::min<int64_t>(nt, t0 + rt);
+                const int r2 = h2d_tiles_data(t0, t1, i);
+                if (r2 & 4) throw Fail{-(int)hipErrorUnknown};
+                if (r2) early_bad = true;
               }
-              CK(mark(M_OPS, w.side));
-            };
-            // the first DMLP_QB_LEAD image slices, the query blocks, the rest of the image (the
-            // plane: the query blocks, then the node's slices)
-            const int lead = NQB ? (pl ? 0 : std::min(qb_lead(), NS)) : -1;
-            if (lead == 0) qblocks();
-            if (pl && plane_image(hx.xhi, hx.xin, rdy, xnm_sl, nullptr)) early_bad = true;
-            for (int i = 0; i < NS && !pl; ++i) {
-              if (i == lead && i > 0) qblocks();
-              if (dly) std::this_thread::sleep_for(std::chrono::microseconds(dly));
-              const int64_t t0 = (int64_t)i * rt, t1 = std::min<int64_t>(nt, t0 + rt);
-              const int r2 = h2d_tiles_data(t0, t1, i);
-              if (r2 & 4) throw Fail{-(int)hipErrorUnknown};
-              if (r2) early_bad = true;
-              CK(put_word(rdy + i, 1u, one, w.side));
             }
-            if (!pl && lead >= NS) qblocks();
             CK(mark(M_DATA, w.side));
           }
           if (with_hx && KT <= 2 && rowmajor_on()) {
@@ -1465,7 +1341,7 @@ struct Step {
       L.launch();
       return Lp;
     };
-    hx_data_ctx_ = {&hx, words, xnm_sl, nt, W, KT};
+    hx_ = &hx;
     std::unique_ptr<Local> Lp = run_local(use_hx, true);
     if (early_bad) {
       // a dataset slice outside the fp16 range behind a running early screen: drain, then the
@@ -1474,21 +1350,17 @@ struct Step {
       CK(hipStreamSynchronize(st));
       a->early = 0;
       use_hx = false;
-      ntail = 0;  // (any ranges formatted behind the abandoned screen are rendered again whole)
       Lp = run_local(false, false);
     }
     // ---- the report behind the re-rank, then the one host sync.  The small results (report
     // length, overflow count, early-start counters) are packed on the device and cross in ONE
-    // copy: each separate small D2H cost a copy command's latency on the step's tail.
+    // DMA copy: each separate small D2H cost a copy command's latency on the step's tail.
     int64_t* small = w.small64_h.get(8);
     int64_t* small_d = w.small64_d.get(8);
     unsigned* dr_bad = dr ? w.dr_words.p + 72 : nullptr;  // device render: a value out of range
     auto render = [&]() {
       const int64_t* len_src = nullptr;
-      if (want_report && ntail > 0) {  // formatted range by range behind the re-rank
-        CK(mark(M_FORMAT, st));
-        len_src = tprev;
-      } else if (want_report) {
+      if (want_report) {
         int64_t* off = w.d_off.get((size_t)dmlp_format_scratch((int)Q));
         CKL(dmlp_format_report(ocs, (int)Q, (int)a->qid_base, off, text, st));
         CK(mark(M_FORMAT, st));
@@ -1497,52 +1369,14 @@ struct Step {
       hipLaunchKernelGGL(k_pack_small, dim3(1), dim3(64), 0, st, len_src, Lp->ovf,
                          a->early ? estats : nullptr, dr_bad, small_d);
       CK(hipGetLastError());
-      CK(hipMemcpyAsync(small, small_d, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      if (want_report && a->report_mode == 1 && ntail == 0)
-        CK(hipMemcpyAsync(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q),
-                          hipMemcpyDeviceToHost, st));
+      CK(dmlp::dma_copy(small, small_d, 8 * sizeof(int64_t), st));
+      if (want_report && a->report_mode == 1)
+        CK(dmlp::dma_copy(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q), st));
     };
     a->host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_enter)
                      .count();
     CK(mark(M_REFINE, st));
     render();
-    if (ntail > 0) {
-      // each range's text once its end offset has landed: [previous end, this end)
-      // With a report_sink, range c-1's bytes go to the sink (once their copy landed) while range
-      // c+1 still re-ranks, up to the first range behind which an overflow was counted (those
-      // queries are redone and the report rendered again below; the bytes before stay the same)
-      int64_t s0 = 0;
-      const int64_t bound = dmlp_format_bound((int)Q);
-      bool sink_ok = a->report_sink != nullptr && !dr;
-      int64_t ready = 0;  // the copied bytes the sink may take: [a->report_sunk, ready)
-      int ready_c = -1;   // the range whose copy ends at `ready`
-      auto hand_over = [&]() {
-        if (ready_c < 0 || ready <= a->report_sunk) return;
-        spin_wait(w.ev_tc[ready_c]);
-        a->report_sink(a->report_sink_ctx, a->report_dst + a->report_sunk, ready - a->report_sunk);
-        a->report_sunk = ready;
-      };
-      for (int c = 0; c < ntail; ++c) {
-        spin_wait(w.ev_ts[c]);
-        const int64_t e = tend[c];
-        if (e < s0 || e > bound) throw Fail{-11};
-        if (e > s0)
-          CK(hipMemcpyAsync(a->report_dst + s0, text + s0, (size_t)(e - s0), hipMemcpyDeviceToHost,
-                            w.tail));
-        CK(hipEventRecord(w.ev_tc[c], w.tail));
-        s0 = e;
-        sink_ok = sink_ok && tovf[c] == 0;
-        hand_over();  // the previous range, under this one's copy and the next one's re-rank
-        if (sink_ok) {
-          ready = e;
-          ready_c = c;
-        }
-      }
-      hand_over();
-      CK(hipEventRecord(w.ev_tail, w.tail));
-      CK(hipStreamWaitEvent(st, w.ev_tail, 0));
-      ntail = 0;  // a later render (escalation, device-render redo) formats and copies it whole
-    }
     CK(mark(M_D2H, st));
     CK(hipEventRecord(w.ev_done, st));
     spin_wait(w.ev_done);
@@ -1565,7 +1399,6 @@ struct Step {
       a->early_waits = (int)small[2];
       a->early_grows = (int)small[3];
       a->early_timeouts = (int)small[4];
-      a->early_qwaits = (int)small[5];
       if (small[4] && g_early != 0) {
         std::fprintf(stderr, "[dmlp] early start: %d screen wave(s) timed out waiting for the "
                      "dataset image (overflowed queries were escalated); early start is off for "
@@ -1593,27 +1426,30 @@ struct Step {
     return 0;
   }
 
-  // early start: dataset image tiles [t0, t1) = slice i (its max norm into xnm_sl[i])
-  struct HxData {
-    HostOps* hx;
-    unsigned* words;
-    unsigned* xnm_sl;
-    int64_t nt, W;
-    int KT;
-  } hx_data_ctx_{};
+  // This rank's share of the node render plane's slices of kinds [what_lo, what_hi] (1 image,
+  // 2 rows; i % renderers == rank), rendered and published without consuming any.
+  void render_plane_share(const double* mu, int what_lo, int what_hi) {
+    const dmlp_plane* pl = a->plane;
+    if (!pl || pl->rank >= pl->renderers || a->N <= 0) return;
+    int64_t t0 = 0, t1 = 0;
+    const int ns = dmlp_plane_slice(a->N, a->A, 0, &t0, &t1);
+    for (int what = what_lo; what <= what_hi; ++what)
+      for (int i = pl->rank; i < ns; i += pl->renderers)
+        if (dmlp_plane_render(pl, a->X, a->Xr, a->N, a->A, mu, what, i) < 0) throw Fail{-9};
+  }
+
   // The dataset image from the node render plane: every slice (rendered by this rank or another)
   // copied from the segment into the device image xhi / xin on the side stream.  Early start
-  // (rdy != null): each slice's max norm -> xnm_sl[i], then its ready word.  Else the max over the
-  // slices -> *mx.  Returns 1 when some slice is outside the fp16 range.
-  int plane_image(const void* xhi, const float* xin, unsigned* rdy, unsigned* xnm_sl, float* mx) {
+  // (rdy != null): each slice's ready word (its norm bits) behind its copies.  Else the max over
+  // the slices -> *mx.  Returns 1 when some slice is outside the fp16 range.
+  int plane_image(const void* xhi, const float* xin, unsigned* rdy, float* mx) {
     const dmlp_plane* pl = a->plane;
     const int64_t N = a->N;
     const int A = a->A;
     const int64_t W = (int64_t)dmlp_screen_kt(A) * 32;
     void *img = nullptr, *xi = nullptr;
     CKL(dmlp_plane_regions(pl, N, A, &img, &xi, nullptr, nullptr));
-    unsigned* nh = w.sx_nm.get(2 + kEarlySlices);  // [0] the ready value, [2 + i] slice norms
-    nh[0] = 1u;
+    unsigned* nh = w.sx_nm.get(2 + kEarlySlices);  // [2 + i] slice i's ready word
     const int dly = rdy ? early_delay_us() : 0;
     int bad = 0;
     float m = 0.0f;
@@ -1622,43 +1458,47 @@ struct Step {
       int64_t t0 = 0, t1 = 0;
       dmlp_plane_slice(N, A, i, &t0, &t1);
       if (t1 > t0) {
-        CK(hipMemcpyAsync((short*)const_cast<void*>(xhi) + t0 * 64 * W,
-                          (const uint16_t*)img + t0 * 64 * W, (t1 - t0) * 64 * W * 2,
-                          hipMemcpyHostToDevice, w.side));
-        CK(hipMemcpyAsync(const_cast<float*>(xin) + t0 * 64, (const float*)xi + t0 * 64,
-                          (t1 - t0) * 64 * 4, hipMemcpyHostToDevice, w.side));
+        CK(dmlp::dma_copy((short*)const_cast<void*>(xhi) + t0 * 64 * W,
+                          (const uint16_t*)img + t0 * 64 * W, (t1 - t0) * 64 * W * 2, w.side));
+        CK(dmlp::dma_copy(const_cast<float*>(xin) + t0 * 64, (const float*)xi + t0 * 64,
+                          (t1 - t0) * 64 * 4, w.side));
       }
       bad |= bits & 1;
       m = std::max(m, nm);
       if (rdy) {
-        std::memcpy(nh + 2 + i, &nm, 4);
-        CK(put_word(xnm_sl + i, nh[2 + i], nh + 2 + i, w.side));
-        CK(put_word(rdy + i, 1u, nh, w.side));
+        nh[2 + i] = ready_bits(nm);
+        CK(dmlp::dma_copy(rdy + i, nh + 2 + i, 4, w.side));
       }
     }, [] {});
     if (mx) *mx = bad ? INFINITY : m;
     return bad;
   }
 
+  // early start: dataset image tiles [t0, t1) = slice i rendered on the host and copied, then its
+  // ready word (the slice's max norm bits; +inf when outside the fp16 range)
   int h2d_tiles_data(int64_t t0, int64_t t1, int i) {
-    const HxData& d = hx_data_ctx_;
+    const int64_t W = (int64_t)dmlp_screen_kt(a->A) * 32;
     double* mu = w.s_mu.p;
-    uint16_t* xhi_h = w.sx_hi.p;
-    float* xin_h = w.sx_in.p;
     unsigned* xnm_h = w.sx_nm.p + 2 + i;
-    short* xhi = (short*)const_cast<void*>(d.hx->xhi) + t0 * 64 * d.W;
-    float* xin = const_cast<float*>(d.hx->xin) + t0 * 64;
-    unsigned* xd = g_tune.word_write ? nullptr : d.xnm_sl + i;  // (null: no 4-byte copy)
+    short* xhi = (short*)const_cast<void*>(hx_->xhi) + t0 * 64 * W;
+    float* xin = const_cast<float*>(hx_->xin) + t0 * 64;
+    const int KT = dmlp_screen_kt(a->A);
     const int rc =
-        a->Xr ? dmlp_host_ops_h2d_tiles_rows(a->Xr, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT, xhi_h,
-                                             xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin, xd,
-                                             w.dq_hi.p, w.dq_n.p, 1, w.side)
-              : dmlp_host_ops_h2d_tiles(a->X, a->N, t0, t1, nullptr, 0, a->A, mu, d.KT, xhi_h,
-                                        xin_h, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin, xd, w.dq_hi.p,
-                                        w.dq_n.p, 1, w.side);
-    if (!xd && !(rc & 4)) CK(put_word(d.xnm_sl + i, *xnm_h, xnm_h, w.side));
+        a->Xr ? dmlp_host_ops_h2d_tiles_rows(a->Xr, a->N, t0, t1, nullptr, 0, a->A, mu, KT,
+                                             w.sx_hi.p, w.sx_in.p, xnm_h, w.sq_hi.p, w.sq_n.p, xhi,
+                                             xin, nullptr, w.dq_hi.p, w.dq_n.p, 1, w.side)
+              : dmlp_host_ops_h2d_tiles(a->X, a->N, t0, t1, nullptr, 0, a->A, mu, KT, w.sx_hi.p,
+                                        w.sx_in.p, xnm_h, w.sq_hi.p, w.sq_n.p, xhi, xin, nullptr,
+                                        w.dq_hi.p, w.dq_n.p, 1, w.side);
+    if (!(rc & 4)) {
+      float nm;
+      std::memcpy(&nm, xnm_h, 4);
+      *xnm_h = ready_bits(nm);
+      CK(dmlp::dma_copy(const_cast<unsigned*>(hx_->rdy) + i, xnm_h, 4, w.side));
+    }
     return rc;
   }
+  const HostOps* hx_ = nullptr;  // (run(): the host operands of the early start)
 };
 
 int drain_and_fail(Ctx* w, hipStream_t st, int code) {
@@ -1734,7 +1574,7 @@ extern "C" int dmlp_knn_local(const double* X, int64_t N, int A, const double* Q
     L.lab = out_label; L.cs = out_cs; L.exact = exact != 0; L.st = st;
     L.launch();
     int* h = w.small_h.get(8);
-    CK(hipMemcpyAsync(h, L.ovf, sizeof(int), hipMemcpyDeviceToHost, st));
+    CK(dmlp::dma_copy(h, L.ovf, sizeof(int), st));
     CK(hipStreamSynchronize(st));
     L.finish(h[0]);
     g_stats.n_exact = L.n_exact;
@@ -1773,7 +1613,7 @@ extern "C" int dmlp_step_emit(char* dst, int64_t bytes, void* stream) {
     Ctx& w = ctx();
     if (bytes < 0 || bytes > w.text_len) return -1;
     if (bytes == 0) return 0;
-    CK(hipMemcpyAsync(dst, w.d_text.p, (size_t)bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    CK(dmlp::dma_copy(dst, w.d_text.p, (size_t)bytes, (hipStream_t)stream));
     CK(hipStreamSynchronize((hipStream_t)stream));
     return 0;
   } catch (const Fail& f) {
@@ -1866,23 +1706,13 @@ extern "C" int dmlp_step_timeline(double* ms, const char** names, int cap) {
   }
 }
 
-// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render",
-// "qb_blocks", "word_write", "report_chunks", "x1_ring".  Returns the previous
-// value, or -1 for an unknown key.
+// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render".
+// Returns the previous value, or -1 for an unknown key.
 extern "C" int dmlp_pipeline_set(const char* key, int value) {
   const std::string k = key ? key : "";
-  if (k == "x1_ring") {  // the LDS-ring screen (screen_x1.hip): 0 off, 16 / 14 / 12
-    const int old = dmlp_get_x1_ring();
-    dmlp_set_x1_ring(value);
-    return old;
-  }
-  if (k == "x1_ring_force") return dmlp_set_x1_ring_force(value);  // ... on any grid (tests)
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
-           : k == "device_render" ? &g_tune.device_render
-           : k == "qb_blocks" ? &g_tune.qb_blocks
-           : k == "word_write" ? &g_tune.word_write
-           : k == "report_chunks" ? &g_tune.report_chunks : nullptr;
+           : k == "device_render" ? &g_tune.device_render : nullptr;
   if (!f) return -1;
   const int old = *f;
   *f = value;

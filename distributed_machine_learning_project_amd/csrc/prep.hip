@@ -369,7 +369,7 @@ static int host_ops_h2d_tiles(const double* X, const double* const* Xr, int64_t 
   int rc = 0;
   float m = 0.0f;
   auto h2d = [&](void* d, const void* h, int64_t bytes) {
-    if (bytes > 0 && hipMemcpyAsync(d, h, (size_t)bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (bytes > 0 && dmlp::dma_copy(d, h, (size_t)bytes, st) != hipSuccess)  // (staging page-locked)
       rc |= 4;
   };
   for (int c = 0; c < chunks; ++c) {

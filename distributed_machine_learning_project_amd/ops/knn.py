@@ -248,9 +248,7 @@ class StepArgs(C.Structure):
                 ("path", C.c_int),
                 ("early", C.c_int), ("n_escalated", C.c_int), ("early_waits", C.c_int),
                 ("early_grows", C.c_int), ("early_timeouts", C.c_int),
-                ("early_qwaits", C.c_int), ("host_ms", C.c_float), ("X32d", C.c_void_p),
-                ("report_sink", C.c_void_p), ("report_sink_ctx", C.c_void_p),
-                ("report_sunk", C.c_int64)]
+                ("host_ms", C.c_float), ("X32d", C.c_void_p)]
 
 
 class Plane(C.Structure):
@@ -274,17 +272,12 @@ class StepResult:
     early_waits: int = 0
     early_grows: int = 0
     early_timeouts: int = 0
-    early_qwaits: int = 0
-    report_sunk: int = 0   # report bytes handed to `sink` inside the step (the chunked tail)
-
-
-_SINK_T = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_int64)
 
 
 # calls the native step served and its early-start counters (bench.py reports them for the timed
 # region; tests check that the early start ran)
 STEP_STATS = {"calls": 0, "early": 0, "early_waits": 0, "early_grows": 0, "early_timeouts": 0,
-              "early_qwaits": 0, "escalated": 0, "device_path": 0, "host_ms": 0.0}
+              "escalated": 0, "device_path": 0, "host_ms": 0.0}
 _IO = {"h2d": 0, "d2h": 0}  # host <-> device bytes the steps issued (bench.py diagnostics)
 
 
@@ -298,7 +291,7 @@ def step_stats(reset: bool = False):
 
 def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_base=0,
          exact=False, report=None, lists=False, kstride=None, plane=None,
-         x32=None, sink=None) -> StepResult:
+         x32=None) -> StepResult:
     """One rank's whole Engine::KNN call from host arrays (dmlp_step): X_host [N, A] /
     Q_host [Q, A] fp64, labels_host [N] int32 (page-locked or registered memory for real
     overlap; a node-shared segment is), k_host [Q] int32.
@@ -311,9 +304,6 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
               node, slice by slice, by the plane's renderers into a node-shared segment.
       x32:    the dataset's rows already on this GPU as lossless int32 [N * A] (a torch tensor:
               the xGMI replica, parallel/strategies.py): no dataset rows cross PCIe.
-      sink:   with a report array and the chunked report tail (report_chunks > 1): sink(bytes) is
-              called inside the step with the report's leading pieces as their copies land;
-              StepResult.report_sunk counts them, the rest is only in `report`.
     Returns once everything is complete (one host sync in the common case)."""
     torch = _torch()
     L = _lib.lib()
@@ -361,19 +351,13 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     a.stream = _stream()
     a.plane = C.cast(C.pointer(plane), C.c_void_p) if plane is not None else None
     a.X32d = x32.data_ptr() if x32 is not None else None
-    cb = None
-    if sink is not None:
-        cb = _SINK_T(lambda _ctx, b, n: sink(C.string_at(b, n)))
-        a.report_sink = C.cast(cb, C.c_void_p)
     _lib.check(L.dmlp_step(C.byref(a)), "dmlp_step")
-    del cb
     st = pipeline_stats()
     STEP_STATS["calls"] += 1
     STEP_STATS["early"] += a.early
     STEP_STATS["early_waits"] += a.early_waits
     STEP_STATS["early_grows"] += a.early_grows
     STEP_STATS["early_timeouts"] += a.early_timeouts
-    STEP_STATS["early_qwaits"] += a.early_qwaits
     STEP_STATS["host_ms"] += a.host_ms
     STEP_STATS["escalated"] += a.n_escalated
     STEP_STATS["device_path"] += 1 if a.path == 2 else 0
@@ -385,8 +369,7 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     if _EVENTS[0]:
         _read_timeline()
     return StepResult(lab, cs, od, oi, int(a.report_len), a.path, a.early, a.n_escalated,
-                      int(st["n_exact"]), a.early_waits, a.early_grows, a.early_timeouts,
-                      a.early_qwaits, int(a.report_sunk))
+                      int(st["n_exact"]), a.early_waits, a.early_grows, a.early_timeouts)
 
 
 def step_emit(dst, nbytes: int):

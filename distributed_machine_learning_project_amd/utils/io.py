@@ -202,6 +202,21 @@ def generate(num_data, num_queries, num_attrs, vmin=0.0, vmax=1000.0, minK=16, m
     return KNNInput(labels, X, k, Qx)
 
 
+def write_input(path, inp: KNNInput) -> None:
+    """inp as the reference's input file at `path` — the bytes of to_text(inp), formatted by the
+    native library on its render pool (hundreds of MB for the multi-rank contract runs)."""
+    from .. import _lib
+    lab = np.ascontiguousarray(inp.labels, np.int32)
+    X = np.ascontiguousarray(inp.X, np.float64)
+    k = np.ascontiguousarray(inp.k, np.int32)
+    Qx = np.ascontiguousarray(inp.Qx, np.float64)
+    rc = _lib.lib().dmlp_cpu_write_input(str(path).encode(), lab.ctypes.data, X.ctypes.data,
+                                         X.shape[0], k.ctypes.data, Qx.ctypes.data, Qx.shape[0],
+                                         X.shape[1])
+    if rc != 0:
+        raise OSError(f"cannot write {path}")
+
+
 def to_text(inp: KNNInput) -> str:
     """Serialise a KNNInput in the reference input format (6 decimals, like generate_input.py)."""
     out = [f"{inp.N} {inp.Q} {inp.A}"]

@@ -107,8 +107,8 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     (dmlp_step_early_delay), so the screen provably waits mid-scan; the device counters then show
     waits > 0, eps growths > 0 (the far point sits in the last slice) and no timeout.  Two
     different inputs of equal shape alternate A, B, A, B (early on), then once with the early
-    start off.  The query operands cross in blocks behind the screen's launch (query-block early
-    start): each wave waits for its own block, counted apart; every report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
+    start off.  Each slice's ready word is one DMA copy carrying the slice's max norm; every
+    report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
     variant (one wave per SIMD, 404 of 512 registers).  A = 256 (KT = 8, all 512 registers): the
     step refuses the early start there — its image copies (blit kernels) would find no free wave
     slot beside the spinning screen — and the results stay exact.  One screen slice needs a full
@@ -119,7 +119,6 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
     old_dr = L.dmlp_pipeline_set(b"device_render", 1 if render == "device" else 0)
-    old_qb = L.dmlp_pipeline_set(b"qb_blocks", 16)  # the query-block early start on
     # an early-start step renders on the host whatever the switch says (the device render's
     # kernels get no reliable wave slots beside the spinning screen: pipeline.hip dr_early_ok)
     dr_used = False
@@ -149,139 +148,14 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
                 assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
             if not r.early and early and render == "device":
                 assert K.pipeline_stats()["device_render"] == 1  # (no early start: rendered first)
-            if r.early:  # (the queries in 16 blocks: DMLP_QB_BLOCKS)
+            if r.early:
                 assert r.early_timeouts == 0
                 assert r.early_waits > 0, "the screen never waited for a slice"
-                # query-block early start: the query blocks cross after the first (delayed) image
-                # slice, so waves waited for their own block
-                assert r.early_qwaits > 0, "no wave waited for its query block"
                 assert r.early_grows > 0, "no column's eps grew with a later slice"
     finally:
         L.dmlp_step_early(-1)
         L.dmlp_step_early_delay(-1)
         L.dmlp_pipeline_set(b"device_render", old_dr)
-        L.dmlp_pipeline_set(b"qb_blocks", old_qb)
-
-
-@pytest.mark.parametrize("chunks", [2, 3, 8])
-def test_report_chunked_tail(gpu, chunks):
-    """The chunked report tail (pipeline.hip Step::run, report_chunks): the re-rank runs in query
-    ranges, each range's lines are formatted at their absolute offsets behind it and its text is
-    copied while the next range re-ranks.  Early-start and plain steps on two alternated inputs,
-    then an input whose 120 copies of one point overflow the refine of the queries sitting on it
-    (those escalate and the whole report is rendered again): every report byte == the oracle's,
-    into a destination pre-filled with 0xAA each call (a range never copied would show).  Every
-    other call passes a report_sink: it must see exactly the report's leading bytes — all of them
-    when nothing escalated, none when a query of the first range overflowed."""
-    from distributed_machine_learning_project_amd import _lib
-    import torch
-    L = _lib.lib()
-    old = L.dmlp_pipeline_set(b"report_chunks", chunks)
-    Q = 131072 + 64 * 3
-    cases = _early_inputs(2000, 32, 16, Q, seed=500 + chunks)
-    dup = dmlp.generate(2000, Q, 32, 0.0, 1000.0, 1, 16, 8, seed=600 + chunks)
-    dup.X[1:121] = dup.X[0]
-    dup.Qx[[7, Q // 2, Q - 3]] = dup.X[0]
-    d, i = K.knn_cpu(dup.X, dup.Qx, dup.k)
-    lab_d, cs_d = K.finalize_cpu(i, dup.k, dup.labels)
-    cases.append((dup, lab_d, cs_d, dmlp.format_report(cs_d)))
-    dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
-    try:
-        for rnd, (ci, early) in enumerate(((0, 1), (1, 1), (0, 0), (1, 0), (2, 1), (2, 0), (2, 1),
-                                           (1, 0), (0, 1))):
-            L.dmlp_step_early(early)
-            inp, lab_ref, cs, expect = cases[ci]
-            dst[:] = 0xAA
-            pieces = []
-            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst,
-                       sink=pieces.append if rnd % 2 == 0 else None)
-            assert r.report_len == len(expect), f"round {rnd}"
-            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
-            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
-            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
-            assert r.early == early
-            # the sink (report_sink): the report's leading bytes, in order, during the step
-            assert b"".join(pieces) == expect[:r.report_sunk], f"round {rnd}"
-            if ci == 2:
-                assert r.n_escalated > 0, "the duplicated point overflowed no refine"
-                assert r.report_sunk == 0, "a range behind an overflow went to the sink"
-            else:
-                assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
-                if rnd % 2 == 0:
-                    assert r.report_sunk == r.report_len and len(pieces) >= 2, f"round {rnd}"
-    finally:
-        L.dmlp_step_early(-1)
-        L.dmlp_pipeline_set(b"report_chunks", old)
-
-
-@pytest.mark.parametrize("sub", [16, 14, 12])
-def test_screen_lds_ring(gpu, sub):
-    """The LDS-ring screen (screen_x1.hip RING > 0: 8 waves per workgroup share each fragment
-    tile through an LDS ring filled by LDS-DMA, ready / done counters instead of barriers) at
-    each of its sub-buffer depths: early-start steps (image slices delayed 400 us, query blocks
-    behind the launch) and plain steps, two inputs of one shape alternated through the reused
-    ring slots (94 tiles through 5 / 9 / 13 slots); every report, label and checksum == its
-    oracle's, no escalation, no timed-out wait, and the ring kernel is what ran."""
-    from distributed_machine_learning_project_amd import _lib
-    L = _lib.lib()
-    old_ring = L.dmlp_pipeline_set(b"x1_ring", sub)
-    old_qb = L.dmlp_pipeline_set(b"qb_blocks", 16)
-    Q = 131072 + 64 * 3  # 257 workgroups of 512 queries: one per CU and then some
-    cases = _early_inputs(6000, 32, 16, Q, seed=300 + sub)
-    import torch
-    dsts = [torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy() for _ in cases]
-    n0 = L.dmlp_x1_ring_launches()
-    try:
-        L.dmlp_step_early_delay(400)
-        for rnd, early in enumerate((1, 1, 0, 0)):
-            L.dmlp_step_early(early)
-            inp, lab_ref, cs, expect = cases[rnd % 2]
-            dst = dsts[rnd % 2]
-            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
-            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
-            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
-            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
-            assert r.early == early
-            assert r.n_escalated == 0, f"round {rnd}: {r.n_escalated} queries escalated"
-            if r.early:
-                assert r.early_timeouts == 0
-                assert r.early_waits > 0 and r.early_grows > 0
-        assert L.dmlp_x1_ring_launches() == n0 + 4
-    finally:
-        L.dmlp_step_early(-1)
-        L.dmlp_step_early_delay(-1)
-        L.dmlp_pipeline_set(b"x1_ring", old_ring)
-        L.dmlp_pipeline_set(b"qb_blocks", old_qb)
-
-
-@pytest.mark.parametrize("sub", [14, 12])
-def test_screen_lds_ring_slices(gpu, sub):
-    """The LDS-ring screen over many data slices (a small query set against a large dataset: the
-    step splits the scan into S slices to fill the chip, S % 8 == 0 maps a slice to one XCD) and
-    with k varying per query: report, labels and checksums == the oracle's, no escalation, and
-    the ring kernel ran."""
-    from distributed_machine_learning_project_amd import _lib
-    L = _lib.lib()
-    old_ring = L.dmlp_pipeline_set(b"x1_ring", sub)
-    old_force = L.dmlp_pipeline_set(b"x1_ring_force", 1)  # (a grid smaller than one WG per CU)
-    inp = dmlp.generate(60000, 8192 + 64, 32, 0.0, 1000.0, 1, 16, 8, seed=400 + sub)
-    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
-    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
-    import torch
-    dst = torch.empty(48 * len(inp.k) + 64, dtype=torch.uint8).pin_memory().numpy()
-    n0 = L.dmlp_x1_ring_launches()
-    try:
-        L.dmlp_step_early(0)
-        for _ in range(2):
-            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
-            assert bytes(dst[:r.report_len]) == dmlp.format_report(cs)
-            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
-            assert r.n_escalated == 0
-        assert L.dmlp_x1_ring_launches() >= n0 + 2
-    finally:
-        L.dmlp_step_early(-1)
-        L.dmlp_pipeline_set(b"x1_ring", old_ring)
-        L.dmlp_pipeline_set(b"x1_ring_force", old_force)
 
 
 def test_debug_listing(gpu, workload):

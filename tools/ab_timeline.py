@@ -23,4 +23,4 @@ for name, runs in acc.items():
     ns = runs[-1].get("native_step", {})
     print(f"{name:8s} ms/step {' '.join(f'{m:.3f}' for m in ms)} | " +
           " ".join(f"{k} {sum(v) / len(v):.3f}" for k, v in tl.items()) +
-          f" | qwaits/step {ns.get('early_query_block_waits', 0) / max(1, ns.get('timed_steps', 1)):.0f}")
+          "")

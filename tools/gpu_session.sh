@@ -22,22 +22,16 @@
 #   split      kernel split of the local pipeline at Q = 131072 / 65536 / 32768 (S = 1 / 2 / 4)
 #   merge      K4 merge micro-benchmark (P=8, Q=131072, k=16/128) under rocprofv3 --stats
 #   hostprof   cProfile of the step loop (tools/host_profile.py) + per-call host phase clocks
-#   qb         query-block early start A/B (DMLP_QB_BLOCKS / DMLP_QB_LEAD), step timelines
-#   dr         device render A/B (DMLP_DEVICE_RENDER, DMLP_QB_BLOCKS), step timelines
-#   ww         early-start ready words by stream write-value packets (DMLP_WORD_WRITE) A/B
+#   dr         device render A/B (DMLP_DEVICE_RENDER), step timelines
 #   plane      node render plane rehearsal: bench.py --gpus 3 / 8 on the one GPU, plane on / off
 #   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
+#   blits      copy-engine probe + every runtime kernel / SDMA copy of 6 native steps (step_driver)
+#   lnr        large-N steps: host vs device render at N 1e6 / 1e7 (step_driver)
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
-#   ring       the LDS-ring screen: GPU tests, kernel medians and ms/step off / 16 / 14 / 12
-#   x1mode     screen MODES (e.g. MODES="1024 512") vs production: tests, kernel medians, ms/step
-#   qbsmall    query-block early start with 2 / 4 blocks and write-value words vs the default
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
-#   tail       the chunked report tail: tests, --verify, A/B DMLP_REPORT_CHUNKS 0 / 2 / 4 / 8
-#   sinktail   the drop-in report written from inside the step (KNN_REPORT_TAIL 0 / 2 / 4), contract A/B
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
-#   ringpmc    counter passes of the screen without / with the ring (RINGS="0 12")
 set -u
 TAG=${1:?tag}
 shift
@@ -73,11 +67,6 @@ for task in "$@"; do
       step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
     exact)
       step exact 300 python bench.py --exact --steps 5 --warmup 1 ;;
-    x1modes)  # k_screen_x1 ablations: production / no hits after the first compaction / MFMA+loads only / event counters
-      step x1modes 300 rocprofv3 --kernel-trace --stats -d "$OUT/x1modes" -o run --output-format csv \
-          -- python3 tools/quick_gpu_bench.py --q 131072 --iters 5 --check 0 --modes 0,128,2,0,128,8
-      grep -h "mode\|per call" "$OUT/x1modes.log"
-      find "$OUT/x1modes" -name '*kernel_stats.csv' -exec sh -c 'grep k_screen_x1 "$1" | cut -c1-200' _ {} \; ;;
     early)  # native step early start (default) -- its tests, verify, interleaved step A/B against DMLP_FAST_EARLY=0
       step early_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
           --timeout-method thread -k "native_step"
@@ -87,35 +76,6 @@ for task in "$@"; do
     qchunks)  # early start: query render slices 2 / 4 / 6 (DMLP_FAST_QCHUNKS), interleaved
       AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step qchunks_ab 900 bash tools/kernel_ab.sh \
           q2:DMLP_FAST_QCHUNKS=2 q4:DMLP_FAST_QCHUNKS=4 q6:DMLP_FAST_QCHUNKS=6 ;;
-    tail)  # the chunked report tail (DMLP_REPORT_CHUNKS): GPU tests, --verify, A/B off / 2 / 4 / 8
-      step tail_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
-          --timeout-method thread -k "report_chunked or native_step"
-      DMLP_REPORT_CHUNKS=4 step tail_verify 300 python bench.py --steps 50 --warmup 2 --verify
-      AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step tail_ab 900 bash tools/kernel_ab.sh \
-          c0:DMLP_REPORT_CHUNKS=0 c2:DMLP_REPORT_CHUNKS=2 c4:DMLP_REPORT_CHUNKS=4 c8:DMLP_REPORT_CHUNKS=8
-      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/tail_ab_timeline.txt" ;;
-    sinktail)  # the one-rank drop-in's report written from inside the step (KNN_REPORT_TAIL): GPU
-               # tests, the contract at 0 / 2 / 4 interleaved, stdout bytes equal at Q = 131072
-      step sink_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
-          --timeout-method thread -k "report_chunked or native_step or dropin"
-      for R in 1 2; do
-        for T in 0 2 4; do
-          KNN_REPORT_TAIL=$T step contract_t${T}_$R 600 python bench.py --harness dropin --steps 10 \
-              --warmup 1
-        done
-      done
-      python -m distributed_machine_learning_project_amd.build --dropin \
-          distributed_machine_learning_project_amd/_refharness/common.cpp --dropin-out /tmp/eng_dropin
-      python tools/generate_input.py --num_data 100000 --num_queries 131072 --num_attrs 32 --min 0 \
-          --max 1000 --minK 16 --maxK 16 --num_labels 10 --output /tmp/dropin_bench.in > /dev/null
-      for T in 0 2 4; do
-        KNN_REPORT_TAIL=$T KNN_TRACE=1 timeout -k 10 120 /tmp/eng_dropin < /tmp/dropin_bench.in \
-            > /tmp/dropin_t$T.out 2> "$OUT/dropin_trace_t$T.txt" || exit 1
-      done
-      cmp /tmp/dropin_t0.out /tmp/dropin_t2.out && cmp /tmp/dropin_t0.out /tmp/dropin_t4.out && \
-          echo "report bytes equal at KNN_REPORT_TAIL 0 / 2 / 4" | tee "$OUT/sink_cmp.txt" || exit 1
-      grep -ho '"time_ms_median": [0-9.]*\|"knn_ms_median": [0-9.]*\|"emit_ms_median": [0-9.]*' \
-          "$OUT"/contract_t*.log | tee "$OUT/contract_medians.txt" ;;
     warm)  # the headline bench after a 3 s warm-up instead of 0.6 s (box-to-box host variance)
       step bench_warm3 300 python bench.py --min-warmup-s 3 ;;
     prof)
@@ -188,10 +148,6 @@ for task in "$@"; do
     hostprof)
       step hostprof 300 python tools/host_profile.py --steps 100
       DMLP_PIPE_DEBUG=1 step pipedebug 120 python bench.py --steps 5 --warmup 2 --no-busbw ;;
-    qb)  # query-block early start: off / 16 blocks (lead 1, 2) / 8 blocks, interleaved
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step qb_ab 900 bash tools/kernel_ab.sh qb0:DMLP_QB_BLOCKS=0 \
-          qb16:DMLP_QB_BLOCKS=16 qb16l2:DMLP_QB_BLOCKS=16,DMLP_QB_LEAD=2 qb8:DMLP_QB_BLOCKS=8
-      python3 tools/ab_timeline.py gpurun_out/ab ;;
     dr)  # device render of the screen operands: host render / device render, +/- query blocks
       # (the early-start bench shape renders on the host either way: Q = 32768 per step, no early
       # start, and the bench shape with the early start off)
@@ -203,14 +159,6 @@ for task in "$@"; do
           noearly_dr:DMLP_DEVICE_RENDER=1,DMLP_FAST_EARLY=0
       python3 tools/ab_timeline.py gpurun_out/ab > "$OUT/dr_bench.txt"
       cat "$OUT/dr_q32k.txt" "$OUT/dr_bench.txt" ;;
-    ww)  # early-start ready words as stream write-value packets instead of 4-byte blit copies,
-         # with and without the query-block early start; the early-start tests under the switch
-      DMLP_WORD_WRITE=1 step ww_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
-          --timeout 120 --timeout-method thread -k "early_start or native_step"
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ww_ab 900 bash tools/kernel_ab.sh base:DMLP_WORD_WRITE=0 \
-          ww:DMLP_WORD_WRITE=1 wwqb16:DMLP_WORD_WRITE=1,DMLP_QB_BLOCKS=16 \
-          wwqb8l2:DMLP_WORD_WRITE=1,DMLP_QB_BLOCKS=8,DMLP_QB_LEAD=2
-      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/ww_ab.txt" ;;
     plane)  # node render plane: P = 3 / 8 ranks sharing the one GPU (host-staged plane), --verify,
             # plane on / off: per-rank ms, the cgroup's CPU time in the timed region
       for P in 3 8; do
@@ -235,32 +183,6 @@ for task in "$@"; do
         KNN_DATA_PLANE=host step native_p$P 600 python bench.py --harness native --gpus $P --steps 5 \
             --warmup 1 --q-per-gpu 65536 --ingress shm
       done ;;
-    ring)  # the LDS-ring screen (DMLP_X1_RING): its GPU tests, then off / 16 / 14 / 12 under the
-           # kernel tracer (screen medians) and as plain bench runs (ms/step)
-      step ring_tests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 180 \
-          --timeout-method thread -k "lds_ring"
-      AB_ROUNDS=2 AB_STEPS=30 step ring_prof 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
-          r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
-      python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/ring_kernels.txt"; rm -rf gpurun_out/ab
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step ring_ab 900 bash tools/kernel_ab.sh off:DMLP_X1_RING=0 \
-          r16:DMLP_X1_RING=16 r14:DMLP_X1_RING=14 r12:DMLP_X1_RING=12
-      grep -h '"ms_per_step"' "$OUT"/ring_ab.log | tee "$OUT/ring_ms.txt" ;;
-    x1mode)  # screen modes against the production one (MODES, e.g. "1024 512"): the screen / step
-             # tests on the production mode, kernel medians, plain ms/step
-      step x1mode_tests 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
-          --timeout 180 --timeout-method thread -k "screen or x1 or native_step or early_start or single_term"
-      V=(m0:DMLP_X1_MODE=0)
-      for M in ${MODES:?MODES}; do V+=(m$M:DMLP_X1_MODE=$M); done
-      AB_ROUNDS=2 AB_STEPS=30 step x1mode_prof 600 bash tools/kernel_ab.sh "${V[@]}"
-      python3 tools/ab_summary.py gpurun_out/ab | tee "$OUT/x1mode_kernels.txt"; rm -rf gpurun_out/ab
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step x1mode_ab 600 bash tools/kernel_ab.sh "${V[@]}" ;;
-    qbsmall)  # the query-block early start with few blocks and write-value words, blocks first / after
-              # the first image slice, against the default
-      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=200 step qbsmall_ab 900 bash tools/kernel_ab.sh base:DMLP_QB_BLOCKS=0 \
-          qb2l0:DMLP_QB_BLOCKS=2,DMLP_QB_LEAD=0,DMLP_WORD_WRITE=1 \
-          qb4l0:DMLP_QB_BLOCKS=4,DMLP_QB_LEAD=0,DMLP_WORD_WRITE=1 \
-          qb2l1:DMLP_QB_BLOCKS=2,DMLP_QB_LEAD=1,DMLP_WORD_WRITE=1
-      python3 tools/ab_timeline.py gpurun_out/ab | tee "$OUT/qbsmall_ab.txt" ;;
     exact64)  # the exact path at A = 48 / 64 on the fp64 MFMA screen vs the VALU kernel, --verify
       for A in 48 64; do
         step exact_a${A}_f64 300 python bench.py --exact --attrs $A --steps 3 --warmup 1 \
@@ -284,18 +206,6 @@ for task in "$@"; do
         KNN_PREWARM_US=$US step prewarm_$US 300 python bench.py --harness dropin --steps 10 --warmup 1
       done
       grep -ho '"knn_ms_median": [0-9.]*' "$OUT"/prewarm_*.log ;;
-    ringpmc)  # counters of the screen without / with the LDS ring (RINGS, default "0 12")
-      for R in ${RINGS:-0 12}; do
-        n=0
-        for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
-                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM" \
-                 "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"; do
-          n=$((n + 1))
-          DMLP_X1_RING=$R step ringpmc${R}_$n 120 rocprofv3 --kernel-trace --pmc $C -d "$OUT/ringpmc${R}_$n" \
-              -o run --output-format csv -- python3 tools/quick_gpu_bench.py --q 131072 --iters 2 --check 0
-        done
-      done
-      python3 tools/pmc_summary.py "$OUT" > "$OUT/ringpmc_summary.txt"; cat "$OUT/ringpmc_summary.txt" ;;
     blits)  # which copies / memsets the runtime runs as kernels (tests/native/copy_kind_probe.cpp,
             # built to tools/bin), then every runtime kernel and SDMA copy of 4 bench steps
       step copykind 120 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/ck" -o run \

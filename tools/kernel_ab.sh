@@ -3,7 +3,7 @@
 # X (an alternative build of the library at ab/libdmlp_X.so, loaded through DMLP_LIB) or
 # NAME:VAR=VAL[,VAR=VAL...] (the tree's library with those environment switches).
 #   gpurun -- bash tools/kernel_ab.sh A B                            # library builds, kernel trace
-#   gpurun -- bash tools/kernel_ab.sh base: ct8:DMLP_X1_CT=8          # environment switches
+#   gpurun -- bash tools/kernel_ab.sh base: early0:DMLP_FAST_EARLY=0          # environment switches
 #   AB_PROF=0 AB_ROUNDS=3 gpurun -- bash tools/kernel_ab.sh c1:DMLP_HOST_OPS_CHUNKS=1 c2:DMLP_HOST_OPS_CHUNKS=2
 # AB_ARGS: extra bench.py arguments (e.g. "--q-per-gpu 32768").
 # AB_PROF=1 (default): rocprofv3 --kernel-trace --stats per run (tools/ab_summary.py reads the

@@ -38,7 +38,6 @@ def main():
         for m in [int(x) for x in a.modes.split(",")]:
             _lib.lib().dmlp_set_screen_mode(m)
             _lib.lib().dmlp_set_stream_mode(m)
-            _lib.lib().dmlp_set_x1_mode(m)
             ts = []
             for it in range(a.iters + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -68,14 +67,8 @@ def main():
                 calls = a.iters + 1
                 print("  per call: wave-steps %.4g  cand-path %.4g  appends %.4g  compactions %.4g"
                       % tuple(float(x) / calls for x in cnt[:4]))
-                c3 = np.zeros(8, np.uint64)
-                _lib.lib().dmlp_x1_debug_counters(c3.ctypes.data, 1)
-                if c3[0]:
-                    print("  x1 per call: wave-steps %.4g  cand-path %.4g  appends %.4g  "
-                          "batch compactions %.4g" % tuple(float(x) / calls for x in c3[:4]))
         _lib.lib().dmlp_set_screen_mode(0)
         _lib.lib().dmlp_set_stream_mode(0)
-        _lib.lib().dmlp_set_x1_mode(0)
         return
     inp = dmlp.generate(a.n, a.q, a.a, 0.0, 1000.0, a.kmin, a.kmax, 10, seed=42)
     X = torch.from_numpy(inp.X).cuda()

@@ -1,10 +1,9 @@
 """Micro-benchmark of the single-term screen (screen_x1.hip k_screen_x1) exactly as the native
 step runs it at the bench shape: the host's fp16 operands (host_prep.cpp), one data slice,
-every query in one launch — timed alone with hipEvents, per kernel variant / ablation mode
-(dmlp_set_x1_mode), interleaved over rounds.  Modes that keep the results (0, 256, 8) are also
-checked end to end: the native step's whole report under that mode == the fp64 oracle's.
+every query in one launch — timed alone with hipEvents over rounds, and checked end to end: the
+native step's whole report == the fp64 oracle's.
 
-    python tools/screen_bench.py --modes 0,256 --rounds 3 --iters 20
+    python tools/screen_bench.py --rounds 3 --iters 20
 """
 import argparse
 import ctypes as C
@@ -20,8 +19,6 @@ import distributed_machine_learning_project_amd as dmlp  # noqa: E402
 from distributed_machine_learning_project_amd import _lib  # noqa: E402
 from distributed_machine_learning_project_amd.ops import knn as K  # noqa: E402
 
-EXACT_MODES = {0, 8, 256, 264}  # modes whose results equal the production kernel's
-
 
 def main():
     ap = argparse.ArgumentParser()
@@ -29,7 +26,6 @@ def main():
     ap.add_argument("--q", type=int, default=131072)
     ap.add_argument("--a", type=int, default=32)
     ap.add_argument("--k", type=int, default=16)
-    ap.add_argument("--modes", default="0,256")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--verify", type=int, default=1)
@@ -71,8 +67,8 @@ def main():
 
     NS = 8
     rt = (nt + NS - 1) // NS
-    rdy = torch.ones(NS, dtype=torch.int32, device=dev)  # every slice "landed"
-    xsl = torch.from_numpy(np.full(NS, xnm[0], np.uint32).view(np.int32)).to(dev)
+    # every slice "landed": its ready word carries the image's max norm bits (nonzero)
+    rdy = torch.from_numpy(np.full(NS, max(int(xnm[0]), 1), np.uint32).view(np.int32)).to(dev)
     est = torch.zeros(4, dtype=torch.int32, device=dev)
 
     def launch():
@@ -80,8 +76,8 @@ def main():
             rc = L.dmlp_screen_x1_early(KT, A, d_xhi.data_ptr(), d_xin.data_ptr(), nt, N,
                                         d_qhi.data_ptr(), d_qn.data_ptr(), d_qi.data_ptr(),
                                         d_k.data_ptr(), Q, a.k, wp + 4, rdy.data_ptr(), rt, NS,
-                                        xsl.data_ptr(), ci.data_ptr(), cc.data_ptr(),
-                                        ch.data_ptr(), est.data_ptr(), s)
+                                        ci.data_ptr(), cc.data_ptr(), ch.data_ptr(),
+                                        est.data_ptr(), s)
         else:
             rc = L.dmlp_screen_x1(KT, 1, A, d_xhi.data_ptr(), d_xin.data_ptr(), nt, N,
                                   d_qhi.data_ptr(), d_qn.data_ptr(), d_qi.data_ptr(),
@@ -89,8 +85,7 @@ def main():
                                   cc.data_ptr(), ch.data_ptr(), s)
         assert rc == 0, rc
 
-    modes = [int(m) for m in a.modes.split(",")]
-    res = {m: [] for m in modes}
+    res = []
     expect = None
     if a.verify:
         _, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
@@ -98,28 +93,24 @@ def main():
         expect = dmlp.format_report(cs)
         dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
     for rnd in range(a.rounds):
-        for m in modes:
-            L.dmlp_set_x1_mode(m)
+        launch()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.iters)]
+        for it in range(a.iters):
+            ev[2 * it].record()
             launch()
-            torch.cuda.synchronize()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.iters)]
-            for it in range(a.iters):
-                ev[2 * it].record()
-                launch()
-                ev[2 * it + 1].record()
-            torch.cuda.synchronize()
-            res[m] += [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.iters)]
-            if a.verify and rnd == 0 and m in EXACT_MODES:
-                r = K.step(inp.X, inp.labels, (0, 10), inp.Qx, inp.k, report=dst)
-                ok = bytes(dst[:r.report_len]) == expect
-                print(f"mode {m}: native step report == oracle: {ok} (path {r.path}, early "
-                      f"{r.early}, escalated {r.n_escalated})", flush=True)
-                assert ok
-    L.dmlp_set_x1_mode(0)
-    for m in modes:
-        v = np.array(res[m])
-        print(f"mode {m:4d}: k_screen_x1 median {np.median(v):.4f} ms  p10 {np.percentile(v, 10):.4f}"
-              f"  p90 {np.percentile(v, 90):.4f}  (n={len(v)})", flush=True)
+            ev[2 * it + 1].record()
+        torch.cuda.synchronize()
+        res += [ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(a.iters)]
+        if a.verify and rnd == 0:
+            r = K.step(inp.X, inp.labels, (0, 10), inp.Qx, inp.k, report=dst)
+            ok = bytes(dst[:r.report_len]) == expect
+            print(f"native step report == oracle: {ok} (path {r.path}, early {r.early}, "
+                  f"escalated {r.n_escalated})", flush=True)
+            assert ok
+    v = np.array(res)
+    print(f"k_screen_x1 median {np.median(v):.4f} ms  p10 {np.percentile(v, 10):.4f}"
+          f"  p90 {np.percentile(v, 90):.4f}  (n={len(v)})", flush=True)
 
 
 if __name__ == "__main__":
