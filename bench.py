@@ -236,7 +236,6 @@ def main(argv=None):
                                 "early_start_calls": steps_native["early"],
                                 "early_waits": steps_native["early_waits"],
                                 "early_timeouts": steps_native["early_timeouts"],
-                                "early_query_block_waits": steps_native["early_qwaits"],
                                 # host time per step until everything was issued (render / int32
                                 # pack, plane waits): the per-rank host budget
                                 "host_issue_ms_per_step": round(
@@ -271,23 +270,21 @@ def main(argv=None):
         extra["verify_ok"] = got == ref
         extra["verify_s"] = round(time.perf_counter() - t_v, 1)
 
-    if comm.is_root and world == 1 and a.contract_runs > 0 and comm.on_gpu:
+    if a.contract_runs > 0 and comm.on_gpu:
         # the same config through the reference's own contract (bench_4's binary is timed this
-        # way by run_bench.sh:114-120): fresh processes, median of their Engine::KNN clocks
-        try:
-            t_c = time.perf_counter()
-            res, src = _contract_runs(a, True, (("bench", Q),), a.contract_runs, 0)
-            b = res["bench"]
-            extra["reference_contract"] = {
-                "harness": f"engine.h drop-in + {src}, one process per run, stdout to a file",
-                "runs": b["runs"], "time_ms_median": b["time_ms_median"],
-                "time_ms_min": b["time_ms_min"],
-                "knn_ms_median": b.get("knn_ms_median"), "emit_ms_median": b.get("emit_ms_median"),
-                "harness_time_taken_ms": b.get("harness_time_taken_ms"),
-                "queries_per_s": round(Q / (b["time_ms_median"] / 1e3), 1),
-                "wall_s": round(time.perf_counter() - t_c, 1)}
-        except Exception as e:  # noqa: BLE001 — a diagnostic beside the headline, never fatal
-            extra["reference_contract"] = {"error": str(e)[-300:]}
+        # way by run_bench.sh:114-120): fresh processes, median of their Engine::KNN clocks.  One
+        # GPU: the drop-in run directly with stdout to a file, and as run_bench.sh:84 launches it
+        # (mpiexec, stdout a pipe to the launcher, which writes the file).  P GPUs: rank 0 runs
+        # the drop-in at P ranks through the node window (mpiexec -n P), the others wait.
+        if comm.is_root:
+            runs = ((("reference_contract", 1, "direct", a.contract_runs),
+                     ("reference_contract_mpiexec", 1, "mpiexec", a.contract_runs)) if world == 1
+                    else (("reference_contract_node", world, "mpiexec",
+                           min(2, a.contract_runs)),))
+            for key, P, launcher, nrun in runs:
+                extra[key] = _contract_entry(a, Q, P, launcher, nrun)
+        if world > 1:
+            comm.barrier()
     if comm.is_root:
         value = Q / (ms / 1e3)
         line = {
@@ -347,6 +344,30 @@ def _cgroup_cpu_stat():
     except (OSError, ValueError, StopIteration):
         pass
     return {}
+
+
+def _contract_entry(a, Q, P, launcher, nrun):
+    """One reference-contract record for the bench JSON (never fatal: an error is recorded)."""
+    try:
+        t_c = time.perf_counter()
+        res, src = _contract_runs(a, True, (("bench", Q),), nrun, 0, P=P, launcher=launcher)
+        b = res["bench"]
+        how = ("one process per run, stdout to a file" if launcher == "direct" else
+               f"mpiexec -n {P} per run (run_bench.sh:84,120), stdout a pipe to the launcher "
+               f"which writes a file")
+        out = {"harness": f"engine.h drop-in + {src}, {how}", "ranks": P,
+               "runs": b["runs"], "time_ms_median": b["time_ms_median"],
+               "time_ms_min": b["time_ms_min"],
+               "knn_ms_median": b.get("knn_ms_median"), "emit_ms_median": b.get("emit_ms_median"),
+               "harness_time_taken_ms": b.get("harness_time_taken_ms"),
+               "queries_per_s": round(Q / (b["time_ms_median"] / 1e3), 1),
+               "wall_s": round(time.perf_counter() - t_c, 1)}
+        for key in ("window", "stdout_fifo", "vmsplice_bytes"):
+            if key in b:
+                out[key] = b[key]
+        return out
+    except Exception as e:  # noqa: BLE001 — a diagnostic beside the headline, never fatal
+        return {"error": str(e)[-300:], "ranks": P}
 
 
 def _world_report(comm, host_plane, a):
@@ -466,16 +487,18 @@ def _bench_native(a):
     _print_native(a, res, harness_src, dropin, P, steps, kmin)
 
 
-def _contract_runs(a, dropin, shapes, steps, warmup):
+def _contract_runs(a, dropin, shapes, steps, warmup, P=None, launcher="direct"):
     """Fresh processes through the reference contract at each (tag, Q) of shapes: the drop-in
-    (engine.h + the reference's common.cpp) or knn_engine.  Returns ({tag: entry}, harness)."""
+    (engine.h + the reference's common.cpp) or knn_engine, at P ranks (default --gpus) — one
+    rank run directly ("direct") or under mpiexec ("mpiexec", as run_bench.sh launches it: the
+    engine's stdout is then a pipe to the launcher).  Returns ({tag: entry}, harness)."""
     import json as _json
     import statistics
     import subprocess
     import tempfile
 
     from distributed_machine_learning_project_amd import build
-    from distributed_machine_learning_project_amd.utils.io import generate, to_text
+    from distributed_machine_learning_project_amd.utils.io import generate, write_input
 
     harness_src = None
     if dropin:
@@ -495,7 +518,8 @@ def _contract_runs(a, dropin, shapes, steps, warmup):
                                      extra_flags=['-DDMLP_COMMON_HEADER="contract_types.h"'])
     else:
         exe = build.build_engine()
-    P = max(1, a.gpus)
+    P = max(1, a.gpus if P is None else P)
+    mpi = P > 1 or launcher == "mpiexec"
     kmin = a.k if a.kmin is None else a.kmin
     kmax = max(kmin, a.k if a.kmax is None else a.kmax)
     res = {}
@@ -503,15 +527,14 @@ def _contract_runs(a, dropin, shapes, steps, warmup):
         for tag, q in shapes:
             inp = generate(a.n_data, q, a.attrs, 0.0, 1000.0, kmin, kmax, a.labels, seed=42)
             path = os.path.join(td, f"{tag}.in")
-            with open(path, "w") as f:
-                f.write(to_text(inp))
-            times, out0, harness_ms, parts = [], None, [], {}
+            write_input(path, inp)
+            times, out0, harness_ms, parts, extra_last = [], None, [], {}, {}
             for r in range(warmup + steps):
                 met = os.path.join(td, f"{tag}_{r}.json")
                 env = dict(os.environ, KNN_METRICS=met, KNN_STRATEGY=a.strategy,
                            KNN_INGRESS=a.ingress)  # shm: per-GPU ingress from a shared window
-                cmd = ([] if P == 1 else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [str(exe)]
-                if dropin and P > 1:  # each rank opens the input (MPICH stdin forwarding: H5)
+                cmd = ([] if not mpi else ["/opt/conda/bin/mpiexec", "-n", str(P)]) + [str(exe)]
+                if dropin and mpi:  # each rank opens the input (MPICH stdin forwarding: H5)
                     import shlex
                     cmd = cmd[:-1] + ["sh", "-c", f"exec {shlex.quote(str(exe))} < "
                                                   f"{shlex.quote(path)}"]
@@ -523,8 +546,9 @@ def _contract_runs(a, dropin, shapes, steps, warmup):
                 # time this process's reader draining 6 MB of report, not the engine
                 outp, errp = os.path.join(td, "out.txt"), os.path.join(td, "err.txt")
                 with open(path, "rb") as fin, open(outp, "wb") as fo, open(errp, "wb") as fe:
-                    rc = subprocess.run(cmd, stdin=fin if dropin and P == 1 else None,
-                                        stdout=fo, stderr=fe, env=env, timeout=600).returncode
+                    rc = subprocess.run(cmd, stdin=fin if dropin and not mpi else None,
+                                        stdout=fo, stderr=fe, env=env,
+                                        timeout=600 if P == 1 else 300).returncode
                 pr = subprocess.CompletedProcess(cmd, rc, open(outp, "rb").read(),
                                                  open(errp, "rb").read())
                 if pr.returncode != 0:
@@ -538,6 +562,9 @@ def _contract_runs(a, dropin, shapes, steps, warmup):
                     for key in ("pack_ms", "knn_ms", "emit_ms", "step_ms"):
                         if key in mj:
                             parts.setdefault(key, []).append(float(mj[key]))
+                    for key in ("window", "stdout_fifo", "vmsplice_bytes"):  # (the last run's)
+                        if key in mj:
+                            extra_last[key] = mj[key]
                     for rk in range(1, P):  # the drop-in's node window: each rank's step time
                         rp = f"{met}.r{rk}"
                         if os.path.exists(rp):
@@ -553,6 +580,7 @@ def _contract_runs(a, dropin, shapes, steps, warmup):
                      "time_ms_min": round(min(times), 3), "runs": len(times)}
             if harness_ms:
                 entry["harness_time_taken_ms"] = harness_ms
+            entry.update(extra_last)
             for key, v in parts.items():
                 entry[key + "_median"] = round(statistics.median(v), 3)
             if tag == "q1000":

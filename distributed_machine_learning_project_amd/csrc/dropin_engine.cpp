@@ -25,9 +25,17 @@
 //   * -DDEBUG build (engine.debug, Makefile:14-15 compiles this file with -DDEBUG as well):
 //     every query's sorted (distance, id) list and label go to the harness's reportResult, which
 //     prints the DEBUG listing itself (common.cpp:72-78).
+#include <fcntl.h>
 #include <mpi.h>
+#include <sys/ioctl.h>
+#include <sys/prctl.h>
+#include <sys/stat.h>
+#include <sys/uio.h>
+#include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <fstream>
@@ -41,9 +49,9 @@
 namespace {
 
 // The node window (P > 1, every rank on one node): [control 64 KiB | labels | k | query rows |
-// report text | render plane], rank 0's MPI-3 shared allocation, mapped and page-locked by every
-// rank.  Sized once in the MPI_Init hook (KNN_WINDOW_MB, default 512) and grown collectively when
-// a call's input does not fit.
+// report text | render plane | P fetch scratch regions], rank 0's MPI-3 shared allocation,
+// mapped and page-locked by every rank.  Sized once in the MPI_Init hook (KNN_WINDOW_MB, default
+// 1024) and grown collectively when a call's input does not fit.
 struct NodeWindow {
   MPI_Comm node = MPI_COMM_NULL;
   MPI_Win win = MPI_WIN_NULL;
@@ -52,10 +60,10 @@ struct NodeWindow {
   bool registered = false, gpu = false;
   int64_t gen = 0;  // calls through the window (every rank counts the same calls)
   struct Layout {
-    int64_t labels, k, qx, out, plane, plane_bytes, total;
+    int64_t labels, k, qx, out, plane, plane_bytes, scratch, scratch_bytes, scratch_q, total;
   };
   static int64_t up(int64_t b) { return (b + 4095) & ~int64_t(4095); }
-  static Layout layout(int64_t N, int64_t Q, int A) {
+  static Layout layout(int64_t N, int64_t Q, int A, int P) {
     Layout L;
     L.labels = 65536;
     L.k = L.labels + up(N * 4);
@@ -63,11 +71,21 @@ struct NodeWindow {
     L.out = L.qx + up(Q * A * 8);
     L.plane = L.out + up(dmlp_format_bound((int)std::max<int64_t>(Q, 1)));
     L.plane_bytes = std::max<int64_t>(0, dmlp_plane_bytes(N, A, 1));
-    L.total = L.plane + up(L.plane_bytes);
+    L.scratch = L.plane + up(L.plane_bytes);
+    // per rank: the heap span of its query rows and of its share of the dataset's rows (the CMA
+    // front reads each span in one piece when the rows lie dense in rank 0's heap: the harness's
+    // vectors sit ~A * 8 + 16 bytes apart)
+    const int64_t qb = (Q + P - 1) / P, nb = (N + P - 1) / P;
+    L.scratch_q = up(3 * qb * (A * 8 + 32) / 2 + (1 << 20));
+    L.scratch_bytes = L.scratch_q + up(3 * nb * (A * 8 + 32) / 2 + (1 << 20));
+    L.total = L.scratch + P * L.scratch_bytes;
     return L;
   }
-  // control words: [0] the call's flag (labels, k and the plane header are in place), [8 + r]
-  // rank r's query rows are in place (both = the call's generation)
+  // control words (int64): [kGen] the call's flag (the published pointers, labels, k and the
+  // plane header are in place), [kMode] the front (1 CMA, 2 fill), [kPtr..] rank 0's table / k /
+  // labels addresses, [kT0] rank 0's KNN entry (steady_clock ns), [kRows + r] rank r's query rows
+  // are in place (fill), [kFetch + r] rank r's fetch done (ns, metrics)
+  enum { kGen = 0, kMode = 1, kPtr = 2, kT0 = 6, kRows = 8, kFetch = 1024 };
   int64_t* ctrl() { return (int64_t*)base; }
   bool valid() const { return base != nullptr; }
   // collective over the node: a window of at least `want` bytes
@@ -114,12 +132,173 @@ void wait_word(const int64_t* p, int64_t v, const char* what) {
   }
 }
 
+// ---------------------------------------------------------------- the node window's front (P > 1)
+// Only rank 0 holds the input (common.cpp:93-117): the harness's per-query attribute vectors in
+// its heap.  Two ways to get rank r's query block (and its share of the dataset's rows for the
+// render plane) to rank r, chosen per call from bandwidths probed in the MPI_Init hook:
+//   CMA  — rank 0 only publishes the addresses of its row-pointer tables, k and labels; every
+//          rank reads what it needs straight from rank 0's address space (process_vm_readv, the
+//          mechanism MPI libraries use for large on-node messages) on its own render pool, all
+//          ranks at once, and renders 1/P of the plane itself (renderers = P);
+//   fill — (CMA refused, or slower than this) rank 0's pool gathers the blocks into the window,
+//          rank by rank, releasing each as it lands; rank 0 renders the whole plane.
+// bench_4 replicates the dataset with one MPI_Bcast and hands queries out per task (@0xc199,
+// @0xd64c); neither serialises the front through one memcpy loop.
+struct Cma {
+  bool ok = false;          // every rank read rank 0's probe buffer correctly
+  pid_t pid = 0;            // rank 0's pid
+  double gbps = 0.0;        // the slowest rank's read bandwidth, every rank reading at once
+  double fill_gbps = 0.0;   // rank 0's pool gather bandwidth (the fill front)
+};
+
+// [remote, remote + bytes) of process pid -> local, split over the render pool (>= 1 MiB per
+// part); false on any failed or short read
+bool cma_read(pid_t pid, void* local, const void* remote, int64_t bytes) {
+  if (bytes <= 0) return true;
+  struct Job {
+    pid_t pid;
+    char* l;
+    const char* r;
+    int64_t n;
+    std::atomic<int> bad{0};
+  } j{pid, (char*)local, (const char*)remote, bytes};
+  auto part = [](void* c, int t, int nt) {
+    Job& J = *(Job*)c;
+    const int64_t unit = int64_t(1) << 20;
+    const int64_t parts = std::max<int64_t>(1, std::min<int64_t>(nt, (J.n + unit - 1) / unit));
+    if (t >= parts) return;
+    int64_t a = J.n * t / parts, b = J.n * (t + 1) / parts;
+    while (a < b) {
+      iovec li{J.l + a, (size_t)(b - a)}, ri{(void*)(J.r + a), (size_t)(b - a)};
+      const ssize_t got = process_vm_readv(J.pid, &li, 1, &ri, 1, 0);
+      if (got <= 0) {
+        J.bad = 1;
+        return;
+      }
+      a += got;
+    }
+  };
+  if (bytes < (int64_t(1) << 20)) part(&j, 0, 1);
+  else dmlp_host_pool_run(part, &j);
+  return !j.bad;
+}
+
+// Rows tab[0, n) of rank 0 (tab: the rows' addresses there, copied here) -> readable here: tab[i]
+// is rewritten in place to point at row i's copy — inside `scratch` when the rows lie dense in
+// rank 0's heap (their span, read in one piece, fits it; *used = the span's bytes), else in
+// `flat` (one iovec per row, 1024 rows per call; *used = 0).  false on a failed read.
+bool cma_rows(pid_t pid, const double** tab, int64_t n, int A, char* scratch, int64_t scratch_bytes,
+              double* flat, int64_t* used) {
+  *used = 0;
+  if (n <= 0) return true;
+  uintptr_t lo = UINTPTR_MAX, hi = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    lo = std::min(lo, (uintptr_t)tab[i]);
+    hi = std::max(hi, (uintptr_t)tab[i] + (uintptr_t)A * 8);
+  }
+  const int64_t span = (int64_t)(hi - lo), need = n * A * 8;
+  if (span <= scratch_bytes && span <= 2 * need + (int64_t(1) << 20)) {
+    if (!cma_read(pid, scratch, (const void*)lo, span)) return false;
+    for (int64_t i = 0; i < n; ++i) tab[i] = (const double*)(scratch + ((uintptr_t)tab[i] - lo));
+    *used = (span + 255) & ~int64_t(255);
+    return true;
+  }
+  struct Job {
+    pid_t pid;
+    const double** tab;
+    int64_t n;
+    int A;
+    double* flat;
+    std::atomic<int> bad{0};
+  } j{pid, tab, n, A, flat};
+  dmlp_host_pool_run([](void* c, int t, int nt) {
+    Job& J = *(Job*)c;
+    const int64_t a = J.n * t / nt, b = J.n * (t + 1) / nt;
+    std::vector<iovec> ri(1024);
+    for (int64_t r0 = a; r0 < b; r0 += 1024) {
+      const int64_t m = std::min<int64_t>(1024, b - r0);
+      for (int64_t i = 0; i < m; ++i) ri[i] = {(void*)J.tab[r0 + i], (size_t)J.A * 8};
+      iovec li{J.flat + r0 * J.A, (size_t)(m * J.A * 8)};
+      if (process_vm_readv(J.pid, &li, 1, ri.data(), (unsigned long)m, 0) != m * J.A * 8) {
+        J.bad = 1;
+        return;
+      }
+      for (int64_t i = 0; i < m; ++i) J.tab[r0 + i] = J.flat + (r0 + i) * J.A;
+    }
+  }, &j);
+  return !j.bad;
+}
+
+// Collective, untimed (the MPI_Init hook): can every rank read rank 0's memory, and how fast —
+// against rank 0's own pool gather.  KNN_WINDOW_FRONT=fill skips it (never CMA).
+Cma probe_cma(int rank, int world) {
+  Cma c;
+  const char* fr = getenv("KNN_WINDOW_FRONT");
+  const bool want = !(fr && std::string(fr) == "fill");
+  const int64_t bytes = int64_t(16) << 20;
+  std::vector<uint64_t> buf;
+  int64_t meta[2] = {0, 0};
+  double fill_s = 1.0;
+  if (rank == 0) {
+    buf.resize(bytes / 8);
+    for (size_t i = 0; i < buf.size(); ++i) buf[i] = i * 0x9E3779B97F4A7C15ull;
+    // (Yama ptrace_scope 1: let every process of this user attach; harmless elsewhere)
+    if (want) (void)prctl(PR_SET_PTRACER, PR_SET_PTRACER_ANY, 0, 0, 0);
+    meta[0] = (int64_t)getpid();
+    meta[1] = (int64_t)(uintptr_t)buf.data();
+    // the fill front's gather: 16 MiB of 256-byte rows through the pool, twice (the 2nd timed)
+    std::vector<const double*> rows(bytes / 256);
+    for (size_t i = 0; i < rows.size(); ++i) rows[i] = (const double*)buf.data() + 32 * i;
+    std::vector<double> dst(bytes / 8);
+    for (int it = 0; it < 2; ++it) {
+      const auto t0 = std::chrono::steady_clock::now();
+      dmlp_cpu_gather_rows(rows.data(), (int64_t)rows.size(), 32, dst.data());
+      fill_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+  }
+  MPI_Bcast(meta, 2, MPI_INT64_T, 0, MPI_COMM_WORLD);
+  c.pid = (pid_t)meta[0];
+  int ok = 1;
+  double gbps = 1e30;
+  if (rank != 0 && want) {
+    std::vector<uint64_t> got(bytes / 8);
+    std::memset(got.data(), 0, bytes);  // (pages faulted in before the clock)
+    double t = 1.0;
+    for (int it = 0; it < 2 && ok; ++it) {
+      const auto t0 = std::chrono::steady_clock::now();
+      ok = cma_read(c.pid, got.data(), (const void*)(uintptr_t)meta[1], bytes) ? 1 : 0;
+      t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (size_t i = 0; i < got.size() && ok; i += 4097) ok = got[i] == i * 0x9E3779B97F4A7C15ull;
+    gbps = bytes / t / 1e9;
+  }
+  if (!want) ok = 0;
+  MPI_Barrier(MPI_COMM_WORLD);  // (rank 0's buffer lives until every rank has read it)
+  MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+  MPI_Allreduce(MPI_IN_PLACE, &gbps, 1, MPI_DOUBLE, MPI_MIN, MPI_COMM_WORLD);
+  double fb = bytes / fill_s / 1e9;
+  MPI_Bcast(&fb, 1, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+  c.ok = ok != 0 && world > 1;
+  c.gbps = c.ok ? gbps : 0.0;
+  c.fill_gbps = fb;
+  return c;
+}
+
 struct DropinState {
   dmlp_rt::Runtime rt;
   std::unique_ptr<dmlp_rt::KnnCore> core;
   NodeWindow win;
   bool use_window = false, cpu_window = false;
-  double step_ms = 0.0;  // this rank's native step in the last node-window call
+  Cma cma;                // the node window's CMA front (probed in the MPI_Init hook)
+  bool front_cma = false; // the last node-window call's front
+  int64_t t_enter_ns = 0; // rank 0: the last KNN call's entry (steady_clock)
+  // the last node-window call's phases on this rank: fetch (front), native step, report egress
+  double step_ms = 0.0, fetch_ms = 0.0, egress_ms = 0.0;
+  std::vector<double> release_ms;  // rank 0: each rank's rows ready, ms after rank 0's KNN entry
+  std::vector<double> flat_share;  // CMA front: dataset rows read one iovec per row (sparse heap)
+  // rank 0's output, kept across calls: its report bytes may still sit in the stdout pipe by
+  // reference (vmsplice) when KNN returns — nothing rewrites them before egress_settle()
+  dmlp_rt::Output out;
   // the row index's tables, kept across calls: fresh vectors every call cost ~1 ms of page
   // faults and zero-fills at the bench shape (profiles/r4l_dropin_trace.txt "index")
   std::vector<int> labels, k;
@@ -173,10 +352,11 @@ void start_engine() {
     }
     if (all_here) {
       const char* mb = getenv("KNN_WINDOW_MB");
-      const int64_t want = (mb ? std::max(1L, std::atol(mb)) : 512L) << 20;
+      const int64_t want = (mb ? std::max(1L, std::atol(mb)) : 1024L) << 20;
       s->win.create(s->rt.rank, want, s->rt.gpu);
       s->use_window = true;
       s->cpu_window = !s->rt.gpu;
+      s->cma = probe_cma(s->rt.rank, s->rt.world);
     }
   }
   s->core.reset(new dmlp_rt::KnnCore(s->rt, strategy, kListsMode, ex && std::string(ex) == "1",
@@ -196,9 +376,14 @@ void start_engine() {
   state() = s;
 }
 
+void egress_settle();  // (report egress, below)
+
 void stop_engine() {
   DropinState* s = state();
   if (!s) return;
+  // (after the harness's clock: spliced report pages are referenced by the pipe, but the heap
+  // they sit in must not be reused by MPI_Finalize before the reader took them)
+  if (s->rt.rank == 0) egress_settle();
   s->core.reset();
   s->win.free_all();
   s->rt.finalize();
@@ -284,7 +469,75 @@ void index_rows(const std::vector<DataPoint>& dataset, const std::vector<Query>&
   if (identity) *identity = !renumbered;
 }
 
-void cout_sink(void*, const char* bytes, size_t n) { std::cout.write(bytes, (std::streamsize)n); }
+// ---------------------------------------------------------------- report egress (fd 1)
+// The report goes to the harness's stdout (common.cpp:70, the stream reportResult writes) as raw
+// bytes on fd 1.  run_bench.sh launches the engine under mpirun with stdout redirected there
+// (run_bench.sh:84,120), so fd 1 is usually a PIPE to the launcher, which forwards it: the pipe
+// is widened to /proc/sys/fs/pipe-max-size (F_SETPIPE_SZ) and, unless KNN_VMSPLICE=0, the text's
+// pages are handed to the pipe by vmsplice instead of being copied into it by write() — the
+// launcher's own copy remains.  A buffer whose pages went to the pipe must not change before the
+// reader consumed them: the next call first waits for the pipe to drain (bounded), see
+// egress_settle().  A file or terminal gets write().
+struct Egress {
+  bool init = false, fifo = false, vms = false, spliced = false;
+  int64_t bytes = 0, splice_bytes = 0;
+};
+Egress& egress() {
+  static Egress e;
+  if (!e.init) {
+    e.init = true;
+    struct stat st;
+    e.fifo = fstat(1, &st) == 0 && S_ISFIFO(st.st_mode);
+    if (e.fifo) {
+      int mx = 1 << 20;
+      if (FILE* f = std::fopen("/proc/sys/fs/pipe-max-size", "r")) {
+        if (std::fscanf(f, "%d", &mx) != 1) mx = 1 << 20;
+        std::fclose(f);
+      }
+      for (int sz = mx; sz >= (1 << 16) && fcntl(1, F_SETPIPE_SZ, sz) < 0; sz >>= 1) {
+      }
+      const char* v = getenv("KNN_VMSPLICE");
+      e.vms = !(v && v[0] == '0');
+    }
+  }
+  return e;
+}
+void emit_fd1(const char* p, size_t n) {
+  Egress& e = egress();
+  std::cout.flush();  // (anything the harness wrote before stays in order)
+  size_t off = 0;
+  if (e.vms && n >= 4096) {
+    while (off < n) {
+      iovec v{(void*)(p + off), n - off};
+      const ssize_t k = vmsplice(1, &v, 1, 0);
+      if (k <= 0) break;  // (refused: the rest by write)
+      off += (size_t)k;
+      e.spliced = true;
+    }
+    e.splice_bytes += (int64_t)off;
+  }
+  while (off < n) {
+    const ssize_t k = write(1, p + off, n - off);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) throw std::runtime_error("report egress: write to stdout failed");
+    off += (size_t)k;
+  }
+  e.bytes += (int64_t)n;
+}
+// Before a call that may overwrite text pages a previous call spliced into the pipe: wait until
+// the reader drained it (FIONREAD 0; bounded by 10 s, then the pages are assumed consumed).
+void egress_settle() {
+  Egress& e = egress();
+  if (!e.spliced) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  int q = 0;
+  while (ioctl(1, FIONREAD, &q) == 0 && q > 0 &&
+         std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+    std::this_thread::yield();
+  e.spliced = false;
+}
+
+void cout_sink(void*, const char* bytes, size_t n) { emit_fd1(bytes, n); }
 
 // The GPU report uses the query's index as its id; the harness numbers queries by index too
 // (common.cpp:110).  Any other numbering gets its ids rewritten line by line.
@@ -292,7 +545,7 @@ void write_report(const char* text, size_t len, const std::vector<Query>& querie
   bool identity = true;
   for (size_t i = 0; i < queries.size() && identity; ++i) identity = queries[i].id == (int)i;
   if (identity) {
-    std::cout.write(text, (std::streamsize)len);
+    emit_fd1(text, len);
     return;
   }
   size_t pos = 0;
@@ -311,83 +564,167 @@ void write_report(const char* text, size_t len, const std::vector<Query>& querie
 // ---------------------------------------------------------------- the node-window call (P > 1)
 // Every rank, after the meta broadcast.  Rank 0 (root) holds the harness's vectors; returns on
 // rank 0 the report bytes' location in the window.
-void window_call(DropinState* s, const std::vector<Query>* queries, dmlp_rt::Input* in,
-                 const int64_t meta[6], const char** text, size_t* text_len) {
+void window_call(DropinState* s, dmlp_rt::Input* in, const int64_t meta[6], const char** text,
+                 size_t* text_len) {
   const int P = s->rt.world, r = s->rt.rank;
   const int64_t N = meta[0], Q = meta[1];
   const int A = (int)meta[2];
   NodeWindow& W = s->win;
-  const NodeWindow::Layout L = NodeWindow::layout(N, Q, A);
+  const NodeWindow::Layout L = NodeWindow::layout(N, Q, A, P);
   if (L.total > W.bytes) {  // collective (every rank computed the same size): grow
     W.destroy();
     W.create(r, L.total, W.gpu);
   }
   const int64_t gen = ++W.gen;
   char* b = W.base;
-  int* labels = (int*)(b + L.labels);
-  int* kk = (int*)(b + L.k);
-  double* qx = (double*)(b + L.qx);
+  int64_t* ctl = W.ctrl();
   std::vector<int64_t> cnt, off;
   dmlp_rt::block_partition(Q, P, cnt, off);
+  const int64_t a0 = off[r], nl = cnt[r];
+  // the front: every rank takes the same decision from the same numbers
+  const char* fr = getenv("KNN_WINDOW_FRONT");
+  const std::string front = fr ? fr : "auto";
+  bool cma = s->cma.ok && front != "fill";
+  if (cma && front != "cma") {
+    const double blk = (double)((Q + P - 1) / P) * A * 8, share = (double)((N + P - 1) / P) * A * 8;
+    const double t_cma = (blk + share) / (s->cma.gbps * 1e9);
+    const double t_fill = ((double)(Q - cnt[0]) * A * 8 + (double)N * A * 8 * (P - 1) / P) /
+                          (std::max(1e-3, s->cma.fill_gbps) * 1e9);
+    cma = t_cma < t_fill;
+  }
+  s->front_cma = cma;
   dmlp_plane pl{};
   pl.base = b + L.plane;
   pl.bytes = L.plane_bytes;
   pl.rank = r;
-  pl.renderers = 1;  // only rank 0 holds the dataset (common.cpp:93-117)
-  pl.with_f64 = 1;   // the other ranks have no rows to fall back on
+  pl.renderers = cma ? P : 1;  // fill: only rank 0 holds the dataset (common.cpp:93-117)
+  pl.with_f64 = 1;             // (the consumers have no rows to fall back on)
   pl.gen = gen;
+  const auto ts = std::chrono::steady_clock::now();
+  auto now_ns = [] {
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  // this rank's inputs to its step
+  const int* labels = nullptr;
+  const int* kk = nullptr;
+  const double* qx = nullptr;                 // flat query rows, or
+  const double* const* qr = nullptr;          // row pointers
+  const double* const* xr = nullptr;          // dataset rows this rank renders (its plane share)
+  char* scr = b + L.scratch + (int64_t)r * L.scratch_bytes;
   if (r == 0) {
+    ctl[NodeWindow::kT0] = s->t_enter_ns;
     if (dmlp_plane_init(pl.base, pl.bytes, N, A, 1) != 0) throw std::runtime_error("plane init");
-    std::memcpy(labels, in->labels.data(), N * sizeof(int));
-    std::memcpy(kk, in->k.data(), Q * sizeof(int));
-    store_rel(W.ctrl(), gen);
-    // the other ranks' query rows, rank by rank (each released as soon as it is in place)
-    for (int t = 1; t < P; ++t) {
-      if (cnt[t]) dmlp_cpu_gather_rows(s->qr.data() + off[t], cnt[t], A, qx + off[t] * A);
-      store_rel(W.ctrl() + 8 + t, gen);
+    labels = in->labels.data();
+    kk = in->k.data();
+    qr = s->qr.data();
+    xr = s->xr.data();
+    if (cma) {  // publish the addresses only: every rank fetches its own part
+      ctl[NodeWindow::kPtr + 0] = (int64_t)(uintptr_t)s->xr.data();
+      ctl[NodeWindow::kPtr + 1] = (int64_t)(uintptr_t)s->qr.data();
+      ctl[NodeWindow::kPtr + 2] = (int64_t)(uintptr_t)in->k.data();
+      ctl[NodeWindow::kPtr + 3] = (int64_t)(uintptr_t)in->labels.data();
+      store_rel(ctl + NodeWindow::kGen, gen);
+    } else {
+      std::memcpy(b + L.labels, in->labels.data(), N * sizeof(int));
+      std::memcpy(b + L.k, in->k.data(), Q * sizeof(int));
+      store_rel(ctl + NodeWindow::kGen, gen);
+      // the other ranks' query rows, rank by rank on the whole pool, each released as it lands
+      double* qxw = (double*)(b + L.qx);
+      for (int t = 1; t < P; ++t) {
+        if (cnt[t]) dmlp_cpu_gather_rows(s->qr.data() + off[t], cnt[t], A, qxw + off[t] * A);
+        store_rel(ctl + NodeWindow::kRows + t, gen);
+      }
     }
+    ctl[NodeWindow::kFetch + 0] = now_ns();
   } else {
-    wait_word(W.ctrl(), gen, "the call's labels and k");
-    wait_word(W.ctrl() + 8 + r, gen, "this rank's query rows");
+    wait_word(ctl + NodeWindow::kGen, gen, "the call's front");
+    if (cma) {
+      const pid_t pid = s->cma.pid;
+      auto remote = [&](int i) { return (const void*)(uintptr_t)ctl[NodeWindow::kPtr + i]; };
+      if ((int64_t)s->labels.size() < N) s->labels.resize(N);
+      if ((int64_t)s->k.size() < nl) s->k.resize(nl);
+      if ((int64_t)s->qr.size() < nl) s->qr.resize(nl);
+      if ((int64_t)s->xr.size() < N) s->xr.resize(N);
+      bool ok = cma_read(pid, s->labels.data(), remote(3), N * 4) &&
+                cma_read(pid, s->k.data(), (const int*)remote(2) + a0, nl * 4) &&
+                cma_read(pid, s->qr.data(), (const double* const*)remote(1) + a0, nl * 8);
+      // the query rows: their heap span in the scratch's query part, else one iovec per row
+      // into this rank's block of the window's query region
+      int64_t used = 0;
+      ok = ok && cma_rows(pid, s->qr.data(), nl, A, scr, L.scratch_q, (double*)(b + L.qx) + a0 * A,
+                          &used);
+      // this rank's share of the dataset's rows (plane slices i % P == r) in the other part
+      int64_t t0 = 0, t1 = 0;
+      const int ns = N > 0 ? dmlp_plane_slice(N, A, 0, &t0, &t1) : 0;
+      int64_t xused = 0, share_rows = 0;
+      for (int i = r; i < ns; i += P) {
+        dmlp_plane_slice(N, A, i, &t0, &t1);
+        share_rows += std::min(N, t1 * 64) - std::min(N, t0 * 64);
+      }
+      if ((int64_t)s->flat_share.size() < share_rows * A) s->flat_share.resize(share_rows * A);
+      int64_t frow = 0;
+      for (int i = r; i < ns && ok; i += P) {
+        dmlp_plane_slice(N, A, i, &t0, &t1);
+        const int64_t r0 = std::min(N, t0 * 64), r1 = std::min(N, t1 * 64);
+        ok = cma_read(pid, s->xr.data() + r0, (const double* const*)remote(0) + r0, (r1 - r0) * 8);
+        int64_t u = 0;
+        ok = ok && cma_rows(pid, s->xr.data() + r0, r1 - r0, A, scr + L.scratch_q + xused,
+                            L.scratch_bytes - L.scratch_q - xused,
+                            s->flat_share.data() + frow * A, &u);
+        xused += u;
+        frow += r1 - r0;
+      }
+      if (!ok) throw std::runtime_error("node window: cross-memory read of rank 0 failed");
+      labels = s->labels.data();
+      kk = s->k.data();
+      qr = s->qr.data();
+      xr = s->xr.data();
+    } else {
+      wait_word(ctl + NodeWindow::kRows + r, gen, "this rank's query rows");
+      labels = (const int*)(b + L.labels);
+      kk = (const int*)(b + L.k) + a0;
+      qx = (const double*)(b + L.qx) + a0 * A;
+    }
+    ctl[NodeWindow::kFetch + r] = now_ns();
   }
-  const int64_t a0 = off[r], nl = cnt[r];
+  s->fetch_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
   const int lo = (int)meta[3], hi = (int)meta[4], kmax = (int)meta[5];
   int64_t len = 0;
   std::vector<char> cpu_text;
-  const auto ts = std::chrono::steady_clock::now();
+  const auto tstep = std::chrono::steady_clock::now();
   if (!s->cpu_window) {
-    // the native step: rank 0 renders the dataset into the plane from the harness's vectors
-    len = s->core->step_block(r == 0 ? s->xr.data() : nullptr, N, A, labels, lo, hi, kmax,
-                              r == 0 ? nullptr : qx + a0 * A, r == 0 ? s->qr.data() : nullptr,
-                              kk + a0, nl, a0, &pl);
+    // the native step: the plane's renderers render their slices from `xr`
+    len = s->core->step_block(pl.rank < pl.renderers ? xr : nullptr, N, A, labels, lo, hi, kmax,
+                              qx, qx ? nullptr : qr, r == 0 ? kk + a0 : kk, nl, a0, &pl);
   } else {
-    // the same protocol on the CPU: rank 0 renders the plane's rows, every rank rebuilds the
-    // dataset from them and runs the exact brute force on its block
+    // the same protocol on the CPU: the renderers render the plane's rows, every rank rebuilds
+    // the dataset from them and runs the exact brute force on its block
     int64_t t0 = 0, t1 = 0;
     const int ns = N > 0 ? dmlp_plane_slice(N, A, 0, &t0, &t1) : 0;
-    if (r == 0)
-      for (int i = 0; i < ns; ++i)
-        if (dmlp_plane_render(&pl, nullptr, s->xr.data(), N, A, nullptr, 2, i) < 0)
-          throw std::runtime_error("plane render");
+    for (int i = r; i < ns && r < pl.renderers; i += pl.renderers)
+      if (dmlp_plane_render(&pl, nullptr, xr, N, A, nullptr, 2, i) < 0)
+        throw std::runtime_error("plane render");
     std::vector<double> X((size_t)N * A);
     for (int i = 0; i < ns; ++i)
       if (dmlp_plane_rows_f64(&pl, N, A, i, nullptr, X.data()) != 0)
         throw std::runtime_error("node window: plane rows");
     std::vector<double> qrow((size_t)std::max<int64_t>(nl, 1) * A);
-    if (r == 0) dmlp_cpu_gather_rows(s->qr.data(), nl, A, qrow.data());
-    else std::memcpy(qrow.data(), qx + a0 * A, sizeof(double) * nl * A);
+    if (qx) std::memcpy(qrow.data(), qx, sizeof(double) * nl * A);
+    else dmlp_cpu_gather_rows(r == 0 ? qr + a0 : qr, nl, A, qrow.data());
+    const int* kb = r == 0 ? kk + a0 : kk;
     const int ks = std::max(1, kmax);
     std::vector<double> d((size_t)std::max<int64_t>(nl, 1) * ks);
     std::vector<int> ids(d.size()), lab(std::max<int64_t>(nl, 1));
     std::vector<uint64_t> cs(lab.size());
     if (nl) {
-      dmlp_cpu_knn(X.data(), N, A, qrow.data(), nl, kk + a0, ks, d.data(), ids.data(), 0);
-      dmlp_cpu_finalize(d.data(), ids.data(), ks, kk + a0, nl, labels, lab.data(), cs.data());
+      dmlp_cpu_knn(X.data(), N, A, qrow.data(), nl, kb, ks, d.data(), ids.data(), 0);
+      dmlp_cpu_finalize(d.data(), ids.data(), ks, kb, nl, labels, lab.data(), cs.data());
       cpu_text.resize((size_t)dmlp_format_bound((int)nl));
       len = dmlp_cpu_format_report(cs.data(), nl, a0, cpu_text.data());
     }
   }
-  s->step_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+  s->step_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tstep).count();
   std::vector<int64_t> lens(P);
   MPI_Allgather(&len, 1, MPI_INT64_T, lens.data(), 1, MPI_INT64_T, MPI_COMM_WORLD);
   int64_t at = 0, total = 0;
@@ -397,16 +734,21 @@ void window_call(DropinState* s, const std::vector<Query>* queries, dmlp_rt::Inp
   }
   if (total > dmlp_format_bound((int)std::max<int64_t>(Q, 1)))
     throw std::runtime_error("node window: report region too small");
+  const auto te = std::chrono::steady_clock::now();
   if (len) {
     if (s->cpu_window) std::memcpy(b + L.out + at, cpu_text.data(), (size_t)len);
     else s->core->emit_block(b + L.out + at, len);
   }
+  s->egress_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - te).count();
   MPI_Barrier(MPI_COMM_WORLD);  // every block is in the window (and the next call may reuse it)
   if (r == 0) {
     *text = b + L.out;
     *text_len = (size_t)total;
+    // every rank's fetch-done time against rank 0's KNN entry (one steady clock per node)
+    s->release_ms.assign(P, 0.0);
+    for (int i = 0; i < P; ++i)
+      s->release_ms[i] = (ctl[NodeWindow::kFetch + i] - ctl[NodeWindow::kT0]) / 1e6;
   }
-  (void)queries;
 }
 
 }  // namespace
@@ -445,10 +787,16 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
   start_engine();  // no-op: MPI_Init started it (this harness called PMPI_Init some other way)
   DropinState* s = state();
   if (!s) throw std::runtime_error("Engine::KNN before MPI_Init");
+  if (s->rt.rank == 0) egress_settle();  // (a previous call's spliced text pages are reused now)
   const auto t0 = std::chrono::steady_clock::now();
+  s->t_enter_ns = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                      t0.time_since_epoch()).count();
   const bool root = s->rt.rank == 0;
   dmlp_rt::Input in;
-  dmlp_rt::Output out;
+  dmlp_rt::Output& out = s->out;
+  out.text_len = 0;
+  out.shared_text = nullptr;
+  out.report.clear();
   s->core->trace.begin();
   bool done = false;
   auto t1 = t0;
@@ -482,7 +830,7 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     MPI_Bcast(meta, 6, MPI_INT64_T, 0, MPI_COMM_WORLD);
     t1 = std::chrono::steady_clock::now();
     if (meta[2] >= 1 && meta[2] <= 256 && meta[1] <= (1 << 30)) {
-      window_call(s, &queries, &in, meta, &win_text, &win_len);
+      window_call(s, &in, meta, &win_text, &win_len);
       done = true;
       s->core->trace.mark("window");
     } else if (root) {  // outside the plane's shapes: the strategy pipeline below
@@ -502,7 +850,7 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     t1 = std::chrono::steady_clock::now();
     done = s->core->KNN_rows(&in, s->xr.data(), s->qr.data(), &out,
                              identity ? &cout_sink : nullptr, nullptr);
-    // (streamed: in pieces behind the step, or from inside it — KNN_REPORT_TAIL)
+    // (streamed: in pieces behind the step)
     emitted = done && identity && s->core->last_emit_ms > 0.0;
   }
   if (!done) {
@@ -544,7 +892,8 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
   if (!root && s->use_window) {
     if (const char* m = getenv("KNN_METRICS")) {
       std::ofstream f(std::string(m) + ".r" + std::to_string(s->rt.rank));
-      f << "{\"rank\": " << s->rt.rank << ", \"step_ms\": " << s->step_ms << "}\n";
+      f << "{\"rank\": " << s->rt.rank << ", \"fetch_ms\": " << s->fetch_ms
+        << ", \"step_ms\": " << s->step_ms << ", \"egress_ms\": " << s->egress_ms << "}\n";
     }
   }
   if (root) {
@@ -561,9 +910,22 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
         << ", \"lists_mode\": " << (kListsMode ? "true" : "false")
         << ", \"rows_in_place\": " << (done ? "true" : "false")
         << ", \"node_window\": " << (win_text ? "true" : "false")
-        << ", \"report_tail\": " << s->core->report_tail_
-        << ", \"report_bytes_in_step\": " << s->core->tail_sunk_
-        << ", \"step_ms\": " << s->step_ms << "}\n";
+        << ", \"step_ms\": " << s->step_ms << ", \"stdout_fifo\": "
+        << (egress().fifo ? "true" : "false") << ", \"vmsplice_bytes\": " << egress().splice_bytes;
+      if (win_text) {
+        // the node window's phases on rank 0 and every rank's release (its query rows readable
+        // there), ms after rank 0's KNN entry
+        f << ", \"window\": {\"front\": \"" << (s->front_cma ? "cma" : "fill")
+          << "\", \"cma_ok\": " << (s->cma.ok ? "true" : "false")
+          << ", \"cma_GBps\": " << s->cma.gbps << ", \"fill_GBps\": " << s->cma.fill_gbps
+          << ", \"index_ms\": " << ms_t(t1 - t0).count() << ", \"fetch_ms\": " << s->fetch_ms
+          << ", \"step_ms\": " << s->step_ms << ", \"egress_ms\": " << s->egress_ms
+          << ", \"write_ms\": " << ms_t(t3 - t2).count() << ", \"release_ms\": [";
+        for (size_t i = 0; i < s->release_ms.size(); ++i)
+          f << (i ? ", " : "") << s->release_ms[i];
+        f << "]}";
+      }
+      f << "}\n";
     }
   }
 }

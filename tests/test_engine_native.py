@@ -301,15 +301,22 @@ def _text_with_decimals(inp, decimals):
 
 
 @pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
-@pytest.mark.parametrize("np_", [2, 3])
-@pytest.mark.parametrize("decimals", [6, 9])
-def test_dropin_node_window_cpu(tmp_path, np_, decimals):
+@pytest.mark.parametrize("np_,decimals", [(2, 6), (2, 9), (3, 6), (3, 9), (8, 6)])
+@pytest.mark.parametrize("front", ["cma", "fill"])
+def test_dropin_node_window_cpu(tmp_path, np_, decimals, front):
     """engine.h drop-in at P > 1 through the node window (KNN_DEVICE=cpu KNN_STRATEGY=farm runs
-    the GPU path's protocol on the CPU): rank 0 puts labels, k and the other ranks' query rows
-    into the MPI-3 shared window and renders the dataset's rows into its render plane (int32, or
-    fp64 for 9-decimal data); every rank rebuilds the dataset from the plane, answers its own
-    query block and copies its report lines into the window at its offset.  The window starts at
-    1 MiB and grows collectively.  stdout == the fp64 oracle's bytes; every rank took part."""
+    the GPU path's protocol on the CPU), both fronts:
+      cma  — rank 0 only publishes the addresses of its row tables, k and labels; every rank
+             reads its own query block and its share of the dataset's rows straight from rank 0's
+             address space (process_vm_readv) and renders 1/P of the render plane;
+      fill — rank 0's pool gathers every rank's block into the MPI-3 shared window, releasing
+             each as it lands, and renders the whole plane (int32 rows, or fp64 for 9-decimal
+             data).
+    Every rank rebuilds the dataset from the plane, answers its own query block and copies its
+    report lines into the window at its offset.  The window starts at 1 MiB and grows
+    collectively.  stdout == the fp64 oracle's bytes; every rank took part; the KNN_METRICS
+    sidecar names the front and every rank's release time."""
+    import json
     rng = np.random.default_rng(np_ * 10 + decimals)
     N, Q, A = 2100, 203, 7
     X = rng.uniform(-20, 20, (N, A))
@@ -322,7 +329,9 @@ def test_dropin_node_window_cpu(tmp_path, np_, decimals):
     inp = dmlp.parse_input(txt)
     _, _, cs = ref.knn(inp.X, inp.labels, inp.Qx, inp.k)
     exe = _ref_dropin(tmp_path) if build.reference_harness() is not None else _dropin(tmp_path)
-    env = {"KNN_DEVICE": "cpu", "KNN_STRATEGY": "farm", "KNN_WINDOW_MB": "1", "KNN_TRACE": "1"}
+    met = tmp_path / "m.json"
+    env = {"KNN_DEVICE": "cpu", "KNN_STRATEGY": "farm", "KNN_WINDOW_MB": "1", "KNN_TRACE": "1",
+           "KNN_WINDOW_FRONT": front, "KNN_METRICS": str(met)}
     e = dict(os.environ, **env)
     import shlex
     cmd = [MPIEXEC, "-n", str(np_), "sh", "-c", f"exec {shlex.quote(exe)} < {shlex.quote(str(path))}"]
@@ -332,3 +341,43 @@ def test_dropin_node_window_cpu(tmp_path, np_, decimals):
     err = r.stderr.decode()
     for rank in range(np_):  # the window protocol ran on every rank (not the serial fallback)
         assert f"[dmlp-trace] rank {rank} window " in err, err[-2000:]
+    m = json.loads(met.read_text())
+    w = m["window"]
+    if front == "cma":
+        assert w["cma_ok"], "process_vm_readv on rank 0 was refused"
+    assert w["front"] == front
+    assert len(w["release_ms"]) == np_
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="no mpiexec")
+@pytest.mark.parametrize("np_", [1, 3])
+@pytest.mark.parametrize("vms", ["1", "0"])
+def test_dropin_report_egress_pipe(tmp_path, np_, vms):
+    """the report egress as run_bench.sh launches the engine (mpiexec, the
+    engine's stdout a pipe to the launcher): the pipe is widened and the report's pages are
+    vmspliced into it (KNN_VMSPLICE=0: write()), the buffers stay untouched until the pipe
+    drained; a redirected file gets write().  stdout == the oracle's bytes every way, and the
+    KNN_METRICS sidecar says which path ran."""
+    import json
+    import shlex
+    path, inp, res, lab, cs = _case(tmp_path, N=1500, Q=3000)
+    exe = _ref_dropin(tmp_path) if build.reference_harness() is not None else _dropin(tmp_path)
+    met = tmp_path / "m.json"
+    e = dict(os.environ, KNN_DEVICE="cpu", KNN_STRATEGY="farm", KNN_VMSPLICE=vms,
+             KNN_METRICS=str(met))
+    cmd = [MPIEXEC, "-n", str(np_), "sh", "-c", f"exec {shlex.quote(exe)} < {shlex.quote(str(path))}"]
+    r = subprocess.run(cmd, stdin=subprocess.DEVNULL, capture_output=True, timeout=180, env=e)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout == dmlp.format_report(cs)
+    m = json.loads(met.read_text())
+    assert m["stdout_fifo"] is True
+    assert (m["vmsplice_bytes"] > 0) == (vms == "1")
+    # stdout redirected to a file (the direct run): write(), same bytes
+    out = tmp_path / "o.txt"
+    with open(path, "rb") as fin, open(out, "wb") as fo:
+        r = subprocess.run([exe], stdin=fin, stdout=fo, stderr=subprocess.PIPE, timeout=180,
+                           env=dict(e, KNN_STRATEGY="serial"))
+    assert r.returncode == 0, r.stderr.decode()
+    assert out.read_bytes() == dmlp.format_report(cs)
+    m = json.loads(met.read_text())
+    assert m["stdout_fifo"] is False and m["vmsplice_bytes"] == 0

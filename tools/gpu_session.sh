@@ -26,6 +26,7 @@
 #   plane      node render plane rehearsal: bench.py --gpus 3 / 8 on the one GPU, plane on / off
 #   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
 #   blits      copy-engine probe + every runtime kernel / SDMA copy of 6 native steps (step_driver)
+#   dropin8    drop-in at P = 8, Q = 131072 per rank on the one GPU: CMA / fill / auto fronts
 #   lnr        large-N steps: host vs device render at N 1e6 / 1e7 (step_driver)
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
@@ -214,6 +215,14 @@ for task in "$@"; do
       step blits 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/bl" -o run \
           --output-format csv -- tools/bin/step_driver --steps 6 --warmup 30 --timeline
       python3 tools/copy_kind.py step "$OUT/bl" > "$OUT/step_copies.txt"; tail -80 "$OUT/step_copies.txt" ;;
+    dropin8)  # the engine.h drop-in at P = 8 through the node window on the one GPU, Q = 131072 per
+              # rank (KNN_DATA_PLANE=host), each front (CMA / rank-0 fill), plus the CMA probe
+      step cmaprobe 120 tools/bin/cma_probe
+      for F in cma fill auto; do
+        KNN_WINDOW_FRONT=$F KNN_DATA_PLANE=host step dropin8_$F 900 python bench.py --harness dropin \
+            --gpus 8 --q-per-gpu 131072 --steps 2 --warmup 1
+      done
+      grep -h -o '"window": {[^}]*}' "$OUT"/dropin8_*.log | tee "$OUT/dropin8_window.txt" ;;
     lnr)  # large-N steps (native step driver): host render vs device render (DMLP_DEVICE_RENDER) at
           # the verdict's shapes, alternating, with the step timeline and host issue per step
       for SH in "1000000 32 10" "1000000 128 6" "10000000 32 4"; do
