@@ -565,12 +565,16 @@ def _contract_runs(a, dropin, shapes, steps, warmup, P=None, launcher="direct"):
                     for key in ("window", "stdout_fifo", "vmsplice_bytes"):  # (the last run's)
                         if key in mj:
                             extra_last[key] = mj[key]
-                    for rk in range(1, P):  # the drop-in's node window: each rank's step time
+                    for rk in range(1, P):  # the drop-in's node window: each rank's phases
                         rp = f"{met}.r{rk}"
                         if os.path.exists(rp):
                             with open(rp) as f:
-                                parts.setdefault(f"rank{rk}_step_ms", []).append(
-                                    float(_json.load(f)["step_ms"]))
+                                rj = _json.load(f)
+                            for key in ("step_ms", "fetch_ms", "fetch_rows_ms", "fetch_share_ms"):
+                                if key in rj:
+                                    parts.setdefault(f"rank{rk}_{key}", []).append(float(rj[key]))
+                            if "fetch_rows_span" in rj:
+                                extra_last[f"rank{rk}_fetch_rows_span"] = rj["fetch_rows_span"]
                     if dropin:
                         import re as _re
                         m = _re.search(rb"Time taken: (\d+) ms", pr.stderr)

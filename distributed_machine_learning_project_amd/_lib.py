@@ -70,6 +70,7 @@ _SIGS = {
                              vp, vp, vp, vp]),
     "dmlp_screen_x1_early": (i32, [i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp,
                                    i32, i32, vp, vp, vp, vp, vp]),
+    "dmlp_screen_x1_group_rows": (i32, [i32]),
     "dmlp_screen_x1_part": (i32, [i32, i32, i32, vp, vp, i64, i64, vp, vp, vp, vp, i32, i32, vp, vp,
                                   i32, i32, i32, vp, vp, vp, vp]),
     "dmlp_refine_groups": (i32, [i32, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32, i32, i64, vp, vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp]),

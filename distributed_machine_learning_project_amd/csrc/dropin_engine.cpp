@@ -294,6 +294,10 @@ struct DropinState {
   int64_t t_enter_ns = 0; // rank 0: the last KNN call's entry (steady_clock)
   // the last node-window call's phases on this rank: fetch (front), native step, report egress
   double step_ms = 0.0, fetch_ms = 0.0, egress_ms = 0.0;
+  // CMA front on this rank: tables + k + labels, query rows (span read or one iovec per row),
+  // dataset share
+  double fetch_tab_ms = 0.0, fetch_rows_ms = 0.0, fetch_share_ms = 0.0;
+  bool fetch_span = false;
   std::vector<double> release_ms;  // rank 0: each rank's rows ready, ms after rank 0's KNN entry
   std::vector<double> flat_share;  // CMA front: dataset rows read one iovec per row (sparse heap)
   // rank 0's output, kept across calls: its report bytes may still sit in the stdout pipe by
@@ -646,14 +650,24 @@ void window_call(DropinState* s, dmlp_rt::Input* in, const int64_t meta[6], cons
       if ((int64_t)s->k.size() < nl) s->k.resize(nl);
       if ((int64_t)s->qr.size() < nl) s->qr.resize(nl);
       if ((int64_t)s->xr.size() < N) s->xr.resize(N);
+      auto tick = [] { return std::chrono::steady_clock::now(); };
+      auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+      };
+      auto tf = tick();
       bool ok = cma_read(pid, s->labels.data(), remote(3), N * 4) &&
                 cma_read(pid, s->k.data(), (const int*)remote(2) + a0, nl * 4) &&
                 cma_read(pid, s->qr.data(), (const double* const*)remote(1) + a0, nl * 8);
+      s->fetch_tab_ms = ms_since(tf);
+      tf = tick();
       // the query rows: their heap span in the scratch's query part, else one iovec per row
       // into this rank's block of the window's query region
       int64_t used = 0;
       ok = ok && cma_rows(pid, s->qr.data(), nl, A, scr, L.scratch_q, (double*)(b + L.qx) + a0 * A,
                           &used);
+      s->fetch_rows_ms = ms_since(tf);
+      s->fetch_span = used > 0 || nl == 0;
+      tf = tick();
       // this rank's share of the dataset's rows (plane slices i % P == r) in the other part
       int64_t t0 = 0, t1 = 0;
       const int ns = N > 0 ? dmlp_plane_slice(N, A, 0, &t0, &t1) : 0;
@@ -675,6 +689,7 @@ void window_call(DropinState* s, dmlp_rt::Input* in, const int64_t meta[6], cons
         xused += u;
         frow += r1 - r0;
       }
+      s->fetch_share_ms = ms_since(tf);
       if (!ok) throw std::runtime_error("node window: cross-memory read of rank 0 failed");
       labels = s->labels.data();
       kk = s->k.data();
@@ -893,7 +908,10 @@ void Engine::KNN(Params& p, std::vector<DataPoint>& dataset, std::vector<Query>&
     if (const char* m = getenv("KNN_METRICS")) {
       std::ofstream f(std::string(m) + ".r" + std::to_string(s->rt.rank));
       f << "{\"rank\": " << s->rt.rank << ", \"fetch_ms\": " << s->fetch_ms
-        << ", \"step_ms\": " << s->step_ms << ", \"egress_ms\": " << s->egress_ms << "}\n";
+        << ", \"fetch_tables_ms\": " << s->fetch_tab_ms << ", \"fetch_rows_ms\": "
+        << s->fetch_rows_ms << ", \"fetch_rows_span\": " << (s->fetch_span ? "true" : "false")
+        << ", \"fetch_share_ms\": " << s->fetch_share_ms << ", \"step_ms\": " << s->step_ms
+        << ", \"egress_ms\": " << s->egress_ms << "}\n";
     }
   }
   if (root) {

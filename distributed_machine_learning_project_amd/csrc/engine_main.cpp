@@ -39,8 +39,12 @@ struct SharedWin {
     auto up = [](int64_t b) { return (b + 4095) & ~int64_t(4095); };
     const int64_t oX = 0, oL = up(N * A * 8), oQ = oL + up(N * 4), oK = oQ + up(Q * A * 8),
                   oO = oK + up(Q * 4), ob = up(dmlp_format_bound((int)std::max<int64_t>(Q, 1)));
-    // + the node render plane (plane.cpp): the dataset's image and rows rendered once per call
-    const int64_t pb = std::max<int64_t>(0, dmlp_plane_bytes(N, (int)A, 0)), oP = oO + ob;
+    // + the node render plane (plane.cpp): the dataset's image and rows rendered once per call,
+    // reserved only where ranks share it (P > 1, KNN_PLANE not 0: engine_core.h use_plane)
+    const char* kp = getenv("KNN_PLANE");
+    const bool plane = rt.world > 1 && !(kp && std::string(kp) == "0");
+    const int64_t pb = plane ? std::max<int64_t>(0, dmlp_plane_bytes(N, (int)A, 0)) : 0,
+                  oP = oO + ob;
     bytes = oP + up(pb);
     char* mine = nullptr;
     MPI_Win_allocate_shared(rt.rank == 0 ? (MPI_Aint)bytes : 0, 1, MPI_INFO_NULL, node, &mine,

@@ -236,7 +236,8 @@ struct Tuning {
   int screen = 0;
   int x1k = 1;
   int host_ops = 1;
-  int device_render = 0;  // DMLP_DEVICE_RENDER=1: r9r measured it slower (profiles/r9r_device_render_ab.txt)
+  // device render: -1 (default) by the cost model below, 0 never, 1 always (DMLP_DEVICE_RENDER)
+  int device_render = -1;
 };
 Tuning make_tuning() {
   Tuning t;
@@ -248,13 +249,21 @@ Tuning make_tuning() {
   // host operands when the render pool has at least 2 threads (Step::run: with 1 the device path
   // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
   // 3.74: profiles/r7h_host_budget.md)
-  t.device_render = env_int("DMLP_DEVICE_RENDER", 0) != 0 ? 1 : 0;
+  if (const char* e = std::getenv("DMLP_DEVICE_RENDER"); e && *e) t.device_render = e[0] != '0';
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
 }
 Tuning g_tune = make_tuning();
-bool dr_on() { return g_tune.device_render != 0; }
+bool dr_on() { return g_tune.device_render > 0; }
+// The device render's share of the work by the cost model: the host render ships 6 bytes per
+// value (the fp16 image + the int32 rows) after a host pass that writes both, the device render 4
+// (the int32 rows; the GPU renders the image from them) — at large N the step is bound by that
+// host pass and PCIe (profiles/r10a_large_n_render_ab.jsonl: N = 1e6, A = 128: 21.1 / 22.4 vs
+// 28.8 / 38.2 ms).  Below the early start's reach (one screen slice, nt <= 4096) the host render
+// keeps the early start (the render kernels get no wave slots beside its spinning screen).
+constexpr int64_t kDrMinValues = int64_t(1) << 23;
+bool dr_auto(int64_t N, int A) { return g_tune.device_render < 0 && N * A >= kDrMinValues; }
 // Every small host <-> device copy of the step goes through the SDMA engines (dmlp::dma_copy: a
 // copy below ~32 KiB would otherwise be a blit kernel, a memset a fill kernel) — its words are
 // cleared by a DMA copy from this page-locked block of zeros.
@@ -272,6 +281,19 @@ hipError_t dma_zero(void* dst, size_t bytes, hipStream_t s) {
   const void* z = zero_block();
   if (!z || bytes > (size_t)kZeroBytes) return hipMemsetAsync(dst, 0, bytes, s);
   return dmlp::dma_copy(dst, z, bytes, s);
+}
+// memcpy on the render pool (large host staging copies: labels, k)
+void pool_memcpy(void* dst, const void* src, int64_t bytes) {
+  if (bytes < (int64_t(1) << 18)) {
+    std::memcpy(dst, src, (size_t)std::max<int64_t>(bytes, 0));
+    return;
+  }
+  struct Cp { char* d; const char* s; int64_t n; } cp{(char*)dst, (const char*)src, bytes};
+  dmlp_host_pool_run([](void* c, int t, int nt) {
+    const Cp& p = *(const Cp*)c;
+    const int64_t lo = p.n * t / nt & ~int64_t(63), hi = t + 1 == nt ? p.n : p.n * (t + 1) / nt & ~int64_t(63);
+    if (hi > lo) std::memcpy(p.d + lo, p.s + lo, (size_t)(hi - lo));
+  }, &cp);
 }
 // an early-start slice's ready word: its max norm's fp32 bits, never 0 (0 = not landed): a
 // norm of 0 is published as the smallest denormal (a valid upper bound)
@@ -372,6 +394,7 @@ struct Ctx {
   HBuf<int64_t> s_len, small64_h;
   DBuf<int64_t> small64_d;
   hipEvent_t ev_done = nullptr;
+  hipEvent_t ev_chunk[kEarlySlices] = {};  // the large-N pipeline's chunk events
   DBuf<short> dx_hi, dq_hi;
   DBuf<short> dx_row;  // the fp16 image point-major (dmlp_x1_rowmajor) for the pair refine
   DBuf<double> d_mu;   // device render: the centre
@@ -405,6 +428,7 @@ Ctx& ctx() {
     CK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
+    for (hipEvent_t& e : w.ev_chunk) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   return w;
 }
@@ -471,6 +495,13 @@ struct HostOps {
   const unsigned* rdy = nullptr;  // ready words, one per slice (the slice's norm bits)
   int rdy_tiles = 1, rdy_n = 0;
   unsigned* estats = nullptr;
+  // the large-N pipeline (Step::run): the dataset lands in chunk_n chunks of the S-slice screen,
+  // chunk c = slices [chunk_s[c], chunk_s[c + 1]) complete once chunk_ev[c] fired — each chunk's
+  // screen is launched behind its own event while later chunks still cross PCIe
+  int chunk_n = 0, chunk_S = 0;
+  const int* chunk_s = nullptr;
+  const hipEvent_t* chunk_ev = nullptr;
+  std::function<void(int)> issue_chunk;  // queues chunk c's rows + render on the side stream
   const void* xrow = nullptr;  // xhi point-major (set once its copy kernel is queued), or none
 };
 
@@ -582,7 +613,8 @@ struct Local {
     const bool fin = labels != nullptr;
     if (impl == 0) {
       const int cap = dmlp_screen_x1_cap(kcls);
-      const int S = x1_slices(nq, KT, kcls, nt);
+      // (the large-N pipeline cut its chunks for its own slice count)
+      const int S = hx && hx->chunk_n > 0 && !idx ? hx->chunk_S : x1_slices(nq, KT, kcls, nt);
       int* ci = w.cand_ids.get((size_t)nq * S * cap);
       int* cc = w.cand_cnt.get((size_t)nq * S);
       float* ch = w.cand_h.get((size_t)nq * S * 2);
@@ -597,6 +629,15 @@ struct Local {
         if (S != 1 || idx) throw Fail{-7};
         CKL(dmlp_screen_x1_early(KT, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd + 1, hx->rdy,
                                  hx->rdy_tiles, hx->rdy_n, ci, cc, ch, hx->estats, st));
+      } else if (hx && hx->chunk_n > 0 && !idx) {
+        // the large-N pipeline: each chunk's slices as soon as its rows are rendered
+        for (int c = 0; c < hx->chunk_n; ++c) {
+          hx->issue_chunk(c);  // (the host packs chunk c + 1 while chunk c's screen runs)
+          CK(hipStreamWaitEvent(st, hx->chunk_ev[c], 0));
+          CKL(dmlp_screen_x1_part(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1,
+                                  S, hx->chunk_s[c], hx->chunk_s[c + 1] - hx->chunk_s[c], ci, cc,
+                                  ch, st));
+        }
       } else {
         CKL(dmlp_screen_x1(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1, S, ci,
                            cc, ch, st));
@@ -926,7 +967,7 @@ struct Step {
     const int64_t N = a->N, Q = a->Q, A = a->A;
     if (a->labels && N) {
       int* lh = w.s_lab.get(N);
-      std::memcpy(lh, a->labels, N * sizeof(int));
+      pool_memcpy(lh, a->labels, N * sizeof(int));
       CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
     }
     const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
@@ -1078,11 +1119,12 @@ struct Step {
     const bool x1_front = !a->exact && N > 0 && KT <= 8 && dmlp_screen_x1_qw(KT) > 0 &&
                           g_tune.screen == 0 &&
                           (g_tune.host_ops >= 2 ||
-                           (g_tune.host_ops == 1 && (pl || dr_on() || dmlp_host_threads() >= 2)));
+                           (g_tune.host_ops == 1 &&
+                            (pl || dr_on() || dr_auto(N, A) || dmlp_host_threads() >= 2)));
     // device render (opt-in, DMLP_DEVICE_RENDER=1): the GPU renders the screen operands from the
     // landed rows.  With a plane every rank must render the same slice kinds, so a plane step
     // always renders on the host (a device-render rank never renders its image slices)
-    bool dr = x1_front && dr_on() && !pl;
+    bool dr = x1_front && !pl && (dr_on() || dr_auto(N, A));
     if (Q == 0) {
       a->report_len = 0;
       w.text_len = 0;
@@ -1123,38 +1165,39 @@ struct Step {
     int* kd_pre = nullptr;
     if (x1_front && all_a) {
       int* kh = w.kk_h.get(Q);
-      struct Cp { int* dst; const int* src; int64_t n; } cp{kh, a->k, Q};
-      dmlp_host_pool_run([](void* c, int t, int nt_) {
-        const Cp& p = *(const Cp*)c;
-        const int64_t lo = p.n * t / nt_, hi = p.n * (t + 1) / nt_;
-        if (hi > lo) std::memcpy(p.dst + lo, p.src + lo, (hi - lo) * sizeof(int));
-      }, &cp);
+      pool_memcpy(kh, a->k, Q * sizeof(int));
       kd_pre = w.kdev.get(Q);
       CK(dmlp::dma_copy(kd_pre, kh, Q * sizeof(int), w.side));
     }
     // ---- device render: the rows (lossless int32, fp64 where a block is not 6-decimal) cross
-    // PCIe on the side stream, the query block first, then the dataset in slices, each followed
-    // by its render kernel (prep.hip k_render: the fp64 rows for the re-rank, the fp16 image /
-    // query fragments, the norms)
-    auto dr_issue = [&]() {
-      const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
-      int* h32 = w.s_i32.get(at + nqa);
-      int* d32 = w.d_i32.get(at + nqa);
-      unsigned* drw = w.dr_words.p;
-      unsigned* rbad = drw + 72;
-      const double* mud = w.d_mu.p;
-      short* xhi_d = (short*)const_cast<void*>(hx.xhi);
-      float* xin_d = const_cast<float*>(hx.xin);
-      const int ns = (int)std::min<int64_t>(kEarlySlices, nt);
-      const int64_t rts = (nt + ns - 1) / ns;
-      if (a->labels && N) {
-        int* lh = w.s_lab.get(N);
-        std::memcpy(lh, a->labels, N * sizeof(int));
-        CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
-      }
-      // rows [r0, r1) of X (or Qx) -> int32 staging at h32 + off + r0 A, else fp64; returns the
-      // render's source (device int32 base or the device fp64 rows)
-      auto ship = [&](const double* src, const double* const* tab, int64_t r0, int64_t r1,
+    // PCIe on the side stream, the query block first, then the dataset, each block followed by its
+    // render kernel (prep.hip k_render: the fp64 rows for the re-rank, the fp16 image / query
+    // fragments, the norms).  The large-N pipeline (every k in class a): the dataset in up to 8
+    // chunks of the screen's S slices, each chunk's event recorded behind its render, so the
+    // screen of chunk c runs while chunk c + 1 crosses PCIe (Local::pass); the labels last (only
+    // the vote reads them).  Otherwise one chunk, and every screen waits for all of it.
+    // Each chunk's screen launch must fill the GPU by itself, so the pipeline splits the scan into
+    // kPipeChunks x the slices one launch needs (x1_slices) — more (query, slice) lists for the
+    // refine, each chunk's screen at full occupancy (one slice per chunk ran at 1/8 of the chip:
+    // profiles/r10d_large_n_pipeline.txt)
+    constexpr int kPipeChunks = 4;
+    int S_all = 0, n_chunks = 1;
+    if (dr && x1_front && all_a) {
+      const int S1 = x1_slices((int)Q, KT, kmax, nt);
+      int64_t S_cap = std::min<int64_t>(256, nt / 16);  // (refine: <= 256 slices; >= 16 tiles each)
+      if (kmax > 32) S_cap = std::min<int64_t>(S_cap, nt * 64 / (32 * kmax));
+      S_all = (int)std::max<int64_t>(S1, std::min<int64_t>((int64_t)S1 * kPipeChunks, S_cap));
+      n_chunks = std::min(kEarlySlices, std::max(1, S_all / S1));
+    }
+    int chunk_s[kEarlySlices + 1] = {0};
+    for (int c = 0; c <= n_chunks; ++c)
+      chunk_s[c] = (int)((int64_t)std::max(1, S_all) * c / n_chunks);
+    const int64_t dr_at = (N * A + 3) & ~int64_t(3);  // (16-B aligned)
+    int* h32 = nullptr;
+    int* d32 = nullptr;
+    // rows [r0, r1) of X (or Qx) -> int32 staging at h32 + off + r0 A, else fp64; returns the
+    // render's source (device int32 base or the device fp64 rows)
+    auto ship = [&](const double* src, const double* const* tab, int64_t r0, int64_t r1,
                       int64_t off, double* dst64, const int** s32, const double** s64) {
         const int64_t n = (r1 - r0) * A;
         *s32 = nullptr;
@@ -1169,34 +1212,58 @@ struct Step {
         }
         const double* from = src ? src + r0 * A : nullptr;
         if (tab) {
-          double* h = w.s_f64.get(at + nqa) + off + r0 * A;
+          double* h = w.s_f64.get(dr_at + Q * A) + off + r0 * A;
           dmlp_cpu_gather_rows(tab + r0, r1 - r0, A, h);
           from = h;
         }
         CK(hipMemcpyAsync(dst64 + r0 * A, from, n * 8, hipMemcpyHostToDevice, w.side));
         *s64 = dst64;
-      };
-      {  // the queries
-        const int* s32;
-        const double* s64;
-        ship(a->Qx, a->Qr, 0, Q, at, Qd, &s32, &s64);
-        CKL(dmlp_render_rows(KT, A, s32, s64, 0, Q, Q, mud, Qd, 1, w.dq_hi.p, w.dq_n.p, nullptr,
-                             nullptr, rbad, drw + 8, nullptr, w.side));
-        CK(mark(M_OPS, w.side));
-      }
-      for (int i = 0; i < ns; ++i) {  // the dataset, slice by slice
-        const int64_t t0 = std::min<int64_t>(nt, i * rts), t1 = std::min<int64_t>(nt, t0 + rts);
-        if (t1 <= t0) continue;
-        const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
-        const double* s64 = nullptr;
-        if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
-        CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64, (t1 - t0) * 64,
-                             N, mud, Xd, 0, xhi_d, xin_d, const_cast<void*>(hx.xrow), words + kW_XNMAX,
-                             rbad, drw + i, nullptr, w.side));
-      }
-      CK(mark(M_DATA, w.side));
-      CK(hipEventRecord(w.ev_rows, w.side));
-      CK(mark(M_ROWS, w.side));
+    };
+    // what: 0 the queries, 1 + c dataset chunk c, -1 the labels and the rows' event (the tail)
+    std::function<void(int)> dr_part = [&](int what) {
+        const int64_t nqa = Q * A, at = dr_at;
+        unsigned* drw = w.dr_words.p;
+        unsigned* rbad = drw + 72;
+        const double* mud = w.d_mu.p;
+        short* xhi_d = (short*)const_cast<void*>(hx.xhi);
+        float* xin_d = const_cast<float*>(hx.xin);
+        h32 = w.s_i32.get(dr_at + nqa);
+        d32 = w.d_i32.get(dr_at + nqa);
+        if (what == 0) {
+          const int* s32;
+          const double* s64;
+          ship(a->Qx, a->Qr, 0, Q, at, Qd, &s32, &s64);
+          CKL(dmlp_render_rows(KT, A, s32, s64, 0, Q, Q, mud, Qd, 1, w.dq_hi.p, w.dq_n.p, nullptr,
+                               nullptr, rbad, drw + 8, nullptr, w.side));
+          CK(mark(M_OPS, w.side));
+          if (S_all > 0) CK(hipEventRecord(w.ev_ops, w.side));  // (the pipeline's screens: + chunk)
+          return;
+        }
+        if (what > 0) {  // slices [chunk_s[c], chunk_s[c + 1]) of S_all, tiles of tps each
+          const int c = what - 1;
+          const int64_t tps = S_all > 0 ? (nt + S_all - 1) / S_all : nt;
+          const int64_t t0 = std::min<int64_t>(nt, chunk_s[c] * tps);
+          const int64_t t1 = std::min<int64_t>(nt, chunk_s[c + 1] * tps);
+          if (t1 > t0) {
+            const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
+            const double* s64 = nullptr;
+            if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+            CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64,
+                                 (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
+                                 const_cast<void*>(hx.xrow), words + kW_XNMAX, rbad, drw + c,
+                                 nullptr, w.side));
+          }
+          CK(hipEventRecord(w.ev_chunk[c], w.side));
+          return;
+        }
+        CK(mark(M_DATA, w.side));
+        if (a->labels && N) {
+          int* lh = w.s_lab.get(N);
+          pool_memcpy(lh, a->labels, N * sizeof(int));
+          CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
+        }
+        CK(hipEventRecord(w.ev_rows, w.side));
+        CK(mark(M_ROWS, w.side));
     };
     // ---- front: the host renders the single-term screen's fp16 operands
     if (x1_front) {
@@ -1231,14 +1298,25 @@ struct Step {
       int rc;
       if (dr) {
         // the centre on the device; the render counters cleared; the rows and the render precede
-        // the screen (device render never starts early)
+        // each chunk's screen (device render never starts early)
         double* mud = w.d_mu.get(A);
         CK(dmlp::dma_copy(mud, mu, A * sizeof(double), w.side));
         CK(dma_zero(w.dr_words.get(80), 80 * sizeof(unsigned), w.side));
-        if (KT <= 2 && rowmajor_on()) hx.xrow = w.dx_row.get(nt * 64 * W);
+        // (the pair refine's point-major image: one screen slice only)
+        if (KT <= 2 && rowmajor_on() && S_all <= 1) hx.xrow = w.dx_row.get(nt * 64 * W);
         hx.xhi = xhi;
         hx.xin = xin;
-        dr_issue();
+        dr_part(0);
+        if (S_all > 0) {  // the pipeline: each chunk issued by the screen pass, then its screen
+          hx.chunk_n = n_chunks;
+          hx.chunk_S = S_all;
+          hx.chunk_s = chunk_s;
+          hx.chunk_ev = w.ev_chunk;
+          hx.issue_chunk = [&](int c) { dr_part(1 + c); };
+        } else {  // every chunk and the tail now: the screens wait for all of it
+          for (int c = 0; c < n_chunks; ++c) dr_part(1 + c);
+          dr_part(-1);
+        }
         rc = 0;
       } else if (early) {
         // query operands first (the whole front of the step); the image follows the screen's launch
@@ -1268,7 +1346,7 @@ struct Step {
       }
       if (rc == 0) {
         if (!dr) CK(mark(M_OPS, w.side));
-        CK(hipEventRecord(w.ev_ops, w.side));
+        if (!dr || S_all == 0) CK(hipEventRecord(w.ev_ops, w.side));
         CK(hipStreamWaitEvent(st, w.ev_ops, 0));
         hx.xhi = xhi;
         hx.xin = xin;
@@ -1309,7 +1387,10 @@ struct Step {
           // (host operands: called right after the first screen launch, so this mark completes
           // when it does; the device path calls it before its image is built: no mark)
           if (with_hx) CK(mark(M_SCREEN, st));
-          if (dr) return;  // device render: the rows and their render are queued already
+          if (dr) {  // device render: the rows and their render are queued; the pipeline's tail
+            if (S_all > 0) dr_part(-1);
+            return;
+          }
           if (with_hx && hx.rdy) {
             // the dataset image behind the queries, slice by slice, each followed by its ready
             // word (the slice's norm bits: the running screen waits on it); every word is

@@ -123,7 +123,15 @@ struct GroupIn {
                           // over the lists (cand_h holds the fixed seed, not a final threshold)
   int rescore = 1;        // 0 (screen_f64.hip's fp64 keys): every member of a group at or above
                           // the threshold goes to the exact re-rank (no image to rescore from)
+  int grows = 4;          // rows per group entry: 4 (consecutive) or 8 (the k <= 16 screen's pair
+                          // epilogue: rows 4 kg + i of steps 2p and 2p + 1, entry = 4 p + kg)
 };
+
+// row of member i (< grows) of the group with slice-relative entry index gi
+__device__ __forceinline__ int group_row(unsigned gi, int i, int grows) {
+  return grows == 8 ? (int)(gi >> 2) * 32 + (int)(gi & 3) * 4 + ((i & 4) << 2) + (i & 3)
+                    : (int)gi * 4 + i;
+}
 
 // GROUPS = KT of the single-term screen (1, 2, 4 or 8) for group-mode input, 0 otherwise.  The group
 // variant sizes its LDS for k <= 32 (the screen's limit) and labels in [lo, lo + 256) (wider
@@ -177,7 +185,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
     g_h1 = gin.cand_h[2 * (int64_t)p * S];  // slice 0's (COLLECT: every slice holds the seed)
     if (S == 1 && lane < cap) ebuf = (unsigned)cand_ids[(int64_t)p * cap + lane];
   }
-  // prefix of candidate counts over slices (S <= SMAX)
+  // prefix of candidate counts over slices (S <= SMAX); group mode: the largest eps over the
+  // slices — a screen launched per data chunk (pipeline.hip's large-N pipeline) bounds each
+  // slice's error with the image's max norm seen so far, and the global threshold must hold for
+  // every slice's members (a_k' - 2 max eps <= a_k - eps of any member)
   int* pre = s_pre[wave];
   bool ovf = false;
   if (lane == 0) {
@@ -188,9 +199,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
       if (n < 0) ovf = true;
       acc += n < 0 ? 0 : n;
       pre[s + 1] = acc;
+      if (GROUPS && s > 0) g_eps = fmaxf(g_eps, gin.cand_h[2 * ((int64_t)p * S + s) + 1]);
     }
   }
   ovf = __shfl(ovf ? 1 : 0, 0) != 0;
+  if (GROUPS) g_eps = __shfl(g_eps, 0);
   // the (+inf, -1) padding of slots [k, kstride) is written here, so callers need no fill pass
   // (slots [0, k) of a query handed back below are written by its escalation / exact path)
   for (int i = k + lane; i < kstride; i += 64) {
@@ -279,11 +292,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
     // Entries are fetched 64 groups at a time, one per lane, and dealt to the member lanes by
     // a shuffle: each 64-member step then waits on one gather (the fragments), not two.
     int nm = 0;
-    for (int j0 = 0; j0 < 4 * M; j0 += 64) {
+    const int GR = gin.grows, GS = GR == 8 ? 3 : 2;  // members per group entry, log2
+    for (int j0 = 0; j0 < GR * M; j0 += 64) {
       const int jm = j0 + lane;
-      const int g = jm >> 2;
-      if ((j0 & 255) == 0 && (S > 1 || j0 > 0)) {  // S == 1: block 0 was fetched up front
-        const int gg = (j0 >> 2) + lane;
+      const int g = jm >> GS;
+      // S == 1: block 0 was fetched up front
+      if ((j0 & (64 * GR - 1)) == 0 && (S > 1 || j0 > 0)) {
+        const int gg = (j0 >> GS) + lane;
         ebuf = 0;
         if (gg < M) {
           const int lo = slice_of(gg);
@@ -295,7 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
       bool keep = false;
       if (g < M) {
         const int lo = slice_of(g);
-        id = lo * gin.tiles_per_slice * 64 + (int)(e & 0xffffu) * 4 + (jm & 3);
+        id = lo * gin.tiles_per_slice * 64 + group_row(e & 0xffffu, jm & (GR - 1), GR);
         if (e >= kh && id < gin.n_points && !gin.rescore) {
           keep = true;
         } else if (e >= kh && id < gin.n_points) {
@@ -1075,7 +1090,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
     const float* __restrict__ xinit, const bf16x8* __restrict__ qhi, int n_points,
     double* __restrict__ out_d, int* __restrict__ out_i, int kstride,
     const int* __restrict__ labels, int* __restrict__ out_label, uint64_t* __restrict__ out_cs,
-    int* __restrict__ status, int* __restrict__ ovf_count, int abl) {
+    int* __restrict__ status, int* __restrict__ ovf_count, int abl, int grows) {
   constexpr int PM = 64;   // surviving members per query
   constexpr int KM = 64;   // k
   constexpr int EC = 4;    // group entries held per lane (cap <= 128)
@@ -1138,7 +1153,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
   Mw = max(Mw, __shfl_xor(Mw, 32));
   int nm = 0;
   dmlp::wave_sync();  // s_qf written
-  for (int j0 = 0; j0 < 4 * Mw; j0 += 32 * PAIR_U) {
+  const int GS = grows == 8 ? 3 : 2;  // members per group entry, log2
+  for (int j0 = 0; j0 < (Mw << GS); j0 += 32 * PAIR_U) {
     __asm__ volatile("" ::: "memory");  // keep the s_qf reads in the loop
     int id[PAIR_U];
     bool pass[PAIR_U];
@@ -1147,7 +1163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
 #pragma unroll
     for (int u = 0; u < PAIR_U; ++u) {
       const int jm = j0 + 32 * u + hl;
-      const int g = jm >> 2;
+      const int g = jm >> GS;
       const int src = half * 32 + (g & 31);
       unsigned e = 0;
 #pragma unroll
@@ -1155,7 +1171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
         const unsigned v = (unsigned)__shfl((int)ent[c], src);
         if ((g >> 5) == c) e = v;
       }
-      id[u] = (int)(e & 0xffffu) * 4 + (jm & 3);
+      id[u] = group_row(e & 0xffffu, jm & (grows - 1), grows);
       pass[u] = g < M && e >= kh && id[u] < n_points;
       const int pt = pass[u] ? id[u] : 0;
       if (xrow) {  // the point's 64 * KT bytes in one run (k_x1_rowmajor): one line per member
@@ -1426,14 +1442,16 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
                               const int* qk, int nq, double* out_d, int* out_i, int kstride,
                               const int* labels, int label_lo, int label_hi, int* out_label,
                               uint64_t* out_cs, int* status, int* ovf_count, int collect,
-                              void* stream, int kmax = 64) {
+                              void* stream, int kmax = 64, int grows = 4) {
   if (nq <= 0) return 0;
+  if (grows != 4 && grows != 8) return -1;
   if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
   if (KT != 1 && KT != 2 && KT != 4 && KT != 8) return -1;
   if (hl != 1 && hl != 2) return -1;
   const int64_t n_tiles = (n_points + 63) / 64;
-  const GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
-                    (int)((n_tiles + S - 1) / S), collect ? 1 : 0};
+  GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
+              (int)((n_tiles + S - 1) / S), collect ? 1 : 0};
+  gin.grows = collect ? 4 : grows;
   // collect (the large-k lists, fp16 host operands only): k <= 256 over <= 512 filtered members
   if (collect) {
     if (hl != 1) return -1;
@@ -1463,13 +1481,13 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
                          cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
                          (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
                          kstride, labels, out_label,
-                         out_cs, status, ovf_count, pair_abl);
+                         out_cs, status, ovf_count, pair_abl, gin.grows);
     else
       hipLaunchKernelGGL((k_refine_pair<2>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
                          cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
                          (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
                          kstride, labels, out_label,
-                         out_cs, status, ovf_count, pair_abl);
+                         out_cs, status, ovf_count, pair_abl, gin.grows);
     DMLP_LAUNCH_CHECK();
     return 0;
   }
@@ -1524,10 +1542,12 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
                                    int* out_i, int kstride, const int* labels, int label_lo,
                                    int label_hi, int* out_label, uint64_t* out_cs, int* status,
                                    int* ovf_count, int collect, void* stream) {
+  // (the lists' producer, by its cap: dmlp_screen_x1_cap(kmax) of the screen that wrote them)
+  const int grows = cap == dmlp_screen_x1_cap(16) ? dmlp_screen_x1_group_rows(16) : 4;
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, nullptr, xinit,
                             qhi, KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
                             label_lo, label_hi, out_label, out_cs, status, ovf_count, collect,
-                            stream);
+                            stream, 64, grows);
 }
 
 extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* cand_cnt,
@@ -1541,7 +1561,7 @@ extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* ca
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xrow, xinit, qhi,
                             KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
                             label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream,
-                            kmax);
+                            kmax, dmlp_screen_x1_group_rows(kmax));
 }
 
 // The host-rendered fp16 image (tile layout of the screen's MFMA A operand: point p's 8-element

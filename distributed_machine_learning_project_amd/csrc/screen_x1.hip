@@ -91,6 +91,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
   // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
   using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
+  // PAIR (k <= 16, not COLLECT): the hit test and the append run once per PAIR of steps, on the
+  // 8-row group max (rows 4 kg .. 4 kg + 3 of both steps; entry index = pair * 4 + kg), instead of
+  // per step on 4-row groups: the per-step max stays, the compare, the branch and the taken
+  // step's append VALU halve (the screen is VALU-issue-bound: ~8.6 VALU per MFMA).  The
+  // refine expands each entry to its 8 members (dmlp_screen_x1_group_rows).
+  constexpr bool PAIR = SUB == 16 && !COLLECT;
+  static_assert(!PAIR || (CHECK == 2 && DEPTH == 4), "the pair epilogue assumes 2-step checks");
   constexpr int CT = C::CT;
   constexpr int D = C::D;
   constexpr int NH = C::NCOL / 64;  // columns per lane in the lane-owns-column phases
@@ -411,6 +418,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   bf16x8 A[D][KT];
   f32x4 Xi[D];
   f32x4 acc[2][CT];
+  float pm[CT];  // PAIR: the pair's first step's 4-row maxima
 #define DMLP_LOADA(J, R)                                                                        \
   do {                                                                                          \
     _Pragma("unroll") for (int kt = 0; kt < KT; ++kt)                                           \
@@ -435,18 +443,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
         acc[AB][ct] = mfma16<F16>(A[R][kt], bh[ct][kt], acc[AB][ct]);                           \
     }                                                                                           \
   } while (0)
-#define DMLP_EPILOGUE(AB, J)                                                                    \
+#define DMLP_EPILOGUE(AB, J, ODD)                                                               \
   do {                                                                                          \
-    /* per column tile: the 4-row group max, and the wave's hit mask straight from the        \
-       compare (an SGPR pair: the uniform branch below tests it with one s_cmp) */             \
+    /* per column tile: the 4-row group max (PAIR: on the pair's second step, the 8-row max), \
+       and the wave's hit mask straight from the compare (an SGPR pair: the uniform branch    \
+       below tests it with one s_cmp) */                                                       \
     float m_[CT];                                                                               \
     unsigned long long any_ = 0;                                                                \
+    const bool first_ = PAIR && !(ODD); /* (ODD: J's parity, known at compile time) */          \
     _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                         \
-      m_[ct] = fmaxf(fmaxf(acc[AB][ct][0], acc[AB][ct][1]), fmaxf(acc[AB][ct][2], acc[AB][ct][3])); \
-      any_ |= __builtin_amdgcn_ballot_w64(m_[ct] >= h[ct]);                                     \
+      /* linear chains: the combiner makes 2 v_max3 of the pair's second step (pm + 4 rows) */ \
+      if (PAIR && !first_)                                                                      \
+        m_[ct] = fmaxf(fmaxf(fmaxf(fmaxf(pm[ct], acc[AB][ct][0]), acc[AB][ct][1]),              \
+                             acc[AB][ct][2]), acc[AB][ct][3]);                                  \
+      else                                                                                      \
+        m_[ct] = fmaxf(fmaxf(fmaxf(acc[AB][ct][0], acc[AB][ct][1]), acc[AB][ct][2]),            \
+                       acc[AB][ct][3]);                                                         \
+      if (first_) pm[ct] = m_[ct];                                                              \
+      else any_ |= __builtin_amdgcn_ballot_w64(m_[ct] >= h[ct]);                                \
     }                                                                                           \
-    if ((C::D == 4 || (J) < nsteps) && any_) {                                                  \
-      unsigned gl_ = (unsigned)((J) * 4 + kg);                                                  \
+    if (!first_ && (C::D == 4 || (J) < nsteps) && any_) {                                       \
+      unsigned gl_ = PAIR ? (unsigned)(((J) >> 1) * 4 + kg) : (unsigned)((J) * 4 + kg);        \
       asm volatile("" : "+v"(gl_)); /* one VGPR: each key is a single v_and_or / v_bfi */       \
       /* branch-free: every lane writes its entry to the next free slot and advances only on  \
          a hit (slot cnt <= SUB-1 exists; a miss is overwritten later and never read) */       \
@@ -556,13 +573,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
         DMLP_LOAD(j + D, r);
-        if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1);
+        if (j > 0) DMLP_EPILOGUE((r + 1) & 1, j - 1, (r + 1) & 1);
+        // (PAIR: the appends come at even r — the pairs end at odd steps — and CHECK = 2 puts a
+        // check one step behind each)
         if (r % CHECK == CHECK - 1) DMLP_CHECK();
       }
     }
     // the last issued step (padded up to a multiple of D)
     const int jl = ((nsteps + D - 1) / D) * D - 1;
-    DMLP_EPILOGUE(jl & 1, jl);
+    DMLP_EPILOGUE(jl & 1, jl, 1);  // (jl is odd: nsteps % 4 == 0)
   }
 #undef DMLP_LOAD
 #undef DMLP_LOADA
@@ -652,8 +671,12 @@ extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
   (void)kmax;
   return x1_kt_ok(KT) ? 64 : 0;
 }
-// group ids per (query, slice) (refine expands each to its 4 members)
+// group ids per (query, slice) (refine expands each to its dmlp_screen_x1_group_rows members)
 extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
+// rows per group entry of the screen that serves kmax (and of its early-start form): 8 (k <= 16:
+// the pair epilogue, steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive rows);
+// the COLLECT pass always 4
+extern "C" int dmlp_screen_x1_group_rows(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }
 // resident workgroups (= waves) per CU: LDS-bound at 17.5 KiB (SUB 16, 4 tiles) / 33.5 KiB
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {

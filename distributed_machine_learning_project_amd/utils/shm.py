@@ -22,7 +22,8 @@ RCCL collectives with a host sync each.
 Layout: 64-byte header (magic, N, Q, A, label lo, label hi, k min, k max — a summary for tools;
 the KNN strategies re-scan the labels and k inside every timed call), two int64 work counters at
 byte 64 (the dynamic farm's chunk claims, alternating per call), a barrier counter at byte 96,
-a call generation at byte 80 (the dynamic farm: which counter a call claims from),
+a call generation at byte 80 (the dynamic farm: which counter a call claims from), the render
+plane flag at byte 112 (1: the segment reserves the plane region),
 per-rank int64 slots from byte 128 (report lengths), then labels i32[N], k i32[Q],
 X f64[N*A], Qx f64[Q*A], out u8[48*Q + 64] (report text), res i64[2*Q] (the dynamic farm's
 (label, checksum) per query), plane (the node render plane, csrc/plane.cpp: the dataset's fp16
@@ -40,6 +41,7 @@ from .io import KNNInput
 
 _MAGIC = 0x444D4C50534D4831  # "DMLPSMH1"
 _ALIGN = 4096
+_PLANE_FLAG = 112  # header word: 1 when the segment reserves the render plane
 
 
 def _up(x):
@@ -53,11 +55,14 @@ def _plane_bytes(N, A):
     return max(b, 0)
 
 
-def _layout(N, Q, A):
+def _layout(N, Q, A, plane):
+    """Offsets of the segment's arrays; the render plane region only when the segment carries one
+    (a one-rank job, or KNN_PLANE=0, maps no plane: it would be N * A * 2 bytes of tmpfs unused)."""
     off = {}
     o = _ALIGN
     for name, nbytes in (("labels", 4 * N), ("k", 4 * Q), ("X", 8 * N * A), ("Qx", 8 * Q * A),
-                         ("out", 48 * Q + 64), ("res", 16 * Q), ("plane", _plane_bytes(N, A))):
+                         ("out", 48 * Q + 64), ("res", 16 * Q),
+                         ("plane", _plane_bytes(N, A) if plane else 0)):
         off[name] = o
         o += _up(max(nbytes, 1))
     return off, o
@@ -87,8 +92,8 @@ class SharedInput(KNNInput):
     """KNNInput whose arrays are views of a node-shared mapping (same on every rank)."""
     shared = True
 
-    def __init__(self, mm, path, N, Q, A, owner):
-        off, total = _layout(N, Q, A)
+    def __init__(self, mm, path, N, Q, A, owner, plane):
+        off, total = _layout(N, Q, A, plane)
         labels = np.frombuffer(mm, np.int32, N, off["labels"])
         k = np.frombuffer(mm, np.int32, Q, off["k"])
         X = np.frombuffer(mm, np.float64, N * A, off["X"]).reshape(N, A)
@@ -103,7 +108,7 @@ class SharedInput(KNNInput):
         self._nbar = 0  # barriers this process has entered
         self._mm, self.path, self.owner, self.nbytes = mm, path, owner, total
         self._pinned = False
-        self._plane_off, self._plane_bytes = off["plane"], _plane_bytes(N, A)
+        self._plane_off, self._plane_bytes = off["plane"], _plane_bytes(N, A) if plane else 0
         self._plane_gen = 0  # node render plane calls this process made (same on every rank)
 
     def plane(self, rank: int, renderers: int):
@@ -118,20 +123,23 @@ class SharedInput(KNNInput):
                      wait_s=float(os.environ.get("DMLP_PLANE_WAIT_S", "60")))
 
     @staticmethod
-    def create(inp: KNNInput, directory: str = "/dev/shm", query_nodes=None) -> "SharedInput":
+    def create(inp: KNNInput, directory: str = "/dev/shm", query_nodes=None,
+               plane: bool = False) -> "SharedInput":
         """query_nodes: [(first query, end query, NUMA node), ...] — the query rows (and their
         report bytes) of each block are placed on that node before they are written (the GPU
-        that reads them hangs off it); the dataset is interleaved over the nodes named."""
+        that reads them hangs off it); the dataset is interleaved over the nodes named.
+        plane: reserve the node render plane (P > 1 ranks share the segment's dataset render)."""
         N, A = inp.X.shape
         Q = inp.Qx.shape[0]
-        off, total = _layout(N, Q, A)
+        off, total = _layout(N, Q, A, plane)
         directory = _roomy_dir(directory, total)
         path = os.path.join(directory, f"dmlp_input_{os.getpid()}_{uuid.uuid4().hex[:8]}")
         mm = np.memmap(path, np.uint8, "w+", shape=(total,))
         if query_nodes:
-            _place(mm, off, N, Q, A, query_nodes)
+            _place(mm, off, N, Q, A, query_nodes, plane)
         np.frombuffer(mm, np.int64, 4, 0)[:] = [_MAGIC, N, Q, A]
-        s = SharedInput(mm, path, N, Q, A, owner=True)
+        np.frombuffer(mm, np.int64, 1, _PLANE_FLAG)[0] = int(bool(plane))
+        s = SharedInput(mm, path, N, Q, A, owner=True, plane=plane)
         if s._plane_bytes:
             from .. import _lib
             _lib.check(_lib.lib().dmlp_plane_init(mm.ctypes.data + off["plane"], s._plane_bytes,
@@ -211,7 +219,8 @@ class SharedInput(KNNInput):
         magic, N, Q, A = (int(v) for v in np.frombuffer(mm, np.int64, 4, 0))
         if magic != _MAGIC:
             raise ValueError(f"{path}: not a dmlp input segment")
-        return SharedInput(mm, path, N, Q, A, owner=False)
+        plane = bool(np.frombuffer(mm, np.int64, 1, _PLANE_FLAG)[0])
+        return SharedInput(mm, path, N, Q, A, owner=False, plane=plane)
 
     def pin(self) -> bool:
         """Page-lock the mapping for DMA (GPU ranks).  Returns False if HIP refused it (copies
@@ -256,7 +265,7 @@ def _mbind(addr: int, length: int, nodes, mode: int) -> bool:
     return rc == 0
 
 
-def _place(mm, off, N, Q, A, query_nodes):
+def _place(mm, off, N, Q, A, query_nodes, plane):
     """NUMA placement of a fresh segment (best effort: any failure leaves the default policy).
     MPOL_PREFERRED, not MPOL_BIND: a node short of memory falls back to another node instead of
     failing rank 0's tmpfs writes with SIGBUS."""
@@ -267,7 +276,8 @@ def _place(mm, off, N, Q, A, query_nodes):
         return
     if len(nodes) > 1:
         _mbind(base + off["X"], 8 * N * A, nodes, MPOL_INTERLEAVE)
-        _mbind(base + off["plane"], _plane_bytes(N, A), nodes, MPOL_INTERLEAVE)
+        if plane:
+            _mbind(base + off["plane"], _plane_bytes(N, A), nodes, MPOL_INTERLEAVE)
     for a, b, n in query_nodes:
         if n >= 0 and b > a:
             _mbind(base + off["Qx"] + 8 * A * a, 8 * A * (b - a), [n], MPOL_PREFERRED)
@@ -303,7 +313,9 @@ def share_input(comm, inp: KNNInput | None, pin: bool | None = None) -> SharedIn
             counts, displs = block_partition(inp.Qx.shape[0], comm.world)
             qn = [(displs[r], displs[r] + counts[r], gpu_numa_node(r % ndev))
                   for r in range(comm.world)]
-        s = SharedInput.create(inp, query_nodes=qn)
+        # the render plane only where ranks share a render (parallel/strategies.py farm)
+        s = SharedInput.create(inp, query_nodes=qn,
+                               plane=comm.world > 1 and os.environ.get("KNN_PLANE", "1") != "0")
         path = s.path
     if comm.world > 1:
         obj = [path]

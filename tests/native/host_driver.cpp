@@ -30,7 +30,12 @@ int main() {
     std::snprintf(line, sizeof line, "%d %.6f %.6f %.6f\n", lab[i], pts[i][0], pts[i][1], pts[i][2]);
     txt += line;
   }
-  txt += "Q 3 1 1 1\nQ 9 0 0 0\nQ 0 5 5 5\nQ 6 1.5 1.5 1.5\n";
+  const int qk[4] = {3, 9, 0, 6};
+  const double qp[4] = {1, 0, 5, 1.5};
+  for (int i = 0; i < 4; ++i) {
+    std::snprintf(line, sizeof line, "Q %d %.6f %.6f %.6f\n", qk[i], qp[i], qp[i], qp[i]);
+    txt += line;
+  }
   int64_t N, Q, body;
   int A;
   EXPECT(dmlp_parse_header(txt.data(), txt.size(), &N, &Q, &A, &body) == 0);
@@ -40,6 +45,21 @@ int main() {
   EXPECT(dmlp_parse_body(txt.data(), txt.size(), body, N, Q, A, labels.data(), X.data(), k.data(),
                          Qx.data(), 3) == 0);
   EXPECT(k[1] == 9 && labels[5] == 2);
+  // ---- the pool-formatted input writer reproduces the text byte for byte
+  {
+    const char* wp = "/tmp/dmlp_host_driver_input.txt";
+    EXPECT(dmlp_cpu_write_input(wp, labels.data(), X.data(), N, k.data(), Qx.data(), Q, A) == 0);
+    std::FILE* f = std::fopen(wp, "rb");
+    std::string back;
+    if (f) {
+      char buf[4096];
+      size_t n;
+      while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) back.append(buf, n);
+      std::fclose(f);
+    }
+    std::remove(wp);
+    EXPECT(back == txt);
+  }
   const std::string bad = "2 1 2\n0 1 2\n1 x 2\nQ 1 0 0\n";
   int64_t bN, bQ, bb;
   int bA;

@@ -203,6 +203,26 @@ def test_segment_barrier_and_slots(tmp_path):
             assert row == [1000 * r + i for i in range(world)]
 
 
+def test_segment_plane_only_when_shared(tmp_path):
+    """The node-shared segment reserves the render plane only when asked (P > 1 with the plane on,
+    utils/shm.py share_input): a one-rank segment is the plane's bytes smaller and hands out no
+    plane; an attach reads the flag from the header and lays the segment out the same way."""
+    from distributed_machine_learning_project_amd.utils import shm
+    from distributed_machine_learning_project_amd.utils.io import generate
+    inp = generate(4096, 64, 32, 0.0, 1.0, 1, 8, 5, seed=4)
+    plain = shm.SharedInput.create(inp, directory=str(tmp_path))
+    shared = shm.SharedInput.create(inp, directory=str(tmp_path), plane=True)
+    pb = shm._plane_bytes(4096, 32)
+    assert pb > 0 and shared.nbytes - plain.nbytes == shm._up(pb) - shm._ALIGN  # (a 1-page stub)
+    assert plain.plane(0, 2) is None
+    for s in (shared, shm.SharedInput.attach(shared.path)):
+        assert s._plane_bytes == pb and s.plane(0, 2) is not None
+        assert np.array_equal(s.X, inp.X) and np.array_equal(s.k, inp.k)
+    assert shm.SharedInput.attach(plain.path)._plane_bytes == 0
+    plain.close()
+    shared.close()
+
+
 def test_segment_numa_placement(tmp_path, monkeypatch):
     """NUMA placement of the node-shared segment (utils/shm.py _place/_mbind) is best effort and
     never changes what is stored: a segment created with per-block query nodes holds the same

@@ -158,6 +158,49 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
         L.dmlp_pipeline_set(b"device_render", old_dr)
 
 
+@pytest.mark.parametrize("n,A,Q,kmin,kmax", [(300_000, 32, 4096, 1, 32), (110_000, 100, 2048, 16, 16),
+                                              (270_000, 48, 3000, 40, 64)])
+def test_native_step_large_n_pipeline(gpu, n, A, Q, kmin, kmax):
+    """at large N the step picks the device render by its cost model (the host
+    render's fp16 image + int32 rows vs the int32 rows alone) and runs the screen as a pipeline
+    over up to 8 dataset chunks of its slices — chunk c's screen while chunk c + 1 crosses PCIe,
+    each chunk's eps from the image's max norm seen so far (the refine takes the largest over the
+    slices).  Two alternated inputs, then the host render forced (DMLP_DEVICE_RENDER=0 by the
+    switch) and an input whose last row lies outside the fp16 range (the whole call redone on the
+    device image): every report, label and checksum == the oracle's."""
+    from distributed_machine_learning_project_amd import _lib
+    import torch
+    L = _lib.lib()
+    cases = []
+    for seed in (11, 12, 13):
+        inp = dmlp.generate(n, Q, A, 0.0, 1000.0, kmin, kmax, 8, seed=seed + n)
+        if seed == 13:
+            inp.X[-1, 0] = 5.0e6  # far outside the fp16 screen's range, in the last chunk
+        else:
+            inp.X[-1] = 1000.0  # the largest |x - mu| sits in the last chunk: eps grows there
+        _, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+        lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+        cases.append((inp, lab_ref, cs, dmlp.format_report(cs)))
+    dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
+    old = L.dmlp_pipeline_set(b"device_render", -1)
+    try:
+        for rnd, (ci, dr) in enumerate(((0, -1), (1, -1), (0, -1), (1, 0), (2, -1))):
+            L.dmlp_pipeline_set(b"device_render", dr)
+            inp, lab_ref, cs, expect = cases[ci]
+            r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
+            assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
+            np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
+            np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
+            assert r.early == 0
+            if ci == 2:
+                assert r.path == 2  # (the device image path after the out-of-range render)
+            else:
+                assert r.path == 0
+                assert K.pipeline_stats()["device_render"] == (1 if dr < 0 else 0), f"round {rnd}"
+    finally:
+        L.dmlp_pipeline_set(b"device_render", old)
+
+
 def test_debug_listing(gpu, workload):
     inp, _, d, i = workload
     eng = _engine("ring", debug=True)

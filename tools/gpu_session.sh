@@ -28,6 +28,7 @@
 #   blits      copy-engine probe + every runtime kernel / SDMA copy of 6 native steps (step_driver)
 #   dropin8    drop-in at P = 8, Q = 131072 per rank on the one GPU: CMA / fill / auto fronts
 #   lnr        large-N steps: host vs device render at N 1e6 / 1e7 (step_driver)
+#   rt70       torch's bundled HIP runtime vs /opt/rocm's: copy kinds, the step's copies, step time
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
@@ -215,6 +216,23 @@ for task in "$@"; do
       step blits 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$OUT/bl" -o run \
           --output-format csv -- tools/bin/step_driver --steps 6 --warmup 30 --timeline
       python3 tools/copy_kind.py step "$OUT/bl" > "$OUT/step_copies.txt"; tail -80 "$OUT/step_copies.txt" ;;
+    rt70)  # the HIP runtime torch bundles (torch/lib, ROCm 7.0: what libdmlp runs on inside a
+           # Python process) vs /opt/rocm's: the copy-kind probe and the native step's copies
+           # under it, then bench-shape step time on each runtime
+      TL=$(python3 -c "import os, torch; print(os.path.dirname(torch.__file__) + '/lib')")
+      LD_LIBRARY_PATH=$TL step copykind70 120 rocprofv3 --kernel-trace --memory-copy-trace \
+          -d "$OUT/ck70" -o run --output-format csv -- tools/bin/copy_kind_probe
+      python3 tools/copy_kind.py probe "$OUT/ck70" > "$OUT/copy_kind70.txt"; cat "$OUT/copy_kind70.txt"
+      LD_LIBRARY_PATH=$TL step blits70 300 rocprofv3 --kernel-trace --memory-copy-trace \
+          -d "$OUT/bl70" -o run --output-format csv -- tools/bin/step_driver --steps 6 --warmup 30 \
+          --timeline
+      python3 tools/copy_kind.py step "$OUT/bl70" > "$OUT/step_copies70.txt"
+      tail -60 "$OUT/step_copies70.txt"
+      for R in 1 2; do
+        step sd72_$R 120 tools/bin/step_driver --steps 300 --warmup 200
+        LD_LIBRARY_PATH=$TL step sd70_$R 120 tools/bin/step_driver --steps 300 --warmup 200
+      done
+      grep -H '"ms_per_step"' "$OUT"/sd7*.log | cut -c1-200 ;;
     dropin8)  # the engine.h drop-in at P = 8 through the node window on the one GPU, Q = 131072 per
               # rank (KNN_DATA_PLANE=host), each front (CMA / rank-0 fill), plus the CMA probe
       step cmaprobe 120 tools/bin/cma_probe
@@ -223,18 +241,26 @@ for task in "$@"; do
             --gpus 8 --q-per-gpu 131072 --steps 2 --warmup 1
       done
       grep -h -o '"window": {[^}]*}' "$OUT"/dropin8_*.log | tee "$OUT/dropin8_window.txt" ;;
-    lnr)  # large-N steps (native step driver): host render vs device render (DMLP_DEVICE_RENDER) at
-          # the verdict's shapes, alternating, with the step timeline and host issue per step
+    lnr)  # large-N steps (native step driver): the default (device render by the cost model, the
+          # chunked screen pipeline) vs the host render forced, alternating, step timelines
       for SH in "1000000 32 10" "1000000 128 6" "10000000 32 4"; do
         set -- $SH
         for R in 1 2; do
-          for DR in 0 1; do
-            DMLP_DEVICE_RENDER=$DR step lnr_n$1_a$2_dr${DR}_$R 300 tools/bin/step_driver --n $1 \
-                --a $2 --q 16384 --steps $3 --warmup 2 --timeline
-          done
+          step lnr_n$1_a$2_auto_$R 300 tools/bin/step_driver --n $1 --a $2 --q 16384 --steps $3 \
+              --warmup 2 --timeline
+          DMLP_DEVICE_RENDER=0 step lnr_n$1_a$2_host_$R 300 tools/bin/step_driver --n $1 --a $2 \
+              --q 16384 --steps $3 --warmup 2 --timeline
         done
       done
-      grep -h '^{' "$OUT"/lnr_*.log | tee "$OUT/lnr_summary.txt" ;;
+      grep -H '^{' "$OUT"/lnr_*.log | tee "$OUT/lnr_summary.txt" ;;
+    dropinp)  # the drop-in at P = 4 / 8 through the node window on the one GPU, each front, with
+              # every rank's fetch phases (KNN_METRICS)
+      for P in 4 8; do
+        for F in cma fill; do
+          KNN_WINDOW_FRONT=$F KNN_DATA_PLANE=host step dropin${P}_$F 600 python bench.py \
+              --harness dropin --gpus $P --q-per-gpu 131072 --steps 2 --warmup 1
+        done
+      done ;;
     final)  # end-of-round validation: GPU tier, smoke(), the driver's bench line, --verify of the
             # default and the exact path, the P = 3 host-plane rehearsal with --verify
       step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \

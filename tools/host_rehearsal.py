@@ -98,7 +98,7 @@ def main():
     from distributed_machine_learning_project_amd.utils.shm import SharedInput
     P = a.ranks
     inp0 = generate(a.n_data, a.q_per_gpu * P, 32, 0.0, 1000.0, 16, 16, 10, seed=42)
-    inp = SharedInput.create(inp0)
+    inp = SharedInput.create(inp0, plane=a.plane and P > 1)
     inp.pin()
     total = a.warmup + a.steps
     ctx = mp.get_context("spawn")

@@ -13,11 +13,12 @@ OUT="${1:-/tmp/dmlp_asan}"
 mkdir -p "$OUT"
 SRC="$ROOT/distributed_machine_learning_project_amd/csrc"
 g++ -O1 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -fsanitize=address,undefined \
-    -fno-sanitize-recover=undefined -I"$SRC" "$SRC/cpu.cpp" "$ROOT/tests/native/host_driver.cpp" \
+    -fno-sanitize-recover=undefined -I"$SRC" "$SRC/cpu.cpp" "$SRC/host_prep.cpp" \
+    "$ROOT/tests/native/host_driver.cpp" \
     -pthread -o "$OUT/host_driver"
 ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1 "$OUT/host_driver"
 g++ -O1 -g -std=c++17 -ffp-contract=off -fsanitize=thread -I"$SRC" "$SRC/cpu.cpp" \
-    "$ROOT/tests/native/host_driver.cpp" -pthread -o "$OUT/host_driver_tsan"
+    "$SRC/host_prep.cpp" "$ROOT/tests/native/host_driver.cpp" -pthread -o "$OUT/host_driver_tsan"
 TSAN_OPTIONS=halt_on_error=1 "$OUT/host_driver_tsan"
 g++ -O1 -g -std=c++17 -ffp-contract=off -fno-omit-frame-pointer -fsanitize=address,undefined \
     -fno-sanitize-recover=undefined -I"$SRC" "$SRC/host_prep.cpp" \
