@@ -28,6 +28,8 @@
 #   blits      copy-engine probe + every runtime kernel / SDMA copy of 6 native steps (step_driver)
 #   dropin8    drop-in at P = 8, Q = 131072 per rank on the one GPU: CMA / fill / auto fronts
 #   lnr        large-N steps: host vs device render at N 1e6 / 1e7 (step_driver)
+#   pyck       NoCU copies from Python with / without torch (tools/copy_kind_py.py)
+#   h2dbw      H2D bandwidth over 1 / 2 / 4 streams (tests/native/h2d_bw.cpp)
 #   rt70       torch's bundled HIP runtime vs /opt/rocm's: copy kinds, the step's copies, step time
 #   final      end-of-round validation (GPU tier, smoke, driver bench line, verify, exact, P = 3)
 #   dropin_p   the engine.h drop-in at P = 2 / 3 through the node window (one GPU)
@@ -233,6 +235,17 @@ for task in "$@"; do
         LD_LIBRARY_PATH=$TL step sd70_$R 120 tools/bin/step_driver --steps 300 --warmup 200
       done
       grep -H '"ms_per_step"' "$OUT"/sd7*.log | cut -c1-200 ;;
+    h2dbw)  # H2D bandwidth from page-locked memory over 1 / 2 / 4 concurrent streams
+      step h2dbw 120 tools/bin/h2d_bw ;;
+    pyck)  # the NoCU copies from a Python process, with / without torch initialised first
+      for T in 0 1; do
+        for M in hostmalloc registered; do
+          step pyck_${T}_$M 120 rocprofv3 --kernel-trace --stats -d "$OUT/pyck_${T}_$M" -o run \
+              --output-format csv -- python3 tools/copy_kind_py.py $T $M
+          echo "torch=$T mem=$M copyBuffer kernels: $(grep -c copyBuffer \
+              "$OUT/pyck_${T}_$M/run_kernel_trace.csv" || true)"
+        done
+      done ;;
     dropin8)  # the engine.h drop-in at P = 8 through the node window on the one GPU, Q = 131072 per
               # rank (KNN_DATA_PLANE=host), each front (CMA / rank-0 fill), plus the CMA probe
       step cmaprobe 120 tools/bin/cma_probe
