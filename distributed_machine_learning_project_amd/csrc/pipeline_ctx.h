@@ -150,10 +150,10 @@ inline int early_qchunks() {
   static const int q = std::min(16, std::max(1, env_int("DMLP_FAST_QCHUNKS", 4)));
   return q;
 }
-// Device render (DMLP_DEVICE_RENDER=1): the screen's fp16 operands rendered on the GPU (prep.hip
-// k_render) from the rows that cross PCIe for the exact re-rank anyway (lossless int32): the host
-// only packs int32 rows.  Off by default: the operands then wait for the int32 rows, and it
-// measured slower than the host render (host_prep.cpp) at every size (profiles/r9r).
+// Device render: the screen's fp16 operands rendered on the GPU (prep.hip k_render) from the rows
+// that cross PCIe for the exact re-rank anyway (lossless int32): the host only packs int32 rows.
+// On by the cost model at large N (dr_auto below: the chunked large-N pipeline); at the headline
+// shape the operands would wait for the int32 rows, slower than the host render (profiles/r9r).
 inline bool dr_on();  // (Tuning::device_render below)
 // The render kernels (k_render: one-wave workgroups, 40 VGPRs, no LDS) would have to run beside
 // an early-start screen that fills the GPU and spins on their ready words.  Measured

@@ -27,6 +27,7 @@
 #   rehearsal  8-GPU host budget on one GPU: GPU rank + 7 CPU phantoms (tools/host_rehearsal.py)
 #   blits      copy-engine probe + every runtime kernel / SDMA copy of 6 native steps (step_driver)
 #   dropin8    drop-in at P = 8, Q = 131072 per rank on the one GPU: CMA / fill / auto fronts
+#   dropinp    drop-in at P = 4 / 8 through the node window, each front of FRONTS (cma fill)
 #   lnr        large-N steps: host vs device render at N 1e6 / 1e7 (step_driver)
 #   pyck       NoCU copies from Python with / without torch (tools/copy_kind_py.py)
 #   h2dbw      H2D bandwidth over 1 / 2 / 4 streams (tests/native/h2d_bw.cpp)
@@ -98,10 +99,11 @@ for task in "$@"; do
                "GRBM_GUI_ACTIVE GRBM_COUNT"; do
         n=$((n + 1))
         # counters only: no trace domains beside --pmc
+        # (the headline step itself: the native step driver, early start, host operands)
         step pmc$n 120 rocprofv3 --kernel-trace --pmc $C -d "$OUT/pmc$n" -o run --output-format csv \
-            -- python3 tools/quick_gpu_bench.py --q 131072 --iters 2 --check 0
+            -- tools/bin/step_driver --steps 3 --warmup 3
       done
-      python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
+      python3 tools/pmc_csv_summary.py "$OUT" pmc > "$OUT/pmc_summary.txt"; cat "$OUT/pmc_summary.txt" ;;
     exactprof)  # the fused exact kernel: kernel split + one counter pass
       step exact_stats 300 rocprofv3 --kernel-trace --stats -d "$OUT/exact_stats" -o run \
           --output-format csv -- python3 bench.py --exact --steps 3 --warmup 1 --no-busbw --diag-steps 0
@@ -235,6 +237,20 @@ for task in "$@"; do
         LD_LIBRARY_PATH=$TL step sd70_$R 120 tools/bin/step_driver --steps 300 --warmup 200
       done
       grep -H '"ms_per_step"' "$OUT"/sd7*.log | cut -c1-200 ;;
+    cklog)  # which engine runs each copy WITHOUT a profiler attached: the runtime's own log
+            # (AMD_LOG_LEVEL=4: "HSA Copy ... forceSDMA=" per SDMA copy, a launch per blit kernel),
+            # native probe and Python probe; then the native probe under --kernel-trace alone
+      AMD_LOG_LEVEL=4 step cklog_native 120 tools/bin/copy_kind_probe
+      AMD_LOG_LEVEL=4 step cklog_py 120 python3 tools/copy_kind_py.py 0 hostmalloc
+      step ck_kt 120 rocprofv3 --kernel-trace --stats -d "$OUT/ck_kt" -o run --output-format csv \
+          -- tools/bin/copy_kind_probe
+      for f in cklog_native cklog_py; do
+        echo "$f: HSA Copy $(grep -c 'HSA Copy' "$OUT/$f.log" || true)," \
+             "forceSDMA=1 $(grep -c 'forceSDMA=1' "$OUT/$f.log" || true)," \
+             "copyBuffer $(grep -c 'copyBuffer' "$OUT/$f.log" || true)"
+      done
+      echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
+          "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
     h2dbw)  # H2D bandwidth from page-locked memory over 1 / 2 / 4 concurrent streams
       step h2dbw 120 tools/bin/h2d_bw ;;
     pyck)  # the NoCU copies from a Python process, with / without torch initialised first
@@ -269,7 +285,7 @@ for task in "$@"; do
     dropinp)  # the drop-in at P = 4 / 8 through the node window on the one GPU, each front, with
               # every rank's fetch phases (KNN_METRICS)
       for P in 4 8; do
-        for F in cma fill; do
+        for F in ${FRONTS:-cma fill}; do
           KNN_WINDOW_FRONT=$F KNN_DATA_PLANE=host step dropin${P}_$F 600 python bench.py \
               --harness dropin --gpus $P --q-per-gpu 131072 --steps 2 --warmup 1
         done
