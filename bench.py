@@ -270,6 +270,14 @@ def main(argv=None):
         extra["verify_ok"] = got == ref
         extra["verify_s"] = round(time.perf_counter() - t_v, 1)
 
+    if (world == 1 and comm.on_gpu and not a.exact
+            and os.environ.get("DMLP_BENCH_LARGE_N", "1") != "0"):
+        # the large-N regime beside the headline (after its timed steps; a failure records itself)
+        try:
+            extra["large_n"] = _large_n(a)
+        except Exception as e:  # noqa: BLE001
+            extra["large_n"] = {"error": f"{type(e).__name__}: {e}"[-300:]}
+
     if a.contract_runs > 0 and comm.on_gpu:
         # the same config through the reference's own contract (bench_4's binary is timed this
         # way by run_bench.sh:114-120): fresh processes, median of their Engine::KNN clocks.  One
@@ -325,6 +333,34 @@ def main(argv=None):
         inp.close()
     eng.close()
     return 0
+
+
+def _large_n(a, shapes=((1_000_000, 32), (1_000_000, 128)), q=16384, warmup=2, steps=5):
+    """The native step on larger datasets than the headline's, one GPU: N x A per shape, q
+    queries at the headline's k and labels, synthetic data of the generator's distribution.  The
+    step picks its own render (the cost model: above 2^23 values the device render and the chunked
+    screen pipeline) — per shape the mean ms of `steps` steps after `warmup`, and which render
+    ran."""
+    import torch
+    from distributed_machine_learning_project_amd import _lib
+    from distributed_machine_learning_project_amd.ops import knn as K
+    from distributed_machine_learning_project_amd.utils.io import generate
+    out = {}
+    for N, A in shapes:
+        inp = generate(N, q, A, 0.0, 1000.0, a.k, a.k, a.labels, seed=7)
+        rep = torch.empty(int(_lib.lib().dmlp_format_bound(q)), dtype=torch.uint8).pin_memory().numpy()
+        for _ in range(warmup):
+            K.step(inp.X, inp.labels, (0, a.labels), inp.Qx, inp.k, report=rep)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            K.step(inp.X, inp.labels, (0, a.labels), inp.Qx, inp.k, report=rep)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        out[f"N{N}_A{A}"] = {"ms_per_step": round(ms, 3), "queries": q, "k": a.k, "steps": steps,
+                             "device_render": bool(K.pipeline_stats()["device_render"])}
+        del inp, rep
+    return out
 
 
 def _cgroup_cpu_stat():

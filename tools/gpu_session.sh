@@ -46,7 +46,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 # bench.py's reference-contract runs (fresh drop-in processes after the timed steps) only where a
 # task wants the driver's line: bench, bench3, final
-export DMLP_BENCH_CONTRACT_RUNS=0
+export DMLP_BENCH_CONTRACT_RUNS=0 DMLP_BENCH_LARGE_N=0
 step() {  # name seconds cmd...  (stdout+stderr to $OUT/name.log)
   local name=$1 secs=$2
   shift 2
@@ -65,9 +65,9 @@ for task in "$@"; do
       step ktests 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 \
           --timeout-method thread -k "${KTESTS:?KTESTS}" ;;
     bench)
-      DMLP_BENCH_CONTRACT_RUNS=3 step bench 300 python bench.py ;;
+      DMLP_BENCH_CONTRACT_RUNS=3 DMLP_BENCH_LARGE_N=1 step bench 300 python bench.py ;;
     bench3)  # three headline runs in a row (run-to-run spread: timed_step_ms, cgroup throttling)
-      for r in 1 2 3; do DMLP_BENCH_CONTRACT_RUNS=3 step bench_$r 300 python bench.py; done ;;
+      for r in 1 2 3; do DMLP_BENCH_CONTRACT_RUNS=3 DMLP_BENCH_LARGE_N=1 step bench_$r 300 python bench.py; done ;;
     verify)
       step verify 300 python bench.py --steps 20 --warmup 2 --verify ;;
     exact)
@@ -251,6 +251,13 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    refabl)  # the pair refine's time with its exact-row gathers / member loads ablated
+             # (DMLP_REFINE_ABL 1 / 2 / 3: wrong results, timing only), native step driver
+      for AB in 0 1 2 3; do
+        DMLP_REFINE_ABL=$AB step refabl_$AB 120 rocprofv3 --kernel-trace --stats -d "$OUT/refabl_$AB" \
+            -o run --output-format csv -- tools/bin/step_driver --steps 20 --warmup 5
+        echo "abl=$AB: $(grep -h k_refine_pair "$OUT/refabl_$AB/run_kernel_stats.csv" | cut -d, -f2-4)"
+      done ;;
     h2dbw)  # H2D bandwidth from page-locked memory over 1 / 2 / 4 concurrent streams
       step h2dbw 120 tools/bin/h2d_bw ;;
     pyck)  # the NoCU copies from a Python process, with / without torch initialised first
@@ -295,7 +302,7 @@ for task in "$@"; do
       step tests 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 \
           --timeout-method thread
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-      DMLP_BENCH_CONTRACT_RUNS=3 step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
+      DMLP_BENCH_CONTRACT_RUNS=3 DMLP_BENCH_LARGE_N=1 step bench_driver 300 python bench.py --gpus 1 --steps 20 --warmup 5
       step verify 300 python bench.py --steps 200 --verify
       step exact 300 python bench.py --exact --steps 5 --warmup 1 --min-warmup-s 0 --verify
       DMLP_DATA_PLANE=host step p3 400 python bench.py --gpus 3 --steps 30 --warmup 3 \
