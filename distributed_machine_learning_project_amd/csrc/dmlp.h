@@ -232,7 +232,10 @@ int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* cand_cnt, con
                           int64_t n_points, const int* qidx, const int* qk, int nq, double* out_d,
                           int* out_i, int kstride, const int* labels, int label_lo, int label_hi,
                           int* out_label, uint64_t* out_cs, int* status, int* ovf_count, int kmax,
-                          void* stream);
+                          const int* Xi, const int* Qi, void* stream);
+// 1 when dmlp_refine_groups_rm serves these lists with the pair refine (which also reads lossless
+// int32 rows Xi / Qi instead of X / Qx), 0 when another refine (fp64 rows only)
+int dmlp_refine_pair_path(int S, int hl, int KT, int labels, int cap, int kmax);
 // the host-rendered fp16 tile image (n_tiles x 64 points x 64 KT bytes) copied point-major
 int dmlp_x1_rowmajor(const void* xfrag, int64_t n_tiles, int KT, void* xrow, void* stream);
 

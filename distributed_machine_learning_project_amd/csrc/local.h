@@ -6,6 +6,15 @@
 
 namespace dmlp_pipe {
 
+// (dmlp_step) the rows crossed PCIe as lossless int32 and their fp64 conversion is deferred: the
+// pair refine reads X / Q as int32 (half the gathered bytes); anything else that reads the fp64
+// rows converts them first (to_f64 queues the conversions on the call's stream and clears X / Q)
+struct I32Rows {
+  const int* X = nullptr;
+  const int* Q = nullptr;
+  std::function<void()> to_f64;
+};
+
 // ---------------------------------------------------------------- the dispatcher
 // One local call: launch() queues every pass on `st` without a host sync; the caller reads the
 // overflow counter (*ovf, device) with its own sync and hands it to finish(), which escalates the
@@ -31,6 +40,7 @@ struct Local {
   const HostOps* hx = nullptr;
   hipEvent_t rows = nullptr;
   std::function<void()> issue_rows;
+  I32Rows* i32 = nullptr;  // (dmlp_step) rows still int32 on the device, or none
   // (dmlp_step) k already clamped to N and on the device (kd_pre), every k in [1, 64] and <= N
   // (all_a_pre), the overflow counter zeroed on the device (ovf_pre): no host pass over the
   // queries and no copy or memset on `st` between the operands' event and the screen
@@ -58,12 +68,14 @@ struct Local {
       if (issue_rows) issue_rows();
     }
   }
-  void wait_rows() {
+  // i32_ok: the caller reads the int32 rows (I32Rows) itself; otherwise the fp64 rows are made
+  void wait_rows(bool i32_ok = false) {
     launch_rows();
     if (!rows_waited) {
       if (rows) CK(hipStreamWaitEvent(st, rows, 0));
       rows_waited = true;
     }
+    if (!i32_ok && i32 && (i32->X || i32->Q) && i32->to_f64) i32->to_f64();
   }
   // the device bf16 hi/lo image (prep.hip) and the device query fragments: the 3-term screens'
   // operands, and every screen's when the host did not render any
@@ -143,10 +155,15 @@ struct Local {
         CKL(dmlp_screen_x1(KT, hl, A, xf, xi, nt, N, qh, qnn, qi, kd, nq, kcls, wd, wd + 1, S, ci,
                            cc, ch, st));
       }
-      wait_rows();  // (issues the row copies first) the re-rank reads the fp64 rows
+      // (issues the row copies first) the re-rank reads the rows: the pair refine as int32 when
+      // they crossed that way, the others as fp64
+      const bool pair = dmlp_refine_pair_path(S, hl, KT, fin, cap, kcls) != 0;
+      wait_rows(pair);
       CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
                                 qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
-                                fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls, st));
+                                fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls,
+                                pair && i32 ? i32->X : nullptr, pair && i32 ? i32->Q : nullptr,
+                                st));
       return;
     }
     if (impl == 4) {

@@ -81,6 +81,8 @@ struct Step {
 
   // labels + fp64 rows (X, then Qx) on the side stream: lossless int32 when every value is a
   // 6-decimal number (half the PCIe bytes; the device divides back), else fp64
+  I32Rows i32_;  // the plain path's rows, int32 on the device until something needs them as fp64
+
   void issue_rows_now(double* Xd, double* Qd, int* lab_d) {
     const int64_t N = a->N, Q = a->Q, A = a->A;
     if (a->labels && N) {
@@ -89,8 +91,9 @@ struct Step {
       CK(dmlp::dma_copy(lab_d, lh, N * sizeof(int), w.side));
     }
     const int64_t nx = N * A, nqa = Q * A, at = (nx + 3) & ~int64_t(3);  // (16-B aligned)
+    // defer: keep 6-decimal rows int32 on the device (*defer = them) for the pair refine
     auto rows = [&](const double* src, const double* const* tab, int64_t nr, double* dst,
-                    int64_t off) {
+                    int64_t off, const int** defer = nullptr) {
       const int64_t n = nr * A;
       if (n == 0) return;
       if (rows_i32_on()) {
@@ -99,6 +102,10 @@ struct Step {
             0) {
           int* d32 = w.d_i32.get(at + nqa) + off;
           CK(dmlp::dma_copy(d32, h32, n * 4, w.side));
+          if (defer) {
+            *defer = d32;
+            return;
+          }
           CKL(dmlp_rows_from_i32(d32, n, dst, w.side));
           return;
         }
@@ -136,8 +143,14 @@ struct Step {
         }
       }, [&]() { rows(a->Qx, a->Qr, Q, Qd, at); });
     } else {
-      rows(a->X, a->Xr, N, Xd, 0);
-      rows(a->Qx, a->Qr, Q, Qd, at);
+      rows(a->X, a->Xr, N, Xd, 0, &i32_.X);
+      rows(a->Qx, a->Qr, Q, Qd, at, &i32_.Q);
+      if (i32_.X || i32_.Q)
+        i32_.to_f64 = [this, Xd, Qd, nx, nqa]() {  // (after the rows' event, on the call's stream)
+          if (i32_.X) CKL(dmlp_rows_from_i32(i32_.X, nx, Xd, st));
+          if (i32_.Q) CKL(dmlp_rows_from_i32(i32_.Q, nqa, Qd, st));
+          i32_.X = i32_.Q = nullptr;
+        };
     }
     CK(hipEventRecord(w.ev_rows, w.side));
     CK(mark(M_ROWS, w.side));
@@ -495,6 +508,7 @@ struct Step {
       L.lab = olab; L.cs = ocs; L.exact = a->exact != 0; L.st = st;
       L.hx = with_hx ? &hx : nullptr;
       L.rows = w.ev_rows;
+      L.i32 = &i32_;
       if (with_hx && kd_pre) {
         // (the words' zero copy and k's copy precede the operands' event on the side stream)
         L.kd_pre = kd_pre;

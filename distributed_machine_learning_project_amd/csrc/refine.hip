@@ -1060,6 +1060,13 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
 }
 
 
+// element i of a row table: the fp64 rows, or (Xi non-null) the lossless int32 rows divided back
+// exactly as k_rows_from_i32 does (prep.hip: the host checked x == fl(m / 1e6) for every value)
+__device__ __forceinline__ double row_value(const double* __restrict__ X, const int* __restrict__ Xi,
+                                            int64_t i) {
+  return Xi ? (double)Xi[i] / 1.0e6 : X[i];
+}
+
 // Group refine, TWO queries per wave (32 lanes each): the one-slice single-term screen on the
 // host's fp16 operands (S = 1, hl = 1, KT <= 2), k <= 64, labels given.  k_refine (one query per
 // wave) is bound by its chain of dependent gathers — group entries -> member fragments -> exact
@@ -1085,7 +1092,8 @@ template <int KT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? DMLP_PAIR_WPE : 4))) void k_refine_pair(
     const int* __restrict__ cand_ids, const int* __restrict__ cand_cnt, int cap,
     const float* __restrict__ cand_h, const double* __restrict__ X, int A,
-    const double* __restrict__ Qx, const int* __restrict__ qidx, const int* __restrict__ qk,
+    const double* __restrict__ Qx, const int* __restrict__ Xi, const int* __restrict__ Qi,
+    const int* __restrict__ qidx, const int* __restrict__ qk,
     int nq, const u32x4* __restrict__ xfrag, const u32x4* __restrict__ xrow,
     const float* __restrict__ xinit, const bf16x8* __restrict__ qhi, int n_points,
     double* __restrict__ out_d, int* __restrict__ out_i, int kstride,
@@ -1251,8 +1259,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
 #pragma unroll
     for (int u = 0; u < KT; ++u) {
       const int a0 = 32 * u + 2 * t16;
-      qa[u][0] = a0 < A ? Qx[(int64_t)q * A + a0] : 0.0;
-      qa[u][1] = a0 + 1 < A ? Qx[(int64_t)q * A + a0 + 1] : 0.0;
+      qa[u][0] = a0 < A ? row_value(Qx, Qi, (int64_t)q * A + a0) : 0.0;
+      qa[u][1] = a0 + 1 < A ? row_value(Qx, Qi, (int64_t)q * A + a0 + 1) : 0.0;
     }
     int Msw = Ms;
     Msw = max(Msw, __shfl_xor(Msw, 32));
@@ -1260,13 +1268,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       const int j = r0 + rsel;
       const bool rv = j < Ms;
       const int id = rv ? s_i[slot][j] : 0;
-      const double* xr = X + (int64_t)id * A;
+      const int64_t xb = (int64_t)id * A;
       double pr[KT][2];
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
         const int a0 = 32 * u + 2 * t16;
-        const double x0 = rv && a0 < A && !(abl & 1) ? xr[a0] : 0.0;
-        const double x1 = rv && a0 + 1 < A && !(abl & 1) ? xr[a0 + 1] : 0.0;
+        const double x0 = rv && a0 < A && !(abl & 1) ? row_value(X, Xi, xb + a0) : 0.0;
+        const double x1 = rv && a0 + 1 < A && !(abl & 1) ? row_value(X, Xi, xb + a0 + 1) : 0.0;
         const double d0 = a0 < A ? __dsub_rn(qa[u][0], x0) : 0.0;
         const double d1 = a0 + 1 < A ? __dsub_rn(qa[u][1], x1) : 0.0;
         pr[u][0] = __dmul_rn(d0, d0);
@@ -1304,7 +1312,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int a = 32 * u + E * t8 + e;
-        qa[u][e] = a < A ? Qx[(int64_t)q * A + a] : 0.0;
+        qa[u][e] = a < A ? row_value(Qx, Qi, (int64_t)q * A + a) : 0.0;
       }
     int Msw = Ms;
     Msw = max(Msw, __shfl_xor(Msw, 32));
@@ -1312,22 +1320,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KT == 1 ? D
       const int j = r0 + rsel;
       const bool rv = j < Ms;
       const int id = rv ? s_i[slot][j] : 0;
-      const double* xr = X + (int64_t)id * A;
+      const int64_t xb = (int64_t)id * A;
       double pr[KT][E];
 #pragma unroll
       for (int u = 0; u < KT; ++u) {
         const int a0 = 32 * u + E * t8;
         double x[E];
-        if (rv && !(abl & 1) && a0 + E - 1 < A && (A & 1) == 0) {  // 16-byte aligned pairs
+        if (Xi && rv && !(abl & 1) && a0 + E - 1 < A && (A & 3) == 0 && E % 4 == 0) {
+          // lossless int32 rows: half the bytes of the gather (one 16-byte load per 4 values),
+          // each value divided back exactly as k_rows_from_i32 does
+#pragma unroll
+          for (int e = 0; e < E; e += 4) {
+            const int4 v = *(const int4*)(Xi + xb + a0 + e);
+            x[e] = (double)v.x / 1.0e6;
+            x[e + 1] = (double)v.y / 1.0e6;
+            x[e + 2] = (double)v.z / 1.0e6;
+            x[e + 3] = (double)v.w / 1.0e6;
+          }
+        } else if (!Xi && rv && !(abl & 1) && a0 + E - 1 < A && (A & 1) == 0) {  // 16-byte pairs
 #pragma unroll
           for (int e = 0; e < E; e += 2) {
-            const double2 v = *(const double2*)(xr + a0 + e);
+            const double2 v = *(const double2*)(X + xb + a0 + e);
             x[e] = v.x;
             x[e + 1] = v.y;
           }
         } else {
 #pragma unroll
-          for (int e = 0; e < E; ++e) x[e] = rv && !(abl & 1) && a0 + e < A ? xr[a0 + e] : 0.0;
+          for (int e = 0; e < E; ++e)
+            x[e] = rv && !(abl & 1) && a0 + e < A ? row_value(X, Xi, xb + a0 + e) : 0.0;
         }
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -1442,7 +1462,8 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
                               const int* qk, int nq, double* out_d, int* out_i, int kstride,
                               const int* labels, int label_lo, int label_hi, int* out_label,
                               uint64_t* out_cs, int* status, int* ovf_count, int collect,
-                              void* stream, int kmax = 64, int grows = 4) {
+                              void* stream, int kmax = 64, int grows = 4,
+                              const int* Xi = nullptr, const int* Qi = nullptr) {
   if (nq <= 0) return 0;
   if (grows != 4 && grows != 8) return -1;
   if (S < 1 || S > 256 || cap < 1 || n_points > 0x7fffffff) return -1;
@@ -1471,26 +1492,26 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
   // (k_refine_pair; DMLP_REFINE_PAIR=0: the one-query-per-wave kernel).  Its PM = 64 member slots
   // leave >= 32 of slack above k only for k <= 32: at k near 64 any member inside the 2-eps band
   // would hand the query back, so the class k in (32, 64] takes k_refine (P = 128 slots)
-  static const bool pair_on = !(getenv("DMLP_REFINE_PAIR") && getenv("DMLP_REFINE_PAIR")[0] == '0');
   // DMLP_REFINE_ABL (timing ablations, wrong results): 1 no exact-row gathers, 2 no member loads
   static const int pair_abl = getenv("DMLP_REFINE_ABL") ? atoi(getenv("DMLP_REFINE_ABL")) : 0;
-  if (pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128 && kmax <= 32) {
+  if (dmlp_refine_pair_path(S, hl, KT, labels != nullptr, cap, kmax)) {
     const dim3 grid((unsigned)((nq + 7) / 8));
     if (KT == 1)
       hipLaunchKernelGGL((k_refine_pair<1>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
-                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
+                         cand_cnt, cap, cand_h, X, A, Qx, Xi, Qi, qidx, qk, nq, (const u32x4*)xfrag,
                          (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
                          kstride, labels, out_label,
                          out_cs, status, ovf_count, pair_abl, gin.grows);
     else
       hipLaunchKernelGGL((k_refine_pair<2>), grid, dim3(256), 0, (hipStream_t)stream, cand_ids,
-                         cand_cnt, cap, cand_h, X, A, Qx, qidx, qk, nq, (const u32x4*)xfrag,
+                         cand_cnt, cap, cand_h, X, A, Qx, Xi, Qi, qidx, qk, nq, (const u32x4*)xfrag,
                          (const u32x4*)xrow, xinit, (const bf16x8*)qhi, (int)n_points, out_d, out_i,
                          kstride, labels, out_label,
                          out_cs, status, ovf_count, pair_abl, gin.grows);
     DMLP_LAUNCH_CHECK();
     return 0;
   }
+  if (!X || !Qx) return -3;  // (the other refines read the fp64 rows only)
 #define DMLP_REFINE_G(KTV, F16)                                                                \
   hipLaunchKernelGGL((k_refine<2, KTV, F16>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
@@ -1557,11 +1578,22 @@ extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* ca
                                      int64_t n_points, const int* qidx, const int* qk, int nq,
                                      double* out_d, int* out_i, int kstride, const int* labels,
                                      int label_lo, int label_hi, int* out_label, uint64_t* out_cs,
-                                     int* status, int* ovf_count, int kmax, void* stream) {
+                                     int* status, int* ovf_count, int kmax, const int* Xi,
+                                     const int* Qi, void* stream) {
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xrow, xinit, qhi,
                             KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
                             label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream,
-                            kmax, dmlp_screen_x1_group_rows(kmax));
+                            kmax, dmlp_screen_x1_group_rows(kmax), Xi, Qi);
+}
+
+// Whether refine_groups_impl serves these lists with k_refine_pair: one slice of the host's fp16
+// operands (S = 1, hl = 1, KT <= 2), labels, k <= 32 (PM = 64 member slots leave >= 32 of slack
+// above k only there: at k near 64 any member inside the 2-eps band would hand the query back,
+// so the class k in (32, 64] takes k_refine, P = 128 slots).  DMLP_REFINE_PAIR=0: never.  The
+// pair refine also reads lossless int32 rows (dmlp_refine_groups_rm Xi / Qi), the others fp64.
+extern "C" int dmlp_refine_pair_path(int S, int hl, int KT, int labels, int cap, int kmax) {
+  static const bool pair_on = !(getenv("DMLP_REFINE_PAIR") && getenv("DMLP_REFINE_PAIR")[0] == '0');
+  return pair_on && S == 1 && hl == 1 && KT <= 2 && labels && cap <= 128 && kmax <= 32 ? 1 : 0;
 }
 
 // The host-rendered fp16 image (tile layout of the screen's MFMA A operand: point p's 8-element
