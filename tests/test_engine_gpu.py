@@ -84,6 +84,49 @@ def test_native_step(gpu, kmax, A):
     eng.close()
 
 
+@pytest.mark.parametrize("decimals", [6, None])
+def test_native_step_pair_refine_row_forms(gpu, decimals):
+    """The pair refine (k <= 32, one slice of host operands) reads the dataset rows as they crossed
+    PCIe: lossless int32 for 6-decimal data (each value divided back on the device, no fp64 copy
+    made unless another pass needs it) or fp64 for full-precision data.  Both == the oracle's
+    report, labels and checksums, with an escalated query in the same call (a duplicated point
+    cluster) forcing the deferred fp64 conversion after the refine."""
+    from distributed_machine_learning_project_amd.utils.shm import share_input
+    rng = np.random.default_rng(11)
+    N, Q, A = 9000, 6000, 32
+    X = rng.uniform(0.0, 1000.0, (N, A))
+    Qx = rng.uniform(0.0, 1000.0, (Q, A))
+    if decimals is not None:
+        X, Qx = np.round(X, decimals), np.round(Qx, decimals)
+    X[:80] = X[0]  # 80 identical points: a query on them ties past the 64 member slots
+    Qx[0] = X[0]
+    k = rng.integers(1, 33, Q).astype(np.int32)
+    k[0] = 32
+    labels = rng.integers(0, 6, N).astype(np.int32)
+    inp = dmlp.KNNInput(labels, X, k, Qx)
+    d, i = K.knn_cpu(inp.X, inp.Qx, inp.k)
+    lab_ref, cs = K.finalize_cpu(i, inp.k, inp.labels)
+    from distributed_machine_learning_project_amd import _lib
+    L = _lib.lib()
+    # (one screen slice, the pair refine's case, needs a full round of waves: shrink the CUs the
+    # slice choice fills so 6000 queries make one)
+    old_cus = L.dmlp_pipeline_set(b"num_cus", 4)
+    eng = _engine("farm")
+    sh = share_input(eng.comm, inp)
+    try:
+        for _ in range(2):
+            out = eng.KNN(sh.params, sh, None)
+            assert bytes(eng.report(out)) == dmlp.format_report(cs)
+            np.testing.assert_array_equal(out.labels_np(), lab_ref)
+            np.testing.assert_array_equal(out.checksums_np(), cs)
+            st = K.pipeline_stats()
+            assert st["path"] == 0 and st["n_escalated"] + st["n_exact"] >= 1, st
+    finally:
+        L.dmlp_pipeline_set(b"num_cus", old_cus)
+        sh.close()
+        eng.close()
+
+
 def _early_inputs(n, A, kmax, Q, seed):
     """Two different inputs of one shape (alternated through one engine, so a screen that read a
     slice before its ready word, or a stale line, would read the OTHER input's bytes), each with

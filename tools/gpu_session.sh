@@ -251,6 +251,14 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    drab)  # the render choice per k class at N 1e5 / 1e6 x A 32 / 128: the host render forced
+           # (DMLP_DEVICE_RENDER=0) against the cost model's choice, alternating on one box
+      for R in 1 2; do
+        DMLP_DEVICE_RENDER=0 step drab_host_$R 500 python3 -u tools/bench_sweep.py \
+            --out "$OUT/drab_host_$R.jsonl" --timeout 120 --ns 100000,1000000 --attrs 32,128
+        step drab_auto_$R 500 python3 -u tools/bench_sweep.py --out "$OUT/drab_auto_$R.jsonl" \
+            --timeout 120 --ns 100000,1000000 --attrs 32,128
+      done ;;
     refabl)  # the pair refine's time with its exact-row gathers / member loads ablated
              # (DMLP_REFINE_ABL 1 / 2 / 3: wrong results, timing only), native step driver
       for AB in 0 1 2 3; do
