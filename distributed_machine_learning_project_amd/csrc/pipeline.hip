@@ -251,11 +251,11 @@ struct Step {
                           g_tune.screen == 0 &&
                           (g_tune.host_ops >= 2 ||
                            (g_tune.host_ops == 1 &&
-                            (pl || dr_on() || dr_auto(N, A) || dmlp_host_threads() >= 2)));
+                            (pl || dr_on() || dr_auto(N, A, kmin, kmax) || dmlp_host_threads() >= 2)));
     // device render (opt-in, DMLP_DEVICE_RENDER=1): the GPU renders the screen operands from the
     // landed rows.  With a plane every rank must render the same slice kinds, so a plane step
     // always renders on the host (a device-render rank never renders its image slices)
-    bool dr = x1_front && !pl && (dr_on() || dr_auto(N, A));
+    bool dr = x1_front && !pl && (dr_on() || dr_auto(N, A, kmin, kmax));
     if (Q == 0) {
       a->report_len = 0;
       w.text_len = 0;

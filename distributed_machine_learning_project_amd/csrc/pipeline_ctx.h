@@ -229,8 +229,17 @@ inline bool dr_on() { return g_tune.device_render > 0; }
 // host pass and PCIe (profiles/r10a_large_n_render_ab.jsonl: N = 1e6, A = 128: 21.1 / 22.4 vs
 // 28.8 / 38.2 ms).  Below the early start's reach (one screen slice, nt <= 4096) the host render
 // keeps the early start (the render kernels get no wave slots beside its spinning screen).
-constexpr int64_t kDrMinValues = int64_t(1) << 23;
-inline bool dr_auto(int64_t N, int A) { return g_tune.device_render < 0 && N * A >= kDrMinValues; }
+// It pays where the chunked large-N pipeline runs (every k in the one-pass class) and its extra
+// slices cost the refine little: k <= 32 (the pair groups), or k <= 64 once the host pass is
+// large (N A >= 2^26).  The two-pass class (k > 64) screens after all the rows landed, and the
+// host render's overlap wins there (profiles/r11j_render_ab.txt: N = 1e6, A = 32, k = 200:
+// 6.8-7.1 host vs 11.1-11.4 device; k 1-64: 5.7-6.3 vs 6.4-6.5; A = 128, k 1-64: 21-31 vs 16).
+constexpr int64_t kDrMinValues = int64_t(1) << 23, kDrMinValuesK64 = int64_t(1) << 26;
+inline bool dr_auto(int64_t N, int A, int kmin, int kmax) {
+  if (g_tune.device_render >= 0 || kmin < 1) return false;
+  const int64_t v = N * A;
+  return (kmax <= 32 && v >= kDrMinValues) || (kmax <= 64 && v >= kDrMinValuesK64);
+}
 // Every small host <-> device copy of the step goes through the SDMA engines (dmlp::dma_copy: a
 // copy below ~32 KiB would otherwise be a blit kernel, a memset a fill kernel) — its words are
 // cleared by a DMA copy from this page-locked block of zeros.

@@ -201,16 +201,20 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
         L.dmlp_pipeline_set(b"device_render", old_dr)
 
 
-@pytest.mark.parametrize("n,A,Q,kmin,kmax", [(300_000, 32, 4096, 1, 32), (110_000, 100, 2048, 16, 16),
-                                              (270_000, 48, 3000, 40, 64)])
-def test_native_step_large_n_pipeline(gpu, n, A, Q, kmin, kmax):
+@pytest.mark.parametrize("n,A,Q,kmin,kmax,auto", [(300_000, 32, 4096, 1, 32, 1),
+                                                   (110_000, 100, 2048, 16, 16, 1),
+                                                   (270_000, 48, 3000, 40, 64, 0)])
+def test_native_step_large_n_pipeline(gpu, n, A, Q, kmin, kmax, auto):
     """at large N the step picks the device render by its cost model (the host
     render's fp16 image + int32 rows vs the int32 rows alone) and runs the screen as a pipeline
     over up to 8 dataset chunks of its slices — chunk c's screen while chunk c + 1 crosses PCIe,
     each chunk's eps from the image's max norm seen so far (the refine takes the largest over the
     slices).  Two alternated inputs, then the host render forced (DMLP_DEVICE_RENDER=0 by the
     switch) and an input whose last row lies outside the fp16 range (the whole call redone on the
-    device image): every report, label and checksum == the oracle's."""
+    device image): every report, label and checksum == the oracle's.  The device render is forced
+    (DMLP_DEVICE_RENDER=1 by the switch) so every shape runs the pipeline; a last call checks the
+    cost model's own choice (auto: 1 device, 0 host — k in (32, 64] below 2^26 values renders on
+    the host)."""
     from distributed_machine_learning_project_amd import _lib
     import torch
     L = _lib.lib()
@@ -227,7 +231,7 @@ def test_native_step_large_n_pipeline(gpu, n, A, Q, kmin, kmax):
     dst = torch.empty(48 * Q + 64, dtype=torch.uint8).pin_memory().numpy()
     old = L.dmlp_pipeline_set(b"device_render", -1)
     try:
-        for rnd, (ci, dr) in enumerate(((0, -1), (1, -1), (0, -1), (1, 0), (2, -1))):
+        for rnd, (ci, dr) in enumerate(((0, 1), (1, 1), (0, 1), (1, 0), (2, 1), (0, -1))):
             L.dmlp_pipeline_set(b"device_render", dr)
             inp, lab_ref, cs, expect = cases[ci]
             r = K.step(inp.X, inp.labels, (0, 8), inp.Qx, inp.k, report=dst)
@@ -239,7 +243,8 @@ def test_native_step_large_n_pipeline(gpu, n, A, Q, kmin, kmax):
                 assert r.path == 2  # (the device image path after the out-of-range render)
             else:
                 assert r.path == 0
-                assert K.pipeline_stats()["device_render"] == (1 if dr < 0 else 0), f"round {rnd}"
+                want = auto if dr < 0 else dr
+                assert K.pipeline_stats()["device_render"] == want, f"round {rnd}"
     finally:
         L.dmlp_pipeline_set(b"device_render", old)
 
