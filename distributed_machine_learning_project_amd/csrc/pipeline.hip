@@ -354,6 +354,7 @@ struct Step {
         *s64 = dst64;
     };
     // what: 0 the queries, 1 + c dataset chunk c, -1 the labels and the rows' event (the tail)
+    int rendered = -1;  // the last chunk issued
     std::function<void(int)> dr_part = [&](int what) {
         const int64_t nqa = Q * A, at = dr_at;
         unsigned* drw = w.dr_words.p;
@@ -378,18 +379,28 @@ struct Step {
           const int64_t tps = S_all > 0 ? (nt + S_all - 1) / S_all : nt;
           const int64_t t0 = std::min<int64_t>(nt, chunk_s[c] * tps);
           const int64_t t1 = std::min<int64_t>(nt, chunk_s[c + 1] * tps);
+          // the chunk's rows on the side stream, its render on the render stream behind them:
+          // the copies run back to back on the SDMA engine while the renders overlap them (in
+          // one stream each copy waited for the previous chunk's render)
           if (t1 > t0) {
             const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
             const double* s64 = nullptr;
             if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+            CK(hipEventRecord(w.ev_copy[c], w.side));
+            CK(hipStreamWaitEvent(w.rnd, w.ev_copy[c], 0));
             CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64,
                                  (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
                                  const_cast<void*>(hx.xrow), words + kW_XNMAX, rbad, drw + c,
-                                 nullptr, w.side));
+                                 nullptr, w.rnd));
+            CK(hipEventRecord(w.ev_chunk[c], w.rnd));
+          } else {
+            CK(hipEventRecord(w.ev_chunk[c], w.side));
           }
-          CK(hipEventRecord(w.ev_chunk[c], w.side));
+          rendered = c;
           return;
         }
+        // (the renders are in order on their stream: the last chunk's event covers them all)
+        if (rendered >= 0) CK(hipStreamWaitEvent(w.side, w.ev_chunk[rendered], 0));
         CK(mark(M_DATA, w.side));
         if (a->labels && N) {
           int* lh = w.s_lab.get(N);

@@ -343,6 +343,7 @@ inline constexpr const char* kMarkNames[M_N] = {"enter", "operands_landed", "dat
 struct Ctx {
   int dev = -1;
   hipStream_t side = nullptr;  // host->device copies of dmlp_step
+  hipStream_t rnd = nullptr;   // the large-N device render's kernels (off the copies' stream)
   hipEvent_t ev_ops = nullptr, ev_rows = nullptr;
   bool marks_on = false, marks_valid = false;
   hipEvent_t marks[M_N] = {};
@@ -370,7 +371,8 @@ struct Ctx {
   HBuf<int64_t> s_len, small64_h;
   DBuf<int64_t> small64_d;
   hipEvent_t ev_done = nullptr;
-  hipEvent_t ev_chunk[kEarlySlices] = {};  // the large-N pipeline's chunk events
+  hipEvent_t ev_chunk[kEarlySlices] = {};  // the large-N pipeline's chunk events (rendered)
+  hipEvent_t ev_copy[kEarlySlices] = {};   // ... and its chunks' rows landed
   DBuf<short> dx_hi, dq_hi;
   DBuf<short> dx_row;  // the fp16 image point-major (dmlp_x1_rowmajor) for the pair refine
   DBuf<double> d_mu;   // device render: the centre
@@ -405,6 +407,8 @@ inline Ctx& ctx() {
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
     for (hipEvent_t& e : w.ev_chunk) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : w.ev_copy) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CK(hipStreamCreateWithFlags(&w.rnd, hipStreamNonBlocking));
   }
   return w;
 }
@@ -462,6 +466,7 @@ inline int drain_and_fail(Ctx* w, hipStream_t st, int code) {
   // every error path drains the streams before returning: nothing may still be writing the
   // caller's tensors or reading the page-locked staging when it frees or reuses them
   if (w && w->side) (void)hipStreamSynchronize(w->side);
+  if (w && w->rnd) (void)hipStreamSynchronize(w->rnd);
   if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
