@@ -386,13 +386,14 @@ struct Step {
             const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
             const double* s64 = nullptr;
             if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+            hipStream_t rs = w.render_stream();
             CK(hipEventRecord(w.ev_copy[c], w.side));
-            CK(hipStreamWaitEvent(w.rnd, w.ev_copy[c], 0));
+            CK(hipStreamWaitEvent(rs, w.ev_copy[c], 0));
             CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64,
                                  (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
                                  const_cast<void*>(hx.xrow), words + kW_XNMAX, rbad, drw + c,
-                                 nullptr, w.rnd));
-            CK(hipEventRecord(w.ev_chunk[c], w.rnd));
+                                 nullptr, rs));
+            CK(hipEventRecord(w.ev_chunk[c], rs));
           } else {
             CK(hipEventRecord(w.ev_chunk[c], w.side));
           }

@@ -343,7 +343,23 @@ inline constexpr const char* kMarkNames[M_N] = {"enter", "operands_landed", "dat
 struct Ctx {
   int dev = -1;
   hipStream_t side = nullptr;  // host->device copies of dmlp_step
-  hipStream_t rnd = nullptr;   // the large-N device render's kernels (off the copies' stream)
+  // the large-N device render's kernels (off the copies' stream), created on first use: another
+  // stream changes how the process's streams share the runtime's hardware queues, and an
+  // early-start step needs its copies' queue apart from its screen's (one on the same queue as
+  // the spinning screen waits behind it: every wave timed out in a GPU test, r11m)
+  hipStream_t rnd = nullptr;
+  hipStream_t render_stream() {
+    if (!rnd && hipStreamCreateWithPriority(&rnd, hipStreamNonBlocking, high_priority()) !=
+                    hipSuccess)
+      rnd = nullptr;
+    return rnd ? rnd : side;
+  }
+  static int high_priority() {  // (DMLP_SIDE_PRIORITY=0: the default priority, A/B)
+    if (env_off("DMLP_SIDE_PRIORITY")) return 0;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    return greatest;
+  }
   hipEvent_t ev_ops = nullptr, ev_rows = nullptr;
   bool marks_on = false, marks_valid = false;
   hipEvent_t marks[M_N] = {};
@@ -402,13 +418,15 @@ inline Ctx& ctx() {
   Ctx& w = c[d];
   if (!w.side) {
     w.dev = d;
-    CK(hipStreamCreateWithFlags(&w.side, hipStreamNonBlocking));
+    // the copies' stream at the high priority: the runtime keeps a separate pool of hardware
+    // queues per priority, so it never shares one with a (normal-priority) stream whose screen
+    // spins on the words these copies write (the early start)
+    CK(hipStreamCreateWithPriority(&w.side, hipStreamNonBlocking, Ctx::high_priority()));
     CK(hipEventCreateWithFlags(&w.ev_ops, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_rows, hipEventDisableTiming));
     CK(hipEventCreateWithFlags(&w.ev_done, hipEventDisableTiming));
     for (hipEvent_t& e : w.ev_chunk) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : w.ev_copy) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    CK(hipStreamCreateWithFlags(&w.rnd, hipStreamNonBlocking));
   }
   return w;
 }

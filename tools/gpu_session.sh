@@ -259,6 +259,10 @@ for task in "$@"; do
         step drab_auto_$R 500 python3 -u tools/bench_sweep.py --out "$OUT/drab_auto_$R.jsonl" \
             --timeout 120 --ns 100000,1000000 --attrs 32,128
       done ;;
+    prio)  # the copies' stream at the high priority vs the default, interleaved (bench shape)
+      AB_PROF=0 AB_ROUNDS=4 AB_STEPS=200 step prio_ab 900 bash tools/kernel_ab.sh \
+          p0:DMLP_SIDE_PRIORITY=0 p1:DMLP_SIDE_PRIORITY=1
+      grep -Ho '"ms_per_step": [0-9.]*' gpurun_out/ab/p*.log | tee "$OUT/prio_ab.txt" ;;
     refabl)  # the pair refine's time with its exact-row gathers / member loads ablated
              # (DMLP_REFINE_ABL 1 / 2 / 3: wrong results, timing only), native step driver
       for AB in 0 1 2 3; do
