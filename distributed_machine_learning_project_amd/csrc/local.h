@@ -7,12 +7,13 @@
 namespace dmlp_pipe {
 
 // (dmlp_step) the rows crossed PCIe as lossless int32 and their fp64 conversion is deferred: the
-// pair refine reads X / Q as int32 (half the gathered bytes); anything else that reads the fp64
-// rows converts them first (to_f64 queues the conversions on the call's stream and clears X / Q)
+// refines read X as int32 (the pair refine Q too: half the gathered bytes); anything else that
+// reads the fp64 rows converts them first — to_f64(need): bit 0 X, bit 1 Q, each queued on the
+// call's stream once and cleared
 struct I32Rows {
   const int* X = nullptr;
   const int* Q = nullptr;
-  std::function<void()> to_f64;
+  std::function<void(int)> to_f64;
 };
 
 // ---------------------------------------------------------------- the dispatcher
@@ -68,14 +69,16 @@ struct Local {
       if (issue_rows) issue_rows();
     }
   }
-  // i32_ok: the caller reads the int32 rows (I32Rows) itself; otherwise the fp64 rows are made
-  void wait_rows(bool i32_ok = false) {
+  // need: the rows the caller reads as fp64 (bit 0 X, bit 1 Q); the others it reads as int32
+  // (I32Rows) when they are
+  void wait_rows(int need = 3) {
     launch_rows();
     if (!rows_waited) {
       if (rows) CK(hipStreamWaitEvent(st, rows, 0));
       rows_waited = true;
     }
-    if (!i32_ok && i32 && (i32->X || i32->Q) && i32->to_f64) i32->to_f64();
+    if (i32 && i32->to_f64 && (((need & 1) && i32->X) || ((need & 2) && i32->Q)))
+      i32->to_f64(need);
   }
   // the device bf16 hi/lo image (prep.hip) and the device query fragments: the 3-term screens'
   // operands, and every screen's when the host did not render any
@@ -157,13 +160,13 @@ struct Local {
       }
       // (issues the row copies first) the re-rank reads the rows: the pair refine as int32 when
       // they crossed that way, the others as fp64
+      // (the pair refine reads both as int32, the group refine the dataset's rows only)
       const bool pair = dmlp_refine_pair_path(S, hl, KT, fin, cap, kcls) != 0;
-      wait_rows(pair);
+      wait_rows(pair ? 0 : 2);
       CKL(dmlp_refine_groups_rm(cap, ci, cc, ch, S, X, A, Qx, xf, hx ? hx->xrow : nullptr, xi,
                                 qh, KT, hl, N, idx ? qi : nullptr, kd, nq, out_d, out_i, kstride,
                                 fin ? labels : nullptr, lo, hi, lab, cs, stat, ovf, kcls,
-                                pair && i32 ? i32->X : nullptr, pair && i32 ? i32->Q : nullptr,
-                                st));
+                                i32 ? i32->X : nullptr, pair && i32 ? i32->Q : nullptr, st));
       return;
     }
     if (impl == 4) {

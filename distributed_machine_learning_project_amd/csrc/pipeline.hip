@@ -81,7 +81,22 @@ struct Step {
 
   // labels + fp64 rows (X, then Qx) on the side stream: lossless int32 when every value is a
   // 6-decimal number (half the PCIe bytes; the device divides back), else fp64
-  I32Rows i32_;  // the plain path's rows, int32 on the device until something needs them as fp64
+  I32Rows i32_;  // rows int32 on the device until something needs them as fp64 (I32Rows)
+  // the conversions i32_ defers, queued when a reader needs them (after the rows' event, on the
+  // call's stream)
+  void defer_f64(double* Xd, double* Qd, int64_t nx, int64_t nqa) {
+    if (!i32_.X && !i32_.Q) return;
+    i32_.to_f64 = [this, Xd, Qd, nx, nqa](int need) {
+      if ((need & 1) && i32_.X) {
+        CKL(dmlp_rows_from_i32(i32_.X, nx, Xd, st));
+        i32_.X = nullptr;
+      }
+      if ((need & 2) && i32_.Q) {
+        CKL(dmlp_rows_from_i32(i32_.Q, nqa, Qd, st));
+        i32_.Q = nullptr;
+      }
+    };
+  }
 
   void issue_rows_now(double* Xd, double* Qd, int* lab_d) {
     const int64_t N = a->N, Q = a->Q, A = a->A;
@@ -145,12 +160,7 @@ struct Step {
     } else {
       rows(a->X, a->Xr, N, Xd, 0, &i32_.X);
       rows(a->Qx, a->Qr, Q, Qd, at, &i32_.Q);
-      if (i32_.X || i32_.Q)
-        i32_.to_f64 = [this, Xd, Qd, nx, nqa]() {  // (after the rows' event, on the call's stream)
-          if (i32_.X) CKL(dmlp_rows_from_i32(i32_.X, nx, Xd, st));
-          if (i32_.Q) CKL(dmlp_rows_from_i32(i32_.Q, nqa, Qd, st));
-          i32_.X = i32_.Q = nullptr;
-        };
+      defer_f64(Xd, Qd, nx, nqa);
     }
     CK(hipEventRecord(w.ev_rows, w.side));
     CK(mark(M_ROWS, w.side));
@@ -355,6 +365,9 @@ struct Step {
     };
     // what: 0 the queries, 1 + c dataset chunk c, -1 the labels and the rows' event (the tail)
     int rendered = -1;  // the last chunk issued
+    std::vector<std::pair<int64_t, int64_t>> x_i32_rows;  // dataset rows rendered from int32
+    bool x_f64_rows = false;                               // ... and some from fp64
+    const int* x_i32_base = nullptr;                       // (the int32 rows' base: row 0)
     std::function<void(int)> dr_part = [&](int what) {
         const int64_t nqa = Q * A, at = dr_at;
         unsigned* drw = w.dr_words.p;
@@ -386,11 +399,15 @@ struct Step {
             const int* s32 = a->X32d;  // (the xGMI replica: rendered straight from the device)
             const double* s64 = nullptr;
             if (!s32) ship(a->X, a->Xr, std::min(N, t0 * 64), std::min(N, t1 * 64), 0, Xd, &s32, &s64);
+            // int32 rows stay int32 (the refines read them; fp64 only on demand, defer_f64)
+            if (s32) x_i32_rows.emplace_back(std::min(N, t0 * 64), std::min(N, t1 * 64));
+            else x_f64_rows = true;
+            x_i32_base = s32 ? s32 : x_i32_base;
             hipStream_t rs = w.render_stream();
             CK(hipEventRecord(w.ev_copy[c], w.side));
             CK(hipStreamWaitEvent(rs, w.ev_copy[c], 0));
             CKL(dmlp_render_rows(KT, A, s32, s64 ? s64 : s32 ? nullptr : Xd, t0 * 64,
-                                 (t1 - t0) * 64, N, mud, Xd, 0, xhi_d, xin_d,
+                                 (t1 - t0) * 64, N, mud, nullptr, 0, xhi_d, xin_d,
                                  const_cast<void*>(hx.xrow), words + kW_XNMAX, rbad, drw + c,
                                  nullptr, rs));
             CK(hipEventRecord(w.ev_chunk[c], rs));
@@ -399,6 +416,18 @@ struct Step {
           }
           rendered = c;
           return;
+        }
+        if (!x_i32_rows.empty()) {
+          if (!x_f64_rows) {  // every chunk int32: the refines read them, fp64 on demand
+            i32_.X = x_i32_base;
+            defer_f64(Xd, Qd, N * A, Q * A);
+          } else {  // a chunk crossed as fp64: the int32 chunks' fp64 rows now, behind the renders
+            hipStream_t rs = w.render_stream();
+            for (auto& rg : x_i32_rows)
+              CKL(dmlp_rows_from_i32(x_i32_base + rg.first * A, (rg.second - rg.first) * A,
+                                     Xd + rg.first * A, rs));
+            CK(hipEventRecord(w.ev_chunk[std::max(0, rendered)], rs));
+          }
         }
         // (the renders are in order on their stream: the last chunk's event covers them all)
         if (rendered >= 0) CK(hipStreamWaitEvent(w.side, w.ev_chunk[rendered], 0));

@@ -517,7 +517,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) void k_
           double x;
           if (I32) {
             x = (double)src32[p * A + a] / 1.0e6;  // IEEE division: the exact input double
-            dst64[p * A + a] = x;
+            if (dst64) dst64[p * A + a] = x;  // (null: the refine reads the int32 rows)
           } else {
             x = src64[p * A + a];
           }
@@ -575,7 +575,7 @@ extern "C" int dmlp_render_rows(int KT, int A, const int* src32, const double* s
   if (n <= 0) {
     return 0;
   }
-  if ((!src32 && !src64) || (src32 && !dst64) || A < 1 || A > KT * 32 || !img || !xq ||
+  if ((!src32 && !src64) || A < 1 || A > KT * 32 || !img || !xq ||
       (mode != 0 && mode != 1) || (mode == 0 && ((r0 & 63) || (n & 63))))
     return -1;
   const dim3 grid((unsigned)((n + 63) / 64)), block(64);

@@ -25,6 +25,17 @@ namespace {
 
 constexpr int kHistCap = 512;  // per-wave label histogram (labels in [lo, lo+512))
 
+// the same over a lossless int32 row, each value divided back exactly as k_rows_from_i32 does
+__device__ __forceinline__ double exact_dist_row_i32(const double* __restrict__ q,
+                                                     const int* __restrict__ x, int A) {
+  double s = 0.0;
+  for (int a = 0; a < A; ++a) {
+    const double d = __dsub_rn(q[a], (double)x[a] / 1.0e6);
+    s = __dadd_rn(s, __dmul_rn(d, d));
+  }
+  return s;
+}
+
 __device__ __forceinline__ double exact_dist_row(const double* __restrict__ q,
                                                  const double* __restrict__ x, int A) {
   double s = 0.0;
@@ -125,6 +136,7 @@ struct GroupIn {
                           // the threshold goes to the exact re-rank (no image to rescore from)
   int grows = 4;          // rows per group entry: 4 (consecutive) or 8 (the k <= 16 screen's pair
                           // epilogue: rows 4 kg + i of steps 2p and 2p + 1, entry = 4 p + kg)
+  const int* xi32 = nullptr;  // the dataset's lossless int32 rows (X unused), or null
 };
 
 // row of member i (< grows) of the group with slice-relative entry index gi
@@ -237,7 +249,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((GROUPS && 
       const int lo = slice_of(j);
       id = cand_ids[((int64_t)p * S + lo) * cap + (j - pre[lo])];
     }
-    dv = exact_dist_row(qv, X + (int64_t)id * A, A);
+    dv = gin.xi32 ? exact_dist_row_i32(qv, gin.xi32 + (int64_t)id * A, A)
+                  : exact_dist_row(qv, X + (int64_t)id * A, A);
   };
   if (GROUPS) {
     // ---- global threshold: k-th largest group key over all slices (two 8-bit histogram passes)
@@ -1473,6 +1486,7 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
   GroupIn gin{cand_h, (const u32x4*)xfrag, xinit, (const bf16x8*)qhi, KT, hl, (int)n_points,
               (int)((n_tiles + S - 1) / S), collect ? 1 : 0};
   gin.grows = collect ? 4 : grows;
+  gin.xi32 = Xi;
   // collect (the large-k lists, fp16 host operands only): k <= 256 over <= 512 filtered members
   if (collect) {
     if (hl != 1) return -1;
@@ -1511,7 +1525,7 @@ static int refine_groups_impl(int cap, const int* cand_ids, const int* cand_cnt,
     DMLP_LAUNCH_CHECK();
     return 0;
   }
-  if (!X || !Qx) return -3;  // (the other refines read the fp64 rows only)
+  if ((!X && !Xi) || !Qx) return -3;  // (the other refines read fp64 queries)
 #define DMLP_REFINE_G(KTV, F16)                                                                \
   hipLaunchKernelGGL((k_refine<2, KTV, F16>), dim3((nq + 3) / 4), dim3(256), 0, (hipStream_t)stream, \
                      cand_ids, cand_cnt, S, cap, X, A, Qx, qidx, qk, nq, out_d, out_i, kstride, \
