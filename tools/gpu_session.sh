@@ -251,6 +251,9 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    sweep7)  # the sweep's N = 1e7 rows (A 32 / 128 x k 16 / 1-64 / 200)
+      step sweep7 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep7.jsonl" --timeout 240 \
+          --ns 10000000 --attrs 32,128 ;;
     drab)  # the render choice per k class at N 1e5 / 1e6 x A 32 / 128: the host render forced
            # (DMLP_DEVICE_RENDER=0) against the cost model's choice, alternating on one box
       for R in 1 2; do
