@@ -251,6 +251,14 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    k200)  # the two-pass class (k = 200) at N = 1e7: device vs host render, alternating
+      for R in 1 2; do
+        for DR in 1 0; do
+          DMLP_DEVICE_RENDER=$DR step k200_dr${DR}_$R 300 tools/bin/step_driver --n 10000000 --a 32 \
+              --q 16384 --k 200 --steps 3 --warmup 1 --timeline
+        done
+      done
+      grep -H '^{' "$OUT"/k200_*.log | sed 's/"timeline.*//' ;;
     sweep7)  # the sweep's N = 1e7 rows (A 32 / 128 x k 16 / 1-64 / 200)
       step sweep7 1150 python3 -u tools/bench_sweep.py --out "$OUT/sweep7.jsonl" --timeout 240 \
           --ns 10000000 --attrs 32,128 ;;
