@@ -292,7 +292,12 @@ def main(argv=None):
             for key, P, launcher, nrun in runs:
                 extra[key] = _contract_entry(a, Q, P, launcher, nrun)
         if world > 1:
-            comm.barrier()
+            # the other ranks wait on the host (a GPU collective would keep a kernel spinning on
+            # every other GPU the contract's processes use), sleeping between polls
+            if a.ingress == "shm":
+                inp.barrier(world, timeout_s=1800.0, idle_s=0.01)
+            else:
+                comm.barrier()
     if comm.is_root:
         value = Q / (ms / 1e3)
         line = {
@@ -438,19 +443,30 @@ def _diagnostics(comm, eng, step, n, my_ms, steps_native=None):
     """Untimed traced steps after the timed ones (the tracer syncs around every phase, so they
     never run inside the timed region): per rank the mean phase times, the host<->device bytes
     the pipeline issued and the collective bytes, gathered on rank 0 together with the
-    rank-by-rank comparison of the collective sequence."""
+    rank-by-rank comparison of the collective sequence.  Every rank runs the same steps and the
+    same one gather whatever happens locally: a rank whose own bookkeeping fails (timeline reads,
+    summaries) reports the error in its row instead, and the sequence check is skipped.
+    DMLP_DIAG_FAIL=<ranks>|all (tests): that bookkeeping fails on those ranks."""
     import torch
     from distributed_machine_learning_project_amd.ops import knn as K
     from distributed_machine_learning_project_amd.parallel import dist_api as dist
+    err = []
+
+    def local(f, *args):
+        try:
+            return f(*args)
+        except Exception as e:  # noqa: BLE001
+            err.append(f"{type(e).__name__}: {e}"[-300:])
+            return None
     tr = eng.tracer
     # GPU-timestamped phase boundaries of the pipeline (hipEvents, no syncs) over n steps
     tl = []
     if comm.on_gpu:
-        K.set_pipe_events(True)
+        local(K.set_pipe_events, True)
         for _ in range(n + 1):
             step()
-            tl.append(K.pipe_timeline())
-        K.set_pipe_events(False)
+            tl.append(local(K.pipe_timeline) or [])
+        local(K.set_pipe_events, False)
         tl = tl[1:]  # the first has no previous call to measure the gap from
     was = tr.enabled
     tr.enabled, tr.records = True, []
@@ -465,32 +481,41 @@ def _diagnostics(comm, eng, step, n, my_ms, steps_native=None):
     comm.sync()
     log = dist.coll_log_stop() if comm.world > 1 else []
     tr.enabled = was
-    phases = {}
-    for name, v in tr.records:
-        phases[name] = phases.get(name, 0.0) + v / n
-    io_b = {k: v // n for k, v in K.io_bytes().items()}
-    coll_b = {}
-    for op, _, nb, _, _ in log:
-        coll_b[op] = coll_b.get(op, 0) + nb // n
-    timeline = {}
-    for row in tl:
-        for name, ms in row:
-            timeline[name] = timeline.get(name, 0.0) + ms / max(1, len(tl))
-    mine = {"rank": comm.rank, "device": str(comm.device), "numa_node": type(comm)._numa,
-            "ms_per_step": round(my_ms, 4),
-            "timed_native_step_calls": (steps_native or {}).get("calls"),
-            "host_issue_ms_per_step": round((steps_native or {}).get("host_ms", 0.0) /
-                                            max(1, (steps_native or {}).get("calls") or 1), 4),
-            "host_threads": _host_threads(),
-            "step_timeline_ms": {k: round(v, 4) for k, v in timeline.items()},
-            "phases_ms": {k: round(v, 4) for k, v in phases.items()},
-            "pcie_bytes_per_step": io_b, "collective_bytes_per_step": coll_b}
+
+    def summary():
+        inj = os.environ.get("DMLP_DIAG_FAIL", "")
+        if inj == "all" or str(comm.rank) in inj.split(","):
+            raise RuntimeError("injected diagnostics failure")
+        phases = {}
+        for name, v in tr.records:
+            phases[name] = phases.get(name, 0.0) + v / n
+        io_b = {k: v // n for k, v in K.io_bytes().items()}
+        coll_b = {}
+        for op, _, nb, _, _ in log:
+            coll_b[op] = coll_b.get(op, 0) + nb // n
+        timeline = {}
+        for row in tl:
+            for name, ms in row:
+                timeline[name] = timeline.get(name, 0.0) + ms / max(1, len(tl))
+        return {"rank": comm.rank, "device": str(comm.device), "numa_node": type(comm)._numa,
+                "ms_per_step": round(my_ms, 4),
+                "timed_native_step_calls": (steps_native or {}).get("calls"),
+                "host_issue_ms_per_step": round((steps_native or {}).get("host_ms", 0.0) /
+                                                max(1, (steps_native or {}).get("calls") or 1), 4),
+                "host_threads": _host_threads(),
+                "step_timeline_ms": {k: round(v, 4) for k, v in timeline.items()},
+                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+                "pcie_bytes_per_step": io_b, "collective_bytes_per_step": coll_b}
+    mine = local(summary) or {"rank": comm.rank}
+    if err:
+        mine["error"] = err[0]
     rows = [mine]
     check = None
     if comm.world > 1:
         rows = [None] * comm.world
         torch.distributed.all_gather_object(rows, mine)
-        check = dist.check_collective_sequence(log)
+        if all("error" not in r for r in rows):
+            check = dist.check_collective_sequence(log)
     if not comm.is_root:
         return {}
     out = {"per_rank": rows, "diag_steps": n}

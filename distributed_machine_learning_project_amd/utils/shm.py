@@ -165,10 +165,12 @@ class SharedInput(KNNInput):
         from .. import _lib
         return int(_lib.lib().dmlp_atomic_fetch_add_i64(self.counters.ctypes.data + 8 * slot, 1))
 
-    def barrier(self, world: int, timeout_s: float = 600.0):
+    def barrier(self, world: int, timeout_s: float = 600.0, idle_s: float = 0.0):
         """Barrier of the `world` processes mapping the segment: one atomic add on a monotonic
         counter, then a spin until every rank's add of this round has landed (the atomic is
-        sequentially consistent, so stores before it are visible to every rank after it)."""
+        sequentially consistent, so stores before it are visible to every rank after it).
+        idle_s > 0: a long wait sleeps that long between polls instead of yielding (ranks that
+        wait seconds for rank 0 leave the CPUs to the work it runs)."""
         import time
         from .. import _lib
         L = _lib.lib()
@@ -185,7 +187,7 @@ class SharedInput(KNNInput):
                     t0 = time.monotonic()
                 elif time.monotonic() - t0 > timeout_s:
                     raise TimeoutError("node-shared barrier: a rank did not arrive")
-                time.sleep(0)
+                time.sleep(idle_s)
 
     def reset_counter(self, slot: int):
         from .. import _lib

@@ -310,6 +310,23 @@ def test_bench_survives_replication_probe_failure(inject):
     assert res["replication_mode"] == "h2d"
 
 
+def test_bench_survives_diagnostics_failure():
+    """The untimed diagnostic steps after the timed ones (per-rank phases, collective-sequence
+    check) must not cost the headline line when one rank's part fails: every rank still takes
+    part in the one gather, the failing rank's row carries its error, the sequence check is
+    skipped, and rank 0 prints a valid, verified line (np 3)."""
+    import json
+    r = _bench(["--gpus", "3", "--steps", "2", "--warmup", "1", "--min-warmup-s", "0",
+                "--n-data", "1500", "--q-per-gpu", "200", "--verify", "--diag-steps", "1"],
+               {"DMLP_DATA_PLANE": "host", "DMLP_DIAG_FAIL": "1"})
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert res["n_gpus"] == 3 and res["verify_ok"] and res["value"] > 0
+    rows = res["per_rank"]
+    assert "error" in rows[1] and "error" not in rows[0] and "error" not in rows[2]
+    assert "collective_check" not in res
+
+
 def test_collective_log_compare():
     """The collective-sequence comparison (parallel/dist_api.py compare_logs) flags a rank that
     enters a different collective, a different size, a missing call and an unmatched send."""
