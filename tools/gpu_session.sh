@@ -251,6 +251,11 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    p3c)  # the P = 3 host-plane rehearsal with the node contract after the timed steps (rank 0
+          # runs the drop-in through mpiexec -n 3, the other ranks wait on the segment)
+      DMLP_BENCH_CONTRACT_RUNS=2 KNN_DATA_PLANE=host DMLP_DATA_PLANE=host step p3c 600 python bench.py \
+          --gpus 3 --steps 20 --warmup 2 --min-warmup-s 1 --no-busbw
+      grep -o '"reference_contract_node": {[^}]*' "$OUT/p3c.log" | head -c 600; echo ;;
     k200)  # the two-pass class (k = 200) at N = 1e7: device vs host render, alternating
       for R in 1 2; do
         for DR in 1 0; do
