@@ -134,7 +134,7 @@ struct GroupIn {
                           // over the lists (cand_h holds the fixed seed, not a final threshold)
   int rescore = 1;        // 0 (screen_f64.hip's fp64 keys): every member of a group at or above
                           // the threshold goes to the exact re-rank (no image to rescore from)
-  int grows = 4;          // rows per group entry: 4 (consecutive) or 8 (the k <= 16 screen's pair
+  int grows = 4;          // rows per group entry: 4 (consecutive) or 8 (the SUB = 16 screen's pair
                           // epilogue: rows 4 kg + i of steps 2p and 2p + 1, entry = 4 p + kg)
   const int* xi32 = nullptr;  // the dataset's lossless int32 rows (X unused), or null
 };

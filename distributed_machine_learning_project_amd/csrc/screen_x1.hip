@@ -91,7 +91,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
   // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
   using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
-  // PAIR (k <= 16, not COLLECT): the hit test and the append run once per PAIR of steps, on the
+  // PAIR (SUB = 16: k <= 32, not COLLECT): the hit test and the append run once per PAIR of steps, on the
   // 8-row group max (rows 4 kg .. 4 kg + 3 of both steps; entry index = pair * 4 + kg), instead of
   // per step on 4-row groups: the per-step max stays, the compare, the branch and the taken
   // step's append VALU halve (the screen is VALU-issue-bound: ~8.6 VALU per MFMA).  The
@@ -598,7 +598,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   }
 }
 
-int x1_sub(int kmax) { return kmax <= 16 ? 16 : 32; }
+// the k class served by the SUB = 16 variant (two waves per SIMD, the pair epilogue): k <= 32,
+// the pair refine's limit (its 56 kept group entries per column hold 32 groups + the 2 eps band:
+// k = 32 at the bench shape 3.49 -> 2.40 ms, k 1-32 3.27 -> 2.20, no escalation,
+// profiles/r11t_sub16_ab.txt); DMLP_X1_SUB16_KMAX narrows it (16: the SUB = 32 variant from k 17)
+int x1_sub16_kmax() {
+  static const int v = [] {
+    const char* e = getenv("DMLP_X1_SUB16_KMAX");
+    const int k = e && *e ? atoi(e) : 32;
+    return k < 1 ? 32 : k > 32 ? 32 : k;
+  }();
+  return v;
+}
+int x1_sub(int kmax) { return kmax <= x1_sub16_kmax() ? 16 : 32; }
 
 // One launch over slices [s_first, s_first + S_l) of an S-slice split (cand_* laid out for S).
 // (Variants measured slower and deleted — the LDS-ring screen, 8 column tiles per wave, the
@@ -673,7 +685,7 @@ extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
 }
 // group ids per (query, slice) (refine expands each to its dmlp_screen_x1_group_rows members)
 extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
-// rows per group entry of the screen that serves kmax (and of its early-start form): 8 (k <= 16:
+// rows per group entry of the screen that serves kmax (and of its early-start form): 8 (SUB = 16, k <= 32:
 // the pair epilogue, steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive rows);
 // the COLLECT pass always 4
 extern "C" int dmlp_screen_x1_group_rows(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }

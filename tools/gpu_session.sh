@@ -251,6 +251,27 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    sub16)  # k in (16, 32] on the SUB = 16 screen (pair epilogue, two waves per SIMD) vs SUB = 32,
+            # interleaved, bench shape at k = 32 and k 1-32 (escalations in the JSON)
+      for R in 1 2; do
+        for V in 16 32; do
+          DMLP_X1_SUB16_KMAX=$V step sub16_k32_${V}_$R 300 python bench.py --k 32 --steps 100 \
+              --min-warmup-s 1 --no-busbw --diag-steps 0
+          DMLP_X1_SUB16_KMAX=$V step sub16_k1_32_${V}_$R 300 python bench.py --k 32 --kmin 1 \
+              --kmax 32 --steps 100 --min-warmup-s 1 --no-busbw --diag-steps 0
+        done
+      done
+      for f in "$OUT"/sub16_*.log; do
+        echo "$f $(grep -o '"ms_per_step": [0-9.]*' "$f" | head -1) $(grep -o '"escalated_queries": [0-9]*' "$f" | head -1)"
+      done ;;
+    kverify)  # --verify at k = 24 / 32 / 1-32 / 17-64 (the k classes around the SUB 16 / 32 line)
+      for KS in "24 24 24" "32 32 32" "32 1 32" "40 17 64"; do
+        set -- $KS
+        step kv_$1_$2_$3 300 python bench.py --k $1 --kmin $2 --kmax $3 --steps 20 --warmup 2 \
+            --min-warmup-s 1 --no-busbw --diag-steps 0 --verify
+      done
+      grep -Ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*\|"escalated_queries": [0-9]*' \
+          "$OUT"/kv_*.log ;;
     p3c)  # the P = 3 host-plane rehearsal with the node contract after the timed steps (rank 0
           # runs the drop-in through mpiexec -n 3, the other ranks wait on the segment)
       DMLP_BENCH_CONTRACT_RUNS=2 KNN_DATA_PLANE=host DMLP_DATA_PLANE=host step p3c 600 python bench.py \
