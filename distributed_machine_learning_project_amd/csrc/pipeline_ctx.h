@@ -170,8 +170,8 @@ inline bool dr_early_ok(int, int) { return false; }
 // KT 2 k > 16 350, KT 4 322 / 415 — but KT 2 k <= 16 takes 2 x 241 (16 free after the allocation
 // granule: every wave timed out, profiles/r9h) and KT 8 up to all 512.
 inline bool early_room(int KT, int kmax) {
-  // (KT 2: only the SUB = 32 variant, whose groups are 4 rows)
-  return KT == 1 || (KT == 2 && dmlp_screen_x1_group_rows(kmax) == 4) || KT == 4;
+  // (KT 2: only the SUB = 32 variant, the larger candidate lists)
+  return KT == 1 || (KT == 2 && dmlp_screen_x1_cap(kmax) > dmlp_screen_x1_cap(1)) || KT == 4;
 }
 // test knob: the host sleeps this long before each dataset image slice of an early-start call,
 // so the screen provably waits mid-scan (tests/test_engine_gpu.py)

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   // per step on 4-row groups: the per-step max stays, the compare, the branch and the taken
   // step's append VALU halve (the screen is VALU-issue-bound: ~8.6 VALU per MFMA).  The
   // refine expands each entry to its 8 members (dmlp_screen_x1_group_rows).
-  constexpr bool PAIR = SUB == 16 && !COLLECT;
+  constexpr bool PAIR = !COLLECT;
   static_assert(!PAIR || (CHECK == 2 && DEPTH == 4), "the pair epilogue assumes 2-step checks");
   constexpr int CT = C::CT;
   constexpr int D = C::D;
@@ -688,7 +688,7 @@ extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
 // rows per group entry of the screen that serves kmax (and of its early-start form): 8 (SUB = 16, k <= 32:
 // the pair epilogue, steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive rows);
 // the COLLECT pass always 4
-extern "C" int dmlp_screen_x1_group_rows(int kmax) { return x1_sub(kmax) == 16 ? 8 : 4; }
+extern "C" int dmlp_screen_x1_group_rows(int kmax) { (void)kmax; return 8; }
 // resident workgroups (= waves) per CU: LDS-bound at 17.5 KiB (SUB 16, 4 tiles) / 33.5 KiB
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {

@@ -251,6 +251,12 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    pair32)  # the pair epilogue on the 32-entry screen too (k in (32, 64]): library builds
+             # ab/libdmlp_base.so vs ab/libdmlp_pair32.so, interleaved, at k 17-64 and 33-64
+      AB_PROF=0 AB_ROUNDS=2 AB_STEPS=100 AB_ARGS="--k 40 --kmin 17 --kmax 64 --diag-steps 0" \
+          step pair32_a 600 bash tools/kernel_ab.sh base pair32
+      AB_PROF=0 AB_ROUNDS=2 AB_STEPS=100 AB_ARGS="--k 48 --kmin 33 --kmax 64 --diag-steps 0" \
+          step pair32_b 600 bash tools/kernel_ab.sh base pair32 ;;
     sub16)  # k in (16, 32] on the SUB = 16 screen (pair epilogue, two waves per SIMD) vs SUB = 32,
             # interleaved, bench shape at k = 32 and k 1-32 (escalations in the JSON)
       for R in 1 2; do
