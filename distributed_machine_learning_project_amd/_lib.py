@@ -60,6 +60,7 @@ _SIGS = {
     "dmlp_screen_x1_qw": (i32, [i32]),
     "dmlp_screen_x1_cols": (i32, [i32, i32]),
     "dmlp_screen_x1_cap": (i32, [i32]),
+    "dmlp_screen_x1_cap_kt": (i32, [i32, i32]),
     "dmlp_screen_x1_waves_per_cu": (i32, [i32]),
     "dmlp_screen_x1_waves_per_cu_kt": (i32, [i32, i32]),
     "dmlp_screen_x1_min_slices": (i64, [i64]),

@@ -162,7 +162,8 @@ static inline int dmlp_screen_kt(int A) {
 int dmlp_screen_x1_kmax(void);
 int dmlp_screen_x1_qw(int KT);
 int dmlp_screen_x1_cols(int KT, int kmax);
-int dmlp_screen_x1_cap(int kmax);
+int dmlp_screen_x1_cap(int kmax);  // (KT 1's; the image of KT fragments per step: _kt)
+int dmlp_screen_x1_cap_kt(int KT, int kmax);
 // rows per group entry of that screen's lists: 8 for kmax <= 16 (hit test and append once per two
 // MFMA steps on the 8-row max: rows 4 kg .. 4 kg + 3 of steps 2p and 2p + 1, entry index 4 p + kg),
 // else 4 (consecutive rows, entry index = row / 4); the refines expand each entry to its rows

@@ -128,7 +128,7 @@ struct Local {
     const int64_t nt = (N + 63) / 64;
     const bool fin = labels != nullptr;
     if (impl == 0) {
-      const int cap = dmlp_screen_x1_cap(kcls);
+      const int cap = dmlp_screen_x1_cap_kt(KT, kcls);
       // (the large-N pipeline cut its chunks for its own slice count)
       const int S = hx && hx->chunk_n > 0 && !idx ? hx->chunk_S : x1_slices(nq, KT, kcls, nt);
       int* ci = w.cand_ids.get((size_t)nq * S * cap);
@@ -181,7 +181,7 @@ struct Local {
       for (int q : *idx) kmax1 = std::max(kmax1, kp[q]);
       int* kpd = w.kp_d.get(Q);
       CK(dmlp::dma_copy(kpd, kp, Q * sizeof(int), st));
-      const int cap1 = dmlp_screen_x1_cap(kmax1);
+      const int cap1 = dmlp_screen_x1_cap_kt(KT, kmax1);
       int* i1 = w.k1_ids.get((size_t)nq * S1 * cap1);
       int* c1 = w.k1_cnt.get((size_t)nq * S1);
       float* h1 = w.k1_h.get((size_t)nq * S1 * 2);

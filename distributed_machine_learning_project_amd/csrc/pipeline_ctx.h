@@ -166,12 +166,14 @@ inline bool dr_on();  // (Tuning::device_render below)
 inline bool dr_early_ok(int, int) { return false; }
 // The early start's copies (small ones run as blit kernels) need a wave slot beside the spinning
 // screen: the screen variant must leave registers free (of 512 per SIMD lane; hipcc
-// -Rpass-analysis=kernel-resource-usage): KT 1 k <= 16 2 x 208 (96 free), KT 1 k > 16 320,
-// KT 2 k > 16 350, KT 4 322 / 415 — but KT 2 k <= 16 takes 2 x 241 (16 free after the allocation
-// granule: every wave timed out, profiles/r9h) and KT 8 up to all 512.
+// -Rpass-analysis=kernel-resource-usage, VGPR + AGPR): KT 1 SUB 16 2 x 223, KT 1 SUB 32 317,
+// KT 2 SUB 32 350 — but KT 2 SUB 16 takes 2 x 256 (every wave timed out, profiles/r9h) and KT 8
+// up to all 512.  KT 4 (SUB 16 322, SUB 32 414) has the room on paper, yet its copies found no
+// slot in 2 of 7 test sessions (every wave timed out: profiles/r12a_kt4_early.txt), so KT 4
+// runs without the early start too.
 inline bool early_room(int KT, int kmax) {
   // (KT 2: only the SUB = 32 variant, the larger candidate lists)
-  return KT == 1 || (KT == 2 && dmlp_screen_x1_cap(kmax) > dmlp_screen_x1_cap(1)) || KT == 4;
+  return KT == 1 || (KT == 2 && dmlp_screen_x1_cap_kt(2, kmax) > dmlp_screen_x1_cap_kt(2, 1));
 }
 // test knob: the host sleeps this long before each dataset image slice of an early-start call,
 // so the screen provably waits mid-scan (tests/test_engine_gpu.py)

@@ -610,7 +610,10 @@ int x1_sub16_kmax() {
   }();
   return v;
 }
-int x1_sub(int kmax) { return kmax <= x1_sub16_kmax() ? 16 : 32; }
+// KT 2 keeps k in (16, 32] on the 32-entry variant: the early start needs its registers free
+// (the 16-entry KT 2 screen leaves the copies no wave slot) and with it that one is faster
+// (A = 48 / 64, k = 32: 4.26-4.48 vs 4.45-4.71 ms, profiles/r11z_kt2_ab.txt)
+int x1_sub(int KT, int kmax) { return kmax <= (KT == 2 ? 16 : x1_sub16_kmax()) ? 16 : 32; }
 
 // One launch over slices [s_first, s_first + S_l) of an S-slice split (cand_* laid out for S).
 // (Variants measured slower and deleted — the LDS-ring screen, 8 column tiles per wave, the
@@ -684,7 +687,8 @@ extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
   return x1_kt_ok(KT) ? 64 : 0;
 }
 // group ids per (query, slice) (refine expands each to its dmlp_screen_x1_group_rows members)
-extern "C" int dmlp_screen_x1_cap(int kmax) { return 4 * (x1_sub(kmax) - 1); }
+extern "C" int dmlp_screen_x1_cap_kt(int KT, int kmax) { return 4 * (x1_sub(KT, kmax) - 1); }
+extern "C" int dmlp_screen_x1_cap(int kmax) { return dmlp_screen_x1_cap_kt(1, kmax); }
 // rows per group entry of the screen that serves kmax (and of its early-start form): 8 (SUB = 16, k <= 32:
 // the pair epilogue, steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive rows);
 // the COLLECT pass always 4
@@ -692,12 +696,12 @@ extern "C" int dmlp_screen_x1_group_rows(int kmax) { (void)kmax; return 8; }
 // resident workgroups (= waves) per CU: LDS-bound at 17.5 KiB (SUB 16, 4 tiles) / 33.5 KiB
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {
-  return x1_sub(kmax) == 16 ? 8 : 4;
+  return x1_sub(1, kmax) == 16 ? 8 : 4;
 }
 // the same for an image of KT fragments per step: A > 64 (KT = 4, 8) runs one wave per SIMD (the
 // query and ring fragments take the registers of two)
 extern "C" int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax) {
-  return KT >= 4 ? 4 : dmlp_screen_x1_waves_per_cu(kmax);
+  return KT >= 4 ? 4 : x1_sub(KT, kmax) == 16 ? 8 : 4;
 }
 // a slice must stay below 2^16 4-row groups (16-bit group index in an entry)
 extern "C" int64_t dmlp_screen_x1_min_slices(int64_t n_tiles) { return (n_tiles + 4095) / 4096; }
@@ -782,7 +786,7 @@ extern "C" int dmlp_screen_x1_part(int KT, int hl, int A, const void* xfrag, con
   hipStream_t st = (hipStream_t)stream;
 #define DMLP_X1_ARGS hl, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx, qk, nq, xnmax_bits, bad, r1, \
                      r2, r3, S, s_first, S_l, cand_ids, cand_cnt, cand_h, st
-  const bool s32 = x1_sub(kmax) == 32;
+  const bool s32 = x1_sub(KT, kmax) == 32;
   // hl = 1: the host's fp16 image + fp16 query fragments; hl = 2: prep.hip's bf16 hi/lo image
 #define DMLP_X1_PICK(F16)                                                                      \
   do {                                                                                         \
@@ -838,7 +842,7 @@ extern "C" int dmlp_screen_x1_early(int KT, int A, const void* xfrag, const floa
     const double ms = e ? atof(e) : 50.0;
     return (long long)(ms * khz);
   }();
-  const bool s32 = x1_sub(kmax) == 32;
+  const bool s32 = x1_sub(KT, kmax) == 32;
 #define DMLP_X1E(KTV, SUBV)                                                                     \
   return launch_x1<KTV, SUBV, 4, 2, true>(1, xfrag, xinit, n_tiles, n_points, qhi, qn, qidx,    \
                                          qk, nq, bad, bad, r1, r2, r3, 1, 0, 1, cand_ids,       \

@@ -143,7 +143,8 @@ def _early_inputs(n, A, kmax, Q, seed):
 
 @pytest.mark.parametrize("render", ["device", "host"])
 @pytest.mark.parametrize("n,A,kmax", [(2000, 32, 16), (5000, 32, 32), (3000, 64, 64),
-                                        (3000, 64, 16), (3000, 128, 32), (3000, 256, 32)])
+                                        (3000, 64, 32), (3000, 64, 16), (3000, 128, 32),
+                                        (3000, 256, 32)])
 def test_native_step_early_start(gpu, n, A, kmax, render):
     """Early start: the screen starts on the query operands while the dataset image crosses
     PCIe in slices with ready words.  The host sleeps 400 us before each image slice
@@ -151,12 +152,14 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     waits > 0, eps growths > 0 (the far point sits in the last slice) and no timeout.  Two
     different inputs of equal shape alternate A, B, A, B (early on), then once with the early
     start off.  Each slice's ready word is one DMA copy carrying the slice's max norm; every
-    report, label and checksum == its own oracle's.  A = 128 runs the KT = 4
-    variant (one wave per SIMD, 404 of 512 registers).  A = 256 (KT = 8, all 512 registers): the
-    step refuses the early start there — its image copies (blit kernels) would find no free wave
-    slot beside the spinning screen — and the results stay exact.  One screen slice needs a full
-    round of waves (>= 131072 queries at KT = 1, >= 65536 at KT >= 4).  A = 64 / k <= 16 (KT 2,
-    2 x 244 registers) leaves no slot for the copies: no early start there.  render: the device
+    report, label and checksum == its own oracle's.  A = 64 / k = 32 runs the KT = 2 screen on
+    its 32-entry variant (screen_x1.hip x1_sub: KT 2 keeps that variant for k in (16, 32] so the
+    early start stays on).  A = 128 (KT = 4) and A = 256 (KT = 8): the step refuses the early start
+    there — its image copies (blit kernels in this process) found no wave slot beside the spinning
+    KT 4 screen in 2 of 7 sessions (profiles/r12a_kt4_early.txt), KT 8 takes all 512 registers —
+    and the results stay exact.  One screen slice needs a full round of waves (>= 131072 queries
+    at KT = 1, >= 65536 at KT >= 4).  A = 64 / k <= 16 (KT 2, 2 x 256 registers) leaves no slot
+    for the copies: no early start there.  render: the device
     render switch on or off — an early-start step renders on the host either way
     (pipeline.hip dr_early_ok); without the early start the switch's render runs."""
     from distributed_machine_learning_project_amd import _lib
@@ -184,7 +187,7 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
             assert bytes(dst[:r.report_len]) == expect, f"round {rnd}"
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
-            assert r.early == (early if A <= 128 and not no_room else 0)
+            assert r.early == (early if A <= 64 and not no_room else 0)
             if r.early:
                 assert K.pipeline_stats()["device_render"] == (1 if dr_used else 0)
             if A <= 64:

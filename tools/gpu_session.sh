@@ -251,6 +251,20 @@ for task in "$@"; do
       done
       echo "native probe, kernel trace only: copyBuffer $(grep -c copyBuffer \
           "$OUT/ck_kt/run_kernel_trace.csv" || true)" ;;
+    kverify2)  # --verify at A = 48 / 64 (KT 2) across the k classes
+      for AK in "48 32 32" "64 1 32" "64 17 64" "48 1 16"; do
+        set -- $AK
+        step kv2_$1_$2_$3 300 python bench.py --attrs $1 --k $3 --kmin $2 --kmax $3 --steps 20 \
+            --warmup 2 --min-warmup-s 1 --no-busbw --diag-steps 0 --verify
+      done
+      grep -Ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*\|"escalated_queries": [0-9]*\|"early_start_calls": [0-9]*' \
+          "$OUT"/kv2_*.log ;;
+    kt2)  # A = 48 / 64 (KT 2) at k = 32: the 16-entry screen (no early start there) vs the 32-entry
+          # screen with the early start, interleaved
+      for A in 48 64; do
+        AB_PROF=0 AB_ROUNDS=2 AB_STEPS=100 AB_ARGS="--attrs $A --k 32 --diag-steps 0" \
+            step kt2_a$A 600 bash tools/kernel_ab.sh s16:DMLP_X1_SUB16_KMAX=32 s32:DMLP_X1_SUB16_KMAX=16
+      done ;;
     pair32)  # the pair epilogue on the 32-entry screen too (k in (32, 64]): library builds
              # ab/libdmlp_base.so vs ab/libdmlp_pair32.so, interleaved, at k 17-64 and 33-64
       AB_PROF=0 AB_ROUNDS=2 AB_STEPS=100 AB_ARGS="--k 40 --kmin 17 --kmax 64 --diag-steps 0" \

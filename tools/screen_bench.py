@@ -57,7 +57,7 @@ def main():
     d_qn = torch.from_numpy(qn).to(dev)
     d_k = torch.from_numpy(inp.k).to(dev)
     d_qi = torch.arange(Q, dtype=torch.int32, device=dev)
-    cap = L.dmlp_screen_x1_cap(a.k)
+    cap = L.dmlp_screen_x1_cap_kt(KT, a.k)
     S = 1
     ci = torch.empty(Q * S * cap, dtype=torch.int32, device=dev)
     cc = torch.empty(Q * S, dtype=torch.int32, device=dev)
