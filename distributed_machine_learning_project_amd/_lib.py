@@ -141,6 +141,7 @@ _SIGS = {
     "dmlp_plane_wait": (i32, [vp, i32, i32, i32p, C.POINTER(C.c_float)]),
     "dmlp_plane_ready": (i32, [vp, i32, i32]),
     "dmlp_host_register": (i32, [vp, i64]),
+    "dmlp_host_device_view": (vp, [vp, i64, vp]),
     "dmlp_host_unregister": (i32, [vp]),
 }
 

@@ -360,6 +360,9 @@ typedef struct dmlp_step_args {
 int dmlp_step(dmlp_step_args* args);
 // The last step's device report bytes [0, bytes) -> dst (page-locked / registered), synchronous.
 int dmlp_step_emit(char* dst, int64_t bytes, void* stream);
+// The device address a report_mode 1 step writes its text to for [p, p + bytes) of page-locked
+// host memory, or null when it stages the text on the device and copies it (pageable memory).
+void* dmlp_host_device_view(void* p, int64_t bytes, int64_t* info);
 // The last dmlp_step's report text as it sits on the device (report_mode 2) and its length.
 int dmlp_step_text(const char** dev, int64_t* len);
 void dmlp_step_early(int on);          // 1 on, 0 off, < 0: DMLP_FAST_EARLY (default on)

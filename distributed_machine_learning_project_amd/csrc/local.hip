@@ -72,6 +72,7 @@ extern "C" int dmlp_knn_local(const double* X, int64_t N, int A, const double* Q
     g_stats.path = 2;
     g_stats.early = 0;
     g_stats.device_render = 0;
+    g_stats.report_direct = 0;
     return 0;
   } catch (const Fail& f) {
     return drain_and_fail(wp, st, f.code);
@@ -81,13 +82,15 @@ extern "C" int dmlp_knn_local(const double* X, int64_t N, int A, const double* Q
 }
 
 
-// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render".
+// Tuning / A-B switches (see Tuning): "num_cus", "screen", "x1k", "host_ops", "device_render",
+// "report_direct".
 // Returns the previous value, or -1 for an unknown key.
 extern "C" int dmlp_pipeline_set(const char* key, int value) {
   const std::string k = key ? key : "";
   int* f = k == "num_cus" ? &g_tune.num_cus : k == "screen" ? &g_tune.screen
            : k == "x1k" ? &g_tune.x1k : k == "host_ops" ? &g_tune.host_ops
-           : k == "device_render" ? &g_tune.device_render : nullptr;
+           : k == "device_render" ? &g_tune.device_render
+           : k == "report_direct" ? &g_tune.report_direct : nullptr;
   if (!f) return -1;
   const int old = *f;
   *f = value;
@@ -97,7 +100,8 @@ extern "C" int dmlp_pipeline_set(const char* key, int value) {
 
 // What the last dmlp_step / dmlp_knn_local did: [0] queries on the exact fp64 path, [1] queries
 // escalated from a single-term to a 3-term screen, [2] path (0 host-rendered operands, 2 device
-// image), [3] early start.
+// image), [3] early start, [4] / [5] exact-path queries on the fp64 MFMA screen / those redone
+// by the VALU kernel, [6] device render, [7] report written straight into host memory.
 extern "C" void dmlp_pipeline_stats(int64_t* out) {
   out[0] = g_stats.n_exact;
   out[1] = g_stats.n_escalated;
@@ -106,6 +110,7 @@ extern "C" void dmlp_pipeline_stats(int64_t* out) {
   out[4] = g_stats.n_exact_f64;
   out[5] = g_stats.n_exact_f64_redo;
   out[6] = g_stats.device_render;
+  out[7] = g_stats.report_direct;
 }
 
 extern "C" void* dmlp_dev_alloc(int64_t bytes) { return dev_alloc((size_t)std::max<int64_t>(bytes, 1)); }

@@ -66,6 +66,48 @@ __global__ void k_busy(long long ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
 }
 
+// The device's address for [p, p + bytes) of page-locked host memory (hipHostMalloc'd or
+// registered, the whole range inside one allocation), or nullptr when the GPU cannot address it
+// there (pageable memory: the step then stages the report on the device and copies it).  Both ends
+// must map with one offset, and the allocation's address range (hipMemGetAddressRange) must hold
+// the whole range — for registered memory this runtime reports the range's size with a null base
+// (tools/probe/host_view_probe.py), so there both ends must lie in ranges of that one size.  Asked
+// per call, never cached: a freed buffer's address can come back as pageable memory.
+char* host_device_view(char* p, size_t bytes, int64_t* info = nullptr) {
+  if (info) std::memset(info, 0, 8 * sizeof(int64_t));
+  if (!p || bytes == 0) return nullptr;
+  struct End {
+    hipPointerAttribute_t at{};
+    hipError_t e1 = hipErrorInvalidValue, e2 = hipErrorInvalidValue;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+  } lo, hi;
+  auto query = [](char* q, End& e) {
+    e.e1 = hipPointerGetAttributes(&e.at, q);
+    if (e.e1 == hipSuccess && e.at.devicePointer)
+      e.e2 = hipMemGetAddressRange(&e.base, &e.size, (hipDeviceptr_t)e.at.devicePointer);
+    if (e.e1 != hipSuccess || e.e2 != hipSuccess) (void)hipGetLastError();
+    return e.e1 == hipSuccess && e.e2 == hipSuccess && e.at.type == hipMemoryTypeHost &&
+           e.at.devicePointer && e.at.hostPointer == q;
+  };
+  const bool ok_lo = query(p, lo);
+  const bool ok_hi = ok_lo && query(p + bytes - 1, hi);
+  if (info) {
+    const int64_t v[8] = {(int64_t)lo.e1, (int64_t)lo.at.type, (int64_t)(intptr_t)lo.at.devicePointer,
+                          (int64_t)(intptr_t)lo.at.hostPointer, (int64_t)lo.e2,
+                          (int64_t)(intptr_t)lo.base, (int64_t)lo.size, (int64_t)(intptr_t)p};
+    std::memcpy(info, v, sizeof v);
+  }
+  if (!ok_hi) return nullptr;
+  const char* d = (const char*)lo.at.devicePointer;
+  if ((const char*)hi.at.devicePointer - d != (ptrdiff_t)(bytes - 1)) return nullptr;
+  if (lo.base) {
+    const char* b = (const char*)lo.base;
+    return d >= b && d + bytes <= b + lo.size ? (char*)lo.at.devicePointer : nullptr;
+  }
+  return !hi.base && hi.size == lo.size && lo.size >= bytes ? (char*)lo.at.devicePointer : nullptr;
+}
+
 // ---------------------------------------------------------------- dmlp_step
 struct Step {
   Ctx& w;
@@ -539,7 +581,14 @@ struct Step {
       }
       // (rc != 0: data or queries outside the fp16 screen's range -> the device image path)
     }
-    char* text = want_report ? w.d_text.get((size_t)dmlp_format_bound((int)Q)) : nullptr;
+    // report_mode 1 into page-locked memory the GPU addresses: the format kernel writes the text
+    // there across PCIe, no device staging and no D2H copy of the whole bound on the tail
+    char* direct = want_report && a->report_mode == 1 && g_tune.report_direct
+                       ? host_device_view(a->report_dst, (size_t)dmlp_format_bound((int)Q))
+                       : nullptr;
+    char* text = !want_report ? nullptr
+                 : direct     ? direct
+                              : w.d_text.get((size_t)dmlp_format_bound((int)Q));
     // ---- dispatch: screens on `st`, the rows behind the first of them on the side stream
     auto run_local = [&](bool with_hx, bool rows_pending) {
       std::unique_ptr<Local> Lp(new Local(w));
@@ -627,7 +676,7 @@ struct Step {
                          a->early ? estats : nullptr, dr_bad, small_d);
       CK(hipGetLastError());
       CK(dmlp::dma_copy(small, small_d, 8 * sizeof(int64_t), st));
-      if (want_report && a->report_mode == 1)
+      if (want_report && a->report_mode == 1 && !direct)
         CK(dmlp::dma_copy(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q), st));
     };
     a->host_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t_enter)
@@ -680,6 +729,7 @@ struct Step {
     g_stats.path = a->path;
     g_stats.early = a->early;
     g_stats.device_render = dr && use_hx ? 1 : 0;
+    g_stats.report_direct = direct ? 1 : 0;
     return 0;
   }
 
@@ -776,6 +826,12 @@ extern "C" int dmlp_step(dmlp_step_args* a) {
   } catch (const std::bad_alloc&) {
     return drain_and_fail(wp, st, -(int)hipErrorOutOfMemory);
   }
+}
+
+// The device address the step would write a report_mode 1 text to for [p, p + bytes), or null
+// (host_device_view); info (8 words, may be null): the attribute and address-range queries.
+extern "C" void* dmlp_host_device_view(void* p, int64_t bytes, int64_t* info) {
+  return host_device_view((char*)p, (size_t)std::max<int64_t>(bytes, 0), info);
 }
 
 // The last dmlp_step's report bytes (report_mode 2: kept on the device) -> dst (page-locked or

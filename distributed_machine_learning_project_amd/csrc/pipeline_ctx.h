@@ -210,6 +210,10 @@ struct Tuning {
   int host_ops = 1;
   // device render: -1 (default) by the cost model below, 0 never, 1 always (DMLP_DEVICE_RENDER)
   int device_render = -1;
+  // report_mode 1 into page-locked memory the GPU can address: 1 the format kernel writes the
+  // text straight across PCIe, 0 into device memory, then one D2H copy of the bound
+  // (DMLP_REPORT_DIRECT)
+  int report_direct = 1;
 };
 inline Tuning make_tuning() {
   Tuning t;
@@ -222,6 +226,7 @@ inline Tuning make_tuning() {
   // measured faster, 4.86 vs 5.64 ms/step; at 2 threads the host operands still win, 3.58 vs
   // 3.74: profiles/r7h_host_budget.md)
   if (const char* e = std::getenv("DMLP_DEVICE_RENDER"); e && *e) t.device_render = e[0] != '0';
+  if (env_off("DMLP_REPORT_DIRECT")) t.report_direct = 0;
   if (env_off("DMLP_HOST_OPS")) t.host_ops = 0;
   else if (const char* e = std::getenv("DMLP_HOST_OPS"); e && *e) t.host_ops = 2;  // forced on
   return t;
@@ -288,6 +293,7 @@ struct Stats {
   int64_t n_exact = 0, n_escalated = 0, path = 0, early = 0;
   int64_t n_exact_f64 = 0, n_exact_f64_redo = 0;  // exact-path queries on the fp64 MFMA screen
   int64_t device_render = 0;  // the screen operands were rendered on the device
+  int64_t report_direct = 0;  // the report text went straight into the caller's host buffer
 };
 inline Stats g_stats;
 

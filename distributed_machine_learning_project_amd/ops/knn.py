@@ -152,12 +152,15 @@ def pipeline_options(**kw):
 
 def pipeline_stats():
     """What the last native call did: {"n_exact", "n_escalated", "path", "early", "n_exact_f64",
-    "n_exact_f64_redo", "device_render"} (exact-path queries on the fp64 MFMA screen, and those of
-    them that overflowed to the fused VALU kernel; whether the GPU rendered the screen operands)."""
+    "n_exact_f64_redo", "device_render", "report_direct"} (exact-path queries on the fp64 MFMA
+    screen, and those of them that overflowed to the fused VALU kernel; whether the GPU rendered
+    the screen operands; whether the report text went straight into the caller's page-locked
+    buffer)."""
     out = (C.c_int64 * 8)()
     _lib.lib().dmlp_pipeline_stats(out)
     return {"n_exact": out[0], "n_escalated": out[1], "path": out[2], "early": out[3],
-            "n_exact_f64": out[4], "n_exact_f64_redo": out[5], "device_render": out[6]}
+            "n_exact_f64": out[4], "n_exact_f64_redo": out[5], "device_render": out[6],
+            "report_direct": out[7]}
 
 
 # ---------------------------------------------------------------- rows on the device
@@ -364,8 +367,8 @@ def step(X_host, labels_host, label_range, Q_host, k_host, *, k_range=None, qid_
     kt = screen_kt(A)
     _IO["h2d"] += ((N + 63) // 64 * 64 * (kt * 64 + 4) + Q * (kt * 64 + 4) if a.path == 0 else 0)
     _IO["h2d"] += (Q if x32 is not None else N + Q) * A * 4 + N * 4  # (lossless int32 rows)
-    if a.report_mode == 1:
-        _IO["d2h"] += L.dmlp_format_bound(Q)
+    if a.report_mode == 1:  # (written straight across PCIe: the text; else the staged bound)
+        _IO["d2h"] += int(a.report_len) if st["report_direct"] else L.dmlp_format_bound(Q)
     if _EVENTS[0]:
         _read_timeline()
     return StepResult(lab, cs, od, oi, int(a.report_len), a.path, a.early, a.n_escalated,
