@@ -22,9 +22,10 @@
 //                   on a side stream; the screen starts on them while the fp64 rows (lossless
 //                   int32 when every value is a 6-decimal number) cross PCIe behind it; k in
 //                   (64, 256] takes the two-pass single-term screen on the same operands; then
-//                   exact re-rank + vote + FNV checksum, the report text rendered on the GPU and
-//                   copied into the caller's page-locked buffer (or kept on the device for a
-//                   multi-rank egress, dmlp_step_emit).  One host sync in the common case; an
+//                   exact re-rank + vote + FNV checksum, the report text rendered on the GPU
+//                   straight into the caller's page-locked buffer (host_device_view; staged and
+//                   copied for pageable memory), or kept on the device for a multi-rank egress
+//                   (dmlp_step_emit).  One host sync in the common case; an
 //                   overflowed query escalates natively (no call is ever re-run elsewhere).
 //
 // Early start (dmlp_step, every k in [1, 64], one screen slice): the query operands cross first
