@@ -37,6 +37,7 @@
 #   exact64    the exact path at A = 48 / 64: fp64 MFMA screen vs VALU kernel, --verify
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
+#   cmpab      pair refine over compacted group entries vs the previous tree (library A/B)
 #   rdab       report straight into pinned host memory vs staged + D2H (DMLP_REPORT_DIRECT A/B)
 set -u
 TAG=${1:?tag}
@@ -260,6 +261,11 @@ for task in "$@"; do
       done
       grep -Ho '"ms_per_step": [0-9.]*\|"verify_ok": [a-z]*\|"escalated_queries": [0-9]*\|"early_start_calls": [0-9]*' \
           "$OUT"/kv2_*.log ;;
+    cmpab)  # pair refine over the compacted passing group entries (ab/libdmlp_cmp.so) vs the
+            # previous tree (ab/libdmlp_base.so), interleaved under the kernel tracer
+      rm -rf gpurun_out/ab
+      AB_ROUNDS=3 AB_STEPS=30 step cmpab 900 bash tools/kernel_ab.sh base cmp
+      python tools/ab_summary.py gpurun_out/ab | tee "$OUT/cmpab_kernels.txt" ;;
     rdab)  # the report written straight into the caller's pinned buffer vs staged + one D2H copy,
            # interleaved (AB_ROUNDS x 100 steps), then the contract (drop-in, mpiexec) both ways
       AB_PROF=0 AB_ROUNDS=${AB_ROUNDS:-3} AB_STEPS=100 AB_ARGS="--diag-steps 30" \
