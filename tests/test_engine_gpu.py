@@ -84,12 +84,14 @@ def test_native_step(gpu, kmax, A):
     eng.close()
 
 
-def test_native_step_report_direct(gpu):
-    """report_mode 1 into page-locked memory: the format kernel writes the text straight into the
-    caller's buffer across PCIe (pipeline.hip host_device_view), no device staging or D2H copy.
-    A pinned buffer, an interior view of one, pageable memory (staged + copied) and the switch off
-    (report_direct 0) all give the oracle's bytes; the stats say which way the text went.  One
-    escalated query (a duplicated point cluster) renders the report a second time in the call."""
+@pytest.mark.parametrize("escalate", [False, True])
+def test_native_step_report_direct(gpu, escalate):
+    """report_mode 1 into page-locked memory (pipeline.hip host_device_view): the format kernels
+    write the text straight into the caller's buffer across PCIe (report_direct 1); pageable
+    memory, or the switch off, is staged on the device and copied (0).  Every case == the oracle's
+    bytes, labels and checksums, at qid_base 0 and 123456789 (wider ids).  escalate: a duplicated
+    point cluster hands a query back from the refine, so the report is rendered a second time in
+    the call, after the escalation."""
     import torch
     from distributed_machine_learning_project_amd import _lib
     L = _lib.lib()
@@ -97,34 +99,36 @@ def test_native_step_report_direct(gpu):
     N, Q, A = 6000, 5000, 32
     X = np.round(rng.uniform(0.0, 1000.0, (N, A)), 6)
     Qx = np.round(rng.uniform(0.0, 1000.0, (Q, A)), 6)
-    X[:80] = X[0]
-    Qx[0] = X[0]
+    if escalate:
+        X[:80] = X[0]
+        Qx[0] = X[0]
     k = rng.integers(1, 33, Q).astype(np.int32)
     k[0] = 32
     labels = rng.integers(0, 8, N).astype(np.int32)
     d, i = K.knn_cpu(X, Qx, k)
     lab_ref, cs = K.finalize_cpu(i, k, labels)
-    expect = dmlp.format_report(cs)
     bound = L.dmlp_format_bound(Q)
     pinned = torch.empty(bound + 4096, dtype=torch.uint8).pin_memory().numpy()
-    cases = [("pinned", pinned, 1, 1), ("pinned view", pinned[4096:], 1, None),
-             ("pageable", np.empty(bound, np.uint8), 1, 0), ("switch off", pinned, 0, 0)]
+    # name, buffer, report_direct, qid_base, expected report_direct stat
+    cases = [("pinned", pinned, 1, 0, 1), ("pinned view", pinned[4096:], 1, 0, 1),
+             ("pinned qid_base", pinned, 1, 123456789, 1),
+             ("pageable", np.empty(bound, np.uint8), 1, 0, 0), ("staged", pinned, 0, 0, 0),
+             ("staged qid_base", pinned, 0, 123456789, 0)]
     old_cus = L.dmlp_pipeline_set(b"num_cus", 4)  # (one screen slice: the pair refine's case)
     try:
-        for name, dst, on, want in cases:
-            old = L.dmlp_pipeline_set(b"report_direct", on)
+        for name, dst, direct, base, want in cases:
+            od = L.dmlp_pipeline_set(b"report_direct", direct)
             try:
                 dst[:] = 0
-                r = K.step(X, labels, (0, 8), Qx, k, report=dst)
+                r = K.step(X, labels, (0, 8), Qx, k, report=dst, qid_base=base)
             finally:
-                L.dmlp_pipeline_set(b"report_direct", old)
-            assert bytes(dst[:r.report_len]) == expect, name
+                L.dmlp_pipeline_set(b"report_direct", od)
+            assert bytes(dst[:r.report_len]) == dmlp.format_report(cs, base), name
             np.testing.assert_array_equal(r.label.cpu().numpy(), lab_ref)
             np.testing.assert_array_equal(r.checksum.cpu().numpy().view(np.uint64), cs)
             st = K.pipeline_stats()
-            assert st["n_escalated"] + st["n_exact"] >= 1, (name, st)
-            if want is not None:
-                assert st["report_direct"] == want, (name, st)
+            assert (st["n_escalated"] + st["n_exact"] >= 1) == escalate, (name, st)
+            assert st["report_direct"] == want, (name, st)
     finally:
         L.dmlp_pipeline_set(b"num_cus", old_cus)
 
