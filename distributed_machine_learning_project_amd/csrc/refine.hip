@@ -961,21 +961,23 @@ __device__ __forceinline__ int line_len(int64_t qid, uint64_t cs) {
   return 6 + ndig_u64((uint64_t)qid) + 11 + ndig_u64(cs) + 1;
 }
 
-__global__ void k_fmt_len(const uint64_t* __restrict__ cs, int nq, int qid_base,
-                          int64_t* __restrict__ off, int64_t* __restrict__ blocksum) {
-  __shared__ int64_t sh[1024];
-  const int i = blockIdx.x * 1024 + threadIdx.x;
+template <int FB>
+__global__ void __launch_bounds__(FB) k_fmt_len(const uint64_t* __restrict__ cs, int nq,
+                                                int qid_base, int64_t* __restrict__ off,
+                                                int64_t* __restrict__ blocksum) {
+  __shared__ int64_t sh[FB];
+  const int i = blockIdx.x * FB + threadIdx.x;
   const int64_t v = i < nq ? line_len((int64_t)qid_base + i, cs[i]) : 0;
   sh[threadIdx.x] = v;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+  for (int o = 1; o < FB; o <<= 1) {  // inclusive Hillis-Steele scan
     const int64_t t = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
     __syncthreads();
     sh[threadIdx.x] += t;
     __syncthreads();
   }
   if (i < nq) off[i + 1] = sh[threadIdx.x];  // block-local inclusive
-  if (threadIdx.x == 1023) blocksum[blockIdx.x] = sh[1023];
+  if (threadIdx.x == FB - 1) blocksum[blockIdx.x] = sh[FB - 1];
 }
 
 // Exclusive scan of the block sums in place (+ the total at [nb]): one 1024-thread block,
@@ -1024,17 +1026,18 @@ __device__ __forceinline__ void put_dec(char* txt, int end, uint64_t v) {
   } while (r);
 }
 
-// Each block renders its 1024 lines into LDS, then stores the block's byte range with dword
+// Each block renders its FB lines into LDS, then stores the block's byte range with dword
 // stores (bytes only at the two unaligned ends).  The target may be page-locked host memory
 // (the native engine writes the report straight into its output buffer): wide, contiguous
 // stores keep the link busy where per-character stores would not.
-__global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__ cs, int nq,
-                                                   int qid_base, int64_t* __restrict__ off,
-                                                   const int64_t* __restrict__ blocksum,
-                                                   const int64_t* __restrict__ base,
-                                                   char* __restrict__ out) {
-  __shared__ char txt[1024 * 48 + 4];
-  const int i = blockIdx.x * 1024 + threadIdx.x;
+template <int FB>
+__global__ void __launch_bounds__(FB) k_fmt_write(const uint64_t* __restrict__ cs, int nq,
+                                                 int qid_base, int64_t* __restrict__ off,
+                                                 const int64_t* __restrict__ blocksum,
+                                                 const int64_t* __restrict__ base,
+                                                 char* __restrict__ out) {
+  __shared__ char txt[FB * 48 + 4];
+  const int i = blockIdx.x * FB + threadIdx.x;
   const int64_t b0 = base ? *base : 0;  // byte offset of this run's first line in out
   const int64_t g0 = b0 + blocksum[blockIdx.x], g1 = b0 + blocksum[blockIdx.x + 1];
   if (i < nq) {
@@ -1062,7 +1065,7 @@ __global__ void __launch_bounds__(1024) k_fmt_write(const uint64_t* __restrict__
   }
   unsigned* o32 = reinterpret_cast<unsigned*>(out + a0);
   const int nw = (int)((a1 - a0) >> 2), b = (int)(a0 - g0);
-  for (int w = threadIdx.x; w < nw; w += 1024) {
+  for (int w = threadIdx.x; w < nw; w += FB) {
     const int s = b + 4 * w;
     o32[w] = (unsigned)(unsigned char)txt[s] | ((unsigned)(unsigned char)txt[s + 1] << 8) |
              ((unsigned)(unsigned char)txt[s + 2] << 16) |
@@ -1757,8 +1760,14 @@ extern "C" int dmlp_fill_f64(double* p, int64_t n, double v, void* stream) {
 
 extern "C" int64_t dmlp_format_bound(int nq) { return (int64_t)nq * 48 + 64; }
 
-// line_off needs nq + 1 + (nq/1024 + 2) int64 of scratch; on completion line_off[nq] = bytes.
-extern "C" int64_t dmlp_format_scratch(int nq) { return (int64_t)nq + 1 + (nq + 1023) / 1024 + 1; }
+// lines per format block: 256 (512 blocks for the headline's 131072 lines push the report's
+// PCIe writes from more CUs than 1024-line blocks: 106.5 vs 109.4 us, profiles/r12k_fmt_block_ab.txt)
+constexpr int kFmtBlock = 256;
+
+// line_off needs nq + 1 + (nq/FB + 2) int64 of scratch; on completion line_off[nq] = bytes.
+extern "C" int64_t dmlp_format_scratch(int nq) {
+  return (int64_t)nq + 1 + (nq + kFmtBlock - 1) / kFmtBlock + 1;
+}
 
 extern "C" int dmlp_format_report(const uint64_t* cs, int nq, int qid_base, int64_t* line_off,
                                   char* out, void* stream) {
@@ -1771,14 +1780,15 @@ extern "C" int dmlp_format_report_at(const uint64_t* cs, int nq, int qid_base, i
                                      char* out, const int64_t* base, void* stream) {
   if (nq <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int nb = (nq + 1023) / 1024;
+  const int nb = (nq + kFmtBlock - 1) / kFmtBlock;
   int64_t* blocksum = line_off + nq + 1;
-  hipLaunchKernelGGL(k_fmt_len, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off, blocksum);
+  hipLaunchKernelGGL(k_fmt_len<kFmtBlock>, dim3(nb), dim3(kFmtBlock), 0, st, cs, nq, qid_base,
+                     line_off, blocksum);
   DMLP_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_fmt_scan_blocks, dim3(1), dim3(1024), 0, st, blocksum, nb);
   DMLP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_fmt_write, dim3(nb), dim3(1024), 0, st, cs, nq, qid_base, line_off,
-                     blocksum, base, out);
+  hipLaunchKernelGGL(k_fmt_write<kFmtBlock>, dim3(nb), dim3(kFmtBlock), 0, st, cs, nq, qid_base,
+                     line_off, blocksum, base, out);
   DMLP_LAUNCH_CHECK();
   return 0;
 }
