@@ -664,6 +664,8 @@ struct Step {
     // DMA copy: each separate small D2H cost a copy command's latency on the step's tail.
     int64_t* small = w.small64_h.get(8);
     int64_t* small_d = w.small64_d.get(8);
+    // (page-locked: the pack kernel writes the words straight there, no copy on the tail)
+    int64_t* small_dev = (int64_t*)host_device_view((char*)small, 8 * sizeof(int64_t));
     unsigned* dr_bad = dr ? w.dr_words.p + 72 : nullptr;  // device render: a value out of range
     auto render = [&]() {
       const int64_t* len_src = nullptr;
@@ -674,9 +676,9 @@ struct Step {
         len_src = off + Q;
       }
       hipLaunchKernelGGL(k_pack_small, dim3(1), dim3(64), 0, st, len_src, Lp->ovf,
-                         a->early ? estats : nullptr, dr_bad, small_d);
+                         a->early ? estats : nullptr, dr_bad, small_dev ? small_dev : small_d);
       CK(hipGetLastError());
-      CK(dmlp::dma_copy(small, small_d, 8 * sizeof(int64_t), st));
+      if (!small_dev) CK(dmlp::dma_copy(small, small_d, 8 * sizeof(int64_t), st));
       if (want_report && a->report_mode == 1 && !direct)
         CK(dmlp::dma_copy(a->report_dst, w.d_text.p, (size_t)dmlp_format_bound((int)Q), st));
     };
