@@ -38,6 +38,7 @@
 #   modes      h2d / xgmi dataset ingress at P = 3 / 4 (host plane) with --verify
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   cmpab      pair refine over compacted group entries vs the previous tree (library A/B)
+#   qcab       early start query-operand slices 4 / 6 / 8 (DMLP_FAST_QCHUNKS A/B, timelines)
 #   rdab       report straight into pinned host memory vs staged + D2H (DMLP_REPORT_DIRECT A/B)
 set -u
 TAG=${1:?tag}
@@ -266,6 +267,14 @@ for task in "$@"; do
       rm -rf gpurun_out/ab
       AB_ROUNDS=3 AB_STEPS=30 step cmpab 900 bash tools/kernel_ab.sh base cmp
       python tools/ab_summary.py gpurun_out/ab | tee "$OUT/cmpab_kernels.txt" ;;
+    qcab)  # early start: the query operands rendered + copied in 4 / 6 / 8 slices, interleaved,
+           # with step timelines (operands_landed)
+      rm -rf gpurun_out/ab
+      AB_PROF=0 AB_ROUNDS=3 AB_STEPS=100 AB_ARGS="--diag-steps 30" \
+          step qcab 900 bash tools/kernel_ab.sh qc4:DMLP_FAST_QCHUNKS=4 qc6:DMLP_FAST_QCHUNKS=6 qc8:DMLP_FAST_QCHUNKS=8
+      for f in gpurun_out/ab/*.log; do
+        echo "$f $(grep -o '"p50": [0-9.]*' "$f" | head -1) $(grep -o '"operands_landed": [0-9.]*' "$f")"
+      done | tee "$OUT/qcab_summary.txt" ;;
     rdab)  # the report written straight into the caller's pinned buffer vs staged + one D2H copy,
            # interleaved (AB_ROUNDS x 100 steps), then the contract (drop-in, mpiexec) both ways
       AB_PROF=0 AB_ROUNDS=${AB_ROUNDS:-3} AB_STEPS=100 AB_ARGS="--diag-steps 30" \
