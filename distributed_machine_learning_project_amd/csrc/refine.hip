@@ -1095,7 +1095,7 @@ __device__ __forceinline__ double row_value(const double* __restrict__ X, const 
 #endif
 constexpr int PAIR_U = DMLP_PAIR_U;
 #ifndef DMLP_PAIR_RL
-#define DMLP_PAIR_RL 8  // lanes per exact row in the survivors' phase: 8 (218 us) or 16 (239 us), r8c
+#define DMLP_PAIR_RL 8  // lanes per exact row in the survivors' phase: 8 (218 us), 16 (239 us, r8c) or 4 (222 us, r12p)
 #endif
 #ifndef DMLP_PAIR_DOT2
 #define DMLP_PAIR_DOT2 1  // member scores by v_dot2c_f32_f16 (219 -> 212 us, 0 spills; r8h) or cvt + fma

@@ -39,6 +39,7 @@
 #   prewarm    the drop-in contract at KNN_PREWARM_US 0 / 300 / 2000 / 5000
 #   cmpab      pair refine over compacted group entries vs the previous tree (library A/B)
 #   qcab       early start query-operand slices 4 / 6 / 8 (DMLP_FAST_QCHUNKS A/B, timelines)
+#   rl4ab      pair refine at 4 vs 8 lanes per exact row (library A/B, --verify of the variant)
 #   rdab       report straight into pinned host memory vs staged + D2H (DMLP_REPORT_DIRECT A/B)
 set -u
 TAG=${1:?tag}
@@ -275,6 +276,13 @@ for task in "$@"; do
       for f in gpurun_out/ab/*.log; do
         echo "$f $(grep -o '"p50": [0-9.]*' "$f" | head -1) $(grep -o '"operands_landed": [0-9.]*' "$f")"
       done | tee "$OUT/qcab_summary.txt" ;;
+    rl4ab)  # pair refine exact rows at 4 lanes per row (ab/libdmlp_rl4.so) vs 8 (ab/libdmlp_base.so):
+            # --verify of the variant, then interleaved under the kernel tracer
+      DMLP_LIB=ab/libdmlp_rl4.so step rl4_verify 300 python bench.py --steps 20 --warmup 2 --verify
+      grep -o '"verify_ok": [a-z]*' "$OUT/rl4_verify.log"
+      rm -rf gpurun_out/ab
+      AB_ROUNDS=3 AB_STEPS=30 step rl4ab 900 bash tools/kernel_ab.sh base rl4
+      python tools/ab_summary.py gpurun_out/ab | tee "$OUT/rl4ab_kernels.txt" ;;
     rdab)  # the report written straight into the caller's pinned buffer vs staged + one D2H copy,
            # interleaved (AB_ROUNDS x 100 steps), then the contract (drop-in, mpiexec) both ways
       AB_PROF=0 AB_ROUNDS=${AB_ROUNDS:-3} AB_STEPS=100 AB_ARGS="--diag-steps 30" \
