@@ -168,6 +168,7 @@ int dmlp_screen_x1_cap_kt(int KT, int kmax);
 // MFMA steps on the 8-row max: rows 4 kg .. 4 kg + 3 of steps 2p and 2p + 1, entry index 4 p + kg),
 // else 4 (consecutive rows, entry index = row / 4); the refines expand each entry to its rows
 int dmlp_screen_x1_group_rows(int kmax);
+int dmlp_screen_x1_group_rows_kt(int KT, int kmax);
 int dmlp_screen_x1_waves_per_cu(int kmax);
 int dmlp_screen_x1_waves_per_cu_kt(int KT, int kmax);  // A > 64: one wave per SIMD
 int64_t dmlp_screen_x1_min_slices(int64_t n_tiles);

@@ -1581,7 +1581,7 @@ extern "C" int dmlp_refine_groups2(int cap, const int* cand_ids, const int* cand
                                    int label_hi, int* out_label, uint64_t* out_cs, int* status,
                                    int* ovf_count, int collect, void* stream) {
   // (the lists' producer, by its cap: dmlp_screen_x1_cap(kmax) of the screen that wrote them)
-  const int grows = collect ? 4 : dmlp_screen_x1_group_rows(64);
+  const int grows = collect ? 4 : dmlp_screen_x1_group_rows_kt(KT, 64);
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, nullptr, xinit,
                             qhi, KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
                             label_lo, label_hi, out_label, out_cs, status, ovf_count, collect,
@@ -1600,7 +1600,7 @@ extern "C" int dmlp_refine_groups_rm(int cap, const int* cand_ids, const int* ca
   return refine_groups_impl(cap, cand_ids, cand_cnt, cand_h, S, X, A, Qx, xfrag, xrow, xinit, qhi,
                             KT, hl, n_points, qidx, qk, nq, out_d, out_i, kstride, labels,
                             label_lo, label_hi, out_label, out_cs, status, ovf_count, 0, stream,
-                            kmax, dmlp_screen_x1_group_rows(kmax), Xi, Qi);
+                            kmax, dmlp_screen_x1_group_rows_kt(KT, kmax), Xi, Qi);
 }
 
 // Whether refine_groups_impl serves these lists with k_refine_pair: one slice of the host's fp16

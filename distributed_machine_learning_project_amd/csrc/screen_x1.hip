@@ -34,6 +34,16 @@
 
 namespace {
 
+// The pair epilogue (k_screen_x1 PAIR): every 16-entry screen, and the 32-entry one up to
+// KT = DMLP_X1_PAIR32_KTMAX (1) — at KT >= 2 its 8-row groups cost the k in (32, 64] refine more
+// (4-8 fragments per member) than the screen saves (profiles/r12r_pair32_kt_ab.txt)
+#ifndef DMLP_X1_PAIR32_KTMAX
+#define DMLP_X1_PAIR32_KTMAX 1
+#endif
+__host__ __device__ constexpr bool x1_pair(bool collect, int KT, int SUB) {
+  return !collect && (SUB == 16 || KT <= DMLP_X1_PAIR32_KTMAX);
+}
+
 template <int KT, int SUB, int DEPTH, int CHECK>
 struct X1Cfg {
   static constexpr int CT = 4;                  // MFMA column tiles per wave
@@ -91,12 +101,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((SUB == 32 |
   // lower bound on its k-th best score - 2 eps from the first pass); a full buffer is flushed to
   // the column's global list (up to ccap group entries per (query, slice)) instead of compacted
   using C = X1Cfg<KT, SUB, DEPTH, CHECK>;
-  // PAIR (SUB = 16: k <= 32, not COLLECT): the hit test and the append run once per PAIR of steps, on the
+  // PAIR (not COLLECT; x1_pair): the hit test and the append run once per PAIR of steps, on the
   // 8-row group max (rows 4 kg .. 4 kg + 3 of both steps; entry index = pair * 4 + kg), instead of
   // per step on 4-row groups: the per-step max stays, the compare, the branch and the taken
   // step's append VALU halve (the screen is VALU-issue-bound: ~8.6 VALU per MFMA).  The
   // refine expands each entry to its 8 members (dmlp_screen_x1_group_rows).
-  constexpr bool PAIR = !COLLECT;
+  constexpr bool PAIR = x1_pair(COLLECT, KT, SUB);
   static_assert(!PAIR || (CHECK == 2 && DEPTH == 4), "the pair epilogue assumes 2-step checks");
   constexpr int CT = C::CT;
   constexpr int D = C::D;
@@ -689,10 +699,13 @@ extern "C" int dmlp_screen_x1_cols(int KT, int kmax) {
 // group ids per (query, slice) (refine expands each to its dmlp_screen_x1_group_rows members)
 extern "C" int dmlp_screen_x1_cap_kt(int KT, int kmax) { return 4 * (x1_sub(KT, kmax) - 1); }
 extern "C" int dmlp_screen_x1_cap(int kmax) { return dmlp_screen_x1_cap_kt(1, kmax); }
-// rows per group entry of the screen that serves kmax (and of its early-start form): 8 (SUB = 16, k <= 32:
-// the pair epilogue, steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive rows);
-// the COLLECT pass always 4
-extern "C" int dmlp_screen_x1_group_rows(int kmax) { (void)kmax; return 8; }
+// rows per group entry of the screen that serves (KT, kmax) (and of its early-start form): 8 (the
+// pair epilogue, x1_pair: steps 2p and 2p + 1, rows 4 kg .. 4 kg + 3 of each) or 4 (consecutive
+// rows); the COLLECT pass always 4
+extern "C" int dmlp_screen_x1_group_rows_kt(int KT, int kmax) {
+  return x1_pair(false, KT, x1_sub(KT, kmax)) ? 8 : 4;
+}
+extern "C" int dmlp_screen_x1_group_rows(int kmax) { return dmlp_screen_x1_group_rows_kt(1, kmax); }
 // resident workgroups (= waves) per CU: LDS-bound at 17.5 KiB (SUB 16, 4 tiles) / 33.5 KiB
 // (SUB 32); the 8-tile variant runs one wave per SIMD (register-bound)
 extern "C" int dmlp_screen_x1_waves_per_cu(int kmax) {

@@ -40,6 +40,8 @@
 #   cmpab      pair refine over compacted group entries vs the previous tree (library A/B)
 #   qcab       early start query-operand slices 4 / 6 / 8 (DMLP_FAST_QCHUNKS A/B, timelines)
 #   rl4ab      pair refine at 4 vs 8 lanes per exact row (library A/B, --verify of the variant)
+#   p32kt      pair epilogue on the 32-entry screen up to KT 8 / 2 / 1 (library A/B over the sweep rows)
+#   p32q       the pair-epilogue KT limit A/B at Q = 131072 (A = 64 / 128, k 17-64)
 #   rdab       report straight into pinned host memory vs staged + D2H (DMLP_REPORT_DIRECT A/B)
 set -u
 TAG=${1:?tag}
@@ -283,6 +285,27 @@ for task in "$@"; do
       rm -rf gpurun_out/ab
       AB_ROUNDS=3 AB_STEPS=30 step rl4ab 900 bash tools/kernel_ab.sh base rl4
       python tools/ab_summary.py gpurun_out/ab | tee "$OUT/rl4ab_kernels.txt" ;;
+    p32kt)  # the pair epilogue on the 32-entry screen (k in (32, 64]) up to KT = 8 / 2 / 1
+            # (ab/libdmlp_k{8,2,1}.so): --verify of each variant at A = 64 / 128, then the sweep's
+            # k 1-64 / 33-64 rows at A = 64 / 128 / 256 alternating over the variants, two rounds
+      for V in 2 1; do
+        DMLP_LIB=ab/libdmlp_k$V.so step p32kt_verify_k$V 300 python bench.py --attrs $((64 * V)) \
+            --k 48 --kmin 33 --kmax 64 --q-per-gpu 16384 --steps 5 --warmup 1 --min-warmup-s 0 \
+            --no-busbw --diag-steps 0 --verify
+      done
+      grep -Ho '"verify_ok": [a-z]*' "$OUT"/p32kt_verify_*.log
+      for R in 1 2; do
+        for V in 8 2 1; do
+          DMLP_LIB=ab/libdmlp_k$V.so step p32kt_k${V}_$R 400 python3 -u tools/bench_sweep.py \
+              --out "$OUT/p32kt_k${V}_$R.jsonl" --timeout 120 --ns 100000 --attrs 64,128,256 \
+              --ks 1-64,33-64
+        done
+      done ;;
+    p32q)  # the same A/B at the headline's Q = 131072: A = 64 / 128 at k 17-64, interleaved
+      for A in 64 128; do
+        AB_PROF=0 AB_ROUNDS=3 AB_STEPS=60 AB_ARGS="--attrs $A --k 40 --kmin 17 --kmax 64 --diag-steps 0" \
+            step p32q_a$A 600 bash tools/kernel_ab.sh k8 k1
+      done ;;
     rdab)  # the report written straight into the caller's pinned buffer vs staged + one D2H copy,
            # interleaved (AB_ROUNDS x 100 steps), then the contract (drop-in, mpiexec) both ways
       AB_PROF=0 AB_ROUNDS=${AB_ROUNDS:-3} AB_STEPS=100 AB_ARGS="--diag-steps 30" \
