@@ -620,10 +620,14 @@ int x1_sub16_kmax() {
   }();
   return v;
 }
-// KT 2 keeps k in (16, 32] on the 32-entry variant: the early start needs its registers free
-// (the 16-entry KT 2 screen leaves the copies no wave slot) and with it that one is faster
-// (A = 48 / 64, k = 32: 4.26-4.48 vs 4.45-4.71 ms, profiles/r11z_kt2_ab.txt)
-int x1_sub(int KT, int kmax) { return kmax <= (KT == 2 ? 16 : x1_sub16_kmax()) ? 16 : 32; }
+// The same class boundary at every KT.  (KT 2's 16-entry screen leaves the early start's copies
+// no wave slot, and with the pair epilogue on the 32-entry screen KT 2 once ran k in (16, 32]
+// faster there with the early start (r11z); with that epilogue at KT 1 only (x1_pair) the 16-entry
+// screen wins: A = 48 / 64, k = 32, 3.98-4.64 vs 4.45-4.88 ms, profiles/r12w_kt2_sub_ab.txt.)
+int x1_sub(int KT, int kmax) {
+  (void)KT;
+  return kmax <= x1_sub16_kmax() ? 16 : 32;
+}
 
 // One launch over slices [s_first, s_first + S_l) of an S-slice split (cand_* laid out for S).
 // (Variants measured slower and deleted — the LDS-ring screen, 8 column tiles per wave, the

@@ -201,14 +201,13 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     waits > 0, eps growths > 0 (the far point sits in the last slice) and no timeout.  Two
     different inputs of equal shape alternate A, B, A, B (early on), then once with the early
     start off.  Each slice's ready word is one DMA copy carrying the slice's max norm; every
-    report, label and checksum == its own oracle's.  A = 64 / k = 32 runs the KT = 2 screen on
-    its 32-entry variant (screen_x1.hip x1_sub: KT 2 keeps that variant for k in (16, 32] so the
-    early start stays on).  A = 128 (KT = 4) and A = 256 (KT = 8): the step refuses the early start
+    report, label and checksum == its own oracle's.  A = 64 / k = 64 runs the KT = 2 screen on its
+    32-entry variant with the early start; A = 64 / k <= 32 its 16-entry variant (2 x 256
+    registers), which leaves no slot for the copies: no early start there.  A = 128 (KT = 4) and A = 256 (KT = 8): the step refuses the early start
     there — its image copies (blit kernels in this process) found no wave slot beside the spinning
     KT 4 screen in 2 of 7 sessions (profiles/r12a_kt4_early.txt), KT 8 takes all 512 registers —
     and the results stay exact.  One screen slice needs a full round of waves (>= 131072 queries
-    at KT = 1, >= 65536 at KT >= 4).  A = 64 / k <= 16 (KT 2, 2 x 256 registers) leaves no slot
-    for the copies: no early start there.  render: the device
+    at KT = 1, >= 65536 at KT >= 4).  render: the device
     render switch on or off — an early-start step renders on the host either way
     (pipeline.hip dr_early_ok); without the early start the switch's render runs."""
     from distributed_machine_learning_project_amd import _lib
@@ -217,9 +216,9 @@ def test_native_step_early_start(gpu, n, A, kmax, render):
     # an early-start step renders on the host whatever the switch says (the device render's
     # kernels get no reliable wave slots beside the spinning screen: pipeline.hip dr_early_ok)
     dr_used = False
-    # KT 2 / k <= 16: its screen leaves no registers for the early start's copies (pipeline.hip
-    # early_room): no early start there
-    no_room = A > 32 and A <= 64 and kmax <= 16
+    # KT 2 / k <= 32 (the 16-entry screen): no registers for the early start's copies
+    # (pipeline.hip early_room): no early start there
+    no_room = A > 32 and A <= 64 and kmax <= 32
     Q = 131072 + 64 * 3 if A <= 64 else 65536 + 64
     cases = _early_inputs(n, A, kmax, Q, seed=n + A + kmax)
     dsts = []

@@ -42,6 +42,7 @@
 #   rl4ab      pair refine at 4 vs 8 lanes per exact row (library A/B, --verify of the variant)
 #   p32kt      pair epilogue on the 32-entry screen up to KT 8 / 2 / 1 (library A/B over the sweep rows)
 #   p32q       the pair-epilogue KT limit A/B at Q = 131072 (A = 64 / 128, k 17-64)
+#   kt2b       KT 2 at k = 32: 16- vs 32-entry screen (library A/B, after the pair limit)
 #   rdab       report straight into pinned host memory vs staged + D2H (DMLP_REPORT_DIRECT A/B)
 set -u
 TAG=${1:?tag}
@@ -305,6 +306,12 @@ for task in "$@"; do
       for A in 64 128; do
         AB_PROF=0 AB_ROUNDS=3 AB_STEPS=60 AB_ARGS="--attrs $A --k 40 --kmin 17 --kmax 64 --diag-steps 0" \
             step p32q_a$A 600 bash tools/kernel_ab.sh k8 k1
+      done ;;
+    kt2b)  # A = 48 / 64 at k = 32 with the pair epilogue off on the 32-entry screen: the 16-entry
+           # screen (ab/libdmlp_s16.so, no early start) vs the 32-entry one (ab/libdmlp_s32.so)
+      for A in 48 64; do
+        AB_PROF=0 AB_ROUNDS=3 AB_STEPS=60 AB_ARGS="--attrs $A --k 32 --diag-steps 0" \
+            step kt2b_a$A 600 bash tools/kernel_ab.sh s16 s32
       done ;;
     rdab)  # the report written straight into the caller's pinned buffer vs staged + one D2H copy,
            # interleaved (AB_ROUNDS x 100 steps), then the contract (drop-in, mpiexec) both ways
